@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark of the FastSLAM 2.0 particle update (BASELINE.json metric).
+
+One step = one FastSLAM2.iterate (reference fast_slam_2/algorithms/fast_slam_2.py:33-67)
+over every particle: motion sample, M = 4 measurement updates (3 associating,
+1 new landmark), normalise, N_eff, resample when N_eff < N/2, estimate.
+Synthetic workload of SURVEY.md §8(d); particle state resident in HBM before
+the timed region starts.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, particles sharded)
+
+Default workload: BASELINE config 3, 1e6 particles per GPU x 500 landmarks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "fast-slam_amd"))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    "1": dict(N=100, L=20, P=180, icp=False, name="cfg1_N100_L20_180beam"),
+    "2": dict(N=100_000, L=200, P=180, icp=False, name="cfg2_N1e5_L200_180beam"),
+    "3": dict(N=1_000_000, L=500, P=180, icp=False, name="cfg3_N1e6_L500_180beam"),
+    "4": dict(N=1_000_000, L=500, P=720, icp=True, name="cfg4_N1e6_L500_720beam_icp"),
+}
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
+    ap.add_argument("--particles", type=int, default=0, help="override particles per GPU")
+    ap.add_argument("--landmarks", type=int, default=0, help="override landmarks per particle")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def populate(f, n_local, L, seed, rank):
+    """Synthetic initial state generated on the GPU in chunks."""
+    import torch
+    import fs2_synthetic as syn
+    from fast_slam_2 import _native as nat
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev)
+    g.manual_seed(1_000_003 * (seed + 1) + rank)
+    base = torch.tensor(syn.common_landmarks(L, seed), dtype=torch.float64, device=dev)
+    x = torch.randn(n_local, generator=g, dtype=torch.float64, device=dev) * 0.05
+    y = torch.randn(n_local, generator=g, dtype=torch.float64, device=dev) * 0.05
+    yaw = torch.randn(n_local, generator=g, dtype=torch.float64, device=dev) * 0.01
+    w = torch.full((n_local,), 1.0 / f.num_particles, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    nat.check(f._lib.fs2_set_state(f._h, 0, n_local, x.data_ptr(), y.data_ptr(), yaw.data_ptr(),
+                                   w.data_ptr(), None, None, 0, nat.FS2_DEVICE), f._h)
+    chunk = max(1, (512 << 20) // (L * 48))
+    for o in range(0, n_local, chunk):
+        k = min(chunk, n_local - o)
+        lm = torch.empty((k, L, 6), dtype=torch.float64, device=dev)
+        lm[:, :, 0:2] = base + syn.MAP_JITTER * torch.randn((k, L, 2), generator=g,
+                                                            dtype=torch.float64, device=dev)
+        lm[:, :, 2] = syn.INIT_COV
+        lm[:, :, 3] = 0.0
+        lm[:, :, 4] = 0.0
+        lm[:, :, 5] = syn.INIT_COV
+        cnt = torch.full((k,), L, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        nat.check(f._lib.fs2_set_state(f._h, o, k, None, None, None, None, cnt.data_ptr(),
+                                       lm.data_ptr(), L, nat.FS2_DEVICE), f._h)
+        del lm, cnt
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(L, P, budget_s, seed):
+    """The C oracle (oracle/fs2_oracle.c, reference semantics, 1 thread) on a sample."""
+    import fs2_synthetic as syn
+    from oracle import oracle as orc
+    n = 6000
+    wl = syn.Workload(n, L, seed)
+    x, y, yaw = wl.poses()
+    o = orc.OracleFilter(n, L + 64)
+    o.set_state(x, y, yaw, np.full(n, 1.0 / n), np.full(n, L), wl.maps())
+    rng = np.random.default_rng(seed)
+    t_work, scans = 0.0, 0
+    while t_work < budget_s and scans < 60:
+        rot, tr = syn.odometry(scans)
+        ms = wl.measurements(scans)
+        nz = rng.normal(0, 0.001 if rot else 0.0055, n)
+        u0 = rng.uniform(0, 1.0 / n)
+        t0 = time.perf_counter()
+        o.iterate(rot, tr, ms, nz, u0)
+        t_work += time.perf_counter() - t0
+        scans += 1
+    return dict(value=n * scans / t_work, unit="particle-updates/s", cores=1, kind="port",
+                sample=f"{n} particles x {L} landmarks, M=4, {scans} scans "
+                       f"(C oracle, reference semantics, 1 thread, {t_work:.1f} s)")
+
+
+def pmc_traffic(workload):
+    p = os.path.join(REPO, "profiles", f"pmc_update_{workload}.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from fast_slam_2 import _native as nat
+
+    cfg = dict(CONFIGS[args.config])
+    n_per_gpu = args.particles or cfg["N"]
+    L = args.landmarks or cfg["L"]
+    N = n_per_gpu * world
+    comm_id = None
+    if world > 1:
+        obj = [nat.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    total_scans = args.warmup + args.steps
+    f = fast_slam_2.FastSLAM2(N, device=local, rng="device", seed=args.seed, reduce="auto",
+                              landmark_capacity=L + total_scans + 8, rank=rank,
+                              world_size=world, comm_id=comm_id, verbose=False)
+    populate(f, f.n_local, L, args.seed, rank)
+    scans_pts = None
+    if cfg["icp"]:
+        scans_pts = [syn.room_scan((0.03 * s, 0.0, 0.0), cfg["P"], args.seed, s)
+                     for s in range(total_scans + 1)]
+
+    def one_scan(s):
+        rot, tr = syn.odometry(s)
+        if scans_pts is not None:
+            R, t = fast_slam_2.ICP.get_transformation(scans_pts[s], scans_pts[s + 1])
+            # Robot.get_transformation_icp (robot.py:108-120)
+            if tr != 0:
+                rot, tr = 0.0, float(np.linalg.norm(t))
+            else:
+                rot, tr = float(-np.arctan2(R[1, 0], R[0, 0])), 0.0
+        return f.step(rot, tr, syn.scan_measurements(L, s, args.seed))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for s in range(args.warmup):
+        one_scan(s)
+    f.set_profiling(True)
+    resamples = 0
+    visited = 0
+    barrier()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, total_scans):
+        _, st = one_scan(s)
+        resamples += st.resampled
+        visited += st.slots_visited
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    prof = f.profile()
+    icp_us = None
+    if scans_pts is not None:
+        t1 = time.perf_counter()
+        for s in range(5):
+            fast_slam_2.ICP.get_transformation(scans_pts[s], scans_pts[s + 1])
+        icp_us = (time.perf_counter() - t1) / 5 * 1e6
+
+    if rank == 0:
+        launches = max(prof["update_launches"], 1)
+        ms_launch = prof["update_ms"] / launches
+        bytes_launch = prof["update_bytes"] / launches
+        achieved = bytes_launch / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(L, cfg["P"], args.cpu_seconds, args.seed)
+        out = {
+            "metric": "particle-updates/s",
+            "value": N * args.steps / dt,
+            "unit": "particle-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8d: 6 m landmark grid, 3 hits + 1 miss per scan, "
+                    "odometry 4x0.03 m then 0.05 rad; device Philox motion noise)",
+            "config": {"workload": cfg["name"], "particles_per_gpu": n_per_gpu,
+                       "particles_total": N, "landmarks": L, "beams": cfg["P"],
+                       "measurements_per_scan": 4, "icp": cfg["icp"],
+                       "parallelism": f"particle-shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(cfg["name"]),
+                         "kernel": "k_update", "bytes_per_launch": bytes_launch,
+                         "ms_per_launch": ms_launch},
+            "cpu_baseline": cpu,
+            "extra": {"scan_device_ms": prof["scan_ms"] / max(prof["scans"], 1),
+                      "update_ms": ms_launch,
+                      "reduce_ms": prof["reduce_ms"] / max(prof["scans"], 1),
+                      "resample_ms_total": prof["resample_ms"],
+                      "resamples": resamples,
+                      "slots_visited_per_particle_scan": visited / (f.n_local * args.steps),
+                      "icp_us": icp_us},
+        }
+        print(json.dumps(out), flush=True)
+    f.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

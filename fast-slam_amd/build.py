@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Build libfs2.so for gfx950 in-tree (fast-slam_amd/lib/libfs2.so).
+
+hipcc cross-compiles without a GPU.  -ffp-contract=off: the kernels place
+every FMA explicitly to follow the reference's numpy/OpenBLAS operation order.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB_DIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIB_DIR, "libfs2.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("FS2_OFFLOAD_ARCH", "gfx950")
+SOURCES = ["fs2_api.hip", "fs2_kernels.hip"]
+HEADERS = ["fs2_device.hpp", "fs2_kernels.hpp", "fs2_comm.hpp"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "fs2.h"))
+    deps.append(os.path.abspath(__file__))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value",
+           "-I", os.path.join(ROCM, "include"),
+           *[os.path.join(CSRC, s) for s in SOURCES],
+           "-o", LIB + ".tmp", "-L", os.path.join(ROCM, "lib"), "-lrccl",
+           "-Wl,-rpath," + os.path.join(ROCM, "lib")]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,793 @@
+// fs2_api.hip -- C ABI of libfs2.so (include/fs2.h): handle, HBM state, the
+// per-scan launch sequence of the FastSLAM 2.0 update, state import/export and
+// the stateless ICP / LineFilter / association helpers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fs2.h"
+#include "fs2_comm.hpp"
+#include "fs2_kernels.hpp"
+
+using namespace fs2;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_err(std::string *dst, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    if (dst) *dst = buf;
+    return code;
+}
+
+#define HIP_TRY(h, expr)                                                                       \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return set_err((h) ? &(h)->err : nullptr,                                          \
+                           e_ == hipErrorOutOfMemory ? FS2_ERR_OOM : FS2_ERR_HIP,              \
+                           "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,    \
+                           __LINE__);                                                          \
+    } while (0)
+
+// Smallest q >= 0 with sqrt(q) >= gate: sqrt(q) < gate  <=>  q < gate2.
+double gate_to_q(double gate) {
+    if (!(gate > 0.0)) return 0.0;          // never matches (q >= 0 && q < 0)
+    if (std::isinf(gate)) return INFINITY;
+    double q = gate * gate;
+    while (q > 0.0 && std::sqrt(std::nextafter(q, 0.0)) >= gate) q = std::nextafter(q, 0.0);
+    while (std::sqrt(q) < gate) q = std::nextafter(q, INFINITY);
+    return q;
+}
+
+struct ProfEvents {
+    hipEvent_t e[6] = {};
+    bool ok = false;
+};
+
+}  // namespace
+
+struct fs2_handle {
+    fs2_config cfg{};
+    int64_t n_global = 0, n = 0, first = 0;
+    hipStream_t stream = nullptr;
+    int cur = 0;
+    double *x[2] = {}, *y[2] = {}, *yaw[2] = {}, *w[2] = {};
+    int32_t *cnt[2] = {};
+    std::vector<char *> pages[2];
+    char **pages_dev[2] = {};
+    int cap = 0, max_cap = 4096;
+    double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
+    int64_t *part_best_i = nullptr;
+    int32_t *part_maxcnt = nullptr;
+    double *cbuf = nullptr, *bsum = nullptr;
+    int32_t *src = nullptr;
+    DevStats *stats_dev = nullptr, *stats_host = nullptr;
+    double *noise_dev = nullptr, *noise_pin = nullptr, *u0_dev = nullptr, *u0_pin = nullptr;
+    int32_t *assoc_dev = nullptr;
+    int64_t assoc_cap = 0;
+    int32_t last_m = 0;
+    uint64_t scan = 0;
+    int32_t cnt_upper = 0;
+    double gate2 = 64.0;
+    std::string err;
+    bool profiling = false;
+    ProfEvents ev;
+    fs2_profile prof{};
+    fs2comm::Comm *comm = nullptr;
+
+    MapRef map(int set) const { return MapRef{pages_dev[set], n}; }
+    int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
+    bool sequential() const {
+        const int mode = cfg.reduce_mode;
+        if (mode == FS2_REDUCE_SEQUENTIAL) return true;
+        if (mode == FS2_REDUCE_PARALLEL) return false;
+        return n_global <= 4096;
+    }
+};
+
+static int grow_pages(fs2_handle *h, int need_slots) {
+    if (need_slots <= h->cap) return FS2_OK;
+    if (need_slots > h->max_cap)
+        return set_err(&h->err, FS2_ERR_CAPACITY, "map needs %d landmark slots, limit is %d",
+                       need_slots, h->max_cap);
+    const int need_pages = (need_slots + kPageSlots - 1) / kPageSlots;
+    const size_t page_bytes = (size_t)kPageSlots * (size_t)MapRef{nullptr, h->n}.slot_stride();
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    for (int set = 0; set < 2; ++set) {
+        while ((int)h->pages[set].size() < need_pages) {
+            char *p = nullptr;
+            HIP_TRY(h, hipMalloc(&p, page_bytes > 0 ? page_bytes : 16));
+            h->pages[set].push_back(p);
+        }
+        HIP_TRY(h, hipMemcpy(h->pages_dev[set], h->pages[set].data(),
+                             sizeof(char *) * h->pages[set].size(), hipMemcpyHostToDevice));
+    }
+    h->cap = need_pages * kPageSlots;
+    return FS2_OK;
+}
+
+extern "C" {
+
+int32_t fs2_abi_version(void) { return FS2_ABI_VERSION; }
+
+void fs2_config_default(fs2_config *c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof *c);
+    c->num_particles = 20;                 // config.py:7
+    c->translation_noise = 0.0055;         // config.py:11
+    c->rotation_noise = 0.001;             // config.py:12
+    c->measurement_noise[0] = 0.001;       // config.py:15
+    c->measurement_noise[3] = 0.001;
+    c->max_landmark_distance = 8.0;        // config.py:18
+    c->init_landmark_cov[0] = 0.1;         // landmark.py:13
+    c->init_landmark_cov[3] = 0.1;
+    c->weight_floor = 1e-5;                // fast_slam_2.py:168,173
+    c->landmark_capacity = 64;
+    c->max_landmark_capacity = 4096;
+    c->device = 0;
+    c->reduce_mode = FS2_REDUCE_AUTO;
+    c->seed = 0x5EEDF5A2ull;
+    c->record_assoc = 0;
+    c->gate_filter = 0;
+    c->rank = 0;
+    c->world_size = 1;
+}
+
+const char *fs2_last_error(const fs2_handle *h) {
+    if (h && !h->err.empty()) return h->err.c_str();
+    return g_last_error.c_str();
+}
+
+static void free_handle(fs2_handle *h) {
+    if (!h) return;
+    if (h->stream) hipStreamSynchronize(h->stream);
+    for (int s = 0; s < 2; ++s) {
+        hipFree(h->x[s]); hipFree(h->y[s]); hipFree(h->yaw[s]); hipFree(h->w[s]); hipFree(h->cnt[s]);
+        for (char *p : h->pages[s]) hipFree(p);
+        hipFree(h->pages_dev[s]);
+    }
+    hipFree(h->wpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
+    hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum); hipFree(h->src);
+    hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
+    if (h->stats_host) hipHostFree(h->stats_host);
+    if (h->noise_pin) hipHostFree(h->noise_pin);
+    if (h->u0_pin) hipHostFree(h->u0_pin);
+    if (h->ev.ok)
+        for (auto &e : h->ev.e) hipEventDestroy(e);
+    if (h->comm) fs2comm::destroy(h->comm);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int fs2_create(const fs2_config *cfg, fs2_handle **out) {
+    if (!cfg || !out) return set_err(nullptr, FS2_ERR_ARG, "fs2_create: null argument");
+    *out = nullptr;
+    if (cfg->num_particles <= 0)
+        return set_err(nullptr, FS2_ERR_ARG, "num_particles must be positive");
+    if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size)
+        return set_err(nullptr, FS2_ERR_ARG, "bad rank %d / world_size %d", cfg->rank, cfg->world_size);
+    if (cfg->num_particles > (int64_t)INT32_MAX * cfg->world_size)
+        return set_err(nullptr, FS2_ERR_ARG, "too many particles per rank");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_err(nullptr, FS2_ERR_HIP, "no HIP device available (libfs2 has no CPU path)");
+    if (cfg->device < 0 || cfg->device >= ndev)
+        return set_err(nullptr, FS2_ERR_ARG, "device %d out of range (%d devices)", cfg->device, ndev);
+
+    fs2_handle *h = new fs2_handle();
+    h->cfg = *cfg;
+    h->n_global = cfg->num_particles;
+    const int64_t G = cfg->world_size, r = cfg->rank;
+    h->first = (h->n_global * r) / G;
+    h->n = (h->n_global * (r + 1)) / G - h->first;
+    h->max_cap = cfg->max_landmark_capacity > 0 ? std::min(cfg->max_landmark_capacity, kMaxPages * kPageSlots)
+                                                : kMaxPages * kPageSlots;
+    h->gate2 = gate_to_q(cfg->max_landmark_distance);
+    auto fail = [&](int code) {
+        std::string msg = h->err;
+        free_handle(h);
+        g_last_error = msg;
+        return code;
+    };
+    if (hipSetDevice(cfg->device) != hipSuccess) return fail(set_err(&h->err, FS2_ERR_HIP, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
+    const int64_t n = std::max<int64_t>(h->n, 1);
+    const int64_t nb = (n + kBlock - 1) / kBlock;
+    const int64_t nsb = (n + 1023) / 1024;
+    auto alloc = [&](void **p, size_t bytes) { return hipMalloc(p, bytes > 0 ? bytes : 16); };
+    bool ok = true;
+    for (int s = 0; s < 2; ++s) {
+        ok &= alloc((void **)&h->x[s], n * 8) == hipSuccess;
+        ok &= alloc((void **)&h->y[s], n * 8) == hipSuccess;
+        ok &= alloc((void **)&h->yaw[s], n * 8) == hipSuccess;
+        ok &= alloc((void **)&h->w[s], n * 8) == hipSuccess;
+        ok &= alloc((void **)&h->cnt[s], n * 4) == hipSuccess;
+        ok &= alloc((void **)&h->pages_dev[s], sizeof(char *) * kMaxPages) == hipSuccess;
+    }
+    ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->part_best_i, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->part_maxcnt, nb * 4) == hipSuccess;
+    ok &= alloc((void **)&h->cbuf, n * 8) == hipSuccess;
+    ok &= alloc((void **)&h->bsum, nsb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->src, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->stats_dev, sizeof(DevStats)) == hipSuccess;
+    ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
+    ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
+    ok &= hipHostMalloc((void **)&h->stats_host, sizeof(DevStats), 0) == hipSuccess;
+    ok &= hipHostMalloc((void **)&h->noise_pin, n * 8, 0) == hipSuccess;
+    ok &= hipHostMalloc((void **)&h->u0_pin, 8, 0) == hipSuccess;
+    if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
+    // Particle.__init__: (0, 0, 0), weight 1/NUM_PARTICLES, empty map (particle.py:11-20)
+    for (int s = 0; s < 2; ++s) {
+        if (hipMemsetAsync(h->x[s], 0, n * 8, h->stream) != hipSuccess ||
+            hipMemsetAsync(h->y[s], 0, n * 8, h->stream) != hipSuccess ||
+            hipMemsetAsync(h->yaw[s], 0, n * 8, h->stream) != hipSuccess ||
+            hipMemsetAsync(h->cnt[s], 0, n * 4, h->stream) != hipSuccess ||
+            launch_fill(h->w[s], 1.0 / (double)h->n_global, n, h->stream) != hipSuccess)
+            return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
+    }
+    int rc = grow_pages(h, std::max(cfg->landmark_capacity, 1));
+    if (rc) return fail(rc);
+    if (G > 1) {
+        rc = fs2comm::create(cfg->comm_id, (int)G, (int)r, &h->comm, &h->err);
+        if (rc) return fail(rc);
+    }
+    if (hipStreamSynchronize(h->stream) != hipSuccess)
+        return fail(set_err(&h->err, FS2_ERR_HIP, "initialisation sync failed"));
+    *out = h;
+    return FS2_OK;
+}
+
+void fs2_destroy(fs2_handle *h) { free_handle(h); }
+
+int fs2_shard_info(const fs2_handle *h, int64_t *n_local, int64_t *first_global, int32_t *capacity) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (n_local) *n_local = h->n;
+    if (first_global) *first_global = h->first;
+    if (capacity) *capacity = h->cap;
+    return FS2_OK;
+}
+
+int fs2_synchronize(fs2_handle *h) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return FS2_OK;
+}
+
+int fs2_set_profiling(fs2_handle *h, int32_t enable) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (enable && !h->ev.ok) {
+        for (auto &e : h->ev.e) HIP_TRY(h, hipEventCreate(&e));
+        h->ev.ok = true;
+    }
+    h->profiling = enable != 0;
+    h->prof = fs2_profile{};
+    return FS2_OK;
+}
+
+int fs2_get_profile(const fs2_handle *h, fs2_profile *out) {
+    if (!h || !out) return set_err(nullptr, FS2_ERR_ARG, "null argument");
+    *out = h->prof;
+    return FS2_OK;
+}
+
+int fs2_iterate(fs2_handle *h, double rotation, double translation, const double *meas,
+                const double *observed, int32_t M, const double *noise, const double *u0,
+                double out_pose[3], fs2_iter_stats *stats) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    int rc = grow_pages(h, h->cnt_upper + M);
+    if (rc) return rc;
+    const int cur = h->cur;
+    hipStream_t s = h->stream;
+    const bool seq = h->sequential();
+    const bool prof = h->profiling;
+
+    if (noise) {
+        std::memcpy(h->noise_pin, noise, sizeof(double) * h->n);
+        HIP_TRY(h, hipMemcpyAsync(h->noise_dev, h->noise_pin, sizeof(double) * h->n,
+                                  hipMemcpyHostToDevice, s));
+    }
+    if (u0) {
+        *h->u0_pin = *u0;
+        HIP_TRY(h, hipMemcpyAsync(h->u0_dev, h->u0_pin, 8, hipMemcpyHostToDevice, s));
+    }
+    if (h->cfg.record_assoc && (int64_t)M * h->n > h->assoc_cap) {
+        HIP_TRY(h, hipStreamSynchronize(s));
+        hipFree(h->assoc_dev);
+        h->assoc_dev = nullptr;
+        HIP_TRY(h, hipMalloc(&h->assoc_dev, sizeof(int32_t) * (size_t)M * h->n));
+        h->assoc_cap = (int64_t)M * h->n;
+    }
+    HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
+    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[0], s));
+
+    // ---- fused update passes (move in the first) ----
+    UpdateParams up{};
+    up.n = h->n;
+    up.gidx0 = h->first;
+    up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
+    up.map = h->map(cur);
+    up.noise = noise ? h->noise_dev : nullptr;
+    up.seed = h->cfg.seed;
+    up.scan = h->scan;
+    up.sigma = (rotation != 0) ? h->cfg.rotation_noise : h->cfg.translation_noise;
+    up.rotation = rotation;
+    up.translation = translation;
+    up.gate2 = h->gate2;
+    std::memcpy(up.R, h->cfg.measurement_noise, sizeof up.R);
+    std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
+    up.assoc = h->cfg.record_assoc ? h->assoc_dev : nullptr;
+    up.wpart = h->wpart;
+    up.stats = h->stats_dev;
+    int passes = 0;
+    uint64_t fixed_bytes = 0;
+    for (int32_t k0 = 0; k0 < std::max(M, 1); k0 += kMaxM) {
+        const int32_t m = std::min(kMaxM, M - k0);
+        up.do_move = (k0 == 0);
+        up.k0 = k0;
+        up.m = std::max(m, 0);
+        up.last_pass = (k0 + kMaxM >= M);
+        for (int k = 0; k < kMaxM; ++k) {
+            if (k < up.m) {
+                const double d = meas[2 * (k0 + k)], b = meas[2 * (k0 + k) + 1];
+                up.meas.d[k] = d;
+                up.meas.b[k] = b;
+                up.meas.ox[k] = observed ? observed[2 * (k0 + k)] : d * std::cos(b);
+                up.meas.oy[k] = observed ? observed[2 * (k0 + k) + 1] : d * std::sin(b);
+            } else {
+                up.meas.d[k] = up.meas.b[k] = up.meas.ox[k] = up.meas.oy[k] = 0.0;
+            }
+        }
+        HIP_TRY(h, launch_update(up, s));
+        ++passes;
+        // pose/weight/count read + weight/count write; pose write on the move pass
+        fixed_bytes += (uint64_t)h->n * (32 + 4 + 8 + 4 + (up.do_move ? 24 : 0));
+        if (up.do_move && noise) fixed_bytes += (uint64_t)h->n * 8;
+        if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
+    }
+    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[1], s));
+
+    // ---- normalise, N_eff, estimate ----
+    ReduceParams rp{};
+    rp.n = h->n;
+    rp.n_global = h->n_global;
+    rp.gidx0 = h->first;
+    rp.w = h->w[cur];
+    rp.cnt = h->cnt[cur];
+    rp.x = h->x[cur]; rp.y = h->y[cur]; rp.yaw = h->yaw[cur];
+    rp.wpart = h->wpart;
+    rp.nwpart = (int32_t)h->nblocks();
+    rp.part_sq = h->part_sq;
+    rp.part_best_w = h->part_best_w;
+    rp.part_best_i = h->part_best_i;
+    rp.part_maxcnt = h->part_maxcnt;
+    rp.nparts = (int32_t)h->nblocks();
+    rp.floor = h->cfg.weight_floor;
+    rp.sequential = seq ? 1 : 0;
+    rp.u0_host = u0 ? h->u0_dev : nullptr;
+    rp.seed = h->cfg.seed;
+    rp.scan = h->scan;
+    rp.stats = h->stats_dev;
+    HIP_TRY(h, launch_wsum(rp, s));
+    HIP_TRY(h, launch_normalize(rp, s));
+    HIP_TRY(h, launch_finalize(rp, s));
+    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[2], s));
+
+    // ---- low-variance resample (kernels exit unless the rule fired) ----
+    const int nxt = 1 - cur;
+    ResampleParams rs{};
+    rs.n = h->n;
+    rs.w = h->w[cur];
+    rs.c = h->cbuf;
+    rs.bsum = h->bsum;
+    rs.nblk = (int32_t)((h->n + 1023) / 1024);
+    rs.src = h->src;
+    rs.x = h->x[cur]; rs.y = h->y[cur]; rs.yaw = h->yaw[cur]; rs.cnt = h->cnt[cur];
+    rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
+    rs.in = h->map(cur);
+    rs.out = h->map(nxt);
+    rs.part_best_w = h->part_best_w;
+    rs.part_best_i = h->part_best_i;
+    rs.stats = h->stats_dev;
+    HIP_TRY(h, launch_resample(rs, seq ? 1 : 0, std::min(h->cap, h->cnt_upper + M), s));
+    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[3], s));
+
+    HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
+    HIP_TRY(h, hipStreamSynchronize(s));
+    const DevStats &st = *h->stats_host;
+    if (st.resampled) h->cur = nxt;
+    h->cnt_upper = st.max_count;
+    h->last_m = M;
+    h->scan += 1;
+    if (prof) {
+        float a = 0, b = 0, c = 0;
+        hipEventElapsedTime(&a, h->ev.e[0], h->ev.e[1]);
+        hipEventElapsedTime(&b, h->ev.e[1], h->ev.e[2]);
+        hipEventElapsedTime(&c, h->ev.e[2], h->ev.e[3]);
+        h->prof.scans += 1;
+        h->prof.update_launches += passes;
+        h->prof.update_ms += a;
+        h->prof.reduce_ms += b;
+        h->prof.resample_ms += c;
+        h->prof.scan_ms += a + b + c;
+        h->prof.update_bytes += 48ull * st.candidates + 48ull * st.written + fixed_bytes +
+                                8ull * (uint64_t)h->nblocks();
+        if (st.resampled)
+            h->prof.resample_bytes += 2ull * 48ull * st.resample_slots + 2ull * 36ull * (uint64_t)h->n;
+    }
+    if (out_pose) {
+        out_pose[0] = st.pose[0];
+        out_pose[1] = st.pose[1];
+        out_pose[2] = st.pose[2];
+    }
+    if (stats) {
+        stats->resampled = st.resampled;
+        stats->max_count = st.max_count;
+        stats->n_eff = st.n_eff;
+        stats->total_weight = st.total;
+        stats->best_index = st.best_index + h->first;
+        stats->slots_visited = st.visited;
+        stats->candidates = st.candidates;
+        stats->hits = st.hits;
+        stats->appends = st.appends;
+        stats->slots_written = st.written;
+        stats->ambiguous = st.ambiguous;
+        stats->resample_slots = st.resample_slots;
+        stats->error_flags = st.error_flags;
+        stats->reserved = 0;
+    }
+    if (st.error_flags & 1)
+        return set_err(&h->err, FS2_ERR_LINALG, "Singular matrix (landmark or observation covariance)");
+    return FS2_OK;
+}
+
+int fs2_get_assoc(fs2_handle *h, int32_t *idx, int64_t capacity, int32_t *m_out) {
+    if (!h || !idx) return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "null argument");
+    if (!h->cfg.record_assoc) return set_err(&h->err, FS2_ERR_STATE, "record_assoc is off");
+    const int64_t need = (int64_t)h->last_m * h->n;
+    if (capacity < need) return set_err(&h->err, FS2_ERR_ARG, "assoc buffer too small (%lld < %lld)",
+                                        (long long)capacity, (long long)need);
+    if (m_out) *m_out = h->last_m;
+    if (need) HIP_TRY(h, hipMemcpy(idx, h->assoc_dev, sizeof(int32_t) * need, hipMemcpyDeviceToHost));
+    return FS2_OK;
+}
+
+static hipMemcpyKind kind_in(int32_t where) {
+    return where == FS2_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+}
+static hipMemcpyKind kind_out(int32_t where) {
+    return where == FS2_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+}
+
+int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, const double *y,
+                  const double *yaw, const double *w, const int32_t *cnt, const double *lm,
+                  int32_t lm_cap, int32_t where) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (first < 0 || count < 0 || first + count > h->n)
+        return set_err(&h->err, FS2_ERR_ARG, "range [%lld, %lld) outside %lld local particles",
+                       (long long)first, (long long)(first + count), (long long)h->n);
+    if ((cnt == nullptr) != (lm == nullptr) || (lm && lm_cap < 0))
+        return set_err(&h->err, FS2_ERR_ARG, "cnt and lm must be given together");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    hipStream_t s = h->stream;
+    const int c = h->cur;
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (count == 0) return FS2_OK;
+    const size_t b8 = sizeof(double) * count;
+    if (x) HIP_TRY(h, hipMemcpy(h->x[c] + first, x, b8, kind_in(where)));
+    if (y) HIP_TRY(h, hipMemcpy(h->y[c] + first, y, b8, kind_in(where)));
+    if (yaw) HIP_TRY(h, hipMemcpy(h->yaw[c] + first, yaw, b8, kind_in(where)));
+    if (w) HIP_TRY(h, hipMemcpy(h->w[c] + first, w, b8, kind_in(where)));
+    if (cnt) {
+        std::vector<int32_t> hc(count);
+        HIP_TRY(h, hipMemcpy(hc.data(), cnt, sizeof(int32_t) * count,
+                             where == FS2_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost));
+        int32_t mx = 0;
+        for (int32_t v : hc) {
+            if (v < 0 || v > lm_cap) return set_err(&h->err, FS2_ERR_ARG, "count %d outside [0, %d]", v, lm_cap);
+            mx = std::max(mx, v);
+        }
+        int rc = grow_pages(h, mx);
+        if (rc) return rc;
+        h->cnt_upper = std::max(h->cnt_upper, mx);
+        // stage in chunks of <= 256 MiB
+        const int64_t per = (int64_t)std::max(1, lm_cap) * 6 * 8;
+        const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / per);
+        double *stage = nullptr;
+        int32_t *cstage = nullptr;
+        HIP_TRY(h, hipMalloc(&stage, (size_t)std::min(chunk, count) * per));
+        HIP_TRY(h, hipMalloc(&cstage, sizeof(int32_t) * std::min(chunk, count)));
+        int rc2 = FS2_OK;
+        for (int64_t o = 0; o < count && rc2 == FS2_OK; o += chunk) {
+            const int64_t k = std::min(chunk, count - o);
+            hipError_t e = hipMemcpy(stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
+            if (e == hipSuccess) e = hipMemcpy(cstage, hc.data() + o, sizeof(int32_t) * k, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(c), h->cnt[c], s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
+        }
+        hipFree(stage);
+        hipFree(cstage);
+        if (rc2) return rc2;
+    }
+    HIP_TRY(h, hipStreamSynchronize(s));
+    return FS2_OK;
+}
+
+int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double *y, double *yaw,
+                  double *w, int32_t *cnt, double *lm, int32_t lm_cap, int32_t where) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (first < 0 || count < 0 || first + count > h->n)
+        return set_err(&h->err, FS2_ERR_ARG, "range outside local particles");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    hipStream_t s = h->stream;
+    const int c = h->cur;
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (count == 0) return FS2_OK;
+    const size_t b8 = sizeof(double) * count;
+    if (x) HIP_TRY(h, hipMemcpy(x, h->x[c] + first, b8, kind_out(where)));
+    if (y) HIP_TRY(h, hipMemcpy(y, h->y[c] + first, b8, kind_out(where)));
+    if (yaw) HIP_TRY(h, hipMemcpy(yaw, h->yaw[c] + first, b8, kind_out(where)));
+    if (w) HIP_TRY(h, hipMemcpy(w, h->w[c] + first, b8, kind_out(where)));
+    if (cnt) HIP_TRY(h, hipMemcpy(cnt, h->cnt[c] + first, sizeof(int32_t) * count, kind_out(where)));
+    if (lm) {
+        if (lm_cap < 0) return set_err(&h->err, FS2_ERR_ARG, "lm_cap < 0");
+        std::vector<int32_t> hc(count);
+        HIP_TRY(h, hipMemcpy(hc.data(), h->cnt[c] + first, sizeof(int32_t) * count, hipMemcpyDeviceToHost));
+        for (int32_t v : hc)
+            if (v > lm_cap) return set_err(&h->err, FS2_ERR_ARG, "lm_cap %d < map size %d", lm_cap, v);
+        const int64_t per = (int64_t)std::max(1, lm_cap) * 6 * 8;
+        const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / per);
+        double *stage = nullptr;
+        HIP_TRY(h, hipMalloc(&stage, (size_t)std::min(chunk, count) * per));
+        int rc2 = FS2_OK;
+        for (int64_t o = 0; o < count && rc2 == FS2_OK; o += chunk) {
+            const int64_t k = std::min(chunk, count - o);
+            hipError_t e = hipMemsetAsync(stage, 0, (size_t)k * per, s);
+            if (e == hipSuccess) e = launch_export(stage, first + o, k, lm_cap, h->map(c), h->cnt[c], s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) e = hipMemcpy(lm + o * lm_cap * 6, stage, (size_t)k * per, kind_out(where));
+            if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state export failed: %s", hipGetErrorString(e));
+        }
+        hipFree(stage);
+        if (rc2) return rc2;
+    }
+    return FS2_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ stateless ---
+
+namespace {
+
+struct Scratch {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    char *buf = nullptr;
+    size_t bytes = 0;
+};
+
+std::mutex g_scratch_mu;
+Scratch g_scratch[64];
+
+int scratch_get(int32_t device, size_t bytes, Scratch **out) {
+    if (device < 0 || device >= 64) return set_err(nullptr, FS2_ERR_ARG, "bad device %d", device);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev)
+        return set_err(nullptr, FS2_ERR_HIP, "no HIP device %d (libfs2 has no CPU path)", device);
+    Scratch &s = g_scratch[device];
+    if (hipSetDevice(device) != hipSuccess) return set_err(nullptr, FS2_ERR_HIP, "hipSetDevice failed");
+    if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess)
+        return set_err(nullptr, FS2_ERR_HIP, "hipStreamCreate failed");
+    if (s.bytes < bytes) {
+        hipFree(s.buf);
+        s.buf = nullptr;
+        s.bytes = 0;
+        if (hipMalloc(&s.buf, bytes) != hipSuccess) return set_err(nullptr, FS2_ERR_OOM, "scratch alloc failed");
+        s.bytes = bytes;
+    }
+    s.device = device;
+    *out = &s;
+    return FS2_OK;
+}
+
+#define SHIP(expr)                                                                               \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return set_err(nullptr, FS2_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
+
+}  // namespace
+
+extern "C" {
+
+int fs2_icp_batched(int32_t device, int32_t B, int32_t P, const double *src, const double *tgt,
+                    int32_t max_iterations, double threshold, double *R, double *t,
+                    int32_t *iterations, int32_t where) {
+    if (B < 0 || P <= 0 || P > 1024 || !src || !tgt || !R || !t)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_icp_batched: bad arguments (B=%d, P=%d; P <= 1024)", B, P);
+    if (B == 0) return FS2_OK;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t cb = al16((size_t)B * P * 16);
+    const size_t need = 2 * cb + al16((size_t)B * 32) + al16((size_t)B * 16) + al16((size_t)B * 4);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, need, &sc);
+    if (rc) return rc;
+    char *p = sc->buf;
+    double *ds = (double *)p, *dt = (double *)(p + cb), *dR = (double *)(p + 2 * cb);
+    double *dT = (double *)(p + 2 * cb + al16((size_t)B * 32));
+    int32_t *dI = (int32_t *)(p + 2 * cb + al16((size_t)B * 32) + al16((size_t)B * 16));
+    const hipMemcpyKind kin = where == FS2_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const hipMemcpyKind kout = where == FS2_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    SHIP(hipMemcpyAsync(ds, src, (size_t)B * P * 16, kin, sc->stream));
+    SHIP(hipMemcpyAsync(dt, tgt, (size_t)B * P * 16, kin, sc->stream));
+    SHIP(launch_icp(B, P, ds, dt, P, max_iterations, threshold, dR, dT, dI, nullptr, sc->stream));
+    SHIP(hipMemcpyAsync(R, dR, (size_t)B * 32, kout, sc->stream));
+    SHIP(hipMemcpyAsync(t, dT, (size_t)B * 16, kout, sc->stream));
+    if (iterations) SHIP(hipMemcpyAsync(iterations, dI, (size_t)B * 4, kout, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    return FS2_OK;
+}
+
+int fs2_icp(int32_t device, const double *src, int32_t n_src, const double *tgt, int32_t n_tgt,
+            int32_t max_iterations, double threshold, double R[4], double t[2], int32_t *iterations) {
+    if (n_src <= 0 || n_tgt <= 0 || n_src > 1024 || n_tgt > 1024 || !src || !tgt || !R || !t)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_icp: bad arguments (point counts must be 1..1024)");
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t bs = al16((size_t)n_src * 16), bt = al16((size_t)n_tgt * 16);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, bs + bt + 64, &sc);
+    if (rc) return rc;
+    double *ds = (double *)sc->buf, *dt = (double *)(sc->buf + bs);
+    double *dR = (double *)(sc->buf + bs + bt), *dT = dR + 4;
+    int32_t *dI = (int32_t *)(dT + 2);
+    SHIP(hipMemcpyAsync(ds, src, (size_t)n_src * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(dt, tgt, (size_t)n_tgt * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_icp(1, n_src, ds, dt, n_tgt, max_iterations, threshold, dR, dT, dI, nullptr, sc->stream));
+    double out[6];
+    int32_t it = 0;
+    SHIP(hipMemcpyAsync(out, dR, 48, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipMemcpyAsync(&it, dI, 4, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    std::memcpy(R, out, 32);
+    t[0] = out[4];
+    t[1] = out[5];
+    if (iterations) *iterations = it;
+    return FS2_OK;
+}
+
+int fs2_best_fit_transform(int32_t device, const double *src, const double *tgt, int32_t n, double R[4],
+                           double t[2]) {
+    if (n <= 0 || !src || !tgt || !R || !t) return set_err(nullptr, FS2_ERR_ARG, "fs2_best_fit_transform: bad arguments");
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t b = al16((size_t)n * 16);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 2 * b + 64, &sc);
+    if (rc) return rc;
+    double *ds = (double *)sc->buf, *dt = (double *)(sc->buf + b), *dRt = (double *)(sc->buf + 2 * b);
+    SHIP(hipMemcpyAsync(ds, src, (size_t)n * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(dt, tgt, (size_t)n * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_best_fit(ds, dt, n, dRt, sc->stream));
+    double out[6];
+    SHIP(hipMemcpyAsync(out, dRt, 48, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    std::memcpy(R, out, 32);
+    t[0] = out[4];
+    t[1] = out[5];
+    return FS2_OK;
+}
+
+int32_t fs2_gaussian_taps(double sigma, double truncate, double *taps, int32_t max_taps) {
+    const int32_t r = (int32_t)(truncate * sigma + 0.5);
+    if (r < 0 || 2 * r + 1 > max_taps || !taps) return -1;
+    const double s2 = sigma * sigma;
+    double sum = 0.0;
+    std::vector<double> phi(2 * r + 1);
+    for (int32_t k = -r; k <= r; ++k) phi[k + r] = std::exp(-0.5 / s2 * (double)(k * k));
+    for (double v : phi) sum += v;
+    for (int32_t k = 0; k < 2 * r + 1; ++k) taps[k] = phi[2 * r - k] / sum;
+    return r;
+}
+
+int fs2_line_filter(int32_t device, const double *points, int32_t n, const double *taps, int32_t radius,
+                    double *out) {
+    if (n < 0 || radius < 0 || (n > 0 && (!points || !out)) || !taps)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_line_filter: bad arguments");
+    if (n == 0) return FS2_OK;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t bp = al16((size_t)n * 16), bt = al16((size_t)(2 * radius + 1) * 8);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 2 * bp + bt, &sc);
+    if (rc) return rc;
+    double *din = (double *)sc->buf, *dout = (double *)(sc->buf + bp), *dtap = (double *)(sc->buf + 2 * bp);
+    SHIP(hipMemcpyAsync(din, points, (size_t)n * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(dtap, taps, (size_t)(2 * radius + 1) * 8, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_line_filter(din, n, dtap, radius, dout, sc->stream));
+    SHIP(hipMemcpyAsync(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    return FS2_OK;
+}
+
+int fs2_associate(int32_t device, const double observed[2], const double *lm, int32_t L, double gate,
+                  int32_t *index) {
+    if (!observed || !index || L < 0 || (L > 0 && !lm)) return set_err(nullptr, FS2_ERR_ARG, "fs2_associate: bad arguments");
+    if (L == 0) {
+        *index = -1;
+        return FS2_OK;
+    }
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t bl = al16((size_t)L * 48);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, bl + 32, &sc);
+    if (rc) return rc;
+    double *dl = (double *)sc->buf, *dobs = (double *)(sc->buf + bl);
+    int32_t *dout = (int32_t *)(dobs + 2);
+    SHIP(hipMemcpyAsync(dl, lm, (size_t)L * 48, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(dobs, observed, 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_associate(dobs, dl, L, gate_to_q(gate), dout, sc->stream));
+    int32_t r = -1;
+    SHIP(hipMemcpyAsync(&r, dout, 4, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    if (r == -2) return set_err(nullptr, FS2_ERR_LINALG, "Singular matrix");
+    *index = r;
+    return FS2_OK;
+}
+
+int fs2_mahalanobis(int32_t device, const double *a, const double *b, const double *cov, int32_t K,
+                    double *out) {
+    if (K < 0 || (K > 0 && (!a || !b || !cov || !out)))
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_mahalanobis: bad arguments");
+    if (K == 0) return FS2_OK;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t b2 = al16((size_t)K * 16), b4 = al16((size_t)K * 32), b1 = al16((size_t)K * 8);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 2 * b2 + b4 + b1 + 16, &sc);
+    if (rc) return rc;
+    double *da = (double *)sc->buf, *db = (double *)(sc->buf + b2), *dc = (double *)(sc->buf + 2 * b2);
+    double *dout = (double *)(sc->buf + 2 * b2 + b4);
+    int32_t *dsing = (int32_t *)(sc->buf + 2 * b2 + b4 + b1);
+    SHIP(hipMemsetAsync(dsing, 0, 4, sc->stream));
+    SHIP(hipMemcpyAsync(da, a, (size_t)K * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(db, b, (size_t)K * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(dc, cov, (size_t)K * 32, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_mahalanobis(da, db, dc, K, dout, dsing, sc->stream));
+    int32_t sing = 0;
+    SHIP(hipMemcpyAsync(out, dout, (size_t)K * 8, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipMemcpyAsync(&sing, dsing, 4, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    if (sing) return set_err(nullptr, FS2_ERR_LINALG, "Singular matrix");
+    return FS2_OK;
+}
+
+int fs2_comm_unique_id(uint8_t out[128]) {
+    if (!out) return set_err(nullptr, FS2_ERR_ARG, "null argument");
+    std::string err;
+    int rc = fs2comm::unique_id(out, &err);
+    if (rc) return set_err(nullptr, rc, "%s", err.c_str());
+    return FS2_OK;
+}
+
+}  // extern "C"

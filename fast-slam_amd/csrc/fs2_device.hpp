@@ -1,0 +1,177 @@
+// fs2_device.hpp -- device math for the FastSLAM 2.0 hot path (gfx950, fp64).
+//
+// Operation order follows the reference (cy-rae/fast-slam) as executed by
+// numpy 2.2 / OpenBLAS 0.3.29; where numpy delegates to BLAS/LAPACK the FMA
+// placement was identified empirically and is restated with explicit fma()
+// (the translation unit is compiled with -ffp-contract=off):
+//   2x2 @ 2x2 (gemm)  C[i][j] = fma(A[i][1], B[1][j], A[i][0]*B[0][j])
+//   2x2 @ vec (gemv)  r[i]    = fma(A[i][0], v[0],    A[i][1]*v[1])
+//   vec @ 2x2         r[j]    = fma(v[1],   A[1][j],  v[0]*A[0][j])
+//   dot               s       = fma(a[1],   b[1],     a[0]*b[0])
+//   np.linalg.inv     LAPACK dgesv, partial pivoting, reciprocal scaling.
+// This makes the association gate bit-identical to the reference.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fs2 {
+
+constexpr double kPi = 3.141592653589793;         // np.pi
+constexpr double kTwoPi = 6.283185307179586;      // 2 * np.pi
+constexpr double kLog2Pi = 1.8378770664093453;    // scipy _LOG_2PI = np.log(2 * np.pi)
+
+// Python/numpy float floor-mod (numpy npy_divmod), b > 0 here.
+__device__ __forceinline__ double pymod(double a, double b) {
+    double m = fmod(a, b);
+    if (m != 0.0) {
+        if ((b < 0.0) != (m < 0.0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+
+struct M2 {
+    double a00, a01, a10, a11;
+};
+
+__device__ __forceinline__ M2 mm2(const M2 &A, const M2 &B) {
+    M2 C;
+    C.a00 = fma(A.a01, B.a10, A.a00 * B.a00);
+    C.a01 = fma(A.a01, B.a11, A.a00 * B.a01);
+    C.a10 = fma(A.a11, B.a10, A.a10 * B.a00);
+    C.a11 = fma(A.a11, B.a11, A.a10 * B.a01);
+    return C;
+}
+
+__device__ __forceinline__ M2 tr2(const M2 &A) { return M2{A.a00, A.a10, A.a01, A.a11}; }
+
+// np.linalg.inv (2x2) -- see header comment.  Returns false when U is exactly
+// singular (numpy raises LinAlgError).
+__device__ __forceinline__ bool inv2(const M2 &A, M2 &out) {
+    double r00 = A.a00, r01 = A.a01, r10 = A.a10, r11 = A.a11;
+    const bool p = fabs(A.a10) > fabs(A.a00);
+    if (p) {
+        r00 = A.a10; r01 = A.a11; r10 = A.a00; r11 = A.a01;
+    }
+    if (r00 == 0.0) return false;
+    const double ir00 = 1.0 / r00;
+    const double l = r10 * ir00;
+    const double u11 = r11 - l * r01;
+    if (u11 == 0.0) return false;
+    const double iu11 = 1.0 / u11;
+    // column 0: b = P e0 ; column 1: b = P e1
+    const double b00 = p ? 0.0 : 1.0, b01 = p ? 1.0 : 0.0;   // column 0 (b0, b1)
+    const double b10 = p ? 1.0 : 0.0, b11 = p ? 0.0 : 1.0;   // column 1 (b0, b1)
+    {
+        const double y0 = b00, y1 = b01 - l * y0;
+        const double x1 = y1 * iu11;
+        out.a10 = x1;
+        out.a00 = fma(-r01, x1, y0) * ir00;
+    }
+    {
+        const double y0 = b10, y1 = b11 - l * y0;
+        const double x1 = y1 * iu11;
+        out.a11 = x1;
+        out.a01 = fma(-r01, x1, y0) * ir00;
+    }
+    return true;
+}
+
+// delta^T inv delta with numpy's (vec @ 2x2) @ vec order (geometry_utils.py:22).
+__device__ __forceinline__ double quad(const M2 &I, double d0, double d1) {
+    const double r0 = fma(d1, I.a10, d0 * I.a00);
+    const double r1 = fma(d1, I.a11, d0 * I.a01);
+    return fma(r1, d1, r0 * d0);
+}
+
+// One landmark slot: mean and full (possibly asymmetric) covariance.
+struct Slot {
+    double mx, my;
+    M2 P;
+};
+
+struct Meas {
+    double d, b, ox, oy;
+};
+
+// EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line:
+// it runs at most M times per particle and scan, and inlining it doubles the
+// streaming loop's register footprint (occupancy 2 -> 4 waves/SIMD).  Updates `s`
+// in place and returns the scipy multivariate_normal.pdf value.
+static __device__ __noinline__ double ekf_update(Slot &s, double px, double py, double pyaw,
+                                                    const Meas &m, const M2 &R, bool &singular) {
+    const double dx = s.mx - px, dy = s.my - py;
+    const double q = dx * dx + dy * dy;          // reference: pow(dx, 2) + pow(dy, 2)
+    const double r = sqrt(q);
+    const double ang = atan2(dy, dx) - pyaw;
+    const double nu0 = m.d - r;
+    const double nu1 = pymod((m.b - ang) + kPi, kTwoPi) - kPi;
+    const M2 H{dx / r, dy / r, -dy / q, dx / q};
+    const M2 Ht = tr2(H);
+    M2 S = mm2(mm2(H, s.P), Ht);
+    S.a00 += R.a00; S.a01 += R.a01; S.a10 += R.a10; S.a11 += R.a11;
+    M2 Si;
+    if (!inv2(S, Si)) {
+        singular = true;
+        return 0.0;
+    }
+    const M2 K = mm2(mm2(s.P, Ht), Si);
+    const double kn0 = fma(K.a00, nu0, K.a01 * nu1);
+    const double kn1 = fma(K.a10, nu0, K.a11 * nu1);
+    const M2 KH = mm2(K, H);
+    const M2 IKH{1.0 - KH.a00, 0.0 - KH.a01, 0.0 - KH.a10, 1.0 - KH.a11};
+    const M2 Pn = mm2(IKH, s.P);
+    s.mx = s.mx + kn0;
+    s.my = s.my + kn1;
+    s.P = Pn;
+    // scipy: eigh on the lower triangle; closed form of log|S| and nu^T S^-1 nu.
+    const double a = S.a00, b = S.a10, c = S.a11;
+    const double det = a * c - b * b;
+    const double maha = (c * nu0 * nu0 - 2.0 * b * nu0 * nu1 + a * nu1 * nu1) / det;
+    return exp(-0.5 * (2.0 * kLog2Pi + log(det) + maha));
+}
+
+// ------------------------------------------------------------- Philox4x32-10
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Uniform in (0, 1] from 53 random bits.
+__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
+    const uint64_t v = (((uint64_t)hi << 21) ^ (uint64_t)(lo >> 11)) & ((1ull << 53) - 1);
+    return ((double)v + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+// Standard normal for (stream, index) via Box-Muller on one Philox block.
+__device__ __forceinline__ double philox_normal(uint64_t seed, uint64_t stream, uint64_t idx) {
+    const U4 r = philox(U4{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)stream,
+                           (uint32_t)(stream >> 32)},
+                        (uint32_t)seed, (uint32_t)(seed >> 32));
+    const double u1 = u53(r.x, r.y), u2 = u53(r.z, r.w);
+    return sqrt(-2.0 * log(u1)) * cos(kTwoPi * u2);
+}
+
+__device__ __forceinline__ double philox_uniform01(uint64_t seed, uint64_t stream, uint64_t idx) {
+    const U4 r = philox(U4{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)stream,
+                           (uint32_t)(stream >> 32)},
+                        (uint32_t)seed, (uint32_t)(seed >> 32));
+    return u53(r.x, r.y) - (1.0 / 9007199254740992.0);   // [0, 1)
+}
+
+}  // namespace fs2

@@ -1,0 +1,32 @@
+"""fast_slam_2 -- MI355X-native drop-in for the reference's FastSLAM 2.0 hot path.
+
+Same public names as cy-rae/fast-slam's `fast_slam_2` package
+(fast_slam_2/__init__.py:5-22).  The particle update, ICP, LineFilter and the
+association / Mahalanobis helpers run in libfs2.so (HIP, gfx950).  Robot,
+EvaluationUtils, HoughTransformation and Serializer are simulator- or
+front-end-bound and outside this build's scope.
+"""
+from .algorithms.fast_slam_2 import FastSLAM2
+from .algorithms.icp import ICP
+from .algorithms.line_filter import LineFilter
+from .models.directed_point import DirectedPoint
+from .models.landmark import Landmark
+from .models.measurement import Measurement
+from .models.particle import Particle
+from .models.point import Point
+from .utils.geometry_utils import GeometryUtils
+from .utils.landmark_utils import LandmarkUtils
+
+_OUT_OF_SCOPE = {"Robot", "EvaluationUtils", "HoughTransformation", "Serializer",
+                 "EvaluationResults"}
+
+
+def __getattr__(name):
+    if name in _OUT_OF_SCOPE:
+        raise ImportError(f"fast_slam_2.{name} is outside the particle-update hot path this "
+                          f"build replaces (simulator/front-end bound; SURVEY.md §2, §8f)")
+    raise AttributeError(name)
+
+
+__all__ = ["FastSLAM2", "ICP", "LineFilter", "DirectedPoint", "Landmark", "Measurement",
+           "Particle", "Point", "GeometryUtils", "LandmarkUtils"]

@@ -1,0 +1,196 @@
+"""ctypes binding of libfs2.so (include/fs2.h).
+
+There is no CPU fallback: if the library or a HIP device is missing, every
+entry point raises.  Build the library with `python fast-slam_amd/build.py`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FS2_LIB", os.path.join(os.path.dirname(_PKG), "lib", "libfs2.so"))
+
+FS2_OK = 0
+FS2_ERR_ARG = -1
+FS2_ERR_HIP = -2
+FS2_ERR_OOM = -3
+FS2_ERR_LINALG = -4
+FS2_ERR_STATE = -5
+FS2_ERR_COMM = -6
+FS2_ERR_CAPACITY = -7
+
+FS2_REDUCE_AUTO = 0
+FS2_REDUCE_SEQUENTIAL = 1
+FS2_REDUCE_PARALLEL = 2
+FS2_HOST = 0
+FS2_DEVICE = 1
+
+
+class fs2_config(C.Structure):
+    _fields_ = [
+        ("num_particles", C.c_int64),
+        ("translation_noise", C.c_double),
+        ("rotation_noise", C.c_double),
+        ("measurement_noise", C.c_double * 4),
+        ("max_landmark_distance", C.c_double),
+        ("init_landmark_cov", C.c_double * 4),
+        ("weight_floor", C.c_double),
+        ("landmark_capacity", C.c_int32),
+        ("max_landmark_capacity", C.c_int32),
+        ("device", C.c_int32),
+        ("reduce_mode", C.c_int32),
+        ("seed", C.c_uint64),
+        ("record_assoc", C.c_int32),
+        ("gate_filter", C.c_int32),
+        ("rank", C.c_int32),
+        ("world_size", C.c_int32),
+        ("comm_id", C.c_uint8 * 128),
+    ]
+
+
+class fs2_iter_stats(C.Structure):
+    _fields_ = [
+        ("resampled", C.c_int32),
+        ("max_count", C.c_int32),
+        ("n_eff", C.c_double),
+        ("total_weight", C.c_double),
+        ("best_index", C.c_int64),
+        ("slots_visited", C.c_uint64),
+        ("candidates", C.c_uint64),
+        ("hits", C.c_uint64),
+        ("appends", C.c_uint64),
+        ("slots_written", C.c_uint64),
+        ("ambiguous", C.c_uint64),
+        ("resample_slots", C.c_uint64),
+        ("error_flags", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+
+
+class fs2_profile(C.Structure):
+    _fields_ = [
+        ("scans", C.c_int64),
+        ("update_launches", C.c_int64),
+        ("update_ms", C.c_double),
+        ("reduce_ms", C.c_double),
+        ("resample_ms", C.c_double),
+        ("scan_ms", C.c_double),
+        ("update_bytes", C.c_uint64),
+        ("resample_bytes", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class FS2Error(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libfs2 error {code}: {msg}")
+        self.code = code
+
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+_vp = C.c_void_p
+_H = C.c_void_p
+
+# (name, restype, argtypes) for every entry point declared in include/fs2.h
+SIGNATURES = [
+    ("fs2_abi_version", C.c_int32, []),
+    ("fs2_config_default", None, [C.POINTER(fs2_config)]),
+    ("fs2_create", C.c_int, [C.POINTER(fs2_config), C.POINTER(_H)]),
+    ("fs2_destroy", None, [_H]),
+    ("fs2_last_error", C.c_char_p, [_H]),
+    ("fs2_iterate", C.c_int, [_H, C.c_double, C.c_double, _vp, _vp, C.c_int32, _vp, _vp, _dp,
+                              C.POINTER(fs2_iter_stats)]),
+    ("fs2_get_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,
+                                C.c_int32]),
+    ("fs2_set_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,
+                                C.c_int32]),
+    ("fs2_get_assoc", C.c_int, [_H, _ip, C.c_int64, _ip]),
+    ("fs2_shard_info", C.c_int, [_H, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_int32)]),
+    ("fs2_synchronize", C.c_int, [_H]),
+    ("fs2_set_profiling", C.c_int, [_H, C.c_int32]),
+    ("fs2_get_profile", C.c_int, [_H, C.POINTER(fs2_profile)]),
+    ("fs2_icp", C.c_int, [C.c_int32, _dp, C.c_int32, _dp, C.c_int32, C.c_int32, C.c_double, _dp,
+                          _dp, _ip]),
+    ("fs2_icp_batched", C.c_int, [C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_int32,
+                                  C.c_double, _vp, _vp, _vp, C.c_int32]),
+    ("fs2_best_fit_transform", C.c_int, [C.c_int32, _dp, _dp, C.c_int32, _dp, _dp]),
+    ("fs2_line_filter", C.c_int, [C.c_int32, _dp, C.c_int32, _dp, C.c_int32, _dp]),
+    ("fs2_gaussian_taps", C.c_int32, [C.c_double, C.c_double, _dp, C.c_int32]),
+    ("fs2_associate", C.c_int, [C.c_int32, _dp, _dp, C.c_int32, C.c_double, _ip]),
+    ("fs2_mahalanobis", C.c_int, [C.c_int32, _dp, _dp, _dp, C.c_int32, _dp]),
+    ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+]
+
+_lib = None
+
+
+def load():
+    """Load libfs2.so (raises ImportError when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libfs2.so not found at {LIB_PATH}; build it with "
+                          f"`python fast-slam_amd/build.py` (there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fs2_abi_version() != 1:
+        raise ImportError(f"libfs2 ABI {lib.fs2_abi_version()} != 1")
+    _lib = lib
+    return lib
+
+
+def last_error(h=None) -> str:
+    msg = load().fs2_last_error(h)
+    return msg.decode() if msg else ""
+
+
+def check(rc, h=None):
+    if rc == FS2_OK:
+        return
+    msg = last_error(h)
+    if rc == FS2_ERR_LINALG:
+        raise np.linalg.LinAlgError(msg or "Singular matrix")
+    if rc == FS2_ERR_ARG:
+        raise ValueError(msg)
+    if rc == FS2_ERR_OOM:
+        raise MemoryError(msg)
+    raise FS2Error(rc, msg)
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp)
+
+
+def f64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a if shape is None else a.reshape(shape)
+
+
+def default_config() -> fs2_config:
+    cfg = fs2_config()
+    load().fs2_config_default(C.byref(cfg))
+    return cfg
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    check(load().fs2_comm_unique_id(buf))
+    return bytes(buf)

@@ -1,0 +1,225 @@
+"""FastSLAM2: drop-in for the reference's fast_slam_2.algorithms.FastSLAM2.
+
+The per-scan hot path -- motion sample, association, EKF, likelihood,
+normalisation, N_eff, low-variance resample, estimate
+(reference fast_slam_2/algorithms/fast_slam_2.py:33-223) -- runs in libfs2.so on
+the GPU; particle state stays resident in HBM between scans.
+
+Randomness.  By default the motion noise and the resample starting point are
+drawn from numpy's global legacy RandomState exactly as the reference draws
+them (N normals in particle order, then one uniform only if resampling fires,
+SURVEY.md Q4/Q5), so a seeded run reproduces the reference's stream.  The
+uniform is drawn speculatively before the scan and the RNG state is rewound
+when no resample happened.  rng="device" draws both with Philox on the GPU
+instead (no host work per particle; used by bench.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .. import _native as nat
+from .. import config
+from ..models.landmark import Landmark
+from ..models.measurement import Measurement
+from ..models.particle import Particle
+
+_REDUCE = {"auto": nat.FS2_REDUCE_AUTO, "sequential": nat.FS2_REDUCE_SEQUENTIAL,
+           "parallel": nat.FS2_REDUCE_PARALLEL}
+
+
+class FastSLAM2:
+    """FastSLAM 2.0 particle filter (reference fast_slam_2.py:15-31)."""
+
+    def __init__(self, num_particles: int | None = None, *, device: int = 0, rng: str = "numpy",
+                 seed: int | None = None, reduce: str = "auto", record_assoc: bool = False,
+                 landmark_capacity: int = 64, rank: int = 0, world_size: int = 1,
+                 comm_id: bytes | None = None, verbose: bool = True):
+        lib = nat.load()
+        cfg = nat.default_config()
+        cfg.num_particles = int(config.NUM_PARTICLES if num_particles is None else num_particles)
+        cfg.translation_noise = float(config.TRANSLATION_NOISE)
+        cfg.rotation_noise = float(config.ROTATION_NOISE)
+        R = np.asarray(config.MEASUREMENT_NOISE, dtype=np.float64).reshape(4)
+        for k in range(4):
+            cfg.measurement_noise[k] = R[k]
+        cfg.max_landmark_distance = float(config.MAXIMUM_LANDMARK_DISTANCE)
+        cfg.landmark_capacity = int(landmark_capacity)
+        cfg.device = int(device)
+        cfg.reduce_mode = _REDUCE[reduce]
+        if seed is not None:
+            cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.record_assoc = 1 if record_assoc else 0
+        cfg.rank = int(rank)
+        cfg.world_size = int(world_size)
+        if comm_id is not None:
+            C.memmove(cfg.comm_id, comm_id, 128)
+        if rng not in ("numpy", "device"):
+            raise ValueError("rng must be 'numpy' or 'device'")
+        self._rng = rng
+        self._verbose = verbose
+        h = C.c_void_p()
+        nat.check(lib.fs2_create(C.byref(cfg), C.byref(h)))
+        self._lib = lib
+        self._h = h
+        self._cfg = cfg
+        n_local, first, cap = C.c_int64(), C.c_int64(), C.c_int32()
+        nat.check(lib.fs2_shard_info(h, C.byref(n_local), C.byref(first), C.byref(cap)), h)
+        self.num_particles = int(cfg.num_particles)
+        self.n_local = int(n_local.value)
+        self.first_global = int(first.value)
+        self._particles = None
+        self.last_stats = None
+
+    # ------------------------------------------------------------------ core
+    def iterate(self, rotation: float, translation: float,
+                measurements: list[Measurement]) -> tuple[float, float, float]:
+        """One FastSLAM step (reference fast_slam_2.py:33-67); returns the estimate pose."""
+        M = len(measurements)
+        meas = np.empty((M, 2))
+        obs = np.empty((M, 2))
+        for k, m in enumerate(measurements):
+            meas[k, 0] = m.distance
+            meas[k, 1] = m.yaw
+            # observed robot-frame point, computed as the reference does (:100-103)
+            obs[k, 0] = m.distance * np.cos(m.yaw)
+            obs[k, 1] = m.distance * np.sin(m.yaw)
+        noise = u0 = None
+        state = None
+        if self._rng == "numpy":
+            sigma = config.ROTATION_NOISE if rotation != 0 else config.TRANSLATION_NOISE
+            noise = np.random.normal(0, sigma, size=self.num_particles)
+            noise = np.ascontiguousarray(noise[self.first_global:self.first_global + self.n_local])
+            state = np.random.get_state()
+            u0 = np.array([np.random.uniform(0, 1 / self.num_particles)])
+        pose = np.empty(3)
+        st = nat.fs2_iter_stats()
+        rc = self._lib.fs2_iterate(self._h, float(rotation), float(translation),
+                                   nat.ptr(meas) if M else None, nat.ptr(obs) if M else None,
+                                   M, nat.ptr(noise), nat.ptr(u0), nat.dptr(pose), C.byref(st))
+        self._particles = None
+        self.last_stats = st
+        if state is not None and not st.resampled:
+            np.random.set_state(state)          # the reference draws u0 only when resampling
+        nat.check(rc, self._h)
+        if st.resampled and self._verbose:
+            print("\nRESAMPLING")               # reference fast_slam_2.py:63
+        return float(pose[0]), float(pose[1]), float(pose[2])
+
+    def step(self, rotation: float, translation: float, meas, observed=None, noise=None,
+             u0=None):
+        """iterate() with explicit inputs: meas [M][2] (distance, yaw); observed [M][2]
+        robot-frame points (None: computed in libfs2); noise [N_local] motion draws and
+        u0 the resample start (None: Philox on the device).  Returns (pose, stats)."""
+        meas = nat.f64(meas, (-1, 2))
+        M = len(meas)
+        obs = None if observed is None else nat.f64(observed, (-1, 2))
+        nz = None if noise is None else nat.f64(noise)
+        if nz is not None and nz.size != self.n_local:
+            raise ValueError(f"noise must have {self.n_local} values")
+        u = None if u0 is None else np.array([float(u0)])
+        pose = np.empty(3)
+        st = nat.fs2_iter_stats()
+        rc = self._lib.fs2_iterate(self._h, float(rotation), float(translation),
+                                   nat.ptr(meas) if M else None,
+                                   nat.ptr(obs) if (M and obs is not None) else None, M,
+                                   nat.ptr(nz), nat.ptr(u), nat.dptr(pose), C.byref(st))
+        self._particles = None
+        self.last_stats = st
+        nat.check(rc, self._h)
+        return pose, st
+
+    # ------------------------------------------------------------ particles
+    def get_state(self, first: int = 0, count: int | None = None, lm_cap: int | None = None):
+        """Local particles [first, first+count) as arrays (x, y, yaw, w, cnt, lm[count][cap][6])."""
+        count = self.n_local - first if count is None else count
+        x, y, yaw, w = (np.empty(count) for _ in range(4))
+        cnt = np.empty(count, dtype=np.int32)
+        nat.check(self._lib.fs2_get_state(self._h, first, count, nat.ptr(x), nat.ptr(y),
+                                          nat.ptr(yaw), nat.ptr(w), nat.ptr(cnt), None, 0,
+                                          nat.FS2_HOST), self._h)
+        cap = int(cnt.max()) if (lm_cap is None and count) else (lm_cap or 0)
+        lm = np.zeros((count, max(cap, 1), 6))
+        if cap:
+            nat.check(self._lib.fs2_get_state(self._h, first, count, None, None, None, None,
+                                              None, nat.ptr(lm), max(cap, 1), nat.FS2_HOST),
+                      self._h)
+        return x, y, yaw, w, cnt, lm
+
+    def set_state(self, x=None, y=None, yaw=None, w=None, cnt=None, lm=None, first: int = 0):
+        """Upload local particles starting at `first`; lm is [count][cap][6] with cnt."""
+        arrs = [None if a is None else nat.f64(a) for a in (x, y, yaw, w)]
+        count = next((len(a) for a in arrs + [cnt] if a is not None), 0)
+        lmh = None
+        cap = 0
+        cnth = None
+        if cnt is not None:
+            cnth = np.ascontiguousarray(cnt, dtype=np.int32)
+            lmh = nat.f64(lm)
+            cap = lmh.shape[1]
+        nat.check(self._lib.fs2_set_state(self._h, first, count, *(nat.ptr(a) for a in arrs),
+                                          nat.ptr(cnth), nat.ptr(lmh), cap, nat.FS2_HOST),
+                  self._h)
+        self._particles = None
+
+    @property
+    def particles(self) -> list[Particle]:
+        """Host snapshot of this rank's particles (reference attribute `particles`)."""
+        if self._particles is None:
+            x, y, yaw, w, cnt, lm = self.get_state()
+            out = []
+            for i in range(self.n_local):
+                p = Particle.__new__(Particle)
+                p.x, p.y, p.yaw, p.weight = float(x[i]), float(y[i]), float(yaw[i]), float(w[i])
+                p.landmarks = [Landmark(float(lm[i, j, 0]), float(lm[i, j, 1]),
+                                        lm[i, j, 2:6].reshape(2, 2).copy())
+                               for j in range(int(cnt[i]))]
+                out.append(p)
+            self._particles = out
+        return self._particles
+
+    @particles.setter
+    def particles(self, plist: list[Particle]):
+        if len(plist) != self.n_local:
+            raise ValueError(f"expected {self.n_local} particles, got {len(plist)}")
+        cnt = np.array([len(p.landmarks) for p in plist], dtype=np.int32)
+        cap = max(int(cnt.max()) if len(cnt) else 0, 1)
+        lm = np.zeros((len(plist), cap, 6))
+        for i, p in enumerate(plist):
+            for j, l in enumerate(p.landmarks):
+                c = np.asarray(l.cov, dtype=np.float64).reshape(4)
+                lm[i, j] = (l.x, l.y, c[0], c[1], c[2], c[3])
+        self.set_state([p.x for p in plist], [p.y for p in plist], [p.yaw for p in plist],
+                       [p.weight for p in plist], cnt, lm)
+
+    # ------------------------------------------------------------ extras
+    def associations(self) -> np.ndarray:
+        """[M][N_local] association indices of the last scan (-1 = appended)."""
+        m = C.c_int32()
+        buf = np.empty(max(self.n_local * 64, 1), dtype=np.int32)
+        nat.check(self._lib.fs2_get_assoc(self._h, buf.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          buf.size, C.byref(m)), self._h)
+        return buf[:m.value * self.n_local].reshape(m.value, self.n_local).copy()
+
+    def set_profiling(self, enable: bool = True):
+        nat.check(self._lib.fs2_set_profiling(self._h, 1 if enable else 0), self._h)
+
+    def profile(self) -> dict:
+        p = nat.fs2_profile()
+        nat.check(self._lib.fs2_get_profile(self._h, C.byref(p)), self._h)
+        return p.as_dict()
+
+    def synchronize(self):
+        nat.check(self._lib.fs2_synchronize(self._h), self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fs2_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,44 @@
+"""Landmark association (reference: fast_slam_2/utils/landmark_utils.py:92-117)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .. import _native as nat
+from .. import config
+
+
+class LandmarkUtils:
+    known_landmarks: list = []
+    device = 0
+
+    @staticmethod
+    def associate_landmarks(observed_landmark, particle_landmarks):
+        """First landmark in list order within the Mahalanobis gate; (None, None) if none."""
+        L = len(particle_landmarks)
+        if L == 0:
+            return None, None
+        lm = np.empty((L, 6))
+        for j, l in enumerate(particle_landmarks):
+            lm[j, 0], lm[j, 1] = l.x, l.y
+            lm[j, 2:] = np.asarray(l.cov, dtype=np.float64).reshape(4)
+        obs = np.array([observed_landmark.x, observed_landmark.y], dtype=np.float64)
+        idx = C.c_int32()
+        nat.check(nat.load().fs2_associate(LandmarkUtils.device, nat.dptr(obs), nat.dptr(lm), L,
+                                           float(config.MAXIMUM_LANDMARK_DISTANCE), C.byref(idx)))
+        if idx.value < 0:
+            return None, None
+        return particle_landmarks[idx.value], int(idx.value)
+
+    @staticmethod
+    def get_measurements_to_landmarks(scanned_points):
+        raise NotImplementedError(
+            "landmark extraction (Hough + DBSCAN front-end, landmark_utils.py:21-89) is outside "
+            "the particle-update hot path (SURVEY.md §8f, NEXT)")
+
+    @staticmethod
+    def update_known_landmarks(particles):
+        raise NotImplementedError(
+            "update_known_landmarks (DBSCAN visualisation, landmark_utils.py:120-144) is outside "
+            "the particle-update hot path (SURVEY.md §8f, NEXT)")

@@ -1,0 +1,215 @@
+/*
+ * fs2.h -- C ABI of libfs2.so, the MI355X (gfx950) FastSLAM 2.0 particle-update engine.
+ *
+ * Drop-in boundary for the reference's `fast_slam_2` hot path (cy-rae/fast-slam).
+ * The reference has no FFI of its own: it is pure Python, and its callers use the
+ * object API `FastSLAM2().iterate(rotation, translation, measurements)` plus the
+ * static helpers of ICP / LineFilter / LandmarkUtils / GeometryUtils.  Each entry
+ * point below names the reference interface it replaces (file:line under
+ * /root/reference).  The Python shim fast-slam_amd/fast_slam_2/ binds these with
+ * ctypes.
+ *
+ * Conventions:
+ *   - plain C types only; every entry point returns FS2_OK (0) or a negative
+ *     FS2_ERR_* code; fs2_last_error() gives the message;
+ *   - the caller owns every array it passes; the library copies in/out and never
+ *     keeps caller pointers;
+ *   - a handle is bound to one HIP device and one stream (and, with
+ *     world_size > 1, one RCCL rank); it is not thread-safe;
+ *   - all state is fp64 like the reference.
+ */
+#ifndef FS2_H
+#define FS2_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS2_ABI_VERSION 1
+
+enum {
+    FS2_OK = 0,
+    FS2_ERR_ARG = -1,       /* invalid argument */
+    FS2_ERR_HIP = -2,       /* HIP runtime error (no device, launch failure, ...) */
+    FS2_ERR_OOM = -3,       /* device allocation failed */
+    FS2_ERR_LINALG = -4,    /* singular covariance: reference raises numpy.linalg.LinAlgError */
+    FS2_ERR_STATE = -5,     /* call not valid in the current state */
+    FS2_ERR_COMM = -6,      /* RCCL error */
+    FS2_ERR_CAPACITY = -7   /* a map needs more landmark slots than allowed */
+};
+
+/* Reduction order for normalise / N_eff / resample prefix. */
+enum {
+    FS2_REDUCE_AUTO = 0,       /* sequential up to 4096 particles, parallel above */
+    FS2_REDUCE_SEQUENTIAL = 1, /* the reference's exact summation orders (single lane) */
+    FS2_REDUCE_PARALLEL = 2    /* fixed-order tree reductions (deterministic) */
+};
+
+enum { FS2_HOST = 0, FS2_DEVICE = 1 };   /* where caller buffers live */
+
+typedef struct fs2_handle fs2_handle;
+
+typedef struct fs2_config {
+    int64_t num_particles;          /* NUM_PARTICLES, global over all ranks (config.py:7) */
+    double translation_noise;       /* TRANSLATION_NOISE (config.py:11) */
+    double rotation_noise;          /* ROTATION_NOISE (config.py:12) */
+    double measurement_noise[4];    /* MEASUREMENT_NOISE, row-major 2x2 (config.py:15) */
+    double max_landmark_distance;   /* MAXIMUM_LANDMARK_DISTANCE (config.py:18) */
+    double init_landmark_cov[4];    /* Landmark default covariance 0.1*I (models/landmark.py:13) */
+    double weight_floor;            /* 1e-5 normalise floor (algorithms/fast_slam_2.py:168,173) */
+    int32_t landmark_capacity;      /* initial map slots per particle; grows on demand */
+    int32_t max_landmark_capacity;  /* hard limit on slots (0 = 4096) */
+    int32_t device;                 /* HIP device ordinal */
+    int32_t reduce_mode;            /* FS2_REDUCE_* */
+    uint64_t seed;                  /* Philox seed for device-drawn noise and u0 */
+    int32_t record_assoc;           /* keep per-(measurement, particle) association indices */
+    int32_t gate_filter;            /* fp32 conservative gate pre-filter (exactness preserved) */
+    int32_t rank;                   /* this rank (particle shard) */
+    int32_t world_size;             /* number of ranks; 1 = single GPU */
+    uint8_t comm_id[128];           /* ncclUniqueId from fs2_comm_unique_id (world_size > 1) */
+} fs2_config;
+
+typedef struct fs2_iter_stats {
+    int32_t resampled;          /* the N_eff < N/2 rule fired (fast_slam_2.py:62) */
+    int32_t max_count;          /* largest map size after the scan */
+    double n_eff;               /* __calculate_effective_particles (fast_slam_2.py:212-223) */
+    double total_weight;        /* __normalize_weights total (fast_slam_2.py:166) */
+    int64_t best_index;         /* global index of the estimate particle */
+    uint64_t slots_visited;     /* landmark slots read by the association pass */
+    uint64_t candidates;        /* slots whose fp64 data was read (== visited without gate_filter) */
+    uint64_t hits;              /* measurement updates that associated (EKF) */
+    uint64_t appends;           /* measurement updates that appended a landmark */
+    uint64_t slots_written;     /* landmark slots written (EKF updates + appends) */
+    uint64_t ambiguous;         /* gate decisions within 1e-9 relative of the threshold */
+    uint64_t resample_slots;    /* landmark slots copied by the resample gather */
+    int32_t error_flags;        /* bit 0: singular covariance met; bit 1: non-finite weight */
+    int32_t reserved;
+} fs2_iter_stats;
+
+typedef struct fs2_profile {
+    int64_t scans;              /* scans timed since profiling was enabled */
+    int64_t update_launches;    /* fused update kernel launches */
+    double update_ms;           /* summed device time of the update kernel (HIP events) */
+    double reduce_ms;           /* normalise / N_eff / estimate kernels */
+    double resample_ms;         /* prefix + gather kernels (scans that resampled) */
+    double scan_ms;             /* summed device time of whole scans */
+    uint64_t update_bytes;      /* algorithmic bytes moved by the update kernel */
+    uint64_t resample_bytes;    /* algorithmic bytes moved by resample gathers */
+} fs2_profile;
+
+/* ---------------------------------------------------------------- core ---- */
+
+int32_t fs2_abi_version(void);
+
+/* Fills cfg with the reference's config.py defaults (NUM_PARTICLES=20, ...). */
+void fs2_config_default(fs2_config *cfg);
+
+/* Replaces FastSLAM2.__init__ (algorithms/fast_slam_2.py:20-31) and
+ * Particle.__init__ (models/particle.py:11-20): N particles at (0, 0, 0), weight
+ * 1/N, empty maps.  Owns all device memory. */
+int fs2_create(const fs2_config *cfg, fs2_handle **out);
+void fs2_destroy(fs2_handle *h);
+
+/* Message for the last error on this handle (h may be NULL: last global error). */
+const char *fs2_last_error(const fs2_handle *h);
+
+/* Replaces FastSLAM2.iterate (algorithms/fast_slam_2.py:33-67):
+ *   move every particle (:69-87), update with each measurement in order (:90-159),
+ *   normalise (:161-175), N_eff (:212-223), low-variance resample when
+ *   N_eff < N/2 (:62, :177-199), return the first max-weight pose (:201-210).
+ * meas:     M x 2 host array (distance, yaw) -- Measurement.as_vector (models/measurement.py:18-23)
+ * observed: M x 2 host array of the robot-frame points d*cos(yaw), d*sin(yaw)
+ *           (fast_slam_2.py:100-103) as the caller computed them, or NULL to
+ *           compute them here with libm.
+ * noise:    NULL -> Philox draws on device; else N_local host values, the
+ *           np.random.normal(0, sigma) draw for each particle (fast_slam_2.py:79,81).
+ * u0:       NULL -> Philox draw on device; else the np.random.uniform(0, 1/N)
+ *           starting point (fast_slam_2.py:183), used only if resampling fires.
+ * out_pose: x, y, yaw of the estimate.  stats: nullable. */
+int fs2_iterate(fs2_handle *h, double rotation, double translation, const double *meas,
+                const double *observed, int32_t M, const double *noise, const double *u0,
+                double out_pose[3], fs2_iter_stats *stats);
+
+/* Particle state in the reference's object layout (Particle.x/.y/.yaw/.weight,
+ * Particle.landmarks[j] = Landmark(x, y, cov) -- models/particle.py:11-20,
+ * models/landmark.py:13-21).  Range [first, first+count) of this rank's local
+ * particles.  lm is [count][lm_cap][6] = x, y, P00, P01, P10, P11; slots
+ * beyond cnt[i] are left untouched.  where = FS2_HOST or FS2_DEVICE. Any of
+ * x/y/yaw/w/cnt/lm may be NULL to skip it (set_state: cnt and lm go together). */
+int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double *y,
+                  double *yaw, double *w, int32_t *cnt, double *lm, int32_t lm_cap,
+                  int32_t where);
+int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x,
+                  const double *y, const double *yaw, const double *w, const int32_t *cnt,
+                  const double *lm, int32_t lm_cap, int32_t where);
+
+/* Association index per (measurement, local particle) of the last scan,
+ * [M][N_local] row-major; -1 = no landmark associated (a new one was appended).
+ * Mirrors the return of LandmarkUtils.associate_landmarks (landmark_utils.py:92-117).
+ * Requires cfg.record_assoc. */
+int fs2_get_assoc(fs2_handle *h, int32_t *idx, int64_t capacity, int32_t *m_out);
+
+/* Local shard geometry and current map capacity. */
+int fs2_shard_info(const fs2_handle *h, int64_t *n_local, int64_t *first_global,
+                   int32_t *capacity);
+
+int fs2_synchronize(fs2_handle *h);
+
+/* Device-event timing of the hot-path kernels (bench.py roofline). */
+int fs2_set_profiling(fs2_handle *h, int32_t enable);
+int fs2_get_profile(const fs2_handle *h, fs2_profile *out);
+
+/* ------------------------------------------------------ stateless helpers ---- */
+
+/* Replaces ICP.get_transformation (algorithms/icp.py:13-57): brute-force
+ * nearest neighbour (lowest index on ties), closed-form 2-D Kabsch, stop when
+ * |prev - mean NN distance| < threshold.  R: 2x2 row-major, t: 2. */
+int fs2_icp(int32_t device, const double *src, int32_t n_src, const double *tgt,
+            int32_t n_tgt, int32_t max_iterations, double threshold, double R[4],
+            double t[2], int32_t *iterations);
+
+/* B independent alignments of P points each (src/tgt [B][P][2]); R [B][4],
+ * t [B][2], iterations [B] (nullable).  where: FS2_HOST or FS2_DEVICE. */
+int fs2_icp_batched(int32_t device, int32_t B, int32_t P, const double *src,
+                    const double *tgt, int32_t max_iterations, double threshold, double *R,
+                    double *t, int32_t *iterations, int32_t where);
+
+/* Replaces ICP.best_fit_transform (algorithms/icp.py:60-90). */
+int fs2_best_fit_transform(int32_t device, const double *src, const double *tgt, int32_t n,
+                           double R[4], double t[2]);
+
+/* Replaces LineFilter.filter (algorithms/line_filter.py:12-21): per-column
+ * correlate1d with a symmetric Gaussian of 2*radius+1 taps, mode='reflect'.
+ * taps as scipy builds them (fs2_gaussian_taps, or numpy in the shim). */
+int fs2_line_filter(int32_t device, const double *points, int32_t n, const double *taps,
+                    int32_t radius, double *out);
+
+/* scipy.ndimage._gaussian_kernel1d(sigma, 0, int(truncate*sigma + 0.5)) with libm
+ * exp; returns the radius, or -1 if more than max_taps taps would be needed. */
+int32_t fs2_gaussian_taps(double sigma, double truncate, double *taps, int32_t max_taps);
+
+/* Replaces LandmarkUtils.associate_landmarks (utils/landmark_utils.py:92-117) with
+ * GeometryUtils.mahalanobis_distance (utils/geometry_utils.py:13-23): first j with
+ * sqrt(d^T inv(P_j) d) < gate, d = observed - landmark_j; lm is [L][6].
+ * *index = -1 when none (reference returns (None, None)). */
+int fs2_associate(int32_t device, const double observed[2], const double *lm, int32_t L,
+                  double gate, int32_t *index);
+
+/* Replaces GeometryUtils.mahalanobis_distance (utils/geometry_utils.py:13-23) for K
+ * pairs: out[k] = sqrt(d^T inv(cov_k) d), d = b_k - a_k.  a, b: [K][2]; cov: [K][4]
+ * row-major.  FS2_ERR_LINALG if a covariance is singular. */
+int fs2_mahalanobis(int32_t device, const double *a, const double *b, const double *cov,
+                    int32_t K, double *out);
+
+/* ---------------------------------------------------------- multi-GPU ---- */
+
+/* ncclUniqueId for fs2_config.comm_id (call on rank 0, broadcast to all ranks). */
+int fs2_comm_unique_id(uint8_t out[128]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FS2_H */
