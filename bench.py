@@ -90,7 +90,7 @@ def cpu_baseline(L, P, budget_s, seed):
     n = 6000
     wl = syn.Workload(n, L, seed)
     x, y, yaw = wl.poses()
-    o = orc.OracleFilter(n, L + 64)
+    o = orc.OracleFilter(n, L + 4 * 61)
     o.set_state(x, y, yaw, np.full(n, 1.0 / n), np.full(n, L), wl.maps())
     rng = np.random.default_rng(seed)
     t_work, scans = 0.0, 0
