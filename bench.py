@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-gate-filter", action="store_true",
+                    help="A/B: read every visited slot's fp64 data (no fp32 gate mirror)")
     return ap.parse_args()
 
 
@@ -144,7 +146,8 @@ def main():
     total_scans = args.warmup + args.steps
     f = fast_slam_2.FastSLAM2(N, device=local, rng="device", seed=args.seed, reduce="auto",
                               landmark_capacity=L + total_scans + 8, rank=rank,
-                              world_size=world, comm_id=comm_id, verbose=False)
+                              world_size=world, comm_id=comm_id, verbose=False,
+                              gate_filter=not args.no_gate_filter)
     populate(f, f.n_local, L, args.seed, rank)
     scans_pts = None
     if cfg["icp"]:
@@ -218,6 +221,7 @@ def main():
             "config": {"workload": cfg["name"], "particles_per_gpu": n_per_gpu,
                        "particles_total": N, "landmarks": L, "beams": cfg["P"],
                        "measurements_per_scan": 4, "icp": cfg["icp"],
+                       "gate_filter": not args.no_gate_filter,
                        "parallelism": f"particle-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

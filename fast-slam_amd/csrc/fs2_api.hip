@@ -142,7 +142,7 @@ void fs2_config_default(fs2_config *c) {
     c->reduce_mode = FS2_REDUCE_AUTO;
     c->seed = 0x5EEDF5A2ull;
     c->record_assoc = 0;
-    c->gate_filter = 0;
+    c->gate_filter = 1;
     c->rank = 0;
     c->world_size = 1;
 }
@@ -333,6 +333,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     up.rotation = rotation;
     up.translation = translation;
     up.gate2 = h->gate2;
+    up.gate2f = std::isinf(h->gate2) ? INFINITY : std::nextafter((float)h->gate2, INFINITY);
+    up.filter = h->cfg.gate_filter ? 1 : 0;
     std::memcpy(up.R, h->cfg.measurement_noise, sizeof up.R);
     std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
     up.assoc = h->cfg.record_assoc ? h->assoc_dev : nullptr;
@@ -356,6 +358,13 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             } else {
                 up.meas.d[k] = up.meas.b[k] = up.meas.ox[k] = up.meas.oy[k] = 0.0;
             }
+            // fp32 observed point for the gate mirror and a bound on its rounding
+            const double ox = up.meas.ox[k], oy = up.meas.oy[k];
+            up.meas.fx[k] = (float)ox;
+            up.meas.fy[k] = (float)oy;
+            const double e = std::max(std::fabs(ox - (double)up.meas.fx[k]),
+                                      std::fabs(oy - (double)up.meas.fy[k]));
+            up.meas.fe[k] = std::isfinite(e) ? std::nextafter((float)e, INFINITY) : INFINITY;
         }
         HIP_TRY(h, launch_update(up, s));
         ++passes;
@@ -429,10 +438,13 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         h->prof.reduce_ms += b;
         h->prof.resample_ms += c;
         h->prof.scan_ms += a + b + c;
-        h->prof.update_bytes += 48ull * st.candidates + 48ull * st.written + fixed_bytes +
+        // mirror reads (16 B) per visited slot when filtering, fp64 slot reads (48 B) per
+        // candidate, full slot writes (48 B + 16 B mirror)
+        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited : 0ull) +
+                                48ull * st.candidates + 64ull * st.written + fixed_bytes +
                                 8ull * (uint64_t)h->nblocks();
         if (st.resampled)
-            h->prof.resample_bytes += 2ull * 48ull * st.resample_slots + 2ull * 36ull * (uint64_t)h->n;
+            h->prof.resample_bytes += 2ull * 64ull * st.resample_slots + 2ull * 36ull * (uint64_t)h->n;
     }
     if (out_pose) {
         out_pose[0] = st.pose[0];

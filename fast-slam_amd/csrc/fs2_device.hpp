@@ -96,6 +96,50 @@ struct Meas {
     double d, b, ox, oy;
 };
 
+// ----------------------------------------------------------- gate mirror ---
+// Every slot carries an fp32 shadow (x, y, s) read by the association pass in
+// place of the 48-byte fp64 slot.  s is a lower bound on the smallest
+// eigenvalue of the symmetric part of inv(P) -- the very inverse the gate uses
+// (inv2) -- shrunk by 1e-6, so for the fp64 gate value q of ANY observed point
+//     q >= s * |delta|^2.
+// A slot whose fp32 lower bound on s*|delta|^2 (rounding of every fp32
+// quantity accounted for, see gate_reject) exceeds gate2 can therefore not
+// match, and is skipped without reading its fp64 data; every other slot takes
+// the exact fp64 test.  Association results are unchanged by construction.
+// s = 0 (never reject) when inv(P) is singular, not positive definite, not
+// finite or worse conditioned than 1e8 (the 1e-6 margin covers the fp64
+// rounding of q up to that condition number).
+__device__ __forceinline__ float4 mirror_of(const Slot &sl) {
+    M2 I;
+    float s = 0.0f;
+    if (inv2(sl.P, I)) {
+        const double a = I.a00, c = I.a11, b = 0.5 * (I.a01 + I.a10);
+        const double half = 0.5 * (a + c);
+        const double dd = 0.5 * (a - c);
+        const double lmax = half + sqrt(dd * dd + b * b);
+        const double det = a * c - b * b;
+        const double lmin = det / lmax;
+        if (lmin > 0.0 && lmax < 1e300 && lmax <= 1e8 * lmin)
+            s = __double2float_rd(lmin * (1.0 - 1e-6));
+    }
+    return make_float4(__double2float_rn(sl.mx), __double2float_rn(sl.my), s, 0.0f);
+}
+
+// true when the mirror proves sqrt(q) >= gate for the observed point (fx, fy)
+// (fe bounds the fp32 rounding of the observed point itself).
+__device__ __forceinline__ bool gate_reject(const float4 &m, float fx, float fy, float fe,
+                                            float gate2f) {
+    const float dx = fx - m.x, dy = fy - m.y;
+    const float ax = fabsf(dx), ay = fabsf(dy);
+    // |true delta| >= |fp32 delta| - (rounding of x_obs, x_lm and the subtraction),
+    // each half-ulp <= 2^-24 |value|; 2^-22 leaves a 4x margin.
+    const float ex = fe + (fabsf(m.x) + ax) * 2.3841858e-7f;
+    const float ey = fe + (fabsf(m.y) + ay) * 2.3841858e-7f;
+    const float lx = fmaxf(ax - ex, 0.0f), ly = fmaxf(ay - ey, 0.0f);
+    const float d2 = (lx * lx + ly * ly) * 0.99999619f;   // (1 - 2^-18): fp32 rounding
+    return m.z * d2 > gate2f;
+}
+
 // EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line:
 // it runs at most M times per particle and scan, and inlining it doubles the
 // streaming loop's register footprint (occupancy 2 -> 4 waves/SIMD).  Updates `s`

@@ -127,11 +127,17 @@ __device__ __forceinline__ Slot load_slot(const MapRef &m, int j, int64_t i) {
     return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
 }
 
+__device__ __forceinline__ float4 load_mirror(const MapRef &m, int j, int64_t i) {
+    return reinterpret_cast<const float4 *>(slot_planes(m, j) + kMirrorPlane * m.n)[i];
+}
+
+// Every slot write keeps the fp32 gate mirror in step with the fp64 slot.
 __device__ __forceinline__ void store_slot(const MapRef &m, int j, int64_t i, const Slot &s) {
     double2 *p = const_cast<double2 *>(slot_planes(m, j));
     p[i] = make_double2(s.mx, s.my);
     p[m.n + i] = make_double2(s.P.a00, s.P.a01);
     p[2 * m.n + i] = make_double2(s.P.a10, s.P.a11);
+    reinterpret_cast<float4 *>(p + kMirrorPlane * m.n)[i] = mirror_of(s);
 }
 
 // Gate decisions this close to the threshold could depend on ulp-level
@@ -202,12 +208,46 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     const double gate2 = P.gate2;
 
     // ---- single pass over the existing map (association + EKF) ----
-    for (int j = 0;; ++j) {
-        const bool act = (pend != 0u) && (j < c);
-        if (!__any(act)) break;
-        if (act) {
+    // Steps of kGroup slots: the fp32 mirrors of the whole group are loaded
+    // first (1 KiB per wave and slot, all in flight together); a slot whose
+    // mirror cannot rule out every still-pending measurement becomes a
+    // candidate and takes the exact fp64 path, in slot order.
+    unsigned candidates = 0;
+    for (int j0 = 0;; j0 += kGroup) {
+        if (!__any((pend != 0u) && (j0 < c))) break;
+        unsigned cmask = 0;
+        if (P.filter) {
+            float4 mir[kGroup];
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u)
+                if (pend != 0u && j0 + u < c) mir[u] = load_mirror(P.map, j0 + u, i);
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                if (pend != 0u && j0 + u < c) {
+                    ++visited;
+                    bool cand = false;
+#pragma unroll
+                    for (int k = 0; k < MAXM; ++k)
+                        if ((pend >> k) & 1u)
+                            cand |= !gate_reject(mir[u], P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
+                                                 P.gate2f);
+                    if (cand) cmask |= 1u << u;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u)
+                if (pend != 0u && j0 + u < c) {
+                    ++visited;
+                    cmask |= 1u << u;
+                }
+        }
+        while (cmask) {
+            const int j = j0 + __builtin_ctz(cmask);
+            cmask &= cmask - 1u;
+            if (pend == 0u) break;
             Slot s = load_slot(P.map, j, i);
-            ++visited;
+            ++candidates;
             bool mod = false;
             M2 I;
             bool ok = inv2(s.P, I);
@@ -252,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         int hit = -1;
         for (int a = 0; a < nap; ++a) {
             const Slot s = load_slot(P.map, c + a, i);
-            ++visited;
+            ++candidates;
             M2 I;
             if (!inv2(s.P, I)) {
                 singular = true;
@@ -307,6 +347,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     // ---- block statistics ----
     const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
+    const unsigned long long bc = block_sum_u64<kBlock>(candidates, lds_u);
     const unsigned long long bw = block_sum_u64<kBlock>(written, lds_u);
     const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
     const unsigned long long bap = block_sum_u64<kBlock>(appends, lds_u);
@@ -322,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
     if (tid == 0) {
         atomicAdd(&P.stats->visited, bv);
-        atomicAdd(&P.stats->candidates, bv);
+        atomicAdd(&P.stats->candidates, bc);
         atomicAdd(&P.stats->written, bw);
         atomicAdd(&P.stats->ambiguous, ba);
         atomicAdd(&P.stats->appends, bap);
@@ -601,9 +642,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_maps(const ResampleParams P) 
             const double2 *ip = slot_planes(P.in, j);
             double2 *op = const_cast<double2 *>(slot_planes(P.out, j));
             const double2 a = ip[s], b = ip[P.in.n + s], c = ip[2 * P.in.n + s];
+            const double2 g = ip[kMirrorPlane * P.in.n + s];   // gate mirror (16 B)
             op[m] = a;
             op[P.out.n + m] = b;
             op[2 * P.out.n + m] = c;
+            op[kMirrorPlane * P.out.n + m] = g;
             ++copied;
         }
     }

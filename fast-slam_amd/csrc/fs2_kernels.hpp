@@ -11,7 +11,11 @@ constexpr int kBlock = 256;          // 4 waves of 64
 constexpr int kPageSlots = 64;       // landmark slots per page
 constexpr int kMaxPages = 64;        // 4096 slots per particle max
 constexpr int kMaxM = 4;             // measurements fused into one map pass
-constexpr int kPlanes = 3;           // double2 planes per slot: (x,y) (P00,P01) (P10,P11)
+// 16-byte planes per slot: (x,y) (P00,P01) (P10,P11) as double2, then the
+// fp32 gate mirror (x, y, s, 0) as float4 -- see k_update.
+constexpr int kPlanes = 4;
+constexpr int kMirrorPlane = 3;
+constexpr int kGroup = 4;            // map slots whose mirrors one lane loads per step
 
 // Device statistics of one scan (zeroed before every scan).
 struct DevStats {
@@ -31,6 +35,8 @@ struct DevStats {
 
 struct MeasPack {
     double d[kMaxM], b[kMaxM], ox[kMaxM], oy[kMaxM];
+    float fx[kMaxM], fy[kMaxM];   // fp32 observed point for the gate mirror
+    float fe[kMaxM];              // >= |ox - fx|, |oy - fy| (rounded up)
 };
 
 struct MapRef {
@@ -54,6 +60,8 @@ struct UpdateParams {
     int32_t k0;              // first measurement index of this pass
     int32_t last_pass;
     double gate2;            // match iff 0 <= q < gate2  (sqrt(q) < gate)
+    float gate2f;            // gate2 rounded up to fp32 (mirror test)
+    int32_t filter;          // use the fp32 gate mirror
     double R[4];
     double init_cov[4];
     int32_t *assoc;          // [M][n] or null

@@ -35,7 +35,7 @@ class FastSLAM2:
     def __init__(self, num_particles: int | None = None, *, device: int = 0, rng: str = "numpy",
                  seed: int | None = None, reduce: str = "auto", record_assoc: bool = False,
                  landmark_capacity: int = 64, rank: int = 0, world_size: int = 1,
-                 comm_id: bytes | None = None, verbose: bool = True):
+                 comm_id: bytes | None = None, verbose: bool = True, gate_filter: bool = True):
         lib = nat.load()
         cfg = nat.default_config()
         cfg.num_particles = int(config.NUM_PARTICLES if num_particles is None else num_particles)
@@ -51,6 +51,7 @@ class FastSLAM2:
         if seed is not None:
             cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         cfg.record_assoc = 1 if record_assoc else 0
+        cfg.gate_filter = 1 if gate_filter else 0
         cfg.rank = int(rank)
         cfg.world_size = int(world_size)
         if comm_id is not None:

@@ -230,6 +230,46 @@ def test_resample_never_hangs(fs):
     f.close()
 
 
+def test_gate_filter_is_exact(fs):
+    """The fp32 gate mirror only skips slots that cannot match: with and without it
+    every association, weight and landmark is bit-identical, and it skips most
+    fp64 slot reads."""
+    import fs2_synthetic as syn
+    N, L = 4096, 80
+    wl = syn.Workload(N, L, seed=11)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    rng = np.random.default_rng(4)
+    # anisotropic and near-singular covariances exercise the conditioning guard
+    th = rng.uniform(0, np.pi, (N, L))
+    l1 = 10 ** rng.uniform(-4, -1, (N, L))
+    l2 = l1 * 10 ** rng.uniform(0, 9, (N, L))
+    c, s = np.cos(th), np.sin(th)
+    lm[:, :, 2] = c * c * l1 + s * s * l2
+    lm[:, :, 3] = c * s * (l1 - l2)
+    lm[:, :, 4] = lm[:, :, 3] + rng.normal(0, 1e-18, (N, L))
+    lm[:, :, 5] = s * s * l1 + c * c * l2
+    fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False)
+          for g in (True, False)]
+    for f in fl:
+        f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    for sc in range(6):
+        rot, tr = syn.odometry(sc)
+        ms = np.concatenate([wl.measurements(sc), rng.normal(0, 12, (3, 2))])
+        ms[:, 0] = np.abs(ms[:, 0])
+        nz = rng.normal(0, 0.001 if rot else 0.0055, N)
+        out = [f.step(rot, tr, ms, None, nz, 0.3 / N) for f in fl]
+        a0, a1 = fl[0].associations(), fl[1].associations()
+        assert np.array_equal(a0, a1), sc
+        assert np.array_equal(out[0][0], out[1][0])
+        assert out[0][1].candidates < out[1][1].candidates
+    s0, s1 = fl[0].get_state(lm_cap=L + 64), fl[1].get_state(lm_cap=L + 64)
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b)
+    for f in fl:
+        f.close()
+
+
 def test_oracle_parity_n20000(fs):
     """N = 20000, L = 50, parallel reductions, 6 scans with injected draws."""
     import fs2_synthetic as syn
