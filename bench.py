@@ -176,12 +176,14 @@ def main():
     f.set_profiling(True)
     resamples = 0
     visited = 0
+    copied_slots = 0
     barrier()
     t0 = time.perf_counter()
     for s in range(args.warmup, total_scans):
         _, st = one_scan(s)
         resamples += st.resampled
         visited += st.slots_visited
+        copied_slots += st.resample_slots
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -234,6 +236,8 @@ def main():
                       "reduce_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resample_ms_total": prof["resample_ms"],
                       "resamples": resamples,
+                      "resample_copied_map_fraction":
+                          copied_slots / max(resamples * f.n_local * (L + total_scans), 1),
                       "slots_visited_per_particle_scan": visited / (f.n_local * args.steps),
                       "icp_us": icp_us},
         }

@@ -67,8 +67,11 @@ struct fs2_handle {
     int cur = 0;
     double *x[2] = {}, *y[2] = {}, *yaw[2] = {}, *w[2] = {};
     int32_t *cnt[2] = {};
-    std::vector<char *> pages[2];
-    char **pages_dev[2] = {};
+    std::vector<char *> arenas;            // arena k: page k of every physical map
+    char **arenas_dev = nullptr;
+    int32_t *phys[2] = {};                 // logical -> physical map (A/B across resamples)
+    int32_t *used = nullptr, *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
+    int32_t *freelist = nullptr, *tasks = nullptr;
     int cap = 0, max_cap = 4096;
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
     int64_t *part_best_i = nullptr;
@@ -89,7 +92,7 @@ struct fs2_handle {
     fs2_profile prof{};
     fs2comm::Comm *comm = nullptr;
 
-    MapRef map(int set) const { return MapRef{pages_dev[set], n}; }
+    MapRef map() const { return MapRef{arenas_dev, phys[cur]}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
     bool sequential() const {
         const int mode = cfg.reduce_mode;
@@ -105,17 +108,15 @@ static int grow_pages(fs2_handle *h, int need_slots) {
         return set_err(&h->err, FS2_ERR_CAPACITY, "map needs %d landmark slots, limit is %d",
                        need_slots, h->max_cap);
     const int need_pages = (need_slots + kPageSlots - 1) / kPageSlots;
-    const size_t page_bytes = (size_t)kPageSlots * (size_t)MapRef{nullptr, h->n}.slot_stride();
+    const size_t arena_bytes = (size_t)std::max<int64_t>(h->n, 1) * kPageBytes;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
-    for (int set = 0; set < 2; ++set) {
-        while ((int)h->pages[set].size() < need_pages) {
-            char *p = nullptr;
-            HIP_TRY(h, hipMalloc(&p, page_bytes > 0 ? page_bytes : 16));
-            h->pages[set].push_back(p);
-        }
-        HIP_TRY(h, hipMemcpy(h->pages_dev[set], h->pages[set].data(),
-                             sizeof(char *) * h->pages[set].size(), hipMemcpyHostToDevice));
+    while ((int)h->arenas.size() < need_pages) {
+        char *p = nullptr;
+        HIP_TRY(h, hipMalloc(&p, arena_bytes));
+        h->arenas.push_back(p);
     }
+    HIP_TRY(h, hipMemcpy(h->arenas_dev, h->arenas.data(), sizeof(char *) * h->arenas.size(),
+                         hipMemcpyHostToDevice));
     h->cap = need_pages * kPageSlots;
     return FS2_OK;
 }
@@ -157,9 +158,12 @@ static void free_handle(fs2_handle *h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     for (int s = 0; s < 2; ++s) {
         hipFree(h->x[s]); hipFree(h->y[s]); hipFree(h->yaw[s]); hipFree(h->w[s]); hipFree(h->cnt[s]);
-        for (char *p : h->pages[s]) hipFree(p);
-        hipFree(h->pages_dev[s]);
+        hipFree(h->phys[s]);
     }
+    for (char *p : h->arenas) hipFree(p);
+    hipFree(h->arenas_dev);
+    hipFree(h->used); hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
+    hipFree(h->freelist); hipFree(h->tasks);
     hipFree(h->wpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum); hipFree(h->src);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -217,8 +221,15 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= alloc((void **)&h->yaw[s], n * 8) == hipSuccess;
         ok &= alloc((void **)&h->w[s], n * 8) == hipSuccess;
         ok &= alloc((void **)&h->cnt[s], n * 4) == hipSuccess;
-        ok &= alloc((void **)&h->pages_dev[s], sizeof(char *) * kMaxPages) == hipSuccess;
+        ok &= alloc((void **)&h->phys[s], n * 4) == hipSuccess;
     }
+    ok &= alloc((void **)&h->arenas_dev, sizeof(char *) * kMaxPages) == hipSuccess;
+    ok &= alloc((void **)&h->used, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->iblk, 2 * nsb * 4) == hipSuccess;
+    ok &= alloc((void **)&h->freelist, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->tasks, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
@@ -240,6 +251,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
             hipMemsetAsync(h->y[s], 0, n * 8, h->stream) != hipSuccess ||
             hipMemsetAsync(h->yaw[s], 0, n * 8, h->stream) != hipSuccess ||
             hipMemsetAsync(h->cnt[s], 0, n * 4, h->stream) != hipSuccess ||
+            launch_iota(h->phys[s], n, h->stream) != hipSuccess ||
             launch_fill(h->w[s], 1.0 / (double)h->n_global, n, h->stream) != hipSuccess)
             return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     }
@@ -325,7 +337,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     up.n = h->n;
     up.gidx0 = h->first;
     up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
-    up.map = h->map(cur);
+    up.map = h->map();
     up.noise = noise ? h->noise_dev : nullptr;
     up.seed = h->cfg.seed;
     up.scan = h->scan;
@@ -333,7 +345,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     up.rotation = rotation;
     up.translation = translation;
     up.gate2 = h->gate2;
-    up.gate2f = std::isinf(h->gate2) ? INFINITY : std::nextafter((float)h->gate2, INFINITY);
+    // gate2 / (1 - 2^-18) rounded up: slack for the fp32 rounding in gate_reject_fast
+    up.gate2f = std::isinf(h->gate2) ? INFINITY
+                                     : std::nextafter((float)(h->gate2 / (1.0 - 0x1p-18)), INFINITY);
     up.filter = h->cfg.gate_filter ? 1 : 0;
     std::memcpy(up.R, h->cfg.measurement_noise, sizeof up.R);
     std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
@@ -412,12 +426,20 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.src = h->src;
     rs.x = h->x[cur]; rs.y = h->y[cur]; rs.yaw = h->yaw[cur]; rs.cnt = h->cnt[cur];
     rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
-    rs.in = h->map(cur);
-    rs.out = h->map(nxt);
+    rs.arenas = h->arenas_dev;
+    rs.phys = h->phys[cur];
+    rs.ophys = h->phys[nxt];
+    rs.used = h->used;
+    rs.rank_d = h->rank_d;
+    rs.rank_e = h->rank_e;
+    rs.iblk = h->iblk;
+    rs.freelist = h->freelist;
+    rs.tasks = h->tasks;
     rs.part_best_w = h->part_best_w;
     rs.part_best_i = h->part_best_i;
     rs.stats = h->stats_dev;
-    HIP_TRY(h, launch_resample(rs, seq ? 1 : 0, std::min(h->cap, h->cnt_upper + M), s));
+    HIP_TRY(h, hipMemsetAsync(h->used, 0, sizeof(int32_t) * std::max<int64_t>(h->n, 1), s));
+    HIP_TRY(h, launch_resample(rs, seq ? 1 : 0, s));
     if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[3], s));
 
     HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
@@ -444,7 +466,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
                                 48ull * st.candidates + 64ull * st.written + fixed_bytes +
                                 8ull * (uint64_t)h->nblocks();
         if (st.resampled)
-            h->prof.resample_bytes += 2ull * 64ull * st.resample_slots + 2ull * 36ull * (uint64_t)h->n;
+            // copied maps (read + write 64 B per slot) + scalar gather + plan arrays
+            h->prof.resample_bytes += 2ull * 64ull * st.resample_slots + 2ull * 36ull * (uint64_t)h->n +
+                                      40ull * (uint64_t)h->n;
     }
     if (out_pose) {
         out_pose[0] = st.pose[0];
@@ -533,7 +557,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             const int64_t k = std::min(chunk, count - o);
             hipError_t e = hipMemcpy(stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
             if (e == hipSuccess) e = hipMemcpy(cstage, hc.data() + o, sizeof(int32_t) * k, hipMemcpyHostToDevice);
-            if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(c), h->cnt[c], s);
+            if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), h->cnt[c], s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
         }
@@ -575,7 +599,7 @@ int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double
         for (int64_t o = 0; o < count && rc2 == FS2_OK; o += chunk) {
             const int64_t k = std::min(chunk, count - o);
             hipError_t e = hipMemsetAsync(stage, 0, (size_t)k * per, s);
-            if (e == hipSuccess) e = launch_export(stage, first + o, k, lm_cap, h->map(c), h->cnt[c], s);
+            if (e == hipSuccess) e = launch_export(stage, first + o, k, lm_cap, h->map(), h->cnt[c], s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e == hipSuccess) e = hipMemcpy(lm + o * lm_cap * 6, stage, (size_t)k * per, kind_out(where));
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state export failed: %s", hipGetErrorString(e));
@@ -656,7 +680,7 @@ int fs2_icp_batched(int32_t device, int32_t B, int32_t P, const double *src, con
     const hipMemcpyKind kout = where == FS2_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     SHIP(hipMemcpyAsync(ds, src, (size_t)B * P * 16, kin, sc->stream));
     SHIP(hipMemcpyAsync(dt, tgt, (size_t)B * P * 16, kin, sc->stream));
-    SHIP(launch_icp(B, P, ds, dt, P, max_iterations, threshold, dR, dT, dI, nullptr, sc->stream));
+    SHIP(launch_icp(B, P, ds, dt, P, max_iterations, threshold, dR, dT, dI, sc->stream));
     SHIP(hipMemcpyAsync(R, dR, (size_t)B * 32, kout, sc->stream));
     SHIP(hipMemcpyAsync(t, dT, (size_t)B * 16, kout, sc->stream));
     if (iterations) SHIP(hipMemcpyAsync(iterations, dI, (size_t)B * 4, kout, sc->stream));
@@ -678,7 +702,7 @@ int fs2_icp(int32_t device, const double *src, int32_t n_src, const double *tgt,
     int32_t *dI = (int32_t *)(dT + 2);
     SHIP(hipMemcpyAsync(ds, src, (size_t)n_src * 16, hipMemcpyHostToDevice, sc->stream));
     SHIP(hipMemcpyAsync(dt, tgt, (size_t)n_tgt * 16, hipMemcpyHostToDevice, sc->stream));
-    SHIP(launch_icp(1, n_src, ds, dt, n_tgt, max_iterations, threshold, dR, dT, dI, nullptr, sc->stream));
+    SHIP(launch_icp(1, n_src, ds, dt, n_tgt, max_iterations, threshold, dR, dT, dI, sc->stream));
     double out[6];
     int32_t it = 0;
     SHIP(hipMemcpyAsync(out, dR, 48, hipMemcpyDeviceToHost, sc->stream));

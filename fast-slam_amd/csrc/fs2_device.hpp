@@ -125,19 +125,18 @@ __device__ __forceinline__ float4 mirror_of(const Slot &sl) {
     return make_float4(__double2float_rn(sl.mx), __double2float_rn(sl.my), s, 0.0f);
 }
 
-// true when the mirror proves sqrt(q) >= gate for the observed point (fx, fy)
-// (fe bounds the fp32 rounding of the observed point itself).
-__device__ __forceinline__ bool gate_reject(const float4 &m, float fx, float fy, float fe,
-                                            float gate2f) {
+// true when the mirror proves sqrt(q) >= gate for the observed point (fx, fy).
+//   |true dx| >= |fp32 dx| - ex,  ex = fe + (|x_lm| + |fp32 dx|) 2^-22
+// (fe bounds the fp32 rounding of the observed point; the rounding of x_lm and
+// of the subtraction is <= 2^-24 |value| each, so 2^-22 leaves a 4x margin).
+// cx = 2^-22 |x_lm| and cy are per slot.  gate2f = gate2 / (1 - 2^-18) rounded
+// up: the relative slack absorbs the fp32 rounding of lx, ly, d2 and s * d2.
+__device__ __forceinline__ bool gate_reject_fast(const float4 &m, float cx, float cy, float fx,
+                                                 float fy, float fe, float gate2f) {
     const float dx = fx - m.x, dy = fy - m.y;
-    const float ax = fabsf(dx), ay = fabsf(dy);
-    // |true delta| >= |fp32 delta| - (rounding of x_obs, x_lm and the subtraction),
-    // each half-ulp <= 2^-24 |value|; 2^-22 leaves a 4x margin.
-    const float ex = fe + (fabsf(m.x) + ax) * 2.3841858e-7f;
-    const float ey = fe + (fabsf(m.y) + ay) * 2.3841858e-7f;
-    const float lx = fmaxf(ax - ex, 0.0f), ly = fmaxf(ay - ey, 0.0f);
-    const float d2 = (lx * lx + ly * ly) * 0.99999619f;   // (1 - 2^-18): fp32 rounding
-    return m.z * d2 > gate2f;
+    const float lx = fmaxf(fmaf(fabsf(dx), 0.99999976f, -(fe + cx)), 0.0f);
+    const float ly = fmaxf(fmaf(fabsf(dy), 0.99999976f, -(fe + cy)), 0.0f);
+    return m.z * fmaf(lx, lx, ly * ly) > gate2f;
 }
 
 // EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line:

@@ -1,0 +1,273 @@
+// fs2_geometry.hip -- gfx950 kernels for the stateless helpers of the hot path:
+// ICP scan matching (algorithms/icp.py:13-90), LineFilter (line_filter.py:12-21),
+// Mahalanobis distance (geometry_utils.py:13-23) and first-match association
+// (landmark_utils.py:92-117).
+#include "fs2_device.hpp"
+#include "fs2_kernels.hpp"
+
+namespace fs2 {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------- ICP ---
+//
+// One workgroup per alignment; the target cloud and the moving source cloud
+// live in LDS for the whole loop; nearest neighbours by brute force with
+// broadcast LDS reads (every lane reads the same target point), lowest index
+// on exact ties; centroids / cross-covariance / mean distance by fixed-order
+// wave + LDS reductions; rotation by the closed-form 2-D Kabsch angle, which
+// equals the reference's SVD + reflection fix (icp.py:76-85).
+
+constexpr int kIcpMaxP = 1024;
+constexpr int kIcpThreads = 1024;
+
+template <int NT>
+__device__ void block_sum5(double v[5], double *lds) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) lds[q * 16 + wid] = v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NT / 64; ++k) t += lds[q * 16 + k];
+        v[q] = t;
+    }
+}
+
+__global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *src_all,
+                                                     const double *tgt_all, int32_t nt,
+                                                     int32_t max_iter, double thr, double *R_out,
+                                                     double *t_out, int32_t *iters_out) {
+    __shared__ double2 s_src[kIcpMaxP];
+    __shared__ double2 s_tgt[kIcpMaxP];
+    __shared__ int32_t s_nn[kIcpMaxP];
+    __shared__ double s_dist[kIcpMaxP];
+    __shared__ double red[5 * 16];
+    __shared__ double s_R[4], s_t[2];
+    __shared__ int s_stop;
+
+    const int b = blockIdx.x;
+    const double2 *src = reinterpret_cast<const double2 *>(src_all) + (int64_t)b * P;
+    const double2 *tgt = reinterpret_cast<const double2 *>(tgt_all) + (int64_t)b * nt;
+    for (int k = threadIdx.x; k < P; k += kIcpThreads) s_src[k] = src[k];
+    for (int k = threadIdx.x; k < nt; k += kIcpThreads) s_tgt[k] = tgt[k];
+    double Rt[4] = {1.0, 0.0, 0.0, 1.0}, tt[2] = {0.0, 0.0};
+    double prev = INFINITY;
+    int it = 0;
+    __syncthreads();
+    while (it < max_iter) {
+        ++it;
+        // nearest neighbours
+        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+            const double2 sp = s_src[k];
+            double best = INFINITY;
+            int bj = 0;
+            for (int j = 0; j < nt; ++j) {
+                const double2 tp = s_tgt[j];
+                const double dx = sp.x - tp.x, dy = sp.y - tp.y;
+                const double d2 = dx * dx + dy * dy;
+                if (d2 < best) {
+                    best = d2;
+                    bj = j;
+                }
+            }
+            s_nn[k] = bj;
+            s_dist[k] = sqrt(best);
+        }
+        __syncthreads();
+        // centroids and mean distance
+        double v[5] = {0, 0, 0, 0, 0};
+        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+            const double2 sp = s_src[k], tp = s_tgt[s_nn[k]];
+            v[0] += sp.x; v[1] += sp.y; v[2] += tp.x; v[3] += tp.y; v[4] += s_dist[k];
+        }
+        block_sum5<kIcpThreads>(v, red);
+        const double cs0 = v[0] / P, cs1 = v[1] / P, ct0 = v[2] / P, ct1 = v[3] / P;
+        const double mean = v[4] / P;
+        // cross-covariance of the centred sets (icp.py:73)
+        double h[5] = {0, 0, 0, 0, 0};
+        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+            const double2 sp = s_src[k], tp = s_tgt[s_nn[k]];
+            const double a0 = sp.x - cs0, a1 = sp.y - cs1, b0 = tp.x - ct0, b1 = tp.y - ct1;
+            h[0] += a0 * b0; h[1] += a0 * b1; h[2] += a1 * b0; h[3] += a1 * b1;
+        }
+        block_sum5<kIcpThreads>(h, red);
+        if (threadIdx.x == 0) {
+            const double th = atan2(h[1] - h[2], h[0] + h[3]);
+            const double c = cos(th), s = sin(th);
+            const M2 Ri{c, -s, s, c};
+            const double t0 = ct0 - fma(Ri.a00, cs0, Ri.a01 * cs1);
+            const double t1 = ct1 - fma(Ri.a10, cs0, Ri.a11 * cs1);
+            s_R[0] = Ri.a00; s_R[1] = Ri.a01; s_R[2] = Ri.a10; s_R[3] = Ri.a11;
+            s_t[0] = t0; s_t[1] = t1;
+            s_stop = fabs(prev - mean) < thr ? 1 : 0;
+        }
+        __syncthreads();
+        const double r00 = s_R[0], r01 = s_R[1], r10 = s_R[2], r11 = s_R[3], t0 = s_t[0], t1 = s_t[1];
+        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+            const double2 sp = s_src[k];
+            s_src[k] = make_double2(fma(sp.y, r01, sp.x * r00) + t0, fma(sp.y, r11, sp.x * r10) + t1);
+        }
+        const M2 Rn = mm2(M2{r00, r01, r10, r11}, M2{Rt[0], Rt[1], Rt[2], Rt[3]});
+        Rt[0] = Rn.a00; Rt[1] = Rn.a01; Rt[2] = Rn.a10; Rt[3] = Rn.a11;
+        const double nt0 = fma(r00, tt[0], r01 * tt[1]) + t0;
+        const double nt1 = fma(r10, tt[0], r11 * tt[1]) + t1;
+        tt[0] = nt0;
+        tt[1] = nt1;
+        const int stop = s_stop;
+        prev = mean;
+        __syncthreads();
+        if (stop) break;
+    }
+    if (threadIdx.x == 0) {
+        for (int q = 0; q < 4; ++q) R_out[b * 4 + q] = Rt[q];
+        t_out[b * 2] = tt[0];
+        t_out[b * 2 + 1] = tt[1];
+        if (iters_out) iters_out[b] = it;
+    }
+}
+
+hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt, int32_t n_tgt,
+                      int32_t max_iter, double thr, double *R, double *t, int32_t *iters,
+                      hipStream_t s) {
+    if (P > kIcpMaxP || n_tgt > kIcpMaxP) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_icp, dim3(B), dim3(kIcpThreads), 0, s, P, src, tgt, n_tgt, max_iter, thr,
+                       R, t, iters);
+    return hipGetLastError();
+}
+
+// best_fit_transform alone: Rt = [R00 R01 R10 R11 t0 t1]
+__global__ __launch_bounds__(kIcpThreads) void k_best_fit(const double *src_, const double *tgt_,
+                                                          int32_t P, double *Rt) {
+    __shared__ double red[5 * 16];
+    const double2 *src = reinterpret_cast<const double2 *>(src_);
+    const double2 *tgt = reinterpret_cast<const double2 *>(tgt_);
+    double v[5] = {0, 0, 0, 0, 0};
+    for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+        v[0] += src[k].x; v[1] += src[k].y; v[2] += tgt[k].x; v[3] += tgt[k].y;
+    }
+    block_sum5<kIcpThreads>(v, red);
+    const double cs0 = v[0] / P, cs1 = v[1] / P, ct0 = v[2] / P, ct1 = v[3] / P;
+    double h[5] = {0, 0, 0, 0, 0};
+    for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+        const double a0 = src[k].x - cs0, a1 = src[k].y - cs1, b0 = tgt[k].x - ct0, b1 = tgt[k].y - ct1;
+        h[0] += a0 * b0; h[1] += a0 * b1; h[2] += a1 * b0; h[3] += a1 * b1;
+    }
+    block_sum5<kIcpThreads>(h, red);
+    if (threadIdx.x == 0) {
+        const double th = atan2(h[1] - h[2], h[0] + h[3]);
+        const double c = cos(th), s = sin(th);
+        Rt[0] = c; Rt[1] = -s; Rt[2] = s; Rt[3] = c;
+        Rt[4] = ct0 - fma(c, cs0, -s * cs1);
+        Rt[5] = ct1 - fma(s, cs0, c * cs1);
+    }
+}
+
+hipError_t launch_best_fit(const double *src, const double *tgt, int32_t n, double *Rt, hipStream_t s) {
+    hipLaunchKernelGGL(k_best_fit, dim3(1), dim3(kIcpThreads), 0, s, src, tgt, n, Rt);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ LineFilter ---
+
+__device__ __forceinline__ int64_t reflect_idx(int64_t i, int64_t n) {
+    const int64_t p = 2 * n;
+    int64_t k = i % p;
+    if (k < 0) k += p;
+    return (k < n) ? k : p - 1 - k;
+}
+
+// scipy correlate1d, symmetric kernel branch, mode='reflect' (ni_filters.c
+// order: centre tap first, then (x[i-k] + x[i+k]) * w for k = r..1).
+__global__ __launch_bounds__(kBlock) void k_line_filter(const double *in, int32_t n,
+                                                        const double *taps, int32_t r,
+                                                        double *out) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= 2 * (int64_t)n) return;
+    const int64_t i = e >> 1;
+    const int col = (int)(e & 1);
+    double acc = in[reflect_idx(i, n) * 2 + col] * taps[r];
+    for (int jj = -r; jj < 0; ++jj)
+        acc += (in[reflect_idx(i + jj, n) * 2 + col] + in[reflect_idx(i - jj, n) * 2 + col]) * taps[r + jj];
+    out[e] = acc;
+}
+
+hipError_t launch_line_filter(const double *in, int32_t n, const double *taps, int32_t r,
+                              double *out, hipStream_t s) {
+    const unsigned g = (unsigned)((2 * (int64_t)n + kBlock - 1) / kBlock);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_line_filter, dim3(g), dim3(kBlock), 0, s, in, n, taps, r, out);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------- mahalanobis ---
+__global__ __launch_bounds__(kBlock) void k_mahalanobis(const double *a, const double *b,
+                                                        const double *cov, int32_t K, double *out,
+                                                        int32_t *singular) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= K) return;
+    M2 I;
+    if (!inv2(M2{cov[4 * k], cov[4 * k + 1], cov[4 * k + 2], cov[4 * k + 3]}, I)) {
+        atomicOr(singular, 1);
+        out[k] = NAN;
+        return;
+    }
+    out[k] = sqrt(quad(I, b[2 * k] - a[2 * k], b[2 * k + 1] - a[2 * k + 1]));
+}
+
+hipError_t launch_mahalanobis(const double *a, const double *b, const double *cov, int32_t K,
+                              double *out, int32_t *singular, hipStream_t s) {
+    const unsigned g = (unsigned)((K + kBlock - 1) / kBlock);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mahalanobis, dim3(g), dim3(kBlock), 0, s, a, b, cov, K, out, singular);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------- associate ---
+// One wave walks the list 64 landmarks at a time; the first match (or the
+// first singular covariance, where the reference raises) in list order wins.
+__global__ __launch_bounds__(64) void k_associate(const double *obs, const double *lm, int32_t L,
+                                                  double gate2, int32_t *out) {
+    const int lane = threadIdx.x;
+    const double ox = obs[0], oy = obs[1];
+    for (int base = 0; base < L; base += 64) {
+        const int j = base + lane;
+        bool match = false, sing = false;
+        if (j < L) {
+            const double *s = lm + (int64_t)j * 6;
+            M2 I;
+            if (!inv2(M2{s[2], s[3], s[4], s[5]}, I)) {
+                sing = true;
+            } else {
+                const double q = quad(I, ox - s[0], oy - s[1]);
+                match = q >= 0.0 && q < gate2;
+            }
+        }
+        const unsigned long long ev = __ballot(match || sing);
+        if (ev) {
+            const int first = __ffsll((long long)ev) - 1;
+            if (lane == first) out[0] = sing ? -2 : j;
+            return;
+        }
+    }
+    if (lane == 0) out[0] = -1;
+}
+
+hipError_t launch_associate(const double *obs, const double *lm, int32_t L, double gate2,
+                            int32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_associate, dim3(1), dim3(64), 0, s, obs, lm, L, gate2, out);
+    return hipGetLastError();
+}
+
+}  // namespace fs2

@@ -11,11 +11,15 @@ constexpr int kBlock = 256;          // 4 waves of 64
 constexpr int kPageSlots = 64;       // landmark slots per page
 constexpr int kMaxPages = 64;        // 4096 slots per particle max
 constexpr int kMaxM = 4;             // measurements fused into one map pass
-// 16-byte planes per slot: (x,y) (P00,P01) (P10,P11) as double2, then the
-// fp32 gate mirror (x, y, s, 0) as float4 -- see k_update.
-constexpr int kPlanes = 4;
-constexpr int kMirrorPlane = 3;
-constexpr int kGroup = 4;            // map slots whose mirrors one lane loads per step
+constexpr int kGroup = 4;            // slots whose mirrors a lane loads per step (64 B)
+
+// A page holds 64 slots of ONE particle's map, contiguous:
+//   [0, 1024)     64 x float4 gate mirror (x, y, s, 0)     -- read every scan
+//   [1024, 4096)  64 x 48 B fp64 slot (x, y, P00, P01, P10, P11) -- read on candidates
+// Arena k holds page k (slots 64k .. 64k+63) of every physical map.
+constexpr int kPageBytes = 4096;
+constexpr int kMirrorBytes = 1024;
+constexpr int kSlotBytes = 48;
 
 // Device statistics of one scan (zeroed before every scan).
 struct DevStats {
@@ -29,7 +33,7 @@ struct DevStats {
     int32_t resampled;
     int32_t max_count;
     int32_t error_flags;
-    int32_t pad;
+    int32_t n_copies;        // maps copied by the resample (duplicated particles)
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
 };
 
@@ -39,10 +43,11 @@ struct MeasPack {
     float fe[kMaxM];              // >= |ox - fx|, |oy - fy| (rounded up)
 };
 
+// Logical particle m's map lives in physical map phys[m]; resampling
+// re-points phys instead of moving most maps.
 struct MapRef {
-    char *const *pages;      // device array of page base pointers
-    int64_t n;               // particles per plane (local)
-    __host__ __device__ int64_t slot_stride() const { return (int64_t)kPlanes * 16 * n; }
+    char *const *arenas;     // device array: arena k = page k of every physical map
+    const int32_t *phys;     // logical -> physical map
 };
 
 struct UpdateParams {
@@ -95,14 +100,22 @@ struct ResampleParams {
     int64_t n;
     double *w;               // normalised weights (current)
     double *c;               // prefix workspace [n]
-    double *bsum;            // block sums
-    int32_t nblk;
-    int32_t *src;            // [n]
+    double *bsum;            // block sums (prefix)
+    int32_t nblk;            // prefix blocks
+    int32_t *src;            // [n] source of each output
     const double *x, *y, *yaw;
     const int32_t *cnt;
     double *ox, *oy, *oyaw, *ow;
     int32_t *ocnt;
-    MapRef in, out;
+    char *const *arenas;
+    const int32_t *phys;     // current logical -> physical
+    int32_t *ophys;          // next logical -> physical
+    int32_t *used;           // [n] particle is a source
+    int32_t *rank_d;         // [n] rank among dropped particles
+    int32_t *rank_e;         // [n] rank among extra outputs
+    int32_t *iblk;           // [2 * nb] per-block counts -> offsets
+    int32_t *freelist;       // [n] physical maps of dropped particles
+    int32_t *tasks;          // [n] extra outputs to copy
     double *part_best_w;
     int64_t *part_best_i;
     DevStats *stats;
@@ -113,8 +126,7 @@ hipError_t launch_update(const UpdateParams &p, hipStream_t s);
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s);
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s);
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s);
-hipError_t launch_resample(const ResampleParams &p, int sequential, int32_t cap, hipStream_t s);
-hipError_t launch_estimate_noresample(const ReduceParams &p, hipStream_t s);
+hipError_t launch_resample(const ResampleParams &p, int sequential, hipStream_t s);
 
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, int32_t *cnt,
@@ -122,10 +134,11 @@ hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t 
 hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm_cap,
                          MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s);
+hipError_t launch_iota(int32_t *p, int64_t n, hipStream_t s);
 
 hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt,
                       int32_t n_tgt, int32_t max_iter, double thr, double *R, double *t,
-                      int32_t *iters, double *scratch, hipStream_t s);
+                      int32_t *iters, hipStream_t s);
 hipError_t launch_best_fit(const double *src, const double *tgt, int32_t n, double *Rt,
                            hipStream_t s);
 hipError_t launch_line_filter(const double *in, int32_t n, const double *taps, int32_t r,

@@ -1,21 +1,21 @@
-// fs2_kernels.hip -- CDNA4 (gfx950) kernels of the FastSLAM 2.0 particle update.
+// fs2_update.hip -- CDNA4 (gfx950) kernels of the FastSLAM 2.0 particle update
+// (reference fast_slam_2/algorithms/fast_slam_2.py:33-223).
 //
-// Layout in HBM: particle SoA x/y/yaw/w (fp64) + cnt (int32);
-// landmark maps in pages of 64 slots, each slot three double2 planes over the
-// particles -- plane 0 (x, y), plane 1 (P00, P01), plane 2 (P10, P11) -- so a
-// wave reading one slot of 64 consecutive particles issues three fully
-// coalesced 1 KiB loads.
+// Layout in HBM (see fs2_kernels.hpp and DESIGN.md):
+//   particle scalars x/y/yaw/w (fp64) and cnt (int32) in logical particle order;
+//   landmark maps in 4 KiB pages, one page = 64 slots of ONE particle
+//   (1 KiB of fp32 gate mirrors, then 3 KiB of fp64 slots); arena k holds page
+//   k of every physical map; logical particle m owns physical map phys[m].
 //
 // Kernels
-//   k_update      fused move + association + EKF/append + likelihood, ONE pass
-//                 over each particle's map for up to kMaxM measurements
-//                 (fast_slam_2.py:33-159);
-//   k_wsum        weight total (fast_slam_2.py:166);
-//   k_normalize   normalise + per-block sum w'^2 / argmax / max count (:161-175);
-//   k_finalize    N_eff, resample decision, estimate, u0 (:60-67, :201-223);
-//   k_scan_*, k_resample_src, k_gather_*, k_estimate   low-variance resample (:177-199);
-//   k_icp         one workgroup per alignment (icp.py:13-90);
-//   k_line_filter, k_associate, k_import/k_export.
+//   k_update        fused move + association + EKF/append + likelihood, one pass
+//                   over each particle's map for up to kMaxM measurements;
+//   k_wsum          weight total (fast_slam_2.py:166);
+//   k_normalize     normalise + per-block sum w'^2 / argmax / max count (:161-175);
+//   k_finalize      N_eff, resample decision, estimate, u0 (:60-67, :201-223);
+//   k_scan_*, k_resample_src, k_plan_*, k_copy_maps, k_gather_particles,
+//   k_estimate      low-variance resample (:177-199);
+//   k_import/k_export, k_fill, k_iota.
 #include "fs2_device.hpp"
 #include "fs2_kernels.hpp"
 
@@ -116,28 +116,29 @@ __device__ int block_max_i(int v, int *lds) {
 
 // ------------------------------------------------------------- map access ---
 
-__device__ __forceinline__ const double2 *slot_planes(const MapRef &m, int j) {
-    return reinterpret_cast<const double2 *>(m.pages[j >> 6] +
-                                             (int64_t)(j & (kPageSlots - 1)) * m.slot_stride());
+// Page of slot j of physical map p.  Slots 4g..4g+3 never straddle a page.
+__device__ __forceinline__ char *page_of(char *const *arenas, int j, int32_t p) {
+    return arenas[j >> 6] + (int64_t)p * kPageBytes;
 }
 
-__device__ __forceinline__ Slot load_slot(const MapRef &m, int j, int64_t i) {
-    const double2 *p = slot_planes(m, j);
-    const double2 a = p[i], b = p[m.n + i], c = p[2 * m.n + i];
+__device__ __forceinline__ float4 load_mirror(const char *page, int j) {
+    return reinterpret_cast<const float4 *>(page)[j & (kPageSlots - 1)];
+}
+
+__device__ __forceinline__ Slot load_slot(const char *page, int j) {
+    const double2 *q =
+        reinterpret_cast<const double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
+    const double2 a = q[0], b = q[1], c = q[2];
     return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
 }
 
-__device__ __forceinline__ float4 load_mirror(const MapRef &m, int j, int64_t i) {
-    return reinterpret_cast<const float4 *>(slot_planes(m, j) + kMirrorPlane * m.n)[i];
-}
-
 // Every slot write keeps the fp32 gate mirror in step with the fp64 slot.
-__device__ __forceinline__ void store_slot(const MapRef &m, int j, int64_t i, const Slot &s) {
-    double2 *p = const_cast<double2 *>(slot_planes(m, j));
-    p[i] = make_double2(s.mx, s.my);
-    p[m.n + i] = make_double2(s.P.a00, s.P.a01);
-    p[2 * m.n + i] = make_double2(s.P.a10, s.P.a11);
-    reinterpret_cast<float4 *>(p + kMirrorPlane * m.n)[i] = mirror_of(s);
+__device__ __forceinline__ void store_slot(char *page, int j, const Slot &s) {
+    double2 *q = reinterpret_cast<double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
+    q[0] = make_double2(s.mx, s.my);
+    q[1] = make_double2(s.P.a00, s.P.a01);
+    q[2] = make_double2(s.P.a10, s.P.a11);
+    reinterpret_cast<float4 *>(page)[j & (kPageSlots - 1)] = mirror_of(s);
 }
 
 // Gate decisions this close to the threshold could depend on ulp-level
@@ -157,6 +158,11 @@ __device__ __forceinline__ unsigned ambiguous(double q, double gate2) {
 // reading each slot once instead of M times.  Slots appended in this scan are
 // resolved afterwards in measurement order.  Likelihoods multiply into the
 // weight in measurement order, as the reference does.
+//
+// The walk reads only the 16-byte fp32 gate mirrors (64 contiguous bytes per
+// lane and group of 4 slots; the next group is in flight while the current
+// one is tested); a slot the mirror cannot rule out for every pending
+// measurement takes the exact fp64 path (see mirror_of / gate_reject).
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ double lds_d[kBlock / 64];
@@ -177,13 +183,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     double px = 0.0, py = 0.0, pyaw = 0.0, w = 0.0;
     int c = 0;
+    int32_t pm = 0;
     if (live) {
         px = P.x[i];
         py = P.y[i];
         pyaw = P.yaw[i];
         w = P.w[i];
         c = P.cnt[i];
+        pm = P.map.phys[i];
     }
+    const int64_t pbase = (int64_t)pm * kPageBytes;
+    char *const *arenas = P.map.arenas;
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
         const double nz = P.noise ? P.noise[i]
@@ -203,34 +213,42 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     const M2 R{P.R[0], P.R[1], P.R[2], P.R[3]};
     unsigned pend = live ? ((1u << P.m) - 1u) : 0u;
-    unsigned visited = 0, written = 0, amb = 0, appends = 0;
+    unsigned visited = 0, candidates = 0, written = 0, amb = 0, appends = 0;
     bool singular = false;
     const double gate2 = P.gate2;
+    const bool filter = P.filter != 0;
 
     // ---- single pass over the existing map (association + EKF) ----
-    // Steps of kGroup slots: the fp32 mirrors of the whole group are loaded
-    // first (1 KiB per wave and slot, all in flight together); a slot whose
-    // mirror cannot rule out every still-pending measurement becomes a
-    // candidate and takes the exact fp64 path, in slot order.
-    unsigned candidates = 0;
+    float4 cur[kGroup], nxt[kGroup];
+    if (filter) {
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u)
+            if (pend != 0u && u < c) cur[u] = load_mirror(arenas[0] + pbase, u);
+    }
     for (int j0 = 0;; j0 += kGroup) {
         if (!__any((pend != 0u) && (j0 < c))) break;
+        const char *page = arenas[j0 >> 6] + pbase;
         unsigned cmask = 0;
-        if (P.filter) {
-            float4 mir[kGroup];
+        if (filter) {
+            // next group in flight while this one is tested
+            const int j1 = j0 + kGroup;
+            const char *npage = arenas[j1 >> 6] + pbase;
 #pragma unroll
             for (int u = 0; u < kGroup; ++u)
-                if (pend != 0u && j0 + u < c) mir[u] = load_mirror(P.map, j0 + u, i);
+                if (pend != 0u && j1 + u < c) nxt[u] = load_mirror(npage, j1 + u);
 #pragma unroll
             for (int u = 0; u < kGroup; ++u) {
                 if (pend != 0u && j0 + u < c) {
                     ++visited;
+                    const float4 mv = cur[u];
+                    const float cx = fabsf(mv.x) * 2.3841858e-7f;   // 2^-22 |x_lm|
+                    const float cy = fabsf(mv.y) * 2.3841858e-7f;
                     bool cand = false;
 #pragma unroll
                     for (int k = 0; k < MAXM; ++k)
                         if ((pend >> k) & 1u)
-                            cand |= !gate_reject(mir[u], P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
-                                                 P.gate2f);
+                            cand |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k],
+                                                      P.meas.fe[k], P.gate2f);
                     if (cand) cmask |= 1u << u;
                 }
             }
@@ -246,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             const int j = j0 + __builtin_ctz(cmask);
             cmask &= cmask - 1u;
             if (pend == 0u) break;
-            Slot s = load_slot(P.map, j, i);
+            Slot s = load_slot(page, j);
             ++candidates;
             bool mod = false;
             M2 I;
@@ -277,9 +295,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 if (!ok) todo = 0u;
             }
             if (mod) {
-                store_slot(P.map, j, i, s);
+                store_slot(const_cast<char *>(page), j, s);
                 ++written;
             }
+        }
+        if (filter) {
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) cur[u] = nxt[u];
         }
     }
 
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         const Meas mk = s_ms[k];
         int hit = -1;
         for (int a = 0; a < nap; ++a) {
-            const Slot s = load_slot(P.map, c + a, i);
+            const Slot s = load_slot(page_of(arenas, c + a, pm), c + a);
             ++candidates;
             M2 I;
             if (!inv2(s.P, I)) {
@@ -306,15 +328,16 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             }
         }
         if (hit >= 0) {
-            Slot s = load_slot(P.map, c + hit, i);
+            char *pg = page_of(arenas, c + hit, pm);
+            Slot s = load_slot(pg, c + hit);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
-            store_slot(P.map, c + hit, i, s);
+            store_slot(pg, c + hit, s);
             s_idx[k][tid] = c + hit;
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
             const Slot s{px + mk.d * cos(pyaw + mk.b), py + mk.d * sin(pyaw + mk.b),
                          M2{P.init_cov[0], P.init_cov[1], P.init_cov[2], P.init_cov[3]}};
-            store_slot(P.map, c + nap, i, s);
+            store_slot(page_of(arenas, c + nap, pm), c + nap, s);
             s_idx[k][tid] = -1;
             ++nap;
             ++appends;
@@ -400,7 +423,6 @@ __device__ double pairwise_sq(const double *a, int64_t n) {
         for (; i < n; ++i) res += a[i] * a[i];
         return res;
     }
-    // iterative split (numpy recursion), at most log2(8192/128)+1 levels deep
     int64_t n2 = n / 2;
     n2 -= n2 % 8;
     return pairwise_sq(a, n2) + pairwise_sq(a + n2, n - n2);
@@ -516,6 +538,14 @@ hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
 }
 
 // -------------------------------------------------------------- resample ---
+//
+// Systematic resampling keeps the logical order of the reference (output m is
+// a deep copy of particle src(m), fast_slam_2.py:188-199) but moves maps only
+// where it must: the first copy of each source keeps the source's physical
+// map; every further copy takes over the map of a particle that was not
+// selected and has it overwritten with the source's landmarks.  Copies are as
+// many as dropped particles (about a third of N at N_eff = N/2), and a source
+// map is never a copy destination, so no double buffer is needed.
 
 constexpr int kScanPer = 4;                       // elements per thread
 constexpr int kScanBlock = kBlock * kScanPer;     // 1024 elements per block
@@ -534,6 +564,16 @@ __device__ __forceinline__ double wave_incl_scan(double v) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const double t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan_i(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
         if (lane >= o) v += t;
     }
     return v;
@@ -583,7 +623,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_add(const ResampleParams P) {
 }
 
 // src(m) = smallest i with prefix c_i >= u_m, else N-1 (fast_slam_2.py:188-196,
-// without the reference's hang when u_m exceeds every reachable sum, Q10).
+// without the reference's hang when u_m exceeds every reachable sum, Q10);
+// marks every selected particle.
 __global__ __launch_bounds__(kBlock) void k_resample_src(const ResampleParams P) {
     if (!P.stats->resampled) return;
     const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -595,7 +636,117 @@ __global__ __launch_bounds__(kBlock) void k_resample_src(const ResampleParams P)
         if (P.c[mid] >= u) hi = mid;
         else lo = mid + 1;
     }
-    P.src[m] = (lo < P.n) ? (int32_t)lo : (int32_t)(P.n - 1);
+    const int32_t s = (lo < P.n) ? (int32_t)lo : (int32_t)(P.n - 1);
+    P.src[m] = s;
+    P.used[s] = 1;
+}
+
+// Ranks of dropped particles (!used) and of extra outputs (src[m] == src[m-1]):
+// block-local exclusive ranks plus per-block totals.
+__global__ __launch_bounds__(kBlock) void k_plan_local(const ResampleParams P) {
+    __shared__ int lds[2][kBlock / 64];
+    if (!P.stats->resampled) return;
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+    int dflag[kScanPer], eflag[kScanPer];
+    int dsum = 0, esum = 0;
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+        const int64_t t = base + e;
+        dflag[e] = (t < P.n && !P.used[t]) ? 1 : 0;
+        eflag[e] = (t < P.n && t > 0 && P.src[t] == P.src[t - 1]) ? 1 : 0;
+        dsum += dflag[e];
+        esum += eflag[e];
+    }
+    const int di = wave_incl_scan_i(dsum), ei = wave_incl_scan_i(esum);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) {
+        lds[0][wid] = di;
+        lds[1][wid] = ei;
+    }
+    __syncthreads();
+    int doff = di - dsum, eoff = ei - esum;
+    for (int k = 0; k < wid; ++k) {
+        doff += lds[0][k];
+        eoff += lds[1][k];
+    }
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+        const int64_t t = base + e;
+        if (t < P.n) {
+            P.rank_d[t] = doff;
+            P.rank_e[t] = eoff;
+        }
+        doff += dflag[e];
+        eoff += eflag[e];
+    }
+    if (threadIdx.x == kBlock - 1) {
+        P.iblk[blockIdx.x] = doff;
+        P.iblk[P.nblk + blockIdx.x] = eoff;
+    }
+}
+
+__global__ __launch_bounds__(1) void k_plan_blocks(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    int dacc = 0, eacc = 0;
+    for (int b = 0; b < P.nblk; ++b) {
+        const int td = P.iblk[b], te = P.iblk[P.nblk + b];
+        P.iblk[b] = dacc;
+        P.iblk[P.nblk + b] = eacc;
+        dacc += td;
+        eacc += te;
+    }
+    P.stats->n_copies = eacc;   // == dacc: as many extra copies as dropped particles
+}
+
+// free list = physical maps of the dropped particles, in particle order
+__global__ __launch_bounds__(kBlock) void k_plan_free(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= P.n || P.used[t]) return;
+    P.freelist[P.iblk[t / kScanBlock] + P.rank_d[t]] = P.phys[t];
+}
+
+// next phys: first copy keeps the source's map, extra copies take free maps
+__global__ __launch_bounds__(kBlock) void k_plan_assign(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= P.n) return;
+    const int32_t s = P.src[m];
+    if (m > 0 && P.src[m - 1] == s) {
+        const int k = P.iblk[P.nblk + m / kScanBlock] + P.rank_e[m];
+        P.ophys[m] = P.freelist[k];
+        P.tasks[k] = (int32_t)m;
+    } else {
+        P.ophys[m] = P.phys[s];
+    }
+}
+
+// Copy the map of src(m) into the map of each extra output m: one workgroup
+// per copy, 16 B per lane, contiguous pages (fast_slam_2.py:196 deepcopy).
+constexpr int kCopyGrid = 4096;
+
+__global__ __launch_bounds__(kBlock) void k_copy_maps(const ResampleParams P) {
+    __shared__ unsigned long long lds_u[kBlock / 64];
+    if (!P.stats->resampled) return;
+    const int ncopy = P.stats->n_copies;
+    unsigned long long slots = 0;
+    for (int k = blockIdx.x; k < ncopy; k += gridDim.x) {
+        const int32_t m = P.tasks[k];
+        const int32_t s = P.src[m];
+        const int32_t from = P.phys[s], to = P.ophys[m];
+        const int cnt = P.cnt[s];
+        if (threadIdx.x == 0) slots += (unsigned long long)cnt;
+        for (int pg = 0; pg * kPageSlots < cnt; ++pg) {
+            const int ns = min(kPageSlots, cnt - pg * kPageSlots);
+            const int4 *sp = reinterpret_cast<const int4 *>(P.arenas[pg] + (int64_t)from * kPageBytes);
+            int4 *dp = reinterpret_cast<int4 *>(P.arenas[pg] + (int64_t)to * kPageBytes);
+            // mirrors: ns x 16 B at offset 0; fp64 slots: ns x 48 B at 1 KiB
+            for (int q = threadIdx.x; q < ns; q += kBlock) dp[q] = sp[q];
+            for (int q = threadIdx.x; q < 3 * ns; q += kBlock) dp[64 + q] = sp[64 + q];
+        }
+    }
+    const unsigned long long b = block_sum_u64<kBlock>(slots, lds_u);
+    if (threadIdx.x == 0 && b) atomicAdd(&P.stats->resample_slots, b);
 }
 
 __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParams P) {
@@ -623,37 +774,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     }
 }
 
-constexpr int kGatherSlots = 16;   // slots per thread in the map gather
-
-// Deep copy of the selected maps (fast_slam_2.py:196): blockIdx.y picks a
-// chunk of 16 slots, lanes run over output particles (coalesced writes; the
-// monotone src keeps reads nearly coalesced).
-__global__ __launch_bounds__(kBlock) void k_gather_maps(const ResampleParams P) {
-    __shared__ unsigned long long lds_u[kBlock / 64];
-    if (!P.stats->resampled) return;
-    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int j0 = blockIdx.y * kGatherSlots;
-    unsigned long long copied = 0;
-    if (m < P.n) {
-        const int32_t s = P.src[m];
-        const int cnt = P.cnt[s];
-        const int jend = min(cnt, j0 + kGatherSlots);
-        for (int j = j0; j < jend; ++j) {
-            const double2 *ip = slot_planes(P.in, j);
-            double2 *op = const_cast<double2 *>(slot_planes(P.out, j));
-            const double2 a = ip[s], b = ip[P.in.n + s], c = ip[2 * P.in.n + s];
-            const double2 g = ip[kMirrorPlane * P.in.n + s];   // gate mirror (16 B)
-            op[m] = a;
-            op[P.out.n + m] = b;
-            op[2 * P.out.n + m] = c;
-            op[kMirrorPlane * P.out.n + m] = g;
-            ++copied;
-        }
-    }
-    const unsigned long long bc = block_sum_u64<kBlock>(copied, lds_u);
-    if (threadIdx.x == 0 && bc) atomicAdd(&P.stats->resample_slots, bc);
-}
-
 __global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32_t nparts) {
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
@@ -672,7 +792,7 @@ __global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32
     }
 }
 
-hipError_t launch_resample(const ResampleParams &p, int sequential, int32_t cap, hipStream_t s) {
+hipError_t launch_resample(const ResampleParams &p, int sequential, hipStream_t s) {
     const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
     if (g == 0) return hipSuccess;
     if (sequential) {
@@ -683,16 +803,19 @@ hipError_t launch_resample(const ResampleParams &p, int sequential, int32_t cap,
         hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(kBlock), 0, s, p);
     }
     hipLaunchKernelGGL(k_resample_src, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_plan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_plan_blocks, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL(k_plan_free, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_plan_assign, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_copy_maps, dim3(kCopyGrid), dim3(kBlock), 0, s, p);
     hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
-    const unsigned gy = (unsigned)((cap + kGatherSlots - 1) / kGatherSlots);
-    if (gy) hipLaunchKernelGGL(k_gather_maps, dim3(g, gy), dim3(kBlock), 0, s, p);
     hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------ state import/export --
 
-// stage: [count][lm_cap][6] -> pages; cnt_stage: [count]
+// stage: [count][lm_cap][6] -> maps of logical particles first .. first+count-1
 __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const int32_t *cnt_stage,
                                                    int64_t first, int64_t count, int32_t lm_cap,
                                                    MapRef map, int32_t *cnt) {
@@ -705,7 +828,8 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         if (j == 0) cnt[first + p] = c;
         if (j >= c) continue;
         const double *s = stage + e * 6;
-        store_slot(map, j, first + p, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}});
+        store_slot(page_of(map.arenas, j, map.phys[first + p]), j,
+                   Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}});
     }
 }
 
@@ -717,7 +841,7 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
         const int64_t p = e / lm_cap;
         const int j = (int)(e % lm_cap);
         if (j >= cnt[first + p]) continue;
-        const Slot s = load_slot(map, j, first + p);
+        const Slot s = load_slot(page_of(map.arenas, j, map.phys[first + p]), j);
         double *d = stage + e * 6;
         d[0] = s.mx; d[1] = s.my;
         d[2] = s.P.a00; d[3] = s.P.a01; d[4] = s.P.a10; d[5] = s.P.a11;
@@ -754,261 +878,13 @@ hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------- ICP ---
-//
-// One workgroup per alignment; the target cloud and the moving source cloud
-// live in LDS for the whole loop; nearest neighbours by brute force with
-// broadcast LDS reads (every lane reads the same target point), lowest index
-// on exact ties; centroids / cross-covariance / mean distance by fixed-order
-// wave + LDS reductions; rotation by the closed-form 2-D Kabsch angle, which
-// equals the reference's SVD + reflection fix (icp.py:76-85).
-
-constexpr int kIcpMaxP = 1024;
-constexpr int kIcpThreads = 1024;
-
-template <int NT>
-__device__ void block_sum5(double v[5], double *lds) {
-#pragma unroll
-    for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 5; ++q) lds[q * 16 + wid] = v[q];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        double t = 0.0;
-#pragma unroll
-        for (int k = 0; k < NT / 64; ++k) t += lds[q * 16 + k];
-        v[q] = t;
-    }
+__global__ void k_iota(int32_t *p, int64_t n) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (int64_t e = t; e < n; e += (int64_t)gridDim.x * kBlock) p[e] = (int32_t)e;
 }
 
-__global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *src_all,
-                                                     const double *tgt_all, int32_t nt,
-                                                     int32_t max_iter, double thr, double *R_out,
-                                                     double *t_out, int32_t *iters_out) {
-    __shared__ double2 s_src[kIcpMaxP];
-    __shared__ double2 s_tgt[kIcpMaxP];
-    __shared__ int32_t s_nn[kIcpMaxP];
-    __shared__ double s_dist[kIcpMaxP];
-    __shared__ double red[5 * 16];
-    __shared__ double s_R[4], s_t[2];
-    __shared__ int s_stop;
-
-    const int b = blockIdx.x;
-    const double2 *src = reinterpret_cast<const double2 *>(src_all) + (int64_t)b * P;
-    const double2 *tgt = reinterpret_cast<const double2 *>(tgt_all) + (int64_t)b * nt;
-    for (int k = threadIdx.x; k < P; k += kIcpThreads) s_src[k] = src[k];
-    for (int k = threadIdx.x; k < nt; k += kIcpThreads) s_tgt[k] = tgt[k];
-    double Rt[4] = {1.0, 0.0, 0.0, 1.0}, tt[2] = {0.0, 0.0};
-    double prev = INFINITY;
-    int it = 0;
-    __syncthreads();
-    while (it < max_iter) {
-        ++it;
-        // nearest neighbours
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k];
-            double best = INFINITY;
-            int bj = 0;
-            for (int j = 0; j < nt; ++j) {
-                const double2 tp = s_tgt[j];
-                const double dx = sp.x - tp.x, dy = sp.y - tp.y;
-                const double d2 = dx * dx + dy * dy;
-                if (d2 < best) {
-                    best = d2;
-                    bj = j;
-                }
-            }
-            s_nn[k] = bj;
-            s_dist[k] = sqrt(best);
-        }
-        __syncthreads();
-        // centroids and mean distance
-        double v[5] = {0, 0, 0, 0, 0};
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k], tp = s_tgt[s_nn[k]];
-            v[0] += sp.x; v[1] += sp.y; v[2] += tp.x; v[3] += tp.y; v[4] += s_dist[k];
-        }
-        block_sum5<kIcpThreads>(v, red);
-        const double cs0 = v[0] / P, cs1 = v[1] / P, ct0 = v[2] / P, ct1 = v[3] / P;
-        const double mean = v[4] / P;
-        // cross-covariance of the centred sets (icp.py:73)
-        double h[5] = {0, 0, 0, 0, 0};
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k], tp = s_tgt[s_nn[k]];
-            const double a0 = sp.x - cs0, a1 = sp.y - cs1, b0 = tp.x - ct0, b1 = tp.y - ct1;
-            h[0] += a0 * b0; h[1] += a0 * b1; h[2] += a1 * b0; h[3] += a1 * b1;
-        }
-        block_sum5<kIcpThreads>(h, red);
-        if (threadIdx.x == 0) {
-            const double th = atan2(h[1] - h[2], h[0] + h[3]);
-            const double c = cos(th), s = sin(th);
-            const M2 Ri{c, -s, s, c};
-            const double t0 = ct0 - fma(Ri.a00, cs0, Ri.a01 * cs1);
-            const double t1 = ct1 - fma(Ri.a10, cs0, Ri.a11 * cs1);
-            s_R[0] = Ri.a00; s_R[1] = Ri.a01; s_R[2] = Ri.a10; s_R[3] = Ri.a11;
-            s_t[0] = t0; s_t[1] = t1;
-            s_stop = fabs(prev - mean) < thr ? 1 : 0;
-        }
-        __syncthreads();
-        const double r00 = s_R[0], r01 = s_R[1], r10 = s_R[2], r11 = s_R[3], t0 = s_t[0], t1 = s_t[1];
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k];
-            s_src[k] = make_double2(fma(sp.y, r01, sp.x * r00) + t0, fma(sp.y, r11, sp.x * r10) + t1);
-        }
-        const M2 Rn = mm2(M2{r00, r01, r10, r11}, M2{Rt[0], Rt[1], Rt[2], Rt[3]});
-        Rt[0] = Rn.a00; Rt[1] = Rn.a01; Rt[2] = Rn.a10; Rt[3] = Rn.a11;
-        const double nt0 = fma(r00, tt[0], r01 * tt[1]) + t0;
-        const double nt1 = fma(r10, tt[0], r11 * tt[1]) + t1;
-        tt[0] = nt0;
-        tt[1] = nt1;
-        const int stop = s_stop;
-        prev = mean;
-        __syncthreads();
-        if (stop) break;
-    }
-    if (threadIdx.x == 0) {
-        for (int q = 0; q < 4; ++q) R_out[b * 4 + q] = Rt[q];
-        t_out[b * 2] = tt[0];
-        t_out[b * 2 + 1] = tt[1];
-        if (iters_out) iters_out[b] = it;
-    }
-}
-
-hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt, int32_t n_tgt,
-                      int32_t max_iter, double thr, double *R, double *t, int32_t *iters,
-                      double *scratch, hipStream_t s) {
-    (void)scratch;
-    if (P > kIcpMaxP || n_tgt > kIcpMaxP) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_icp, dim3(B), dim3(kIcpThreads), 0, s, P, src, tgt, n_tgt, max_iter, thr,
-                       R, t, iters);
-    return hipGetLastError();
-}
-
-// best_fit_transform alone: Rt = [R00 R01 R10 R11 t0 t1]
-__global__ __launch_bounds__(kIcpThreads) void k_best_fit(const double *src_, const double *tgt_,
-                                                          int32_t P, double *Rt) {
-    __shared__ double red[5 * 16];
-    const double2 *src = reinterpret_cast<const double2 *>(src_);
-    const double2 *tgt = reinterpret_cast<const double2 *>(tgt_);
-    double v[5] = {0, 0, 0, 0, 0};
-    for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-        v[0] += src[k].x; v[1] += src[k].y; v[2] += tgt[k].x; v[3] += tgt[k].y;
-    }
-    block_sum5<kIcpThreads>(v, red);
-    const double cs0 = v[0] / P, cs1 = v[1] / P, ct0 = v[2] / P, ct1 = v[3] / P;
-    double h[5] = {0, 0, 0, 0, 0};
-    for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-        const double a0 = src[k].x - cs0, a1 = src[k].y - cs1, b0 = tgt[k].x - ct0, b1 = tgt[k].y - ct1;
-        h[0] += a0 * b0; h[1] += a0 * b1; h[2] += a1 * b0; h[3] += a1 * b1;
-    }
-    block_sum5<kIcpThreads>(h, red);
-    if (threadIdx.x == 0) {
-        const double th = atan2(h[1] - h[2], h[0] + h[3]);
-        const double c = cos(th), s = sin(th);
-        Rt[0] = c; Rt[1] = -s; Rt[2] = s; Rt[3] = c;
-        Rt[4] = ct0 - fma(c, cs0, -s * cs1);
-        Rt[5] = ct1 - fma(s, cs0, c * cs1);
-    }
-}
-
-hipError_t launch_best_fit(const double *src, const double *tgt, int32_t n, double *Rt, hipStream_t s) {
-    hipLaunchKernelGGL(k_best_fit, dim3(1), dim3(kIcpThreads), 0, s, src, tgt, n, Rt);
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------ LineFilter ---
-
-__device__ __forceinline__ int64_t reflect_idx(int64_t i, int64_t n) {
-    const int64_t p = 2 * n;
-    int64_t k = i % p;
-    if (k < 0) k += p;
-    return (k < n) ? k : p - 1 - k;
-}
-
-// scipy correlate1d, symmetric kernel branch, mode='reflect' (ni_filters.c
-// order: centre tap first, then (x[i-k] + x[i+k]) * w for k = r..1).
-__global__ __launch_bounds__(kBlock) void k_line_filter(const double *in, int32_t n,
-                                                        const double *taps, int32_t r,
-                                                        double *out) {
-    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (e >= 2 * (int64_t)n) return;
-    const int64_t i = e >> 1;
-    const int col = (int)(e & 1);
-    double acc = in[reflect_idx(i, n) * 2 + col] * taps[r];
-    for (int jj = -r; jj < 0; ++jj)
-        acc += (in[reflect_idx(i + jj, n) * 2 + col] + in[reflect_idx(i - jj, n) * 2 + col]) * taps[r + jj];
-    out[e] = acc;
-}
-
-hipError_t launch_line_filter(const double *in, int32_t n, const double *taps, int32_t r,
-                              double *out, hipStream_t s) {
-    const unsigned g = (unsigned)((2 * (int64_t)n + kBlock - 1) / kBlock);
-    if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_line_filter, dim3(g), dim3(kBlock), 0, s, in, n, taps, r, out);
-    return hipGetLastError();
-}
-
-// ----------------------------------------------------------- mahalanobis ---
-__global__ __launch_bounds__(kBlock) void k_mahalanobis(const double *a, const double *b,
-                                                        const double *cov, int32_t K, double *out,
-                                                        int32_t *singular) {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    if (k >= K) return;
-    M2 I;
-    if (!inv2(M2{cov[4 * k], cov[4 * k + 1], cov[4 * k + 2], cov[4 * k + 3]}, I)) {
-        atomicOr(singular, 1);
-        out[k] = NAN;
-        return;
-    }
-    out[k] = sqrt(quad(I, b[2 * k] - a[2 * k], b[2 * k + 1] - a[2 * k + 1]));
-}
-
-hipError_t launch_mahalanobis(const double *a, const double *b, const double *cov, int32_t K,
-                              double *out, int32_t *singular, hipStream_t s) {
-    const unsigned g = (unsigned)((K + kBlock - 1) / kBlock);
-    if (g == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mahalanobis, dim3(g), dim3(kBlock), 0, s, a, b, cov, K, out, singular);
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------- associate ---
-// One wave walks the list 64 landmarks at a time; the first match (or the
-// first singular covariance, where the reference raises) in list order wins.
-__global__ __launch_bounds__(64) void k_associate(const double *obs, const double *lm, int32_t L,
-                                                  double gate2, int32_t *out) {
-    const int lane = threadIdx.x;
-    const double ox = obs[0], oy = obs[1];
-    for (int base = 0; base < L; base += 64) {
-        const int j = base + lane;
-        bool match = false, sing = false;
-        if (j < L) {
-            const double *s = lm + (int64_t)j * 6;
-            M2 I;
-            if (!inv2(M2{s[2], s[3], s[4], s[5]}, I)) {
-                sing = true;
-            } else {
-                const double q = quad(I, ox - s[0], oy - s[1]);
-                match = q >= 0.0 && q < gate2;
-            }
-        }
-        const unsigned long long ev = __ballot(match || sing);
-        if (ev) {
-            const int first = __ffsll((long long)ev) - 1;
-            if (lane == first) out[0] = sing ? -2 : j;
-            return;
-        }
-    }
-    if (lane == 0) out[0] = -1;
-}
-
-hipError_t launch_associate(const double *obs, const double *lm, int32_t L, double gate2,
-                            int32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_associate, dim3(1), dim3(64), 0, s, obs, lm, L, gate2, out);
+hipError_t launch_iota(int32_t *p, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kBlock), 0, s, p, n);
     return hipGetLastError();
 }
 

@@ -265,7 +265,7 @@ def test_gate_filter_is_exact(fs):
         assert out[0][1].candidates < out[1][1].candidates
     s0, s1 = fl[0].get_state(lm_cap=L + 64), fl[1].get_state(lm_cap=L + 64)
     for a, b in zip(s0, s1):
-        assert np.array_equal(a, b)
+        assert np.array_equal(a, b, equal_nan=True)
     for f in fl:
         f.close()
 
