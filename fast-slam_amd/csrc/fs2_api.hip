@@ -70,14 +70,13 @@ struct fs2_handle {
     std::vector<char *> arenas;            // arena k: page k of every physical map
     char **arenas_dev = nullptr;
     int32_t *phys[2] = {};                 // logical -> physical map (A/B across resamples)
-    int32_t *used = nullptr, *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
+    int32_t *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
     int32_t *freelist = nullptr, *tasks = nullptr;
     int cap = 0, max_cap = 4096;
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
     int64_t *part_best_i = nullptr;
     int32_t *part_maxcnt = nullptr;
     double *cbuf = nullptr, *bsum = nullptr;
-    int32_t *src = nullptr;
     DevStats *stats_dev = nullptr, *stats_host = nullptr;
     double *noise_dev = nullptr, *noise_pin = nullptr, *u0_dev = nullptr, *u0_pin = nullptr;
     int32_t *assoc_dev = nullptr;
@@ -90,7 +89,15 @@ struct fs2_handle {
     bool profiling = false;
     ProfEvents ev;
     fs2_profile prof{};
-    fs2comm::Comm *comm = nullptr;
+    // sharding (world_size > 1)
+    fs2comm::Transport *tp = nullptr;
+    RankRecord *rec = nullptr, *recs = nullptr;     // this rank's record / all ranks'
+    double *totals = nullptr;                       // all ranks' weight totals
+    int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (records, slots) per peer
+    int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr, *kept = nullptr;
+    std::vector<char *> sendbuf, recvbuf;
+    std::vector<size_t> sendcap, recvcap;
+    int32_t n_recv = 0;                             // particles received by the last resample
 
     MapRef map() const { return MapRef{arenas_dev, phys[cur]}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
@@ -118,6 +125,80 @@ static int grow_pages(fs2_handle *h, int need_slots) {
     HIP_TRY(h, hipMemcpy(h->arenas_dev, h->arenas.data(), sizeof(char *) * h->arenas.size(),
                          hipMemcpyHostToDevice));
     h->cap = need_pages * kPageSlots;
+    return FS2_OK;
+}
+
+static int ensure_buf(fs2_handle *h, std::vector<char *> &bufs, std::vector<size_t> &caps, int p,
+                      size_t bytes) {
+    if (caps[p] >= bytes) return FS2_OK;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    hipFree(bufs[p]);
+    bufs[p] = nullptr;
+    caps[p] = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+    HIP_TRY(h, hipMalloc(&bufs[p], want));
+    caps[p] = want;
+    return FS2_OK;
+}
+
+// Sharded resample: pack the local particles whose output range reaches another
+// rank, agree on transfer sizes, move them with one grouped exchange and
+// describe what arrived to the apply kernels.
+static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
+    const int G = h->cfg.world_size, R = h->cfg.rank;
+    const int64_t N = h->n_global;
+    hipStream_t s = h->stream;
+    HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
+    HIP_TRY(h, hipStreamSynchronize(s));
+    const int64_t omin = h->stats_host->out_min, omax = h->stats_host->out_max;
+    std::vector<int64_t> row(2 * G, 0);
+    int32_t tot[2];
+    for (int p = 0; p < G; ++p) {
+        const int64_t pa = N * p / G, pb = N * (p + 1) / G;
+        if (p == R || omax < pa || omin >= pb) continue;
+        rs.pa = pa;
+        rs.pb = pb;
+        HIP_TRY(h, launch_pack_count(rs, s));
+        HIP_TRY(h, hipMemcpyAsync(tot, h->iblk + 2 * rs.nblk, sizeof tot, hipMemcpyDeviceToHost, s));
+        HIP_TRY(h, hipStreamSynchronize(s));
+        const int64_t K = tot[0], S = tot[1];
+        if (K == 0) continue;
+        int rc = ensure_buf(h, h->sendbuf, h->sendcap, p, (size_t)(K + S) * 64);
+        if (rc) return rc;
+        rs.shdr = reinterpret_cast<PackHeader *>(h->sendbuf[p]);
+        rs.spay = h->sendbuf[p] + K * 64;
+        HIP_TRY(h, launch_pack_write(rs, (int32_t)K, s));
+        row[2 * p] = K;
+        row[2 * p + 1] = S;
+    }
+    HIP_TRY(h, hipMemcpyAsync(h->xrow, row.data(), sizeof(int64_t) * 2 * G, hipMemcpyHostToDevice, s));
+    int rc = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 2 * G, s, &h->err);
+    if (rc) return rc;
+    std::vector<int64_t> mat(2 * G * G);
+    HIP_TRY(h, hipMemcpyAsync(mat.data(), h->xmat, sizeof(int64_t) * 2 * G * G, hipMemcpyDeviceToHost, s));
+    HIP_TRY(h, hipStreamSynchronize(s));
+    std::vector<fs2comm::Xfer> sends, recvs;
+    rs.npeers = 0;
+    int32_t kbase = 0;
+    for (int q = 0; q < G; ++q) {
+        if (q == R) continue;
+        if (row[2 * q])
+            sends.push_back({q, h->sendbuf[q], (size_t)(row[2 * q] + row[2 * q + 1]) * 64});
+        const int64_t K = mat[(size_t)q * 2 * G + 2 * R], S = mat[(size_t)q * 2 * G + 2 * R + 1];
+        if (!K) continue;
+        rc = ensure_buf(h, h->recvbuf, h->recvcap, q, (size_t)(K + S) * 64);
+        if (rc) return rc;
+        recvs.push_back({q, h->recvbuf[q], (size_t)(K + S) * 64});
+        RecvPeer &pp = rs.peers[rs.npeers++];
+        pp.hdr = reinterpret_cast<const PackHeader *>(h->recvbuf[q]);
+        pp.pay = h->recvbuf[q] + K * 64;
+        pp.K = (int32_t)K;
+        pp.kbase = kbase;
+        kbase += (int32_t)K;
+    }
+    rc = h->tp->exchange(sends, recvs, s, &h->err);
+    if (rc) return rc;
+    h->n_recv = kbase;
     return FS2_OK;
 }
 
@@ -162,17 +243,21 @@ static void free_handle(fs2_handle *h) {
     }
     for (char *p : h->arenas) hipFree(p);
     hipFree(h->arenas_dev);
-    hipFree(h->used); hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
+    hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
+    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src); hipFree(h->kept);
+    hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
+    for (char *b : h->sendbuf) hipFree(b);
+    for (char *b : h->recvbuf) hipFree(b);
     hipFree(h->freelist); hipFree(h->tasks);
     hipFree(h->wpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
-    hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum); hipFree(h->src);
+    hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
     if (h->stats_host) hipHostFree(h->stats_host);
     if (h->noise_pin) hipHostFree(h->noise_pin);
     if (h->u0_pin) hipHostFree(h->u0_pin);
     if (h->ev.ok)
         for (auto &e : h->ev.e) hipEventDestroy(e);
-    if (h->comm) fs2comm::destroy(h->comm);
+    delete h->tp;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -184,7 +269,9 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         return set_err(nullptr, FS2_ERR_ARG, "num_particles must be positive");
     if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size)
         return set_err(nullptr, FS2_ERR_ARG, "bad rank %d / world_size %d", cfg->rank, cfg->world_size);
-    if (cfg->num_particles > (int64_t)INT32_MAX * cfg->world_size)
+    if (cfg->world_size > kMaxRanks)
+        return set_err(nullptr, FS2_ERR_ARG, "world_size %d > %d", cfg->world_size, kMaxRanks);
+    if (cfg->num_particles > (int64_t)INT32_MAX)
         return set_err(nullptr, FS2_ERR_ARG, "too many particles per rank");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -224,10 +311,18 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= alloc((void **)&h->phys[s], n * 4) == hipSuccess;
     }
     ok &= alloc((void **)&h->arenas_dev, sizeof(char *) * kMaxPages) == hipSuccess;
-    ok &= alloc((void **)&h->used, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->mlo, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->out_src, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->kept, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
+    ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
+    ok &= alloc((void **)&h->totals, sizeof(double) * G) == hipSuccess;
+    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * 2 * G) == hipSuccess;
+    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 2 * G * G) == hipSuccess;
     ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->iblk, 2 * nsb * 4) == hipSuccess;
+    ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 4) == hipSuccess;
     ok &= alloc((void **)&h->freelist, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->tasks, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
@@ -237,7 +332,6 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->part_maxcnt, nb * 4) == hipSuccess;
     ok &= alloc((void **)&h->cbuf, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->bsum, nsb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->src, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->stats_dev, sizeof(DevStats)) == hipSuccess;
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
@@ -257,8 +351,14 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     }
     int rc = grow_pages(h, std::max(cfg->landmark_capacity, 1));
     if (rc) return fail(rc);
+    h->sendbuf.assign(G, nullptr);
+    h->recvbuf.assign(G, nullptr);
+    h->sendcap.assign(G, 0);
+    h->recvcap.assign(G, 0);
     if (G > 1) {
-        rc = fs2comm::create(cfg->comm_id, (int)G, (int)r, &h->comm, &h->err);
+        rc = (cfg->comm_mode == FS2_COMM_LOCAL)
+                 ? fs2comm::create_local(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
+                 : fs2comm::create_rccl(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err);
         if (rc) return fail(rc);
     }
     if (hipStreamSynchronize(h->stream) != hipSuccess)
@@ -310,7 +410,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     if (rc) return rc;
     const int cur = h->cur;
     hipStream_t s = h->stream;
-    const bool seq = h->sequential();
+    const int G = h->cfg.world_size;
+    const bool seq = h->sequential() && G == 1;   // sharded sums are parallel by nature
     const bool prof = h->profiling;
 
     if (noise) {
@@ -410,26 +511,30 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
     rp.stats = h->stats_dev;
-    HIP_TRY(h, launch_wsum(rp, s));
-    HIP_TRY(h, launch_normalize(rp, s));
-    HIP_TRY(h, launch_finalize(rp, s));
-    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[2], s));
+    rp.world = G;
+    rp.rank = h->cfg.rank;
+    rp.rec = h->rec;
+    rp.recs = (G > 1) ? h->recs : h->rec;
+    rp.totals = h->totals;
 
-    // ---- low-variance resample (kernels exit unless the rule fired) ----
     const int nxt = 1 - cur;
     ResampleParams rs{};
     rs.n = h->n;
+    rs.N = h->n_global;
+    rs.a = h->first;
     rs.w = h->w[cur];
     rs.c = h->cbuf;
     rs.bsum = h->bsum;
     rs.nblk = (int32_t)((h->n + 1023) / 1024);
-    rs.src = h->src;
+    rs.mlo = h->mlo;
+    rs.mhi = h->mhi;
+    rs.out_src = h->out_src;
+    rs.kept = h->kept;
     rs.x = h->x[cur]; rs.y = h->y[cur]; rs.yaw = h->yaw[cur]; rs.cnt = h->cnt[cur];
     rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
     rs.arenas = h->arenas_dev;
     rs.phys = h->phys[cur];
     rs.ophys = h->phys[nxt];
-    rs.used = h->used;
     rs.rank_d = h->rank_d;
     rs.rank_e = h->rank_e;
     rs.iblk = h->iblk;
@@ -438,8 +543,49 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.part_best_w = h->part_best_w;
     rs.part_best_i = h->part_best_i;
     rs.stats = h->stats_dev;
-    HIP_TRY(h, hipMemsetAsync(h->used, 0, sizeof(int32_t) * std::max<int64_t>(h->n, 1), s));
-    HIP_TRY(h, launch_resample(rs, seq ? 1 : 0, s));
+    rs.rec = h->rec;
+
+    // weight total over all ranks (fast_slam_2.py:166)
+    HIP_TRY(h, launch_wsum(rp, s));
+    if (G > 1) {
+        rc = h->tp->allgather(&h->stats_dev->total, h->totals, sizeof(double), s, &h->err);
+        if (rc) return rc;
+        HIP_TRY(h, launch_global_total(rp, s));
+    }
+    // normalise (:161-175), local prefix of the normalised weights, this rank's record
+    HIP_TRY(h, launch_normalize(rp, s));
+    HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    HIP_TRY(h, launch_finalize(rp, s));
+    if (G > 1) {
+        rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+        if (rc) return rc;
+    }
+    // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183)
+    HIP_TRY(h, launch_global_finalize(rp, s));
+    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[2], s));
+
+    // ---- low-variance resample (:177-199); on one GPU the kernels exit unless the
+    // rule fired, sharded ranks learn the decision first (sizes of the transfers) ----
+    bool run_resample = true;
+    if (G > 1) {
+        HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
+        HIP_TRY(h, hipStreamSynchronize(s));
+        run_resample = h->stats_host->resampled != 0;
+    }
+    if (run_resample) {
+        HIP_TRY(h, hipMemsetAsync(h->out_src, 0, sizeof(int32_t) * std::max<int64_t>(h->n, 1), s));
+        HIP_TRY(h, launch_resample_ranges(rs, s));
+        if (G > 1) {
+            rc = exchange_particles(h, rs);
+            if (rc) return rc;
+        }
+        HIP_TRY(h, launch_resample_apply(rs, s));
+        if (G > 1) {
+            rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+            if (rc) return rc;
+        }
+        HIP_TRY(h, launch_global_best(rp, s));
+    }
     if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[3], s));
 
     HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
@@ -480,7 +626,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         stats->max_count = st.max_count;
         stats->n_eff = st.n_eff;
         stats->total_weight = st.total;
-        stats->best_index = st.best_index + h->first;
+        stats->best_index = st.best_index;
         stats->slots_visited = st.visited;
         stats->candidates = st.candidates;
         stats->hits = st.hits;

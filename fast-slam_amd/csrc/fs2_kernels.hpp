@@ -35,6 +35,42 @@ struct DevStats {
     int32_t error_flags;
     int32_t n_copies;        // maps copied by the resample (duplicated particles)
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
+    double offset;           // global prefix of weights before this rank's first particle
+    double t_local;          // sum of this rank's normalised weights (last local prefix)
+    int32_t out_min, out_max;   // smallest / largest output index served by a local particle
+    int32_t n_recv;          // particles received from other ranks by the resample
+    int32_t pad2;
+};
+
+// Per-rank record all-gathered once per scan (and once more after a resample).
+struct RankRecord {
+    double sumsq;            // sum of normalised w^2 (local)
+    double best_w;
+    int64_t best_gidx;       // global index of the local first maximum
+    double pose[3];
+    double t_local;          // local normalised total (prefix end)
+    int32_t max_count;
+    int32_t pad;
+};
+
+// Header of a particle sent to another rank by the resample (64 B); its map
+// follows in the payload region as cnt x 16 B mirrors then cnt x 48 B slots.
+struct PackHeader {
+    int64_t gsrc;            // global index of the source particle
+    int32_t out_lo, out_hi;  // outputs it fills on the receiver (global, inclusive)
+    int32_t cnt;
+    int32_t soff;            // payload offset in slots within the sender's payload
+    double x, y, yaw, w;
+    int64_t pad;
+};
+
+constexpr int kMaxRanks = 16;
+
+struct RecvPeer {
+    const PackHeader *hdr;   // K headers
+    const char *pay;         // payload base
+    int32_t K;               // records from this peer
+    int32_t kbase;           // index of its first record among all received
 };
 
 struct MeasPack {
@@ -94,15 +130,24 @@ struct ReduceParams {
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
     uint64_t seed, scan;
     DevStats *stats;
+    RankRecord *rec;         // this rank's record (written by k_finalize)
+    const RankRecord *recs;  // all ranks' records (== rec when world == 1)
+    const double *totals;    // all ranks' weight totals (world > 1)
+    int32_t world, rank;
 };
 
+// Resample of a shard of n particles / n outputs starting at global index a.
 struct ResampleParams {
     int64_t n;
+    int64_t N;               // global particles
+    int64_t a;               // global index of local particle 0 (and of local output 0)
     double *w;               // normalised weights (current)
-    double *c;               // prefix workspace [n]
+    double *c;               // local inclusive prefix [n]
     double *bsum;            // block sums (prefix)
-    int32_t nblk;            // prefix blocks
-    int32_t *src;            // [n] source of each output
+    int32_t nblk;            // 1024-element blocks
+    int32_t *mlo, *mhi;      // [n] global output range served by each local particle
+    int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
+    int32_t *kept;           // [n] local particle feeds a local output (its map stays)
     const double *x, *y, *yaw;
     const int32_t *cnt;
     double *ox, *oy, *oyaw, *ow;
@@ -110,23 +155,38 @@ struct ResampleParams {
     char *const *arenas;
     const int32_t *phys;     // current logical -> physical
     int32_t *ophys;          // next logical -> physical
-    int32_t *used;           // [n] particle is a source
-    int32_t *rank_d;         // [n] rank among dropped particles
-    int32_t *rank_e;         // [n] rank among extra outputs
-    int32_t *iblk;           // [2 * nb] per-block counts -> offsets
-    int32_t *freelist;       // [n] physical maps of dropped particles
-    int32_t *tasks;          // [n] extra outputs to copy
+    int32_t *rank_d;         // [n] rank among dropped particles / packed records
+    int32_t *rank_e;         // [n] rank among extra outputs / packed slot offset
+    int32_t *iblk;           // [2 * nblk] per-block counts -> offsets
+    int32_t *freelist;       // [n] physical maps free for copies
+    int32_t *tasks;          // [n] outputs whose map is copied
     double *part_best_w;
     int64_t *part_best_i;
     DevStats *stats;
+    RankRecord *rec;         // this rank's post-resample estimate record
+    // packing for one destination rank [pa, pb)
+    int64_t pa, pb;
+    PackHeader *shdr;        // send headers
+    char *spay;              // send payload
+    // received particles
+    int32_t npeers;
+    RecvPeer peers[kMaxRanks];
 };
 
 // ---- launch wrappers (defined in fs2_kernels.hip) ----
 hipError_t launch_update(const UpdateParams &p, hipStream_t s);
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s);
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s);
+hipError_t launch_global_total(const ReduceParams &p, hipStream_t s);
+hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s);
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s);
-hipError_t launch_resample(const ResampleParams &p, int sequential, hipStream_t s);
+hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s);
+// resample, split where the sharded path needs the host (sizes of transfers)
+hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s);
+hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
+hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t s);
+hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s);
+hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, int32_t *cnt,

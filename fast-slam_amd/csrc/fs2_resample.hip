@@ -1,0 +1,623 @@
+// fs2_resample.hip -- N_eff / estimate / low-variance resampling on gfx950
+// (reference fast_slam_2/algorithms/fast_slam_2.py:57-67, 177-223), for one
+// GPU or for particles sharded over G ranks.
+//
+// Resample plan.  With the global inclusive prefix c of the normalised weights
+// and u_m = u0 + m * (1/N) (evaluated exactly as the reference writes it),
+// output m is a copy of the smallest particle i with c_i >= u_m (N-1 when u_m
+// exceeds every prefix: the reference would loop forever there).
+// Equivalently particle i fills the contiguous output range
+//     { m : c_{i-1} < u_m <= c_i }   (particle N-1 also every m with u_m > c_{N-2}),
+// which each rank computes for its own particles from its local prefix and the
+// offset O_r = sum of the normalised totals of the ranks before it.  Outputs
+// are owned by the rank holding the same global index, so a particle moves
+// between ranks only when its range crosses a shard boundary.
+//
+// Maps move only where they must: the first local output of a local source
+// keeps the source's map; every other output (extra copies, particles received
+// from another rank) takes over the map of a local particle that feeds no
+// local output, whose landmarks were already packed if another rank needs them.
+#include "fs2_reduce.hpp"
+
+namespace fs2 {
+
+constexpr int kScanPer = 4;                       // elements per thread
+constexpr int kScanBlock = kBlock * kScanPer;     // 1024 elements per block
+
+// ------------------------------------------------------- global reductions --
+
+// Weight total over ranks, in rank order (world > 1).
+__global__ void k_global_total(const ReduceParams P) {
+    double t = 0.0;
+    for (int g = 0; g < P.world; ++g) t = (g == 0) ? P.totals[0] : t + P.totals[g];
+    P.stats->total = t;
+}
+
+hipError_t launch_global_total(const ReduceParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_global_total, dim3(1), dim3(1), 0, s, p);
+    return hipGetLastError();
+}
+
+// numpy pairwise summation of w[i]^2 (loops_utils.h.src) for the sequential mode.
+__device__ double pairwise_sq(const double *a, int64_t n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int64_t i = 0; i < n; ++i) res += a[i] * a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = a[k] * a[k];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] += a[i + k] * a[i + k];
+        }
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i] * a[i];
+        return res;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return pairwise_sq(a, n2) + pairwise_sq(a + n2, n - n2);
+}
+
+// This rank's record: sum w'^2, first maximum, its pose, normalised total.
+__global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
+    __shared__ double lds_d[16];
+    __shared__ int64_t lds_l[16];
+    __shared__ int lds_i[16];
+    double sq = 0.0;
+    double bv = -INFINITY;
+    int64_t bi = INT64_MAX;
+    int mc = 0;
+    for (int k = threadIdx.x; k < P.nparts; k += 1024) {
+        sq += P.part_sq[k];
+        argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
+        mc = max(mc, P.part_maxcnt[k]);
+    }
+    sq = block_sum<1024>(sq, lds_d);
+    block_argmax<1024>(bv, bi, lds_d, lds_l);
+    mc = block_max_i<1024>(mc, lds_i);
+    if (threadIdx.x == 0) {
+        if (P.sequential) {
+            // np.sum(weights ** 2): pairwise inside 8192-element chunks
+            double s = 0.0;
+            for (int64_t k = 0; k < P.n; k += 8192) {
+                const int64_t m = (P.n - k < 8192) ? P.n - k : 8192;
+                const double p = pairwise_sq(P.w + k, m);
+                s = (k == 0) ? p : s + p;
+            }
+            sq = s;
+        }
+        RankRecord r{};
+        r.sumsq = sq;
+        r.best_w = bv;
+        r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.gidx0 + bi;
+        if (bi != INT64_MAX) {
+            r.pose[0] = P.x[bi];
+            r.pose[1] = P.y[bi];
+            r.pose[2] = P.yaw[bi];
+        }
+        r.t_local = P.stats->t_local;
+        r.max_count = mc;
+        *P.rec = r;
+    }
+}
+
+hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, p);
+    return hipGetLastError();
+}
+
+// N_eff (fast_slam_2.py:212-223), the N_eff < N/2 rule (:62), the estimate
+// (:201-210), u0 (:183) and this rank's prefix offset, from all records.
+__global__ void k_global_finalize(const ReduceParams P) {
+    DevStats *st = P.stats;
+    double sq = P.recs[0].sumsq;
+    double bv = P.recs[0].best_w;
+    int64_t bi = P.recs[0].best_gidx;
+    int gb = 0;
+    double off = 0.0;
+    for (int g = 1; g < P.world; ++g) {
+        sq = sq + P.recs[g].sumsq;
+        const double v = P.recs[g].best_w;
+        const int64_t i = P.recs[g].best_gidx;
+        if (v > bv || (v == bv && i < bi)) {
+            bv = v;
+            bi = i;
+            gb = g;
+        }
+    }
+    for (int g = 0; g < P.rank; ++g) off = (g == 0) ? P.recs[0].t_local : off + P.recs[g].t_local;
+    const double ng = (double)P.n_global;
+    const double ne = (sq < 1.0 / ng) ? ng : 1.0 / sq;
+    st->sumsq = sq;
+    st->n_eff = ne;
+    st->resampled = ne < ng / 2.0 ? 1 : 0;
+    st->max_count = max(st->max_count, P.recs[P.rank].max_count);
+    st->best_index = bi;
+    st->best_w = bv;
+    st->pose[0] = P.recs[gb].pose[0];
+    st->pose[1] = P.recs[gb].pose[1];
+    st->pose[2] = P.recs[gb].pose[2];
+    st->offset = off;
+    st->out_min = INT32_MAX;
+    st->out_max = -1;
+    st->u0 = P.u0_host ? *P.u0_host
+                       : (1.0 / ng) * philox_uniform01(P.seed, P.scan | (1ull << 63), 0);
+}
+
+hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_global_finalize, dim3(1), dim3(1), 0, s, p);
+    return hipGetLastError();
+}
+
+// Estimate after a resample: first maximum over all ranks' outputs.
+__global__ void k_global_best(const ReduceParams P) {
+    DevStats *st = P.stats;
+    if (!st->resampled) return;
+    double bv = P.recs[0].best_w;
+    int64_t bi = P.recs[0].best_gidx;
+    int gb = 0;
+    for (int g = 1; g < P.world; ++g) {
+        const double v = P.recs[g].best_w;
+        const int64_t i = P.recs[g].best_gidx;
+        if (v > bv || (v == bv && i < bi)) {
+            bv = v;
+            bi = i;
+            gb = g;
+        }
+    }
+    st->best_index = bi;
+    st->best_w = bv;
+    st->pose[0] = P.recs[gb].pose[0];
+    st->pose[1] = P.recs[gb].pose[1];
+    st->pose[2] = P.recs[gb].pose[2];
+}
+
+hipError_t launch_global_best(const ReduceParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_global_best, dim3(1), dim3(1), 0, s, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ local prefix --
+
+__device__ __forceinline__ double wave_incl_scan(double v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan_i(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// Sequential running sum, the reference's order (fast_slam_2.py:184-193).
+__global__ __launch_bounds__(1) void k_scan_seq(const ResampleParams P) {
+    double c = 0.0;
+    for (int64_t i = 0; i < P.n; ++i) {
+        c = (i == 0) ? P.w[0] : c + P.w[i];
+        P.c[i] = c;
+    }
+    P.stats->t_local = (P.n > 0) ? c : 0.0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_local(const ResampleParams P) {
+    __shared__ double lds[kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+    double v[kScanPer];
+    double run = 0.0;
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+        const int64_t i = base + e;
+        run += (i < P.n) ? P.w[i] : 0.0;
+        v[e] = run;
+    }
+    const double incl = wave_incl_scan(run);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) lds[wid] = incl;
+    __syncthreads();
+    double woff = 0.0;
+    for (int k = 0; k < wid; ++k) woff += lds[k];
+    const double off = woff + incl - run;
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+        const int64_t i = base + e;
+        if (i < P.n) P.c[i] = off + v[e];
+    }
+    if (threadIdx.x == kBlock - 1) P.bsum[blockIdx.x] = off + v[kScanPer - 1];
+}
+
+__global__ __launch_bounds__(1) void k_scan_blocks(const ResampleParams P) {
+    double acc = 0.0;
+    for (int b = 0; b < P.nblk; ++b) {
+        const double t = P.bsum[b];
+        P.bsum[b] = acc;    // exclusive offset
+        acc += t;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_add(const ResampleParams P) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < P.n) {
+        const double v = P.c[i] + P.bsum[i / kScanBlock];
+        P.c[i] = v;
+        if (i == P.n - 1) P.stats->t_local = v;
+    }
+}
+
+hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s) {
+    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
+    if (g == 0) return hipSuccess;
+    if (sequential) {
+        hipLaunchKernelGGL(k_scan_seq, dim3(1), dim3(1), 0, s, p);
+    } else {
+        hipLaunchKernelGGL(k_scan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1), 0, s, p);
+        hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(kBlock), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------- ranges --
+
+__device__ __forceinline__ double u_of(double u0, int64_t m, int64_t N) {
+    return u0 + (double)m * (1.0 / (double)N);      // fast_slam_2.py:189, as written
+}
+
+// first output m in [0, N] with u_m > v
+__device__ __forceinline__ int64_t first_above(double v, double u0, int64_t N) {
+    int64_t lo = 0, hi = N;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (u_of(u0, mid, N) > v) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P.n) return;
+    const double u0 = P.stats->u0, off = P.stats->offset;
+    const int64_t g = P.a + i;
+    const double cur = (P.a == 0) ? P.c[i] : off + P.c[i];
+    int64_t lo;
+    if (g == 0) lo = 0;
+    else {
+        const double prev = (i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1]);
+        lo = first_above(prev, u0, P.N);
+    }
+    const int64_t hi = (g == P.N - 1) ? P.N - 1 : first_above(cur, u0, P.N) - 1;
+    P.mlo[i] = (int32_t)lo;
+    P.mhi[i] = (int32_t)hi;
+    const int64_t llo = max(lo, P.a), lhi = min(hi, P.a + P.n - 1);
+    P.kept[i] = (llo <= lhi) ? 1 : 0;
+    for (int64_t m = llo; m <= lhi; ++m) P.out_src[m - P.a] = (int32_t)i;
+    if (lo <= hi) {
+        atomicMin(&P.stats->out_min, (int32_t)lo);
+        atomicMax(&P.stats->out_max, (int32_t)hi);
+    }
+}
+
+hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s) {
+    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
+    if (g == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ranges, dim3(g), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------- packing for another rank --
+
+// Block-local exclusive ranks of two 0/1-or-count streams and per-block totals.
+template <typename F>
+__device__ void rank2(const ResampleParams &P, F flags) {
+    __shared__ int lds[2][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+    int fa[kScanPer], fb[kScanPer];
+    int sa = 0, sb = 0;
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+        const int64_t t = base + e;
+        fa[e] = fb[e] = 0;
+        if (t < P.n) flags(t, fa[e], fb[e]);
+        sa += fa[e];
+        sb += fb[e];
+    }
+    const int ia = wave_incl_scan_i(sa), ib = wave_incl_scan_i(sb);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) {
+        lds[0][wid] = ia;
+        lds[1][wid] = ib;
+    }
+    __syncthreads();
+    int oa = ia - sa, ob = ib - sb;
+    for (int k = 0; k < wid; ++k) {
+        oa += lds[0][k];
+        ob += lds[1][k];
+    }
+#pragma unroll
+    for (int e = 0; e < kScanPer; ++e) {
+        const int64_t t = base + e;
+        if (t < P.n) {
+            P.rank_d[t] = oa;
+            P.rank_e[t] = ob;
+        }
+        oa += fa[e];
+        ob += fb[e];
+    }
+    if (threadIdx.x == kBlock - 1) {
+        P.iblk[blockIdx.x] = oa;
+        P.iblk[P.nblk + blockIdx.x] = ob;
+    }
+}
+
+// exclusive scan of the block totals; grand totals at iblk[2*nblk], iblk[2*nblk+1]
+__global__ __launch_bounds__(1) void k_rank_blocks(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    int a = 0, b = 0;
+    for (int k = 0; k < P.nblk; ++k) {
+        const int ta = P.iblk[k], tb = P.iblk[P.nblk + k];
+        P.iblk[k] = a;
+        P.iblk[P.nblk + k] = b;
+        a += ta;
+        b += tb;
+    }
+    P.iblk[2 * P.nblk] = a;
+    P.iblk[2 * P.nblk + 1] = b;
+}
+
+// particles whose output range meets [pa, pb): record rank and payload slot offset
+__global__ __launch_bounds__(kBlock) void k_pack_local(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    rank2(P, [&](int64_t i, int &fa, int &fb) {
+        const int64_t lo = P.mlo[i], hi = P.mhi[i];
+        if (lo <= hi && lo < P.pb && hi >= P.pa) {
+            fa = 1;
+            fb = P.cnt[i];
+        }
+    });
+}
+
+hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_pack_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_rank_blocks, dim3(1), dim3(1), 0, s, p);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P.n) return;
+    const int64_t lo = P.mlo[i], hi = P.mhi[i];
+    if (!(lo <= hi && lo < P.pb && hi >= P.pa)) return;
+    const int b = (int)(i / kScanBlock);
+    const int k = P.iblk[b] + P.rank_d[i];
+    PackHeader h{};
+    h.gsrc = P.a + i;
+    h.out_lo = (int32_t)max(lo, P.pa);
+    h.out_hi = (int32_t)min(hi, P.pb - 1);
+    h.cnt = P.cnt[i];
+    h.soff = P.iblk[P.nblk + b] + P.rank_e[i];
+    h.x = P.x[i];
+    h.y = P.y[i];
+    h.yaw = P.yaw[i];
+    h.w = P.w[i];
+    P.shdr[k] = h;
+}
+
+// one workgroup per record: page -> packed (cnt x 16 B mirrors, cnt x 48 B slots)
+__global__ __launch_bounds__(kBlock) void k_pack_payload(const ResampleParams P, int32_t nrec) {
+    if (!P.stats->resampled) return;
+    for (int k = blockIdx.x; k < nrec; k += gridDim.x) {
+        const PackHeader h = P.shdr[k];
+        const int32_t pm = P.phys[h.gsrc - P.a];
+        int4 *dm = reinterpret_cast<int4 *>(P.spay + (int64_t)h.soff * 64);
+        int4 *df = dm + h.cnt;
+        for (int q = threadIdx.x; q < h.cnt; q += kBlock) {
+            const int4 *pg = reinterpret_cast<const int4 *>(P.arenas[q >> 6] + (int64_t)pm * kPageBytes);
+            dm[q] = pg[q & 63];
+        }
+        for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
+            const int j = q / 3;
+            const int4 *pg = reinterpret_cast<const int4 *>(P.arenas[j >> 6] + (int64_t)pm * kPageBytes);
+            df[q] = pg[64 + (j & 63) * 3 + (q - 3 * j)];
+        }
+    }
+}
+
+hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t s) {
+    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_pack_headers, dim3(g), dim3(kBlock), 0, s, p);
+    if (nrec > 0)
+        hipLaunchKernelGGL(k_pack_payload, dim3(min(nrec, 2048)), dim3(kBlock), 0, s, p, nrec);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- apply ----
+
+__device__ __forceinline__ int peer_of(const ResampleParams &P, int k) {
+    int p = 0;
+    while (p + 1 < P.npeers && k >= P.peers[p + 1].kbase) ++p;
+    return p;
+}
+
+// outputs filled by received particles
+__global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P, int32_t nrecv) {
+    if (!P.stats->resampled) return;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nrecv) return;
+    const int p = peer_of(P, k);
+    const PackHeader &h = P.peers[p].hdr[k - P.peers[p].kbase];
+    for (int64_t m = h.out_lo; m <= h.out_hi; ++m) P.out_src[m - P.a] = -(k + 1);
+}
+
+// dropped (feeds no local output) / extra (any output but a local source's first)
+__global__ __launch_bounds__(kBlock) void k_plan_local(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    rank2(P, [&](int64_t t, int &fd, int &fe) {
+        fd = P.kept[t] ? 0 : 1;
+        const int32_t s = P.out_src[t];
+        const bool keeper = s >= 0 && (P.a + t) == max((int64_t)P.mlo[s], P.a);
+        fe = keeper ? 0 : 1;
+    });
+}
+
+__global__ __launch_bounds__(kBlock) void k_plan_free(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= P.n || P.kept[t]) return;
+    P.freelist[P.iblk[t / kScanBlock] + P.rank_d[t]] = P.phys[t];
+}
+
+__global__ __launch_bounds__(kBlock) void k_plan_assign(const ResampleParams P) {
+    if (!P.stats->resampled) return;
+    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= P.n) return;
+    const int32_t s = P.out_src[m];
+    const bool keeper = s >= 0 && (P.a + m) == max((int64_t)P.mlo[s], P.a);
+    if (keeper) {
+        P.ophys[m] = P.phys[s];
+    } else {
+        const int k = P.iblk[P.nblk + m / kScanBlock] + P.rank_e[m];
+        P.ophys[m] = P.freelist[k];
+        P.tasks[k] = (int32_t)m;
+    }
+    if (m == 0) P.stats->n_copies = P.iblk[2 * P.nblk + 1];
+}
+
+// Copy the source's map into the map of every non-keeper output: one
+// workgroup per copy, 16 B per lane (fast_slam_2.py:196 deepcopy).
+constexpr int kCopyGrid = 4096;
+
+__global__ __launch_bounds__(kBlock) void k_copy_maps(const ResampleParams P) {
+    __shared__ unsigned long long lds_u[kBlock / 64];
+    if (!P.stats->resampled) return;
+    const int ncopy = P.stats->n_copies;
+    unsigned long long slots = 0;
+    for (int k = blockIdx.x; k < ncopy; k += gridDim.x) {
+        const int32_t m = P.tasks[k];
+        const int32_t s = P.out_src[m];
+        const int32_t to = P.ophys[m];
+        if (s >= 0) {
+            const int32_t from = P.phys[s];
+            const int cnt = P.cnt[s];
+            if (threadIdx.x == 0) slots += (unsigned long long)cnt;
+            for (int pg = 0; pg * kPageSlots < cnt; ++pg) {
+                const int ns = min(kPageSlots, cnt - pg * kPageSlots);
+                const int4 *sp = reinterpret_cast<const int4 *>(P.arenas[pg] + (int64_t)from * kPageBytes);
+                int4 *dp = reinterpret_cast<int4 *>(P.arenas[pg] + (int64_t)to * kPageBytes);
+                for (int q = threadIdx.x; q < ns; q += kBlock) dp[q] = sp[q];
+                for (int q = threadIdx.x; q < 3 * ns; q += kBlock) dp[64 + q] = sp[64 + q];
+            }
+        } else {
+            const int r = -s - 1;
+            const int p = peer_of(P, r);
+            const PackHeader &h = P.peers[p].hdr[r - P.peers[p].kbase];
+            const int4 *sm = reinterpret_cast<const int4 *>(P.peers[p].pay + (int64_t)h.soff * 64);
+            const int4 *sf = sm + h.cnt;
+            if (threadIdx.x == 0) slots += (unsigned long long)h.cnt;
+            for (int q = threadIdx.x; q < h.cnt; q += kBlock) {
+                int4 *pg = reinterpret_cast<int4 *>(P.arenas[q >> 6] + (int64_t)to * kPageBytes);
+                pg[q & 63] = sm[q];
+            }
+            for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
+                const int j = q / 3;
+                int4 *pg = reinterpret_cast<int4 *>(P.arenas[j >> 6] + (int64_t)to * kPageBytes);
+                pg[64 + (j & 63) * 3 + (q - 3 * j)] = sf[q];
+            }
+        }
+    }
+    const unsigned long long b = block_sum_u64<kBlock>(slots, lds_u);
+    if (threadIdx.x == 0 && b) atomicAdd(&P.stats->resample_slots, b);
+}
+
+__global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParams P) {
+    __shared__ double lds_d[kBlock / 64];
+    __shared__ int64_t lds_l[kBlock / 64];
+    if (!P.stats->resampled) return;
+    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double bv = -INFINITY;
+    int64_t bi = INT64_MAX;
+    if (m < P.n) {
+        const int32_t s = P.out_src[m];
+        double w;
+        if (s >= 0) {
+            P.ox[m] = P.x[s];
+            P.oy[m] = P.y[s];
+            P.oyaw[m] = P.yaw[s];
+            w = P.w[s];
+            P.ocnt[m] = P.cnt[s];
+        } else {
+            const int r = -s - 1;
+            const int p = peer_of(P, r);
+            const PackHeader &h = P.peers[p].hdr[r - P.peers[p].kbase];
+            P.ox[m] = h.x;
+            P.oy[m] = h.y;
+            P.oyaw[m] = h.yaw;
+            w = h.w;
+            P.ocnt[m] = h.cnt;
+        }
+        P.ow[m] = w;
+        bv = w;
+        bi = m;
+    }
+    block_argmax<kBlock>(bv, bi, lds_d, lds_l);
+    if (threadIdx.x == 0) {
+        P.part_best_w[blockIdx.x] = bv;
+        P.part_best_i[blockIdx.x] = bi;
+    }
+}
+
+// this rank's first maximum over its outputs -> record (post-resample estimate)
+__global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32_t nparts) {
+    __shared__ double lds_d[16];
+    __shared__ int64_t lds_l[16];
+    if (!P.stats->resampled) return;
+    double bv = -INFINITY;
+    int64_t bi = INT64_MAX;
+    for (int k = threadIdx.x; k < nparts; k += 1024) argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
+    block_argmax<1024>(bv, bi, lds_d, lds_l);
+    if (threadIdx.x == 0) {
+        RankRecord r = *P.rec;
+        r.best_w = bv;
+        r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.a + bi;
+        if (bi != INT64_MAX) {
+            r.pose[0] = P.ox[bi];
+            r.pose[1] = P.oy[bi];
+            r.pose[2] = P.oyaw[bi];
+        }
+        *P.rec = r;
+    }
+}
+
+hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s) {
+    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
+    if (g == 0) return hipSuccess;
+    int32_t nrecv = 0;
+    for (int q = 0; q < p.npeers; ++q) nrecv += p.peers[q].K;
+    if (nrecv > 0)
+        hipLaunchKernelGGL(k_scatter_recv, dim3((nrecv + kBlock - 1) / kBlock), dim3(kBlock), 0, s, p, nrecv);
+    hipLaunchKernelGGL(k_plan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_rank_blocks, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL(k_plan_free, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_plan_assign, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_copy_maps, dim3(kCopyGrid), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
+    return hipGetLastError();
+}
+
+}  // namespace fs2

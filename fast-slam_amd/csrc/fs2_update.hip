@@ -16,136 +16,9 @@
 //   k_scan_*, k_resample_src, k_plan_*, k_copy_maps, k_gather_particles,
 //   k_estimate      low-variance resample (:177-199);
 //   k_import/k_export, k_fill, k_iota.
-#include "fs2_device.hpp"
-#include "fs2_kernels.hpp"
+#include "fs2_reduce.hpp"
 
 namespace fs2 {
-
-// ------------------------------------------------------------ reductions ---
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
-// (value, index) argmax, lowest index among equal maxima (Python max).
-__device__ __forceinline__ void argmax_combine(double &v, int64_t &i, double v2, int64_t i2) {
-    if (v2 > v || (v2 == v && i2 < i)) {
-        v = v2;
-        i = i2;
-    }
-}
-
-__device__ __forceinline__ void wave_argmax(double &v, int64_t &i) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double v2 = __shfl_xor(v, o, 64);
-        const int64_t i2 = __shfl_xor(i, o, 64);
-        argmax_combine(v, i, v2, i2);
-    }
-}
-
-// Deterministic block sum (fixed tree), result valid in every thread.
-template <int NT>
-__device__ double block_sum(double v, double *lds) {
-    v = wave_sum(v);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) lds[wid] = v;
-    __syncthreads();
-    double t = 0.0;
-#pragma unroll
-    for (int k = 0; k < NT / 64; ++k) t += lds[k];
-    return t;
-}
-
-template <int NT>
-__device__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long *lds) {
-    v = wave_sum_u64(v);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) lds[wid] = v;
-    __syncthreads();
-    unsigned long long t = 0;
-#pragma unroll
-    for (int k = 0; k < NT / 64; ++k) t += lds[k];
-    return t;
-}
-
-template <int NT>
-__device__ void block_argmax(double &v, int64_t &i, double *ldv, int64_t *ldi) {
-    wave_argmax(v, i);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) {
-        ldv[wid] = v;
-        ldi[wid] = i;
-    }
-    __syncthreads();
-    v = ldv[0];
-    i = ldi[0];
-#pragma unroll
-    for (int k = 1; k < NT / 64; ++k) argmax_combine(v, i, ldv[k], ldi[k]);
-}
-
-template <int NT>
-__device__ int block_max_i(int v, int *lds) {
-    v = wave_max_i(v);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) lds[wid] = v;
-    __syncthreads();
-    int t = lds[0];
-#pragma unroll
-    for (int k = 1; k < NT / 64; ++k) t = max(t, lds[k]);
-    return t;
-}
-
-// ------------------------------------------------------------- map access ---
-
-// Page of slot j of physical map p.  Slots 4g..4g+3 never straddle a page.
-__device__ __forceinline__ char *page_of(char *const *arenas, int j, int32_t p) {
-    return arenas[j >> 6] + (int64_t)p * kPageBytes;
-}
-
-__device__ __forceinline__ float4 load_mirror(const char *page, int j) {
-    return reinterpret_cast<const float4 *>(page)[j & (kPageSlots - 1)];
-}
-
-__device__ __forceinline__ Slot load_slot(const char *page, int j) {
-    const double2 *q =
-        reinterpret_cast<const double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
-    const double2 a = q[0], b = q[1], c = q[2];
-    return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
-}
-
-// Every slot write keeps the fp32 gate mirror in step with the fp64 slot.
-__device__ __forceinline__ void store_slot(char *page, int j, const Slot &s) {
-    double2 *q = reinterpret_cast<double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
-    q[0] = make_double2(s.mx, s.my);
-    q[1] = make_double2(s.P.a00, s.P.a01);
-    q[2] = make_double2(s.P.a10, s.P.a11);
-    reinterpret_cast<float4 *>(page)[j & (kPageSlots - 1)] = mirror_of(s);
-}
-
-// Gate decisions this close to the threshold could depend on ulp-level
-// differences upstream (landmark means after EKF); counted, never altered.
-__device__ __forceinline__ unsigned ambiguous(double q, double gate2) {
-    return fabs(q - gate2) <= 1e-9 * gate2 ? 1u : 0u;
-}
 
 // ------------------------------------------------------------ k_update ------
 //
@@ -483,333 +356,6 @@ hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
     const unsigned grid = (unsigned)((p.n + kBlock - 1) / kBlock);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_normalize, dim3(grid), dim3(kBlock), 0, s, p);
-    return hipGetLastError();
-}
-
-// N_eff, resample decision, estimate (pre-resample), u0.
-__global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
-    __shared__ double lds_d[16];
-    __shared__ int64_t lds_l[16];
-    __shared__ int lds_i[16];
-    double sq = 0.0;
-    double bv = -INFINITY;
-    int64_t bi = INT64_MAX;
-    int mc = 0;
-    for (int k = threadIdx.x; k < P.nparts; k += 1024) {
-        sq += P.part_sq[k];
-        argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
-        mc = max(mc, P.part_maxcnt[k]);
-    }
-    sq = block_sum<1024>(sq, lds_d);
-    block_argmax<1024>(bv, bi, lds_d, lds_l);
-    mc = block_max_i<1024>(mc, lds_i);
-    if (threadIdx.x == 0) {
-        if (P.sequential) {
-            // np.sum(weights ** 2): pairwise inside 8192-element chunks
-            double s = 0.0;
-            for (int64_t k = 0; k < P.n; k += 8192) {
-                const int64_t m = (P.n - k < 8192) ? P.n - k : 8192;
-                const double p = pairwise_sq(P.w + k, m);
-                s = (k == 0) ? p : s + p;
-            }
-            sq = s;
-        }
-        const double ng = (double)P.n_global;
-        const double ne = (sq < 1.0 / ng) ? ng : 1.0 / sq;
-        DevStats *st = P.stats;
-        st->sumsq = sq;
-        st->n_eff = ne;
-        st->resampled = ne < ng / 2.0 ? 1 : 0;
-        st->max_count = max(st->max_count, mc);
-        st->best_index = bi;
-        st->best_w = bv;
-        st->pose[0] = P.x[bi];
-        st->pose[1] = P.y[bi];
-        st->pose[2] = P.yaw[bi];
-        const double r = P.u0_host ? *P.u0_host
-                                   : (1.0 / ng) * philox_uniform01(P.seed, P.scan | (1ull << 63), 0);
-        st->u0 = r;
-    }
-}
-
-hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, p);
-    return hipGetLastError();
-}
-
-// -------------------------------------------------------------- resample ---
-//
-// Systematic resampling keeps the logical order of the reference (output m is
-// a deep copy of particle src(m), fast_slam_2.py:188-199) but moves maps only
-// where it must: the first copy of each source keeps the source's physical
-// map; every further copy takes over the map of a particle that was not
-// selected and has it overwritten with the source's landmarks.  Copies are as
-// many as dropped particles (about a third of N at N_eff = N/2), and a source
-// map is never a copy destination, so no double buffer is needed.
-
-constexpr int kScanPer = 4;                       // elements per thread
-constexpr int kScanBlock = kBlock * kScanPer;     // 1024 elements per block
-
-__global__ __launch_bounds__(1) void k_scan_seq(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    double c = 0.0;
-    for (int64_t i = 0; i < P.n; ++i) {
-        c = (i == 0) ? P.w[0] : c + P.w[i];
-        P.c[i] = c;
-    }
-}
-
-__device__ __forceinline__ double wave_incl_scan(double v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
-
-__device__ __forceinline__ int wave_incl_scan_i(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_local(const ResampleParams P) {
-    __shared__ double lds[kBlock / 64];
-    if (!P.stats->resampled) return;
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
-    double v[kScanPer];
-    double run = 0.0;
-#pragma unroll
-    for (int e = 0; e < kScanPer; ++e) {
-        const int64_t i = base + e;
-        run += (i < P.n) ? P.w[i] : 0.0;
-        v[e] = run;
-    }
-    const double incl = wave_incl_scan(run);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) lds[wid] = incl;
-    __syncthreads();
-    double woff = 0.0;
-    for (int k = 0; k < wid; ++k) woff += lds[k];
-    const double off = woff + incl - run;
-#pragma unroll
-    for (int e = 0; e < kScanPer; ++e) {
-        const int64_t i = base + e;
-        if (i < P.n) P.c[i] = off + v[e];
-    }
-    if (threadIdx.x == kBlock - 1) P.bsum[blockIdx.x] = off + v[kScanPer - 1];
-}
-
-__global__ __launch_bounds__(1) void k_scan_blocks(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    double acc = 0.0;
-    for (int b = 0; b < P.nblk; ++b) {
-        const double t = P.bsum[b];
-        P.bsum[b] = acc;    // exclusive offset
-        acc += t;
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_add(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < P.n) P.c[i] += P.bsum[i / kScanBlock];
-}
-
-// src(m) = smallest i with prefix c_i >= u_m, else N-1 (fast_slam_2.py:188-196,
-// without the reference's hang when u_m exceeds every reachable sum, Q10);
-// marks every selected particle.
-__global__ __launch_bounds__(kBlock) void k_resample_src(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= P.n) return;
-    const double u = P.stats->u0 + (double)m * (1.0 / (double)P.n);
-    int64_t lo = 0, hi = P.n;   // first index with c >= u in [lo, hi)
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (P.c[mid] >= u) hi = mid;
-        else lo = mid + 1;
-    }
-    const int32_t s = (lo < P.n) ? (int32_t)lo : (int32_t)(P.n - 1);
-    P.src[m] = s;
-    P.used[s] = 1;
-}
-
-// Ranks of dropped particles (!used) and of extra outputs (src[m] == src[m-1]):
-// block-local exclusive ranks plus per-block totals.
-__global__ __launch_bounds__(kBlock) void k_plan_local(const ResampleParams P) {
-    __shared__ int lds[2][kBlock / 64];
-    if (!P.stats->resampled) return;
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
-    int dflag[kScanPer], eflag[kScanPer];
-    int dsum = 0, esum = 0;
-#pragma unroll
-    for (int e = 0; e < kScanPer; ++e) {
-        const int64_t t = base + e;
-        dflag[e] = (t < P.n && !P.used[t]) ? 1 : 0;
-        eflag[e] = (t < P.n && t > 0 && P.src[t] == P.src[t - 1]) ? 1 : 0;
-        dsum += dflag[e];
-        esum += eflag[e];
-    }
-    const int di = wave_incl_scan_i(dsum), ei = wave_incl_scan_i(esum);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 63) {
-        lds[0][wid] = di;
-        lds[1][wid] = ei;
-    }
-    __syncthreads();
-    int doff = di - dsum, eoff = ei - esum;
-    for (int k = 0; k < wid; ++k) {
-        doff += lds[0][k];
-        eoff += lds[1][k];
-    }
-#pragma unroll
-    for (int e = 0; e < kScanPer; ++e) {
-        const int64_t t = base + e;
-        if (t < P.n) {
-            P.rank_d[t] = doff;
-            P.rank_e[t] = eoff;
-        }
-        doff += dflag[e];
-        eoff += eflag[e];
-    }
-    if (threadIdx.x == kBlock - 1) {
-        P.iblk[blockIdx.x] = doff;
-        P.iblk[P.nblk + blockIdx.x] = eoff;
-    }
-}
-
-__global__ __launch_bounds__(1) void k_plan_blocks(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    int dacc = 0, eacc = 0;
-    for (int b = 0; b < P.nblk; ++b) {
-        const int td = P.iblk[b], te = P.iblk[P.nblk + b];
-        P.iblk[b] = dacc;
-        P.iblk[P.nblk + b] = eacc;
-        dacc += td;
-        eacc += te;
-    }
-    P.stats->n_copies = eacc;   // == dacc: as many extra copies as dropped particles
-}
-
-// free list = physical maps of the dropped particles, in particle order
-__global__ __launch_bounds__(kBlock) void k_plan_free(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= P.n || P.used[t]) return;
-    P.freelist[P.iblk[t / kScanBlock] + P.rank_d[t]] = P.phys[t];
-}
-
-// next phys: first copy keeps the source's map, extra copies take free maps
-__global__ __launch_bounds__(kBlock) void k_plan_assign(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= P.n) return;
-    const int32_t s = P.src[m];
-    if (m > 0 && P.src[m - 1] == s) {
-        const int k = P.iblk[P.nblk + m / kScanBlock] + P.rank_e[m];
-        P.ophys[m] = P.freelist[k];
-        P.tasks[k] = (int32_t)m;
-    } else {
-        P.ophys[m] = P.phys[s];
-    }
-}
-
-// Copy the map of src(m) into the map of each extra output m: one workgroup
-// per copy, 16 B per lane, contiguous pages (fast_slam_2.py:196 deepcopy).
-constexpr int kCopyGrid = 4096;
-
-__global__ __launch_bounds__(kBlock) void k_copy_maps(const ResampleParams P) {
-    __shared__ unsigned long long lds_u[kBlock / 64];
-    if (!P.stats->resampled) return;
-    const int ncopy = P.stats->n_copies;
-    unsigned long long slots = 0;
-    for (int k = blockIdx.x; k < ncopy; k += gridDim.x) {
-        const int32_t m = P.tasks[k];
-        const int32_t s = P.src[m];
-        const int32_t from = P.phys[s], to = P.ophys[m];
-        const int cnt = P.cnt[s];
-        if (threadIdx.x == 0) slots += (unsigned long long)cnt;
-        for (int pg = 0; pg * kPageSlots < cnt; ++pg) {
-            const int ns = min(kPageSlots, cnt - pg * kPageSlots);
-            const int4 *sp = reinterpret_cast<const int4 *>(P.arenas[pg] + (int64_t)from * kPageBytes);
-            int4 *dp = reinterpret_cast<int4 *>(P.arenas[pg] + (int64_t)to * kPageBytes);
-            // mirrors: ns x 16 B at offset 0; fp64 slots: ns x 48 B at 1 KiB
-            for (int q = threadIdx.x; q < ns; q += kBlock) dp[q] = sp[q];
-            for (int q = threadIdx.x; q < 3 * ns; q += kBlock) dp[64 + q] = sp[64 + q];
-        }
-    }
-    const unsigned long long b = block_sum_u64<kBlock>(slots, lds_u);
-    if (threadIdx.x == 0 && b) atomicAdd(&P.stats->resample_slots, b);
-}
-
-__global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParams P) {
-    __shared__ double lds_d[kBlock / 64];
-    __shared__ int64_t lds_l[kBlock / 64];
-    if (!P.stats->resampled) return;
-    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    double bv = -INFINITY;
-    int64_t bi = INT64_MAX;
-    if (m < P.n) {
-        const int32_t s = P.src[m];
-        P.ox[m] = P.x[s];
-        P.oy[m] = P.y[s];
-        P.oyaw[m] = P.yaw[s];
-        const double w = P.w[s];
-        P.ow[m] = w;
-        P.ocnt[m] = P.cnt[s];
-        bv = w;
-        bi = m;
-    }
-    block_argmax<kBlock>(bv, bi, lds_d, lds_l);
-    if (threadIdx.x == 0) {
-        P.part_best_w[blockIdx.x] = bv;
-        P.part_best_i[blockIdx.x] = bi;
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32_t nparts) {
-    __shared__ double lds_d[16];
-    __shared__ int64_t lds_l[16];
-    if (!P.stats->resampled) return;
-    double bv = -INFINITY;
-    int64_t bi = INT64_MAX;
-    for (int k = threadIdx.x; k < nparts; k += 1024) argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
-    block_argmax<1024>(bv, bi, lds_d, lds_l);
-    if (threadIdx.x == 0) {
-        DevStats *st = P.stats;
-        st->best_index = bi;
-        st->best_w = bv;
-        st->pose[0] = P.ox[bi];
-        st->pose[1] = P.oy[bi];
-        st->pose[2] = P.oyaw[bi];
-    }
-}
-
-hipError_t launch_resample(const ResampleParams &p, int sequential, hipStream_t s) {
-    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
-    if (g == 0) return hipSuccess;
-    if (sequential) {
-        hipLaunchKernelGGL(k_scan_seq, dim3(1), dim3(1), 0, s, p);
-    } else {
-        hipLaunchKernelGGL(k_scan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1), 0, s, p);
-        hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(kBlock), 0, s, p);
-    }
-    hipLaunchKernelGGL(k_resample_src, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_plan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_plan_blocks, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL(k_plan_free, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_plan_assign, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_copy_maps, dim3(kCopyGrid), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
     return hipGetLastError();
 }
 

@@ -27,6 +27,8 @@ FS2_REDUCE_SEQUENTIAL = 1
 FS2_REDUCE_PARALLEL = 2
 FS2_HOST = 0
 FS2_DEVICE = 1
+FS2_COMM_RCCL = 0
+FS2_COMM_LOCAL = 1
 
 
 class fs2_config(C.Structure):
@@ -48,6 +50,8 @@ class fs2_config(C.Structure):
         ("rank", C.c_int32),
         ("world_size", C.c_int32),
         ("comm_id", C.c_uint8 * 128),
+        ("comm_mode", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 

@@ -35,7 +35,8 @@ class FastSLAM2:
     def __init__(self, num_particles: int | None = None, *, device: int = 0, rng: str = "numpy",
                  seed: int | None = None, reduce: str = "auto", record_assoc: bool = False,
                  landmark_capacity: int = 64, rank: int = 0, world_size: int = 1,
-                 comm_id: bytes | None = None, verbose: bool = True, gate_filter: bool = True):
+                 comm_id: bytes | None = None, verbose: bool = True, gate_filter: bool = True,
+                 comm_mode: str = "rccl"):
         lib = nat.load()
         cfg = nat.default_config()
         cfg.num_particles = int(config.NUM_PARTICLES if num_particles is None else num_particles)
@@ -56,6 +57,7 @@ class FastSLAM2:
         cfg.world_size = int(world_size)
         if comm_id is not None:
             C.memmove(cfg.comm_id, comm_id, 128)
+        cfg.comm_mode = {"rccl": nat.FS2_COMM_RCCL, "local": nat.FS2_COMM_LOCAL}[comm_mode]
         if rng not in ("numpy", "device"):
             raise ValueError("rng must be 'numpy' or 'device'")
         self._rng = rng

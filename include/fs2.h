@@ -49,6 +49,12 @@ enum {
 
 enum { FS2_HOST = 0, FS2_DEVICE = 1 };   /* where caller buffers live */
 
+/* How sharded ranks (world_size > 1) talk. */
+enum {
+    FS2_COMM_RCCL = 0,      /* one process per GPU, RCCL over xGMI; comm_id from fs2_comm_unique_id */
+    FS2_COMM_LOCAL = 1      /* ranks are threads of one process (testing); comm_id is a group key */
+};
+
 typedef struct fs2_handle fs2_handle;
 
 typedef struct fs2_config {
@@ -69,6 +75,8 @@ typedef struct fs2_config {
     int32_t rank;                   /* this rank (particle shard) */
     int32_t world_size;             /* number of ranks; 1 = single GPU */
     uint8_t comm_id[128];           /* ncclUniqueId from fs2_comm_unique_id (world_size > 1) */
+    int32_t comm_mode;              /* FS2_COMM_* */
+    int32_t reserved0;
 } fs2_config;
 
 typedef struct fs2_iter_stats {
@@ -135,8 +143,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
 /* Particle state in the reference's object layout (Particle.x/.y/.yaw/.weight,
  * Particle.landmarks[j] = Landmark(x, y, cov) -- models/particle.py:11-20,
  * models/landmark.py:13-21).  Range [first, first+count) of this rank's local
- * particles.  lm is [count][lm_cap][6] = x, y, P00, P01, P10, P11; slots
- * beyond cnt[i] are left untouched.  where = FS2_HOST or FS2_DEVICE. Any of
+ * particles.  lm is [count][lm_cap][6] = x, y, P00, P01, P10, P11; get_state
+ * zero-fills slots beyond cnt[i].  where = FS2_HOST or FS2_DEVICE. Any of
  * x/y/yaw/w/cnt/lm may be NULL to skip it (set_state: cnt and lm go together). */
 int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double *y,
                   double *yaw, double *w, int32_t *cnt, double *lm, int32_t lm_cap,
