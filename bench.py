@@ -110,11 +110,13 @@ def cpu_baseline(L, P, budget_s, seed):
                        f"(C oracle, reference semantics, 1 thread, {t_work:.1f} s)")
 
 
-def pmc_traffic(workload):
-    p = os.path.join(REPO, "profiles", f"pmc_update_{workload}.json")
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (scripts/pmc_round.sh -> profiles/pmc_{workload}.json), or None."""
+    p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get("hbm_bytes_per_launch")
+            return json.load(open(p)).get(kernel, {}).get("hbm_bytes_per_launch")
         except Exception:
             return None
     return None
@@ -200,8 +202,17 @@ def main():
 
     if rank == 0:
         launches = max(prof["update_launches"], 1)
-        ms_launch = prof["update_ms"] / launches
-        bytes_launch = prof["update_bytes"] / launches
+        upd_ms = prof["update_ms"] / launches
+        # dominant kernel: the candidate stream (k_candidates) reads every slot's
+        # mirror; without the gate filter the exact kernel streams the fp64 slots
+        if prof["filter_launches"] > 0:
+            kernel = "k_candidates"
+            ms_launch = prof["filter_ms"] / prof["filter_launches"]
+            bytes_launch = prof["filter_bytes"] / prof["filter_launches"]
+        else:
+            kernel = "k_update"
+            ms_launch = upd_ms
+            bytes_launch = prof["update_bytes"] / launches
         achieved = bytes_launch / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -227,12 +238,13 @@ def main():
                        "parallelism": f"particle-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(cfg["name"]),
-                         "kernel": "k_update", "bytes_per_launch": bytes_launch,
+                         "traffic": pmc_traffic(cfg["name"], kernel),
+                         "kernel": kernel, "bytes_per_launch": bytes_launch,
                          "ms_per_launch": ms_launch},
             "cpu_baseline": cpu,
             "extra": {"scan_device_ms": prof["scan_ms"] / max(prof["scans"], 1),
-                      "update_ms": ms_launch,
+                      "update_pass_ms": upd_ms,
+                      "update_pass_bytes": prof["update_bytes"] / launches,
                       "reduce_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resample_ms_total": prof["resample_ms"],
                       "resamples": resamples,

@@ -95,6 +95,8 @@ struct fs2_handle {
     double *totals = nullptr;                       // all ranks' weight totals
     int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (records, slots) per peer
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr, *kept = nullptr;
+    uint16_t *cand = nullptr;                       // [kMaxCand][n] candidate slots
+    int32_t *ncand = nullptr;
     std::vector<char *> sendbuf, recvbuf;
     std::vector<size_t> sendcap, recvcap;
     int32_t n_recv = 0;                             // particles received by the last resample
@@ -249,6 +251,7 @@ static void free_handle(fs2_handle *h) {
     for (char *b : h->sendbuf) hipFree(b);
     for (char *b : h->recvbuf) hipFree(b);
     hipFree(h->freelist); hipFree(h->tasks);
+    hipFree(h->cand); hipFree(h->ncand);
     hipFree(h->wpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -315,6 +318,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->out_src, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->kept, n * 4) == hipSuccess;
+    ok &= alloc((void **)&h->cand, n * 2 * kMaxCand) == hipSuccess;
+    ok &= alloc((void **)&h->ncand, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
     ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
     ok &= alloc((void **)&h->totals, sizeof(double) * G) == hipSuccess;
@@ -450,6 +455,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     up.gate2f = std::isinf(h->gate2) ? INFINITY
                                      : std::nextafter((float)(h->gate2 / (1.0 - 0x1p-18)), INFINITY);
     up.filter = h->cfg.gate_filter ? 1 : 0;
+    up.cand = h->cand;
+    up.ncand = h->ncand;
     std::memcpy(up.R, h->cfg.measurement_noise, sizeof up.R);
     std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
     up.assoc = h->cfg.record_assoc ? h->assoc_dev : nullptr;
@@ -481,6 +488,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
                                       std::fabs(oy - (double)up.meas.fy[k]));
             up.meas.fe[k] = std::isfinite(e) ? std::nextafter((float)e, INFINITY) : INFINITY;
         }
+        if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(h->ev.e[4], s));
+        HIP_TRY(h, launch_candidates(up, s));
+        if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(h->ev.e[5], s));
         HIP_TRY(h, launch_update(up, s));
         ++passes;
         // pose/weight/count read + weight/count write; pose write on the move pass
@@ -600,6 +610,15 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         hipEventElapsedTime(&a, h->ev.e[0], h->ev.e[1]);
         hipEventElapsedTime(&b, h->ev.e[1], h->ev.e[2]);
         hipEventElapsedTime(&c, h->ev.e[2], h->ev.e[3]);
+        if (h->cfg.gate_filter && M <= kMaxM) {
+            // candidate stream: mirrors of every slot, the lists and their counts
+            float f = 0;
+            hipEventElapsedTime(&f, h->ev.e[4], h->ev.e[5]);
+            h->prof.filter_launches += 1;
+            h->prof.filter_ms += f;
+            // (cnt + phys read, count written: 12 B per particle)
+            h->prof.filter_bytes += 16ull * st.visited + 12ull * (uint64_t)h->n + 2ull * st.listed;
+        }
         h->prof.scans += 1;
         h->prof.update_launches += passes;
         h->prof.update_ms += a;
@@ -608,7 +627,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         h->prof.scan_ms += a + b + c;
         // mirror reads (16 B) per visited slot when filtering, fp64 slot reads (48 B) per
         // candidate, full slot writes (48 B + 16 B mirror)
-        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited : 0ull) +
+        // + candidate lists written and read back (2 B each) and their counts
+        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 4ull * st.listed +
+                                                          8ull * (uint64_t)h->n * passes : 0ull) +
                                 48ull * st.candidates + 64ull * st.written + fixed_bytes +
                                 8ull * (uint64_t)h->nblocks();
         if (st.resampled)

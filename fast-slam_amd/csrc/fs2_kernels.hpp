@@ -11,7 +11,8 @@ constexpr int kBlock = 256;          // 4 waves of 64
 constexpr int kPageSlots = 64;       // landmark slots per page
 constexpr int kMaxPages = 64;        // 4096 slots per particle max
 constexpr int kMaxM = 4;             // measurements fused into one map pass
-constexpr int kGroup = 4;            // slots whose mirrors a lane loads per step (64 B)
+constexpr int kScanGroup = 8;        // slots whose mirrors a lane loads per step (128 B)
+constexpr int kMaxCand = 16;         // candidate slots listed per particle and pass
 
 // A page holds 64 slots of ONE particle's map, contiguous:
 //   [0, 1024)     64 x float4 gate mirror (x, y, s, 0)     -- read every scan
@@ -35,6 +36,7 @@ struct DevStats {
     int32_t error_flags;
     int32_t n_copies;        // maps copied by the resample (duplicated particles)
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
+    unsigned long long listed;   // candidate list entries written by k_candidates
     double offset;           // global prefix of weights before this rank's first particle
     double t_local;          // sum of this rank's normalised weights (last local prefix)
     int32_t out_min, out_max;   // smallest / largest output index served by a local particle
@@ -103,6 +105,8 @@ struct UpdateParams {
     double gate2;            // match iff 0 <= q < gate2  (sqrt(q) < gate)
     float gate2f;            // gate2 rounded up to fp32 (mirror test)
     int32_t filter;          // use the fp32 gate mirror
+    uint16_t *cand;          // [kMaxCand][n] candidate slots (k_candidates -> k_update)
+    int32_t *ncand;          // [n] candidates found (> kMaxCand: list truncated)
     double R[4];
     double init_cov[4];
     int32_t *assoc;          // [M][n] or null
@@ -174,6 +178,7 @@ struct ResampleParams {
 };
 
 // ---- launch wrappers (defined in fs2_kernels.hip) ----
+hipError_t launch_candidates(const UpdateParams &p, hipStream_t s);
 hipError_t launch_update(const UpdateParams &p, hipStream_t s);
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s);
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s);

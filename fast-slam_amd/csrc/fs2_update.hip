@@ -8,8 +8,10 @@
 //   k of every physical map; logical particle m owns physical map phys[m].
 //
 // Kernels
-//   k_update        fused move + association + EKF/append + likelihood, one pass
-//                   over each particle's map for up to kMaxM measurements;
+//   k_candidates    streaming fp32 gate-mirror pass listing each particle's
+//                   candidate slots for up to kMaxM measurements;
+//   k_update        move + exact association + EKF/append + likelihood over the
+//                   candidates;
 //   k_wsum          weight total (fast_slam_2.py:166);
 //   k_normalize     normalise + per-block sum w'^2 / argmax / max count (:161-175);
 //   k_finalize      N_eff, resample decision, estimate, u0 (:60-67, :201-223);
@@ -20,22 +22,91 @@
 
 namespace fs2 {
 
+// ------------------------------------------------------- k_candidates ------
+//
+// Streaming half of the association (fast_slam_2.py:95-106 first-match search).
+// One lane per particle walks its whole map reading only the 16-byte fp32 gate
+// mirrors (128 contiguous bytes = one cache line per lane and group of 8 slots,
+// the next group in flight while this one is tested) and lists, in slot order,
+// every slot the mirror cannot rule out for at least one measurement of the
+// pass.  No fp64, no calls: the kernel stays small enough for full occupancy,
+// which is what an HBM stream needs.
+//
+// Exactness: measurement k can only match slot j in the state slot j had when
+// the first measurement matching it arrived, and that first match sees slot j
+// unmodified (only matches modify slots), so every slot that will ever match
+// passes the conservative mirror test on the pre-scan map.  Slots not listed
+// can therefore never match and are never modified; k_update visits exactly the
+// listed ones.  A list longer than kMaxCand stores its first kMaxCand entries
+// and k_update resumes with an exact scan after the last stored one.
+template <int MAXM>
+__global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
+    __shared__ unsigned long long lds_u[kBlock / 64];
+    const int tid = threadIdx.x;
+    const int64_t n = P.n;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
+    const bool live = i < n;
+    const int c = live ? P.cnt[i] : 0;
+    const int64_t pbase = live ? (int64_t)P.map.phys[i] * kPageBytes : 0;
+    char *const *arenas = P.map.arenas;
+    uint16_t *cand = P.cand + (live ? i : 0);
+    int nc = 0;
+    unsigned visited = 0;
+
+    float4 cur[kScanGroup], nxt[kScanGroup];
+#pragma unroll
+    for (int u = 0; u < kScanGroup; ++u)
+        if (u < c) cur[u] = load_mirror(arenas[0] + pbase, u);
+    for (int j0 = 0; __any(j0 < c); j0 += kScanGroup) {
+        const int j1 = j0 + kScanGroup;
+        const char *npage = arenas[min(j1 >> 6, kMaxPages - 1)] + pbase;
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u)
+            if (j1 + u < c) nxt[u] = load_mirror(npage, j1 + u);
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u) {
+            if (j0 + u < c) {
+                ++visited;
+                const float4 mv = cur[u];
+                const float cx = fabsf(mv.x) * 2.3841858e-7f;   // 2^-22 |x_lm|
+                const float cy = fabsf(mv.y) * 2.3841858e-7f;
+                bool hit = false;
+#pragma unroll
+                for (int k = 0; k < MAXM; ++k)
+                    if (k < P.m)
+                        hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
+                                                 P.gate2f);
+                if (hit) {
+                    if (nc < kMaxCand) cand[(int64_t)nc * n] = (uint16_t)(j0 + u);
+                    ++nc;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u) cur[u] = nxt[u];
+    }
+    if (live) P.ncand[i] = nc;
+    const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
+    const unsigned long long bl = block_sum_u64<kBlock>((unsigned)min(nc, kMaxCand), lds_u);
+    if (tid == 0) {
+        atomicAdd(&P.stats->visited, bv);
+        atomicAdd(&P.stats->listed, bl);
+    }
+}
+
 // ------------------------------------------------------------ k_update ------
 //
-// One lane per particle.  The M measurements of a scan are sequential in the
-// reference (measurement k sees the map left by k-1), but measurement k only
-// ever changes the slot it matched or appends at the end.  Walking the map
-// once and, at every slot j, testing the still-unmatched measurements in
+// One lane per particle: move, then the exact association + EKF over the
+// candidate slots in slot order.  The M measurements of a scan are sequential
+// in the reference (measurement k sees the map left by k-1), but measurement k
+// only ever changes the slot it matched or appends at the end.  Walking the
+// slots once and, at every slot j, testing the still-unmatched measurements in
 // order k = 0..M-1 (an EKF update changes the slot in registers before the
 // next measurement tests it) reproduces the sequential result exactly while
 // reading each slot once instead of M times.  Slots appended in this scan are
 // resolved afterwards in measurement order.  Likelihoods multiply into the
-// weight in measurement order, as the reference does.
-//
-// The walk reads only the 16-byte fp32 gate mirrors (64 contiguous bytes per
-// lane and group of 4 slots; the next group is in flight while the current
-// one is tested); a slot the mirror cannot rule out for every pending
-// measurement takes the exact fp64 path (see mirror_of / gate_reject).
+// weight in measurement order, as the reference does.  Without the gate filter
+// (or past an overflowing candidate list) every slot takes the exact path.
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ double lds_d[kBlock / 64];
@@ -65,7 +136,6 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         c = P.cnt[i];
         pm = P.map.phys[i];
     }
-    const int64_t pbase = (int64_t)pm * kPageBytes;
     char *const *arenas = P.map.arenas;
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
@@ -89,92 +159,60 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     unsigned visited = 0, candidates = 0, written = 0, amb = 0, appends = 0;
     bool singular = false;
     const double gate2 = P.gate2;
-    const bool filter = P.filter != 0;
 
-    // ---- single pass over the existing map (association + EKF) ----
-    float4 cur[kGroup], nxt[kGroup];
-    if (filter) {
-#pragma unroll
-        for (int u = 0; u < kGroup; ++u)
-            if (pend != 0u && u < c) cur[u] = load_mirror(arenas[0] + pbase, u);
+    // ---- exact pass over the candidate slots (association + EKF) ----
+    int ncl = 0, jf = 0;
+    if (live && P.filter) {
+        const int nc = P.ncand[i];
+        ncl = min(nc, kMaxCand);
+        jf = nc > kMaxCand ? (int)P.cand[(int64_t)(kMaxCand - 1) * n + i] + 1 : c;
     }
-    for (int j0 = 0;; j0 += kGroup) {
-        if (!__any((pend != 0u) && (j0 < c))) break;
-        const char *page = arenas[j0 >> 6] + pbase;
-        unsigned cmask = 0;
-        if (filter) {
-            // next group in flight while this one is tested
-            const int j1 = j0 + kGroup;
-            const char *npage = arenas[j1 >> 6] + pbase;
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u)
-                if (pend != 0u && j1 + u < c) nxt[u] = load_mirror(npage, j1 + u);
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                if (pend != 0u && j0 + u < c) {
-                    ++visited;
-                    const float4 mv = cur[u];
-                    const float cx = fabsf(mv.x) * 2.3841858e-7f;   // 2^-22 |x_lm|
-                    const float cy = fabsf(mv.y) * 2.3841858e-7f;
-                    bool cand = false;
-#pragma unroll
-                    for (int k = 0; k < MAXM; ++k)
-                        if ((pend >> k) & 1u)
-                            cand |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k],
-                                                      P.meas.fe[k], P.gate2f);
-                    if (cand) cmask |= 1u << u;
-                }
-            }
+    int q = 0;
+    while (pend) {
+        int j;
+        if (q < ncl) {
+            j = P.cand[(int64_t)q * n + i];
+            ++q;
+        } else if (jf < c) {
+            j = jf++;
+            if (!P.filter) ++visited;
         } else {
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u)
-                if (pend != 0u && j0 + u < c) {
-                    ++visited;
-                    cmask |= 1u << u;
-                }
+            break;
         }
-        while (cmask) {
-            const int j = j0 + __builtin_ctz(cmask);
-            cmask &= cmask - 1u;
-            if (pend == 0u) break;
-            Slot s = load_slot(page, j);
-            ++candidates;
-            bool mod = false;
-            M2 I;
-            bool ok = inv2(s.P, I);
+        char *page = page_of(arenas, j, pm);
+        Slot s = load_slot(page, j);
+        ++candidates;
+        bool mod = false;
+        M2 I;
+        bool ok = inv2(s.P, I);
+        singular |= !ok;
+        unsigned todo = ok ? pend : 0u;   // measurements still to test at this slot
+        while (todo) {
+            // test the pending measurements in order; stop at the first match
+            int km = -1;
+#pragma unroll
+            for (int k = 0; k < MAXM; ++k) {
+                if (km < 0 && ((todo >> k) & 1u)) {
+                    const double qd = quad(I, s_ms[k].ox - s.mx, s_ms[k].oy - s.my);
+                    amb += ambiguous(qd, gate2);
+                    todo &= ~(1u << k);
+                    if (qd >= 0.0 && qd < gate2) km = k;
+                }
+            }
+            if (km < 0) break;
+            // one EKF site: the matched measurement sees the slot as left by
+            // the earlier measurements (fast_slam_2.py:116-153)
+            s_lik[km][tid] = ekf_update(s, px, py, pyaw, s_ms[km], R, singular);
+            s_idx[km][tid] = j;
+            pend &= ~(1u << km);
+            mod = true;
+            ok = inv2(s.P, I);
             singular |= !ok;
-            unsigned todo = ok ? pend : 0u;   // measurements still to test at this slot
-            while (todo) {
-                // test the pending measurements in order; stop at the first match
-                int km = -1;
-#pragma unroll
-                for (int k = 0; k < MAXM; ++k) {
-                    if (km < 0 && ((todo >> k) & 1u)) {
-                        const double q = quad(I, s_ms[k].ox - s.mx, s_ms[k].oy - s.my);
-                        amb += ambiguous(q, gate2);
-                        todo &= ~(1u << k);
-                        if (q >= 0.0 && q < gate2) km = k;
-                    }
-                }
-                if (km < 0) break;
-                // one EKF site: the matched measurement sees the slot as left by
-                // the earlier measurements (fast_slam_2.py:116-153)
-                s_lik[km][tid] = ekf_update(s, px, py, pyaw, s_ms[km], R, singular);
-                s_idx[km][tid] = j;
-                pend &= ~(1u << km);
-                mod = true;
-                ok = inv2(s.P, I);
-                singular |= !ok;
-                if (!ok) todo = 0u;
-            }
-            if (mod) {
-                store_slot(const_cast<char *>(page), j, s);
-                ++written;
-            }
+            if (!ok) todo = 0u;
         }
-        if (filter) {
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u) cur[u] = nxt[u];
+        if (mod) {
+            store_slot(page, j, s);
+            ++written;
         }
     }
 
@@ -266,6 +304,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         atomicAdd(&P.stats->hits, bh);
         if (anysing) atomicOr(&P.stats->error_flags, 1);
     }
+}
+
+hipError_t launch_candidates(const UpdateParams &p, hipStream_t s) {
+    const unsigned grid = (unsigned)((p.n + kBlock - 1) / kBlock);
+    if (grid == 0 || !p.filter) return hipSuccess;
+    hipLaunchKernelGGL(k_candidates<kMaxM>, dim3(grid), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_update(const UpdateParams &p, hipStream_t s) {

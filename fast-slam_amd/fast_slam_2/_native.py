@@ -87,6 +87,9 @@ class fs2_profile(C.Structure):
         ("scan_ms", C.c_double),
         ("update_bytes", C.c_uint64),
         ("resample_bytes", C.c_uint64),
+        ("filter_launches", C.c_int64),
+        ("filter_ms", C.c_double),
+        ("filter_bytes", C.c_uint64),
     ]
 
     def as_dict(self):

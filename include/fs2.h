@@ -98,13 +98,16 @@ typedef struct fs2_iter_stats {
 
 typedef struct fs2_profile {
     int64_t scans;              /* scans timed since profiling was enabled */
-    int64_t update_launches;    /* fused update kernel launches */
-    double update_ms;           /* summed device time of the update kernel (HIP events) */
+    int64_t update_launches;    /* update passes (candidate stream + exact kernel) */
+    double update_ms;           /* summed device time of the update passes (HIP events) */
     double reduce_ms;           /* normalise / N_eff / estimate kernels */
     double resample_ms;         /* prefix + gather kernels (scans that resampled) */
     double scan_ms;             /* summed device time of whole scans */
     uint64_t update_bytes;      /* algorithmic bytes moved by the update kernel */
     uint64_t resample_bytes;    /* algorithmic bytes moved by resample gathers */
+    int64_t filter_launches;    /* timed candidate-stream launches (k_candidates) */
+    double filter_ms;           /* their summed device time (HIP events) */
+    uint64_t filter_bytes;      /* their algorithmic bytes (mirrors, lists, counts) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */

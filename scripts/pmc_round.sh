@@ -1,0 +1,13 @@
+#!/bin/bash
+# PMC passes (one counter group per pass; no --sys/--hip trace): HBM bytes of
+# k_candidates / k_update / k_copy_maps from FETCH_SIZE / WRITE_SIZE, plus a FETCH_SIZE calibration on the
+# layout microbenchmark whose byte count is known (MI355X_MICROARCH.md §HBM).
+set -eu
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ARGS=${BENCH_ARGS:-"--steps 4 --warmup 1 --no-cpu-baseline"}
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_aos|k_soa" -d gpurun_out/pmc_cal -o cal --output-format csv -- ./scripts/ubench_layout > gpurun_out/pmc_cal.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_candidates|k_update|k_copy_maps" -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc_fetch.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_candidates|k_update|k_copy_maps" -d gpurun_out/pmc_write -o write --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc_write.log 2>&1
+python3 scripts/pmc_summary.py gpurun_out "${PMC_WORKLOAD:-cfg3_N1e6_L500_180beam}" "${PMC_TAG:-r01}"

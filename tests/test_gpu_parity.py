@@ -333,3 +333,49 @@ def test_config2_n100k_l200(fs):
     pose1, st1 = f.step(0.0, 0.03, wl.measurements(2))
     assert st1.appends + st1.hits == 4 * N and st1.appends >= N
     f.close()
+
+
+def test_candidate_list_overflow(fs):
+    """More than kMaxCand (16) candidate slots per particle: 40 landmarks crowd the
+    first measurement's point while a far measurement matches nothing, so the
+    exact kernel walks the whole truncated list and then resumes with an exact
+    scan after its last entry.  Bit-identical with and without the gate filter,
+    and equal to the oracle."""
+    import fs2_synthetic as syn
+    from oracle import oracle as orc
+    N, L = 2048, 100
+    wl = syn.Workload(N, L, seed=17)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    rng = np.random.default_rng(8)
+    ms = np.concatenate([wl.measurements(0)[:3], [[40.0, 2.0]]])
+    ox, oy = ms[0, 0] * np.cos(ms[0, 1]), ms[0, 0] * np.sin(ms[0, 1])
+    crowd = np.sort(rng.choice(L, 40, replace=False))
+    lm[:, crowd, 0] = ox + rng.normal(0, 0.05, (N, 40))
+    lm[:, crowd, 1] = oy + rng.normal(0, 0.05, (N, 40))
+    lm[:, crowd, 2] = lm[:, crowd, 5] = 0.5
+    lm[:, crowd, 3] = lm[:, crowd, 4] = 0.0
+    fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False,
+                       landmark_capacity=L + 16) for g in (True, False)]
+    for f in fl:
+        f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, L + 16)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    for sc in range(3):
+        rot, tr = syn.odometry(sc)
+        nz = rng.normal(0, 0.001 if rot else 0.0055, N)
+        u0 = 0.4 / N
+        out = [f.step(rot, tr, ms, None, nz, u0) for f in fl]
+        opose, oassoc, ors, one = o.iterate(rot, tr, ms, nz, u0)
+        assert np.array_equal(fl[0].associations(), fl[1].associations()), sc
+        assert np.array_equal(fl[0].associations(), oassoc), sc
+        assert np.array_equal(out[0][0], out[1][0])
+        assert np.allclose(out[0][0], opose, rtol=RTOL, atol=1e-12), sc
+        assert out[0][1].candidates < out[1][1].candidates
+    s0, s1 = fl[0].get_state(lm_cap=L + 16), fl[1].get_state(lm_cap=L + 16)
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(s0[4], o.cnt)
+    assert np.allclose(s0[5], o.lm, rtol=RTOL, atol=1e-12)
+    for f in fl:
+        f.close()
