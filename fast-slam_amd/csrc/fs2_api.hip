@@ -95,7 +95,7 @@ struct fs2_handle {
     double *totals = nullptr;                       // all ranks' weight totals
     int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (records, slots) per peer
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr, *kept = nullptr;
-    uint16_t *cand = nullptr;                       // [kMaxCand][n] candidate slots
+    uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
     std::vector<char *> sendbuf, recvbuf;
     std::vector<size_t> sendcap, recvcap;
@@ -124,7 +124,11 @@ static int grow_pages(fs2_handle *h, int need_slots) {
         HIP_TRY(h, hipMalloc(&p, arena_bytes));
         h->arenas.push_back(p);
     }
-    HIP_TRY(h, hipMemcpy(h->arenas_dev, h->arenas.data(), sizeof(char *) * h->arenas.size(),
+    // entries past the last arena alias arena 0, so that a streaming kernel may load
+    // (and discard) a whole group past the end of a map without a per-slot branch
+    std::vector<char *> table(kMaxPages, h->arenas[0]);
+    std::copy(h->arenas.begin(), h->arenas.end(), table.begin());
+    HIP_TRY(h, hipMemcpy(h->arenas_dev, table.data(), sizeof(char *) * kMaxPages,
                          hipMemcpyHostToDevice));
     h->cap = need_pages * kPageSlots;
     return FS2_OK;
@@ -617,7 +621,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             h->prof.filter_launches += 1;
             h->prof.filter_ms += f;
             // (cnt + phys read, count written: 12 B per particle)
-            h->prof.filter_bytes += 16ull * st.visited + 12ull * (uint64_t)h->n + 2ull * st.listed;
+            h->prof.filter_bytes += 16ull * st.visited + 12ull * (uint64_t)h->n + 8ull * st.words;
         }
         h->prof.scans += 1;
         h->prof.update_launches += passes;
@@ -627,8 +631,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         h->prof.scan_ms += a + b + c;
         // mirror reads (16 B) per visited slot when filtering, fp64 slot reads (48 B) per
         // candidate, full slot writes (48 B + 16 B mirror)
-        // + candidate lists written and read back (2 B each) and their counts
-        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 4ull * st.listed +
+        // + candidate list words written and read back (8 B each) and their counts
+        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 16ull * st.words +
                                                           8ull * (uint64_t)h->n * passes : 0ull) +
                                 48ull * st.candidates + 64ull * st.written + fixed_bytes +
                                 8ull * (uint64_t)h->nblocks();

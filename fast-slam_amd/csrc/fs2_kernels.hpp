@@ -36,7 +36,7 @@ struct DevStats {
     int32_t error_flags;
     int32_t n_copies;        // maps copied by the resample (duplicated particles)
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
-    unsigned long long listed;   // candidate list entries written by k_candidates
+    unsigned long long words;    // candidate list words (4 slots each) written by k_candidates
     double offset;           // global prefix of weights before this rank's first particle
     double t_local;          // sum of this rank's normalised weights (last local prefix)
     int32_t out_min, out_max;   // smallest / largest output index served by a local particle
@@ -105,7 +105,7 @@ struct UpdateParams {
     double gate2;            // match iff 0 <= q < gate2  (sqrt(q) < gate)
     float gate2f;            // gate2 rounded up to fp32 (mirror test)
     int32_t filter;          // use the fp32 gate mirror
-    uint16_t *cand;          // [kMaxCand][n] candidate slots (k_candidates -> k_update)
+    uint64_t *cand;          // [kMaxCand/4][n] candidate slots, four 16-bit per word
     int32_t *ncand;          // [n] candidates found (> kMaxCand: list truncated)
     double R[4];
     double init_cov[4];

@@ -49,20 +49,25 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const int c = live ? P.cnt[i] : 0;
     const int64_t pbase = live ? (int64_t)P.map.phys[i] * kPageBytes : 0;
     char *const *arenas = P.map.arenas;
-    uint16_t *cand = P.cand + (live ? i : 0);
+    // the list lives in registers until the walk ends: 16-bit slot indices, four
+    // per 64-bit word (a store inside the walk would serialise the prefetch,
+    // since vmcnt counts loads and stores in issue order)
+    uint64_t cw[kMaxCand / 4] = {};
     int nc = 0;
     unsigned visited = 0;
 
+    // Loads are branch-free within a group (a load under a per-slot branch gets a
+    // vmcnt(0) of its own and the prefetch is lost); a lane past the end of its
+    // map skips whole groups, and the arena table aliases arena 0 past the last
+    // page so every address formed here is valid.
     float4 cur[kScanGroup], nxt[kScanGroup];
 #pragma unroll
-    for (int u = 0; u < kScanGroup; ++u)
-        if (u < c) cur[u] = load_mirror(arenas[0] + pbase, u);
+    for (int u = 0; u < kScanGroup; ++u) cur[u] = load_mirror(arenas[0] + pbase, u);
     for (int j0 = 0; __any(j0 < c); j0 += kScanGroup) {
         const int j1 = j0 + kScanGroup;
         const char *npage = arenas[min(j1 >> 6, kMaxPages - 1)] + pbase;
 #pragma unroll
-        for (int u = 0; u < kScanGroup; ++u)
-            if (j1 + u < c) nxt[u] = load_mirror(npage, j1 + u);
+        for (int u = 0; u < kScanGroup; ++u) nxt[u] = load_mirror(npage, j1 + u);
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) {
             if (j0 + u < c) {
@@ -77,7 +82,10 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                         hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
                                                  P.gate2f);
                 if (hit) {
-                    if (nc < kMaxCand) cand[(int64_t)nc * n] = (uint16_t)(j0 + u);
+                    const uint64_t v = (uint64_t)(j0 + u) << (16 * (nc & 3));
+#pragma unroll
+                    for (int q = 0; q < kMaxCand / 4; ++q)
+                        cw[q] |= ((nc >> 2) == q) ? v : 0ull;
                     ++nc;
                 }
             }
@@ -85,12 +93,17 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) cur[u] = nxt[u];
     }
-    if (live) P.ncand[i] = nc;
+    if (live) {
+        P.ncand[i] = nc;
+#pragma unroll
+        for (int q = 0; q < kMaxCand / 4; ++q)
+            if (4 * q < nc) P.cand[(int64_t)q * n + i] = cw[q];
+    }
     const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
-    const unsigned long long bl = block_sum_u64<kBlock>((unsigned)min(nc, kMaxCand), lds_u);
+    const unsigned long long bl = block_sum_u64<kBlock>((unsigned)(min(nc, kMaxCand) + 3) / 4, lds_u);
     if (tid == 0) {
         atomicAdd(&P.stats->visited, bv);
-        atomicAdd(&P.stats->listed, bl);
+        atomicAdd(&P.stats->words, bl);
     }
 }
 
@@ -165,13 +178,16 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     if (live && P.filter) {
         const int nc = P.ncand[i];
         ncl = min(nc, kMaxCand);
-        jf = nc > kMaxCand ? (int)P.cand[(int64_t)(kMaxCand - 1) * n + i] + 1 : c;
+        jf = nc > kMaxCand ? (int)(P.cand[(int64_t)(kMaxCand / 4 - 1) * n + i] >> 48) + 1 : c;
     }
     int q = 0;
+    uint64_t word = 0;
     while (pend) {
         int j;
         if (q < ncl) {
-            j = P.cand[(int64_t)q * n + i];
+            if ((q & 3) == 0) word = P.cand[(int64_t)(q >> 2) * n + i];
+            j = (int)(word & 0xffffu);
+            word >>= 16;
             ++q;
         } else if (jf < c) {
             j = jf++;
