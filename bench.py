@@ -179,6 +179,7 @@ def main():
     resamples = 0
     visited = 0
     copied_slots = 0
+    cow_pages = 0
     barrier()
     t0 = time.perf_counter()
     for s in range(args.warmup, total_scans):
@@ -186,6 +187,7 @@ def main():
         resamples += st.resampled
         visited += st.slots_visited
         copied_slots += st.resample_slots
+        cow_pages += st.cow_pages
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -248,8 +250,10 @@ def main():
                       "reduce_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resample_ms_total": prof["resample_ms"],
                       "resamples": resamples,
-                      "resample_copied_map_fraction":
-                          copied_slots / max(resamples * f.n_local * (L + total_scans), 1),
+                      "resample_shared_slots": copied_slots,
+                      "cow_pages_per_particle_scan": cow_pages / (f.n_local * args.steps),
+                      "pool_collections": st.collections,
+                      "pool_pages": st.pool_pages,
                       "slots_visited_per_particle_scan": visited / (f.n_local * args.steps),
                       "icp_us": icp_us},
         }

@@ -67,12 +67,20 @@ struct fs2_handle {
     int cur = 0;
     double *x[2] = {}, *y[2] = {}, *yaw[2] = {}, *w[2] = {};
     int32_t *cnt[2] = {};
-    std::vector<char *> arenas;            // arena k: page k of every physical map
-    char **arenas_dev = nullptr;
-    int32_t *phys[2] = {};                 // logical -> physical map (A/B across resamples)
+    // landmark pages (fs2_kernels.hpp): pool, page tables A/B, free list
+    char *pool = nullptr;
+    int64_t npool = 0;                     // pages in the pool
+    uint32_t *pt[2] = {};                  // [rows][n] page tables (A/B across resamples)
+    int rows = 0;                          // page-table rows allocated
+    uint32_t *freel = nullptr;             // free page ids [0, nfree)
+    int64_t nfree = 0, cursor = 0;         // free pages listed / reserved since the last collection
+    uint8_t *mark = nullptr;               // collection marks, one byte per page
+    uint8_t epoch = 0;
+    int32_t *bcnt = nullptr;               // sweep block counts
+    int64_t *nfree_dev = nullptr;
+    uint64_t collections = 0;
     int32_t *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
-    int32_t *freelist = nullptr, *tasks = nullptr;
-    int cap = 0, max_cap = 4096;
+    int cap = 0, max_cap = kMaxSlots;
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
     int64_t *part_best_i = nullptr;
     int32_t *part_maxcnt = nullptr;
@@ -94,14 +102,14 @@ struct fs2_handle {
     RankRecord *rec = nullptr, *recs = nullptr;     // this rank's record / all ranks'
     double *totals = nullptr;                       // all ranks' weight totals
     int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (records, slots) per peer
-    int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr, *kept = nullptr;
+    int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr;
     uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
     std::vector<char *> sendbuf, recvbuf;
     std::vector<size_t> sendcap, recvcap;
     int32_t n_recv = 0;                             // particles received by the last resample
 
-    MapRef map() const { return MapRef{arenas_dev, phys[cur]}; }
+    MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
     bool sequential() const {
         const int mode = cfg.reduce_mode;
@@ -111,26 +119,87 @@ struct fs2_handle {
     }
 };
 
-static int grow_pages(fs2_handle *h, int need_slots) {
+// Page-table rows for maps of up to need_slots slots (current buffer kept).
+static int grow_rows(fs2_handle *h, int need_slots) {
     if (need_slots <= h->cap) return FS2_OK;
     if (need_slots > h->max_cap)
         return set_err(&h->err, FS2_ERR_CAPACITY, "map needs %d landmark slots, limit is %d",
                        need_slots, h->max_cap);
-    const int need_pages = (need_slots + kPageSlots - 1) / kPageSlots;
-    const size_t arena_bytes = (size_t)std::max<int64_t>(h->n, 1) * kPageBytes;
+    const int rows = (need_slots + kPageSlots - 1) / kPageSlots;
+    const size_t row_bytes = sizeof(uint32_t) * (size_t)std::max<int64_t>(h->n, 1);
     HIP_TRY(h, hipStreamSynchronize(h->stream));
-    while ((int)h->arenas.size() < need_pages) {
-        char *p = nullptr;
-        HIP_TRY(h, hipMalloc(&p, arena_bytes));
-        h->arenas.push_back(p);
+    for (int b = 0; b < 2; ++b) {
+        uint32_t *p = nullptr;
+        HIP_TRY(h, hipMalloc(&p, row_bytes * rows));
+        if (h->pt[b] && b == h->cur) HIP_TRY(h, hipMemcpy(p, h->pt[b], row_bytes * h->rows, hipMemcpyDeviceToDevice));
+        hipFree(h->pt[b]);
+        h->pt[b] = p;
     }
-    // entries past the last arena alias arena 0, so that a streaming kernel may load
-    // (and discard) a whole group past the end of a map without a per-slot branch
-    std::vector<char *> table(kMaxPages, h->arenas[0]);
-    std::copy(h->arenas.begin(), h->arenas.end(), table.begin());
-    HIP_TRY(h, hipMemcpy(h->arenas_dev, table.data(), sizeof(char *) * kMaxPages,
-                         hipMemcpyHostToDevice));
-    h->cap = need_pages * kPageSlots;
+    h->rows = rows;
+    h->cap = rows * kPageSlots;
+    return FS2_OK;
+}
+
+// Collect the page pool: every page the current page table does not refer to
+// becomes free (fs2_pages.hip); the reservation cursor restarts.
+static int collect(fs2_handle *h) {
+    hipStream_t s = h->stream;
+    if (h->epoch == 255) {
+        HIP_TRY(h, hipMemsetAsync(h->mark, 0, (size_t)h->npool, s));
+        h->epoch = 0;
+    }
+    h->epoch += 1;
+    HIP_TRY(h, launch_collect(h->map(), h->cnt[h->cur], h->npool, h->mark, h->epoch, h->bcnt, h->freel,
+                              h->nfree_dev, s));
+    HIP_TRY(h, hipMemcpyAsync(&h->nfree, h->nfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(h, hipStreamSynchronize(s));
+    h->cursor = 0;
+    h->collections += 1;
+    return FS2_OK;
+}
+
+// Pool of `pages` pages (existing pages keep their ids), its free list and marks.
+static int grow_pool(fs2_handle *h, int64_t pages) {
+    if (pages <= h->npool) return FS2_OK;
+    if (pages > (int64_t)kIdMask)
+        return set_err(&h->err, FS2_ERR_OOM, "page pool of %lld pages exceeds the id space", (long long)pages);
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    char *pool = nullptr;
+    HIP_TRY(h, hipMalloc(&pool, (size_t)pages * kPageBytes));
+    if (h->pool) HIP_TRY(h, hipMemcpy(pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
+    hipFree(h->pool);
+    h->pool = pool;
+    uint8_t *mark = nullptr;
+    HIP_TRY(h, hipMalloc(&mark, (size_t)pages));
+    HIP_TRY(h, hipMemset(mark, 0, (size_t)pages));
+    hipFree(h->mark);
+    h->mark = mark;
+    h->epoch = 0;
+    hipFree(h->freel);
+    h->freel = nullptr;
+    HIP_TRY(h, hipMalloc(&h->freel, sizeof(uint32_t) * (size_t)pages));
+    hipFree(h->bcnt);
+    h->bcnt = nullptr;
+    HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int32_t) * (size_t)collect_blocks(pages)));
+    h->npool = pages;
+    return collect(h);
+}
+
+// Reserve `need` free pages (collecting, then growing the pool, when short);
+// returns the reservation's first index into freel.
+static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
+    if (h->cursor + need > h->nfree) {
+        int rc = collect(h);
+        if (rc) return rc;
+        if (need > h->nfree) {
+            const int64_t live = h->npool - h->nfree;
+            rc = grow_pool(h, std::max(h->npool + h->npool / 2, live + 2 * need));
+            if (rc) return rc;
+        }
+    }
+    out->freel = h->freel;
+    out->base = h->cursor;
+    h->cursor += need;
     return FS2_OK;
 }
 
@@ -245,16 +314,14 @@ static void free_handle(fs2_handle *h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     for (int s = 0; s < 2; ++s) {
         hipFree(h->x[s]); hipFree(h->y[s]); hipFree(h->yaw[s]); hipFree(h->w[s]); hipFree(h->cnt[s]);
-        hipFree(h->phys[s]);
+        hipFree(h->pt[s]);
     }
-    for (char *p : h->arenas) hipFree(p);
-    hipFree(h->arenas_dev);
+    hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
-    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src); hipFree(h->kept);
+    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
     for (char *b : h->sendbuf) hipFree(b);
     for (char *b : h->recvbuf) hipFree(b);
-    hipFree(h->freelist); hipFree(h->tasks);
     hipFree(h->cand); hipFree(h->ncand);
     hipFree(h->wpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
@@ -292,8 +359,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     const int64_t G = cfg->world_size, r = cfg->rank;
     h->first = (h->n_global * r) / G;
     h->n = (h->n_global * (r + 1)) / G - h->first;
-    h->max_cap = cfg->max_landmark_capacity > 0 ? std::min(cfg->max_landmark_capacity, kMaxPages * kPageSlots)
-                                                : kMaxPages * kPageSlots;
+    h->max_cap = cfg->max_landmark_capacity > 0 ? std::min(cfg->max_landmark_capacity, kMaxSlots) : kMaxSlots;
     h->gate2 = gate_to_q(cfg->max_landmark_distance);
     auto fail = [&](int code) {
         std::string msg = h->err;
@@ -315,13 +381,11 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= alloc((void **)&h->yaw[s], n * 8) == hipSuccess;
         ok &= alloc((void **)&h->w[s], n * 8) == hipSuccess;
         ok &= alloc((void **)&h->cnt[s], n * 4) == hipSuccess;
-        ok &= alloc((void **)&h->phys[s], n * 4) == hipSuccess;
     }
-    ok &= alloc((void **)&h->arenas_dev, sizeof(char *) * kMaxPages) == hipSuccess;
+    ok &= alloc((void **)&h->nfree_dev, sizeof(int64_t)) == hipSuccess;
     ok &= alloc((void **)&h->mlo, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->out_src, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->kept, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->cand, n * 2 * kMaxCand) == hipSuccess;
     ok &= alloc((void **)&h->ncand, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
@@ -332,8 +396,6 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 4) == hipSuccess;
-    ok &= alloc((void **)&h->freelist, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->tasks, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
@@ -354,11 +416,13 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
             hipMemsetAsync(h->y[s], 0, n * 8, h->stream) != hipSuccess ||
             hipMemsetAsync(h->yaw[s], 0, n * 8, h->stream) != hipSuccess ||
             hipMemsetAsync(h->cnt[s], 0, n * 4, h->stream) != hipSuccess ||
-            launch_iota(h->phys[s], n, h->stream) != hipSuccess ||
             launch_fill(h->w[s], 1.0 / (double)h->n_global, n, h->stream) != hipSuccess)
             return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     }
-    int rc = grow_pages(h, std::max(cfg->landmark_capacity, 1));
+    int rc = grow_rows(h, std::max(cfg->landmark_capacity, 1));
+    if (rc) return fail(rc);
+    // pool: twice the initial maps plus room for a few scans of new pages
+    rc = grow_pool(h, n * h->rows * 2 + 8 * n + 1024);
     if (rc) return fail(rc);
     h->sendbuf.assign(G, nullptr);
     h->recvbuf.assign(G, nullptr);
@@ -415,7 +479,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
     if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
     HIP_TRY(h, hipSetDevice(h->cfg.device));
-    int rc = grow_pages(h, h->cnt_upper + M);
+    int rc = grow_rows(h, h->cnt_upper + M);
     if (rc) return rc;
     const int cur = h->cur;
     hipStream_t s = h->stream;
@@ -492,6 +556,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
                                       std::fabs(oy - (double)up.meas.fy[k]));
             up.meas.fe[k] = std::isfinite(e) ? std::nextafter((float)e, INFINITY) : INFINITY;
         }
+        rc = reserve_pages(h, (int64_t)up.m * h->n, &up.alloc);
+        if (rc) return rc;
+        up.map = h->map();
         if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(h->ev.e[4], s));
         HIP_TRY(h, launch_candidates(up, s));
         if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(h->ev.e[5], s));
@@ -543,17 +610,13 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.mlo = h->mlo;
     rs.mhi = h->mhi;
     rs.out_src = h->out_src;
-    rs.kept = h->kept;
     rs.x = h->x[cur]; rs.y = h->y[cur]; rs.yaw = h->yaw[cur]; rs.cnt = h->cnt[cur];
     rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
-    rs.arenas = h->arenas_dev;
-    rs.phys = h->phys[cur];
-    rs.ophys = h->phys[nxt];
+    rs.map = h->map();
+    rs.opt = h->pt[nxt];
     rs.rank_d = h->rank_d;
     rs.rank_e = h->rank_e;
     rs.iblk = h->iblk;
-    rs.freelist = h->freelist;
-    rs.tasks = h->tasks;
     rs.part_best_w = h->part_best_w;
     rs.part_best_i = h->part_best_i;
     rs.stats = h->stats_dev;
@@ -592,6 +655,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         if (G > 1) {
             rc = exchange_particles(h, rs);
             if (rc) return rc;
+            // fresh pages for the received maps: record r, row k -> base + r * rows + k
+            rc = reserve_pages(h, (int64_t)h->n_recv * h->rows, &rs.alloc);
+            if (rc) return rc;
+            rs.map = h->map();
         }
         HIP_TRY(h, launch_resample_apply(rs, s));
         if (G > 1) {
@@ -620,8 +687,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             hipEventElapsedTime(&f, h->ev.e[4], h->ev.e[5]);
             h->prof.filter_launches += 1;
             h->prof.filter_ms += f;
-            // (cnt + phys read, count written: 12 B per particle)
-            h->prof.filter_bytes += 16ull * st.visited + 12ull * (uint64_t)h->n + 8ull * st.words;
+            // mirrors, one page-table entry per page group, cnt read + count
+            // written (8 B per particle), list words
+            h->prof.filter_bytes += 16ull * st.visited + 4ull * st.groups + 8ull * (uint64_t)h->n +
+                                    8ull * st.words;
         }
         h->prof.scans += 1;
         h->prof.update_launches += passes;
@@ -631,14 +700,17 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         h->prof.scan_ms += a + b + c;
         // mirror reads (16 B) per visited slot when filtering, fp64 slot reads (48 B) per
         // candidate, full slot writes (48 B + 16 B mirror)
-        // + candidate list words written and read back (8 B each) and their counts
-        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 16ull * st.words +
-                                                          8ull * (uint64_t)h->n * passes : 0ull) +
-                                48ull * st.candidates + 64ull * st.written + fixed_bytes +
-                                8ull * (uint64_t)h->nblocks();
+        // + candidate list words written and read back (8 B each) and their counts,
+        // + page-table entry per page group and per exact slot read, page copies
+        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 4ull * st.groups +
+                                                          16ull * st.words + 8ull * (uint64_t)h->n * passes
+                                                    : 0ull) +
+                                52ull * st.candidates + 64ull * st.written + fixed_bytes +
+                                2ull * kPageBytes * st.cow_pages + 8ull * (uint64_t)h->nblocks();
         if (st.resampled)
-            // copied maps (read + write 64 B per slot) + scalar gather + plan arrays
-            h->prof.resample_bytes += 2ull * 64ull * st.resample_slots + 2ull * 36ull * (uint64_t)h->n +
+            // page-table rows (read + write 4 B per page of every output) + scalar
+            // gather + plan arrays; received maps (64 B per slot)
+            h->prof.resample_bytes += 8ull * (st.resample_slots / kPageSlots) + 2ull * 36ull * (uint64_t)h->n +
                                       40ull * (uint64_t)h->n;
     }
     if (out_pose) {
@@ -661,6 +733,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         stats->resample_slots = st.resample_slots;
         stats->error_flags = st.error_flags;
         stats->reserved = 0;
+        stats->cow_pages = st.cow_pages;
+        stats->new_pages = st.new_pages;
+        stats->collections = h->collections;
+        stats->pool_pages = (uint64_t)h->npool;
     }
     if (st.error_flags & 1)
         return set_err(&h->err, FS2_ERR_LINALG, "Singular matrix (landmark or observation covariance)");
@@ -713,8 +789,9 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             if (v < 0 || v > lm_cap) return set_err(&h->err, FS2_ERR_ARG, "count %d outside [0, %d]", v, lm_cap);
             mx = std::max(mx, v);
         }
-        int rc = grow_pages(h, mx);
+        int rc = grow_rows(h, mx);
         if (rc) return rc;
+        const int32_t rows_each = std::max(1, (mx + kPageSlots - 1) / kPageSlots);
         h->cnt_upper = std::max(h->cnt_upper, mx);
         // stage in chunks of <= 256 MiB
         const int64_t per = (int64_t)std::max(1, lm_cap) * 6 * 8;
@@ -728,7 +805,10 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             const int64_t k = std::min(chunk, count - o);
             hipError_t e = hipMemcpy(stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
             if (e == hipSuccess) e = hipMemcpy(cstage, hc.data() + o, sizeof(int32_t) * k, hipMemcpyHostToDevice);
-            if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), h->cnt[c], s);
+            PageAlloc pa{};
+            rc2 = reserve_pages(h, k * rows_each, &pa);
+            if (rc2) break;
+            if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
         }

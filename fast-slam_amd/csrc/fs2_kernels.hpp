@@ -8,19 +8,26 @@
 namespace fs2 {
 
 constexpr int kBlock = 256;          // 4 waves of 64
-constexpr int kPageSlots = 64;       // landmark slots per page
-constexpr int kMaxPages = 64;        // 4096 slots per particle max
+constexpr int kPageSlots = 8;        // landmark slots per page
+constexpr int kMaxSlots = 4096;      // landmark slots per particle max
+constexpr int kMaxRows = kMaxSlots / kPageSlots;   // page-table rows max
 constexpr int kMaxM = 4;             // measurements fused into one map pass
-constexpr int kScanGroup = 8;        // slots whose mirrors a lane loads per step (128 B)
+constexpr int kScanGroup = kPageSlots;   // slots whose mirrors a lane loads per step (128 B)
 constexpr int kMaxCand = 16;         // candidate slots listed per particle and pass
 
-// A page holds 64 slots of ONE particle's map, contiguous:
-//   [0, 1024)     64 x float4 gate mirror (x, y, s, 0)     -- read every scan
-//   [1024, 4096)  64 x 48 B fp64 slot (x, y, P00, P01, P10, P11) -- read on candidates
-// Arena k holds page k (slots 64k .. 64k+63) of every physical map.
-constexpr int kPageBytes = 4096;
-constexpr int kMirrorBytes = 1024;
+// A page holds 8 consecutive slots of a map:
+//   [0, 128)     8 x float4 gate mirror (x, y, s, 0)           -- read every scan
+//   [128, 512)   8 x 48 B fp64 slot (x, y, P00, P01, P10, P11)  -- read on candidates
+// Pages live in one pool (page id p at pool + 512 p).  A map is a row of page ids
+// in the page table pt[row][particle]; bit 31 of an entry says the map owns the
+// page (no other page-table entry refers to it) and may write it in place;
+// otherwise the first write copies the page (copy-on-write).  Resampling shares
+// pages between a source and its copies instead of copying maps.
+constexpr int kPageBytes = 512;
+constexpr int kMirrorBytes = 128;
 constexpr int kSlotBytes = 48;
+constexpr uint32_t kOwned = 0x80000000u;
+constexpr uint32_t kIdMask = 0x7fffffffu;
 
 // Device statistics of one scan (zeroed before every scan).
 struct DevStats {
@@ -34,9 +41,12 @@ struct DevStats {
     int32_t resampled;
     int32_t max_count;
     int32_t error_flags;
-    int32_t n_copies;        // maps copied by the resample (duplicated particles)
+    int32_t pad1;
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
     unsigned long long words;    // candidate list words (4 slots each) written by k_candidates
+    unsigned long long cow_pages;    // pages copied before their first write (shared)
+    unsigned long long new_pages;    // fresh pages (appends, received particles)
+    unsigned long long groups;       // page groups streamed by k_candidates
     double offset;           // global prefix of weights before this rank's first particle
     double t_local;          // sum of this rank's normalised weights (last local prefix)
     int32_t out_min, out_max;   // smallest / largest output index served by a local particle
@@ -81,11 +91,20 @@ struct MeasPack {
     float fe[kMaxM];              // >= |ox - fx|, |oy - fy| (rounded up)
 };
 
-// Logical particle m's map lives in physical map phys[m]; resampling
-// re-points phys instead of moving most maps.
+// The maps of one particle buffer: page pool + page table.
 struct MapRef {
-    char *const *arenas;     // device array: arena k = page k of every physical map
-    const int32_t *phys;     // logical -> physical map
+    char *pool;              // page id p at pool + p * kPageBytes
+    uint32_t *pt;            // [rows][n] page ids (| kOwned)
+    int64_t n;               // row stride (local particles)
+    int32_t rows;            // rows allocated
+};
+
+// Free pages reserved for one launch: lane i's t-th new page is
+// freel[base + t * n + i] (coalesced across lanes; unused ones return at the
+// next collection).
+struct PageAlloc {
+    const uint32_t *freel;
+    int64_t base;
 };
 
 struct UpdateParams {
@@ -105,6 +124,7 @@ struct UpdateParams {
     double gate2;            // match iff 0 <= q < gate2  (sqrt(q) < gate)
     float gate2f;            // gate2 rounded up to fp32 (mirror test)
     int32_t filter;          // use the fp32 gate mirror
+    PageAlloc alloc;         // up to m new pages per lane (copy-on-write, appends)
     uint64_t *cand;          // [kMaxCand/4][n] candidate slots, four 16-bit per word
     int32_t *ncand;          // [n] candidates found (> kMaxCand: list truncated)
     double R[4];
@@ -151,19 +171,16 @@ struct ResampleParams {
     int32_t nblk;            // 1024-element blocks
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
-    int32_t *kept;           // [n] local particle feeds a local output (its map stays)
     const double *x, *y, *yaw;
     const int32_t *cnt;
     double *ox, *oy, *oyaw, *ow;
     int32_t *ocnt;
-    char *const *arenas;
-    const int32_t *phys;     // current logical -> physical
-    int32_t *ophys;          // next logical -> physical
-    int32_t *rank_d;         // [n] rank among dropped particles / packed records
-    int32_t *rank_e;         // [n] rank among extra outputs / packed slot offset
+    MapRef map;              // current page table
+    uint32_t *opt;           // next page table [rows][n]
+    PageAlloc alloc;         // pages for received particles: record r, row k -> base + r*rows + k
+    int32_t *rank_d;         // [n] rank among packed records
+    int32_t *rank_e;         // [n] packed slot offset
     int32_t *iblk;           // [2 * nblk] per-block counts -> offsets
-    int32_t *freelist;       // [n] physical maps free for copies
-    int32_t *tasks;          // [n] outputs whose map is copied
     double *part_best_w;
     int64_t *part_best_i;
     DevStats *stats;
@@ -194,12 +211,20 @@ hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s);
 hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
-                         int64_t count, int32_t lm_cap, MapRef map, int32_t *cnt,
-                         hipStream_t s);
+                         int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
+                         int32_t rows_each, int32_t *cnt, hipStream_t s);
 hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm_cap,
                          MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s);
-hipError_t launch_iota(int32_t *p, int64_t n, hipStream_t s);
+hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s);
+
+// page pool collection (fs2_pages.hip): mark the pages referenced by the n maps
+// of `map`, then list every unmarked page of [0, npool) in freel; nfree_dev
+// receives the count.
+hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark,
+                          uint8_t epoch, int32_t *bcnt, uint32_t *freel, int64_t *nfree_dev,
+                          hipStream_t s);
+int64_t collect_blocks(int64_t npool);
 
 hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt,
                       int32_t n_tgt, int32_t max_iter, double thr, double *R, double *t,

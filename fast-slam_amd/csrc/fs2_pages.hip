@@ -1,0 +1,136 @@
+// fs2_pages.hip -- collection of the landmark page pool.
+//
+// Pages are shared between particles after a resample and copied on their
+// first write, so a page becomes garbage when the last page-table entry that
+// refers to it is overwritten (a copy-on-write, a dropped particle, an import).
+// Nothing counts references on the hot path; instead, when the host runs out
+// of reserved free pages, it collects: mark every page the live page table
+// refers to, then list every unmarked page as free.  Allocation between two
+// collections is a cursor into that list (PageAlloc), so no kernel takes a
+// lock or an atomic to get a page.
+//
+//   k_mark        one lane per particle, one byte store per page of its map
+//   k_sweep_count free pages per 4096-page block
+//   k_sweep_scan  exclusive scan of the block counts (one workgroup)
+//   k_sweep_write free page ids, in id order, into freel
+#include "fs2_reduce.hpp"
+
+namespace fs2 {
+
+constexpr int kSweepPer = 16;                        // page ids per thread
+constexpr int kSweepBlock = kBlock * kSweepPer;      // page ids per workgroup
+
+int64_t collect_blocks(int64_t npool) { return (npool + kSweepBlock - 1) / kSweepBlock; }
+
+__global__ __launch_bounds__(kBlock) void k_mark(const MapRef map, const int32_t *cnt, uint8_t *mark,
+                                                 uint8_t epoch) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= map.n) return;
+    const int rows = (cnt[i] + kPageSlots - 1) / kPageSlots;
+    for (int r = 0; r < rows; ++r) mark[*pt_entry(map, r, i) & kIdMask] = epoch;
+}
+
+__device__ __forceinline__ int wave_incl_scan_int(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// exclusive prefix of v over the workgroup (kBlock threads); total in *tot
+__device__ __forceinline__ int block_excl_scan(int v, int *lds, int *tot) {
+    const int inc = wave_incl_scan_int(v);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    int off = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) {
+        if (k < wid) off += lds[k];
+        t += lds[k];
+    }
+    *tot = t;
+    return off + inc - v;
+}
+
+__device__ __forceinline__ unsigned free_bits(const uint8_t *mark, int64_t npool, uint8_t epoch,
+                                              int64_t id0) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int e = 0; e < kSweepPer; ++e) {
+        const int64_t id = id0 + e;
+        if (id < npool && mark[id] != epoch) bits |= 1u << e;
+    }
+    return bits;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sweep_count(const uint8_t *mark, int64_t npool, uint8_t epoch,
+                                                        int32_t *bcnt) {
+    __shared__ int lds[kBlock / 64];
+    const int64_t id0 = (int64_t)blockIdx.x * kSweepBlock + (int64_t)threadIdx.x * kSweepPer;
+    const int f = __popc(free_bits(mark, npool, epoch, id0));
+    int tot;
+    block_excl_scan(f, lds, &tot);
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_sweep_scan(int32_t *bcnt, int64_t nb, int64_t *nfree) {
+    __shared__ int64_t lds[1024 / 64];
+    const int64_t per = (nb + 1023) / 1024;
+    const int64_t b0 = threadIdx.x * per;
+    int64_t s = 0;
+    for (int64_t k = b0; k < min(nb, b0 + per); ++k) s += bcnt[k];
+    // inclusive scan of the per-thread sums
+    int64_t v = s;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    if (lane == 63) lds[wid] = v;
+    __syncthreads();
+    int64_t off = 0, tot = 0;
+    for (int k = 0; k < 1024 / 64; ++k) {
+        if (k < wid) off += lds[k];
+        tot += lds[k];
+    }
+    int64_t run = off + v - s;
+    for (int64_t k = b0; k < min(nb, b0 + per); ++k) {
+        const int32_t c = bcnt[k];
+        bcnt[k] = (int32_t)run;
+        run += c;
+    }
+    if (threadIdx.x == 0) *nfree = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sweep_write(const uint8_t *mark, int64_t npool, uint8_t epoch,
+                                                        const int32_t *bcnt, uint32_t *freel) {
+    __shared__ int lds[kBlock / 64];
+    const int64_t id0 = (int64_t)blockIdx.x * kSweepBlock + (int64_t)threadIdx.x * kSweepPer;
+    unsigned bits = free_bits(mark, npool, epoch, id0);
+    int tot;
+    int pos = bcnt[blockIdx.x] + block_excl_scan(__popc(bits), lds, &tot);
+    while (bits) {
+        const int e = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        freel[pos++] = (uint32_t)(id0 + e);
+    }
+}
+
+hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark, uint8_t epoch,
+                          int32_t *bcnt, uint32_t *freel, int64_t *nfree_dev, hipStream_t s) {
+    const int64_t nb = collect_blocks(npool);
+    if (map.n > 0)
+        hipLaunchKernelGGL(k_mark, dim3((unsigned)((map.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, map,
+                           cnt, mark, epoch);
+    hipLaunchKernelGGL(k_sweep_count, dim3((unsigned)nb), dim3(kBlock), 0, s, mark, npool, epoch, bcnt);
+    hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, nfree_dev);
+    hipLaunchKernelGGL(k_sweep_write, dim3((unsigned)nb), dim3(kBlock), 0, s, mark, npool, epoch, bcnt, freel);
+    return hipGetLastError();
+}
+
+}  // namespace fs2

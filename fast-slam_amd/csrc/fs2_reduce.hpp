@@ -102,9 +102,17 @@ __device__ int block_max_i(int v, int *lds) {
 
 // ------------------------------------------------------------- map access ---
 
-// Page of slot j of physical map p.  Slots 4g..4g+3 never straddle a page.
-__device__ __forceinline__ char *page_of(char *const *arenas, int j, int32_t p) {
-    return arenas[j >> 6] + (int64_t)p * kPageBytes;
+__device__ __forceinline__ char *page_ptr(char *pool, uint32_t e) {
+    return pool + (int64_t)(e & kIdMask) * kPageBytes;
+}
+
+__device__ __forceinline__ uint32_t *pt_entry(const MapRef &m, int row, int64_t i) {
+    return m.pt + (int64_t)row * m.n + i;
+}
+
+// Page of slot j of particle i (read access).
+__device__ __forceinline__ char *page_of(const MapRef &m, int j, int64_t i) {
+    return page_ptr(m.pool, *pt_entry(m, j / kPageSlots, i));
 }
 
 __device__ __forceinline__ float4 load_mirror(const char *page, int j) {
@@ -116,6 +124,38 @@ __device__ __forceinline__ Slot load_slot(const char *page, int j) {
         reinterpret_cast<const double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
     const double2 a = q[0], b = q[1], c = q[2];
     return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
+}
+
+// Next reserved free page of lane i (t counts the lane's allocations).
+__device__ __forceinline__ uint32_t take_page(const PageAlloc &a, int64_t n, int64_t i, int &t) {
+    const uint32_t id = a.freel[a.base + (int64_t)t * n + i];
+    ++t;
+    return id;
+}
+
+// Page of row `row` of particle i that this lane may write: its own page, or a
+// private copy of a shared one (copy-on-write; the page table is updated).
+__device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t i,
+                                               const PageAlloc &a, int &t, unsigned &cow) {
+    uint32_t *pe = pt_entry(m, row, i);
+    const uint32_t e = *pe;
+    if (e & kOwned) return page_ptr(m.pool, e);
+    const uint32_t id = take_page(a, m.n, i, t);
+    const int4 *src = reinterpret_cast<const int4 *>(page_ptr(m.pool, e));
+    int4 *dst = reinterpret_cast<int4 *>(page_ptr(m.pool, id));
+#pragma unroll 8
+    for (int q = 0; q < kPageBytes / 16; ++q) dst[q] = src[q];
+    *pe = id | kOwned;
+    ++cow;
+    return reinterpret_cast<char *>(dst);
+}
+
+// A new, owned page for row `row` of particle i (its first slot is being appended).
+__device__ __forceinline__ char *fresh_page(const MapRef &m, int row, int64_t i, const PageAlloc &a,
+                                            int &t) {
+    const uint32_t id = take_page(a, m.n, i, t);
+    *pt_entry(m, row, i) = id | kOwned;
+    return page_ptr(m.pool, id);
 }
 
 // Every slot write keeps the fp32 gate mirror in step with the fp64 slot.

@@ -304,7 +304,6 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     P.mlo[i] = (int32_t)lo;
     P.mhi[i] = (int32_t)hi;
     const int64_t llo = max(lo, P.a), lhi = min(hi, P.a + P.n - 1);
-    P.kept[i] = (llo <= lhi) ? 1 : 0;
     for (int64_t m = llo; m <= lhi; ++m) P.out_src[m - P.a] = (int32_t)i;
     if (lo <= hi) {
         atomicMin(&P.stats->out_min, (int32_t)lo);
@@ -418,22 +417,20 @@ __global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P)
     P.shdr[k] = h;
 }
 
-// one workgroup per record: page -> packed (cnt x 16 B mirrors, cnt x 48 B slots)
+// one workgroup per record: pages -> packed (cnt x 16 B mirrors, cnt x 48 B slots)
 __global__ __launch_bounds__(kBlock) void k_pack_payload(const ResampleParams P, int32_t nrec) {
     if (!P.stats->resampled) return;
     for (int k = blockIdx.x; k < nrec; k += gridDim.x) {
         const PackHeader h = P.shdr[k];
-        const int32_t pm = P.phys[h.gsrc - P.a];
+        const int64_t i = h.gsrc - P.a;
         int4 *dm = reinterpret_cast<int4 *>(P.spay + (int64_t)h.soff * 64);
         int4 *df = dm + h.cnt;
-        for (int q = threadIdx.x; q < h.cnt; q += kBlock) {
-            const int4 *pg = reinterpret_cast<const int4 *>(P.arenas[q >> 6] + (int64_t)pm * kPageBytes);
-            dm[q] = pg[q & 63];
-        }
+        for (int q = threadIdx.x; q < h.cnt; q += kBlock)
+            dm[q] = reinterpret_cast<const int4 *>(page_of(P.map, q, i))[q % kPageSlots];
         for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
             const int j = q / 3;
-            const int4 *pg = reinterpret_cast<const int4 *>(P.arenas[j >> 6] + (int64_t)pm * kPageBytes);
-            df[q] = pg[64 + (j & 63) * 3 + (q - 3 * j)];
+            const int4 *pg = reinterpret_cast<const int4 *>(page_of(P.map, j, i) + kMirrorBytes);
+            df[q] = pg[(j % kPageSlots) * 3 + (q - 3 * j)];
         }
     }
 }
@@ -464,102 +461,59 @@ __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P,
     for (int64_t m = h.out_lo; m <= h.out_hi; ++m) P.out_src[m - P.a] = -(k + 1);
 }
 
-// dropped (feeds no local output) / extra (any output but a local source's first)
-__global__ __launch_bounds__(kBlock) void k_plan_local(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    rank2(P, [&](int64_t t, int &fd, int &fe) {
-        fd = P.kept[t] ? 0 : 1;
-        const int32_t s = P.out_src[t];
-        const bool keeper = s >= 0 && (P.a + t) == max((int64_t)P.mlo[s], P.a);
-        fe = keeper ? 0 : 1;
-    });
-}
-
-__global__ __launch_bounds__(kBlock) void k_plan_free(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= P.n || P.kept[t]) return;
-    P.freelist[P.iblk[t / kScanBlock] + P.rank_d[t]] = P.phys[t];
-}
-
-__global__ __launch_bounds__(kBlock) void k_plan_assign(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= P.n) return;
-    const int32_t s = P.out_src[m];
-    const bool keeper = s >= 0 && (P.a + m) == max((int64_t)P.mlo[s], P.a);
-    if (keeper) {
-        P.ophys[m] = P.phys[s];
-    } else {
-        const int k = P.iblk[P.nblk + m / kScanBlock] + P.rank_e[m];
-        P.ophys[m] = P.freelist[k];
-        P.tasks[k] = (int32_t)m;
-    }
-    if (m == 0) P.stats->n_copies = P.iblk[2 * P.nblk + 1];
-}
-
-// Copy the source's map into the map of every non-keeper output: one
-// workgroup per copy, 16 B per lane (fast_slam_2.py:196 deepcopy).
-constexpr int kCopyGrid = 4096;
-
-__global__ __launch_bounds__(kBlock) void k_copy_maps(const ResampleParams P) {
+// Received particles' maps into fresh pages: record r, row k takes reserved page
+// alloc.base + r * rows + k (one workgroup per record).
+__global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, int32_t nrecv) {
     __shared__ unsigned long long lds_u[kBlock / 64];
     if (!P.stats->resampled) return;
-    const int ncopy = P.stats->n_copies;
-    unsigned long long slots = 0;
-    for (int k = blockIdx.x; k < ncopy; k += gridDim.x) {
-        const int32_t m = P.tasks[k];
-        const int32_t s = P.out_src[m];
-        const int32_t to = P.ophys[m];
-        if (s >= 0) {
-            const int32_t from = P.phys[s];
-            const int cnt = P.cnt[s];
-            if (threadIdx.x == 0) slots += (unsigned long long)cnt;
-            for (int pg = 0; pg * kPageSlots < cnt; ++pg) {
-                const int ns = min(kPageSlots, cnt - pg * kPageSlots);
-                const int4 *sp = reinterpret_cast<const int4 *>(P.arenas[pg] + (int64_t)from * kPageBytes);
-                int4 *dp = reinterpret_cast<int4 *>(P.arenas[pg] + (int64_t)to * kPageBytes);
-                for (int q = threadIdx.x; q < ns; q += kBlock) dp[q] = sp[q];
-                for (int q = threadIdx.x; q < 3 * ns; q += kBlock) dp[64 + q] = sp[64 + q];
-            }
-        } else {
-            const int r = -s - 1;
-            const int p = peer_of(P, r);
-            const PackHeader &h = P.peers[p].hdr[r - P.peers[p].kbase];
-            const int4 *sm = reinterpret_cast<const int4 *>(P.peers[p].pay + (int64_t)h.soff * 64);
-            const int4 *sf = sm + h.cnt;
-            if (threadIdx.x == 0) slots += (unsigned long long)h.cnt;
-            for (int q = threadIdx.x; q < h.cnt; q += kBlock) {
-                int4 *pg = reinterpret_cast<int4 *>(P.arenas[q >> 6] + (int64_t)to * kPageBytes);
-                pg[q & 63] = sm[q];
-            }
-            for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
-                const int j = q / 3;
-                int4 *pg = reinterpret_cast<int4 *>(P.arenas[j >> 6] + (int64_t)to * kPageBytes);
-                pg[64 + (j & 63) * 3 + (q - 3 * j)] = sf[q];
-            }
+    unsigned long long pages = 0;
+    for (int r = blockIdx.x; r < nrecv; r += gridDim.x) {
+        const int p = peer_of(P, r);
+        const PackHeader &h = P.peers[p].hdr[r - P.peers[p].kbase];
+        const int4 *sm = reinterpret_cast<const int4 *>(P.peers[p].pay + (int64_t)h.soff * 64);
+        const int4 *sf = sm + h.cnt;
+        const uint32_t *ids = P.alloc.freel + P.alloc.base + (int64_t)r * P.map.rows;
+        for (int q = threadIdx.x; q < h.cnt; q += kBlock)
+            reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[q / kPageSlots]))[q % kPageSlots] = sm[q];
+        for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
+            const int j = q / 3;
+            int4 *pg = reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[j / kPageSlots]) + kMirrorBytes);
+            pg[(j % kPageSlots) * 3 + (q - 3 * j)] = sf[q];
         }
+        if (threadIdx.x == 0) pages += (h.cnt + kPageSlots - 1) / kPageSlots;
     }
-    const unsigned long long b = block_sum_u64<kBlock>(slots, lds_u);
-    if (threadIdx.x == 0 && b) atomicAdd(&P.stats->resample_slots, b);
+    const unsigned long long b = block_sum_u64<kBlock>(pages, lds_u);
+    if (threadIdx.x == 0 && b) atomicAdd(&P.stats->new_pages, b);
 }
 
+// Outputs take their source's scalars and page-table row (fast_slam_2.py:196
+// deepcopy, without copying the map: the pages are shared).  A page stays owned
+// only when its source fills exactly one local output; otherwise every output
+// copies it before its first write.
 __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParams P) {
     __shared__ double lds_d[kBlock / 64];
     __shared__ int64_t lds_l[kBlock / 64];
     if (!P.stats->resampled) return;
     const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    __shared__ unsigned long long lds_u[kBlock / 64];
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
+    unsigned slots = 0;
     if (m < P.n) {
         const int32_t s = P.out_src[m];
+        const int64_t n = P.n;
         double w;
+        int c;
         if (s >= 0) {
             P.ox[m] = P.x[s];
             P.oy[m] = P.y[s];
             P.oyaw[m] = P.yaw[s];
             w = P.w[s];
-            P.ocnt[m] = P.cnt[s];
+            c = P.cnt[s];
+            const int64_t lo = max((int64_t)P.mlo[s], P.a), hi = min((int64_t)P.mhi[s], P.a + n - 1);
+            const uint32_t keep = (hi == lo) ? 0xffffffffu : kIdMask;
+            for (int k = 0; k * kPageSlots < c; ++k)
+                P.opt[(int64_t)k * n + m] = *pt_entry(P.map, k, s) & keep;
         } else {
             const int r = -s - 1;
             const int p = peer_of(P, r);
@@ -568,12 +522,19 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             P.oy[m] = h.y;
             P.oyaw[m] = h.yaw;
             w = h.w;
-            P.ocnt[m] = h.cnt;
+            c = h.cnt;
+            const uint32_t own = (h.out_hi == h.out_lo) ? kOwned : 0u;
+            const uint32_t *ids = P.alloc.freel + P.alloc.base + (int64_t)r * P.map.rows;
+            for (int k = 0; k * kPageSlots < c; ++k) P.opt[(int64_t)k * n + m] = ids[k] | own;
         }
+        P.ocnt[m] = c;
         P.ow[m] = w;
         bv = w;
         bi = m;
+        slots = (unsigned)c;
     }
+    const unsigned long long bs = block_sum_u64<kBlock>(slots, lds_u);
+    if (threadIdx.x == 0 && bs) atomicAdd(&P.stats->resample_slots, bs);
     block_argmax<kBlock>(bv, bi, lds_d, lds_l);
     if (threadIdx.x == 0) {
         P.part_best_w[blockIdx.x] = bv;
@@ -608,13 +569,10 @@ hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s) {
     if (g == 0) return hipSuccess;
     int32_t nrecv = 0;
     for (int q = 0; q < p.npeers; ++q) nrecv += p.peers[q].K;
-    if (nrecv > 0)
+    if (nrecv > 0) {
         hipLaunchKernelGGL(k_scatter_recv, dim3((nrecv + kBlock - 1) / kBlock), dim3(kBlock), 0, s, p, nrecv);
-    hipLaunchKernelGGL(k_plan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_rank_blocks, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL(k_plan_free, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_plan_assign, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_copy_maps, dim3(kCopyGrid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL(k_unpack_recv, dim3(min(nrecv, 4096)), dim3(kBlock), 0, s, p, nrecv);
+    }
     hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
     hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
     return hipGetLastError();

@@ -3,9 +3,10 @@
 //
 // Layout in HBM (see fs2_kernels.hpp and DESIGN.md):
 //   particle scalars x/y/yaw/w (fp64) and cnt (int32) in logical particle order;
-//   landmark maps in 4 KiB pages, one page = 64 slots of ONE particle
-//   (1 KiB of fp32 gate mirrors, then 3 KiB of fp64 slots); arena k holds page
-//   k of every physical map; logical particle m owns physical map phys[m].
+//   landmark maps in 512-byte pages of 8 slots (128 B of fp32 gate mirrors, then
+//   384 B of fp64 slots) in one pool; particle i's map is row i of the page
+//   table pt[row][i]; pages are shared after resampling and copied on first
+//   write (fs2_kernels.hpp).
 //
 // Kernels
 //   k_candidates    streaming fp32 gate-mirror pass listing each particle's
@@ -47,27 +48,38 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
     const bool live = i < n;
     const int c = live ? P.cnt[i] : 0;
-    const int64_t pbase = live ? (int64_t)P.map.phys[i] * kPageBytes : 0;
-    char *const *arenas = P.map.arenas;
+    const MapRef map = P.map;
+    const uint32_t *ptrow = map.pt + (live ? i : 0);
+    const int rlast = map.rows - 1;
     // the list lives in registers until the walk ends: 16-bit slot indices, four
     // per 64-bit word (a store inside the walk would serialise the prefetch,
     // since vmcnt counts loads and stores in issue order)
     uint64_t cw[kMaxCand / 4] = {};
     int nc = 0;
-    unsigned visited = 0;
+    unsigned visited = 0, groups = 0;
 
-    // Loads are branch-free within a group (a load under a per-slot branch gets a
-    // vmcnt(0) of its own and the prefetch is lost); a lane past the end of its
-    // map skips whole groups, and the arena table aliases arena 0 past the last
-    // page so every address formed here is valid.
+    // Group g = page g of the map.  Loads are branch-free (a load under a
+    // per-slot branch gets a vmcnt(0) of its own and the prefetch is lost): a
+    // lane past the end of its map reads page 0 and discards it.  Pipeline: the
+    // page-table entry of group g+2 and the mirrors of group g+1 are in flight
+    // while group g is tested.
+    auto page_at = [&](int g, uint32_t e) -> const char * {
+        return page_ptr(map.pool, (g * kPageSlots < c) ? e : 0u);
+    };
     float4 cur[kScanGroup], nxt[kScanGroup];
+    uint32_t e1 = ptrow[(int64_t)min(1, rlast) * n];
+    {
+        const char *pg = page_at(0, ptrow[0]);
 #pragma unroll
-    for (int u = 0; u < kScanGroup; ++u) cur[u] = load_mirror(arenas[0] + pbase, u);
-    for (int j0 = 0; __any(j0 < c); j0 += kScanGroup) {
-        const int j1 = j0 + kScanGroup;
-        const char *npage = arenas[min(j1 >> 6, kMaxPages - 1)] + pbase;
+        for (int u = 0; u < kScanGroup; ++u) cur[u] = load_mirror(pg, u);
+    }
+    for (int g = 0; __any(g * kPageSlots < c); ++g) {
+        const int j0 = g * kPageSlots;
+        const uint32_t e2 = ptrow[(int64_t)min(g + 2, rlast) * n];
+        const char *npg = page_at(g + 1, e1);
 #pragma unroll
-        for (int u = 0; u < kScanGroup; ++u) nxt[u] = load_mirror(npage, j1 + u);
+        for (int u = 0; u < kScanGroup; ++u) nxt[u] = load_mirror(npg, u);
+        if (j0 < c) ++groups;
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) {
             if (j0 + u < c) {
@@ -92,6 +104,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         }
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) cur[u] = nxt[u];
+        e1 = e2;
     }
     if (live) {
         P.ncand[i] = nc;
@@ -101,9 +114,11 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
     const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
     const unsigned long long bl = block_sum_u64<kBlock>((unsigned)(min(nc, kMaxCand) + 3) / 4, lds_u);
+    const unsigned long long bg = block_sum_u64<kBlock>(groups, lds_u);
     if (tid == 0) {
         atomicAdd(&P.stats->visited, bv);
         atomicAdd(&P.stats->words, bl);
+        atomicAdd(&P.stats->groups, bg);
     }
 }
 
@@ -140,16 +155,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     double px = 0.0, py = 0.0, pyaw = 0.0, w = 0.0;
     int c = 0;
-    int32_t pm = 0;
     if (live) {
         px = P.x[i];
         py = P.y[i];
         pyaw = P.yaw[i];
         w = P.w[i];
         c = P.cnt[i];
-        pm = P.map.phys[i];
     }
-    char *const *arenas = P.map.arenas;
+    const MapRef map = P.map;
+    const int64_t il = live ? i : 0;
+    int nalloc = 0;                  // pages taken from this pass's reservation
+    unsigned cow = 0, fresh = 0;
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
         const double nz = P.noise ? P.noise[i]
@@ -195,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         } else {
             break;
         }
-        char *page = page_of(arenas, j, pm);
+        const char *page = page_of(map, j, il);
         Slot s = load_slot(page, j);
         ++candidates;
         bool mod = false;
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (!ok) todo = 0u;
         }
         if (mod) {
-            store_slot(page, j, s);
+            store_slot(writable_page(map, j / kPageSlots, il, P.alloc, nalloc, cow), j, s);
             ++written;
         }
     }
@@ -240,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         const Meas mk = s_ms[k];
         int hit = -1;
         for (int a = 0; a < nap; ++a) {
-            const Slot s = load_slot(page_of(arenas, c + a, pm), c + a);
+            const Slot s = load_slot(page_of(map, c + a, il), c + a);
             ++candidates;
             M2 I;
             if (!inv2(s.P, I)) {
@@ -255,16 +271,24 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             }
         }
         if (hit >= 0) {
-            char *pg = page_of(arenas, c + hit, pm);
-            Slot s = load_slot(pg, c + hit);
+            const int jh = c + hit;
+            Slot s = load_slot(page_of(map, jh, il), jh);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
-            store_slot(pg, c + hit, s);
+            store_slot(writable_page(map, jh / kPageSlots, il, P.alloc, nalloc, cow), jh, s);
             s_idx[k][tid] = c + hit;
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
             const Slot s{px + mk.d * cos(pyaw + mk.b), py + mk.d * sin(pyaw + mk.b),
                          M2{P.init_cov[0], P.init_cov[1], P.init_cov[2], P.init_cov[3]}};
-            store_slot(page_of(arenas, c + nap, pm), c + nap, s);
+            const int ja = c + nap;
+            char *pg;
+            if (ja % kPageSlots == 0) {
+                pg = fresh_page(map, ja / kPageSlots, il, P.alloc, nalloc);
+                ++fresh;
+            } else {
+                pg = writable_page(map, ja / kPageSlots, il, P.alloc, nalloc, cow);
+            }
+            store_slot(pg, ja, s);
             s_idx[k][tid] = -1;
             ++nap;
             ++appends;
@@ -302,6 +326,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
     const unsigned long long bap = block_sum_u64<kBlock>(appends, lds_u);
     const unsigned long long bh = block_sum_u64<kBlock>(hits, lds_u);
+    const unsigned long long bcow = block_sum_u64<kBlock>(cow, lds_u);
+    const unsigned long long bnew = block_sum_u64<kBlock>(fresh, lds_u);
     const int anysing = __syncthreads_or(singular ? 1 : 0);
     if (P.last_pass) {
         const double ws = block_sum<kBlock>(live ? w : 0.0, lds_d);
@@ -318,6 +344,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         atomicAdd(&P.stats->ambiguous, ba);
         atomicAdd(&P.stats->appends, bap);
         atomicAdd(&P.stats->hits, bh);
+        if (bcow) atomicAdd(&P.stats->cow_pages, bcow);
+        if (bnew) atomicAdd(&P.stats->new_pages, bnew);
         if (anysing) atomicOr(&P.stats->error_flags, 1);
     }
 }
@@ -422,10 +450,13 @@ hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
 
 // ------------------------------------------------------ state import/export --
 
-// stage: [count][lm_cap][6] -> maps of logical particles first .. first+count-1
+// stage: [count][lm_cap][6] -> maps of particles first .. first+count-1, written
+// into fresh pages (row k of particle p takes reserved page p * rows_each + k);
+// the pages they replace are reclaimed by the next collection.
 __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const int32_t *cnt_stage,
                                                    int64_t first, int64_t count, int32_t lm_cap,
-                                                   MapRef map, int32_t *cnt) {
+                                                   MapRef map, PageAlloc alloc, int32_t rows_each,
+                                                   int32_t *cnt) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t total = count * lm_cap;
     for (int64_t e = t; e < total; e += (int64_t)gridDim.x * kBlock) {
@@ -434,9 +465,11 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         const int c = cnt_stage[p];
         if (j == 0) cnt[first + p] = c;
         if (j >= c) continue;
+        const int row = j / kPageSlots;
+        const uint32_t id = alloc.freel[alloc.base + p * rows_each + row];
+        if (j % kPageSlots == 0) *pt_entry(map, row, first + p) = id | kOwned;
         const double *s = stage + e * 6;
-        store_slot(page_of(map.arenas, j, map.phys[first + p]), j,
-                   Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}});
+        store_slot(page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}});
     }
 }
 
@@ -448,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
         const int64_t p = e / lm_cap;
         const int j = (int)(e % lm_cap);
         if (j >= cnt[first + p]) continue;
-        const Slot s = load_slot(page_of(map.arenas, j, map.phys[first + p]), j);
+        const Slot s = load_slot(page_of(map, j, first + p), j);
         double *d = stage + e * 6;
         d[0] = s.mx; d[1] = s.my;
         d[2] = s.P.a00; d[3] = s.P.a01; d[4] = s.P.a10; d[5] = s.P.a11;
@@ -462,9 +495,10 @@ static unsigned grid_for(int64_t total) {
 }
 
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
-                         int64_t count, int32_t lm_cap, MapRef map, int32_t *cnt, hipStream_t s) {
+                         int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
+                         int32_t rows_each, int32_t *cnt, hipStream_t s) {
     hipLaunchKernelGGL(k_import, dim3(grid_for(count * lm_cap)), dim3(kBlock), 0, s, stage,
-                       cnt_stage, first, count, lm_cap, map, cnt);
+                       cnt_stage, first, count, lm_cap, map, alloc, rows_each, cnt);
     return hipGetLastError();
 }
 
@@ -485,12 +519,12 @@ hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-__global__ void k_iota(int32_t *p, int64_t n) {
+__global__ void k_iota(uint32_t *p, int64_t n) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (int64_t e = t; e < n; e += (int64_t)gridDim.x * kBlock) p[e] = (int32_t)e;
+    for (int64_t e = t; e < n; e += (int64_t)gridDim.x * kBlock) p[e] = (uint32_t)e;
 }
 
-hipError_t launch_iota(int32_t *p, int64_t n, hipStream_t s) {
+hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kBlock), 0, s, p, n);
     return hipGetLastError();
 }

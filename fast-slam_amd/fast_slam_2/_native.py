@@ -71,6 +71,10 @@ class fs2_iter_stats(C.Structure):
         ("resample_slots", C.c_uint64),
         ("error_flags", C.c_int32),
         ("reserved", C.c_int32),
+        ("cow_pages", C.c_uint64),
+        ("new_pages", C.c_uint64),
+        ("collections", C.c_uint64),
+        ("pool_pages", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -91,9 +91,13 @@ typedef struct fs2_iter_stats {
     uint64_t appends;           /* measurement updates that appended a landmark */
     uint64_t slots_written;     /* landmark slots written (EKF updates + appends) */
     uint64_t ambiguous;         /* gate decisions within 1e-9 relative of the threshold */
-    uint64_t resample_slots;    /* landmark slots copied by the resample gather */
+    uint64_t resample_slots;    /* landmark slots the resampled maps refer to (shared, not copied) */
     int32_t error_flags;        /* bit 0: singular covariance met; bit 1: non-finite weight */
     int32_t reserved;
+    uint64_t cow_pages;         /* shared 8-slot pages copied before their first write */
+    uint64_t new_pages;         /* fresh pages (appends, maps received from other ranks) */
+    uint64_t collections;       /* page-pool collections so far (handle lifetime) */
+    uint64_t pool_pages;        /* pages in the pool (512 B each) */
 } fs2_iter_stats;
 
 typedef struct fs2_profile {

@@ -379,3 +379,42 @@ def test_candidate_list_overflow(fs):
     assert np.allclose(s0[5], o.lm, rtol=RTOL, atol=1e-12)
     for f in fl:
         f.close()
+
+
+def test_page_sharing_long_run(fs):
+    """40 scans with frequent resampling: maps share pages after every resample and
+    copy them on first write; the pool is collected and grown along the way.
+    Every scan equals the oracle (which deep-copies maps like the reference)."""
+    import fs2_synthetic as syn
+    from oracle import oracle as orc
+    N, L = 3000, 30
+    wl = syn.Workload(N, L, seed=23)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    lm[:, :, 2] = lm[:, :, 5] = 0.01           # peaked likelihoods: resample often
+    cap = L + 4 * 40 + 8
+    f = fs.FastSLAM2(N, reduce="parallel", record_assoc=True, verbose=False, landmark_capacity=8)
+    f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, cap)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    rng = np.random.default_rng(12)
+    resamples = cow = 0
+    for s in range(40):
+        rot, tr = syn.odometry(s)
+        ms = wl.measurements(s)
+        nz = rng.normal(0, 0.001 if rot else 0.0055, N)
+        u0 = rng.uniform(0, 1.0 / N)
+        pose, st = f.step(rot, tr, ms, None, nz, u0)
+        opose, oassoc, ors, one = o.iterate(rot, tr, ms, nz, u0)
+        assert np.array_equal(f.associations(), oassoc), s
+        assert bool(st.resampled) == ors, s
+        assert np.allclose(pose, opose, rtol=RTOL, atol=1e-12), s
+        resamples += st.resampled
+        cow += st.cow_pages
+    assert resamples >= 5 and cow > 0
+    assert st.collections >= 2
+    xg, yg, yawg, wg, cg, lmg = f.get_state(lm_cap=cap)
+    assert np.array_equal(cg, o.cnt)
+    assert np.allclose(lmg, o.lm, rtol=RTOL, atol=1e-12)
+    assert np.allclose(wg, o.w, rtol=RTOL, atol=1e-300)
+    f.close()
