@@ -180,6 +180,7 @@ def main():
     visited = 0
     copied_slots = 0
     cow_pages = 0
+    exact_slots = 0
     barrier()
     t0 = time.perf_counter()
     for s in range(args.warmup, total_scans):
@@ -188,6 +189,7 @@ def main():
         visited += st.slots_visited
         copied_slots += st.resample_slots
         cow_pages += st.cow_pages
+        exact_slots += st.candidates
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -255,6 +257,7 @@ def main():
                       "pool_collections": st.collections,
                       "pool_pages": st.pool_pages,
                       "slots_visited_per_particle_scan": visited / (f.n_local * args.steps),
+                      "exact_slots_per_particle_scan": exact_slots / (f.n_local * args.steps),
                       "icp_us": icp_us},
         }
         print(json.dumps(out), flush=True)

@@ -70,7 +70,9 @@ struct fs2_handle {
     // landmark pages (fs2_kernels.hpp): pool, page tables A/B, free list
     char *pool = nullptr;
     int64_t npool = 0;                     // pages in the pool
-    uint32_t *pt[2] = {};                  // [rows][n] page tables (A/B across resamples)
+    uint4 *pt[2] = {};                     // [rows][n] page descriptors (A/B across resamples)
+    uint4 *rdesc = nullptr;                // descriptors of received pages [n_recv][rows]
+    size_t rdesc_cap = 0;
     int rows = 0;                          // page-table rows allocated
     uint32_t *freel = nullptr;             // free page ids [0, nfree)
     int64_t nfree = 0, cursor = 0;         // free pages listed / reserved since the last collection
@@ -126,10 +128,10 @@ static int grow_rows(fs2_handle *h, int need_slots) {
         return set_err(&h->err, FS2_ERR_CAPACITY, "map needs %d landmark slots, limit is %d",
                        need_slots, h->max_cap);
     const int rows = (need_slots + kPageSlots - 1) / kPageSlots;
-    const size_t row_bytes = sizeof(uint32_t) * (size_t)std::max<int64_t>(h->n, 1);
+    const size_t row_bytes = sizeof(uint4) * (size_t)std::max<int64_t>(h->n, 1);
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     for (int b = 0; b < 2; ++b) {
-        uint32_t *p = nullptr;
+        uint4 *p = nullptr;
         HIP_TRY(h, hipMalloc(&p, row_bytes * rows));
         if (h->pt[b] && b == h->cur) HIP_TRY(h, hipMemcpy(p, h->pt[b], row_bytes * h->rows, hipMemcpyDeviceToDevice));
         hipFree(h->pt[b]);
@@ -316,6 +318,7 @@ static void free_handle(fs2_handle *h) {
         hipFree(h->x[s]); hipFree(h->y[s]); hipFree(h->yaw[s]); hipFree(h->w[s]); hipFree(h->cnt[s]);
         hipFree(h->pt[s]);
     }
+    hipFree(h->rdesc);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
@@ -659,6 +662,16 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             rc = reserve_pages(h, (int64_t)h->n_recv * h->rows, &rs.alloc);
             if (rc) return rc;
             rs.map = h->map();
+            const size_t rbytes = sizeof(uint4) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
+            if (rbytes > h->rdesc_cap) {
+                HIP_TRY(h, hipStreamSynchronize(s));
+                hipFree(h->rdesc);
+                h->rdesc = nullptr;
+                h->rdesc_cap = 0;
+                HIP_TRY(h, hipMalloc(&h->rdesc, rbytes + rbytes / 4));
+                h->rdesc_cap = rbytes + rbytes / 4;
+            }
+            rs.rdesc = h->rdesc;
         }
         HIP_TRY(h, launch_resample_apply(rs, s));
         if (G > 1) {
@@ -687,9 +700,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             hipEventElapsedTime(&f, h->ev.e[4], h->ev.e[5]);
             h->prof.filter_launches += 1;
             h->prof.filter_ms += f;
-            // mirrors, one page-table entry per page group, cnt read + count
-            // written (8 B per particle), list words
-            h->prof.filter_bytes += 16ull * st.visited + 4ull * st.groups + 8ull * (uint64_t)h->n +
+            // one 16 B descriptor per page, the mirrors of the pages it could not
+            // reject, cnt read + count written (8 B per particle), list words
+            h->prof.filter_bytes += 16ull * st.visited + 16ull * st.groups + 8ull * (uint64_t)h->n +
                                     8ull * st.words;
         }
         h->prof.scans += 1;
@@ -702,7 +715,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         // candidate, full slot writes (48 B + 16 B mirror)
         // + candidate list words written and read back (8 B each) and their counts,
         // + page-table entry per page group and per exact slot read, page copies
-        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 4ull * st.groups +
+        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 16ull * st.groups +
                                                           16ull * st.words + 8ull * (uint64_t)h->n * passes
                                                     : 0ull) +
                                 52ull * st.candidates + 64ull * st.written + fixed_bytes +
@@ -809,6 +822,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             rc2 = reserve_pages(h, k * rows_each, &pa);
             if (rc2) break;
             if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], s);
+            if (e == hipSuccess) e = launch_describe(h->map(), h->cnt[c], first + o, k, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
         }

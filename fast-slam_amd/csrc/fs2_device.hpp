@@ -12,6 +12,7 @@
 // This makes the association gate bit-identical to the reference.
 #pragma once
 
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -139,41 +140,109 @@ __device__ __forceinline__ bool gate_reject_fast(const float4 &m, float cx, floa
     return m.z * fmaf(lx, lx, ly * ly) > gate2f;
 }
 
-// EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line:
-// it runs at most M times per particle and scan, and inlining it doubles the
-// streaming loop's register footprint (occupancy 2 -> 4 waves/SIMD).  Updates `s`
-// in place and returns the scipy multivariate_normal.pdf value.
-static __device__ __noinline__ double ekf_update(Slot &s, double px, double py, double pyaw,
-                                                    const Meas &m, const M2 &R, bool &singular) {
+// ---- page summaries (fs2_kernels.hpp) ----
+
+// fp16 bits of the largest half <= v (finite v).
+__device__ __forceinline__ uint32_t half_down(float v) {
+    uint32_t b = __half_as_ushort(__float2half_rn(v));
+    if (__half2float(__ushort_as_half((unsigned short)b)) > v)
+        b = (b & 0x8000u) ? b + 1u : (b == 0u ? 0x8001u : b - 1u);
+    return b;
+}
+// fp16 bits of the smallest half >= v.
+__device__ __forceinline__ uint32_t half_up(float v) { return half_down(-v) ^ 0x8000u; }
+
+__device__ __forceinline__ float half_lo(uint32_t w) { return __half2float(__ushort_as_half((unsigned short)(w & 0xffffu))); }
+__device__ __forceinline__ float half_hi(uint32_t w) { return __half2float(__ushort_as_half((unsigned short)(w >> 16))); }
+
+// Summary of the first nvalid mirrors of a page (descriptor .y .z .w).
+__device__ __forceinline__ uint4 describe_page(uint32_t entry, const float4 *mir, int nvalid) {
+    float xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY, smin = INFINITY;
+    bool finite = nvalid > 0;
+    for (int u = 0; u < nvalid; ++u) {
+        const float4 m = mir[u];
+        finite &= isfinite(m.x) && isfinite(m.y);
+        xmin = fminf(xmin, m.x);
+        xmax = fmaxf(xmax, m.x);
+        ymin = fminf(ymin, m.y);
+        ymax = fmaxf(ymax, m.y);
+        smin = fminf(smin, m.z);
+    }
+    if (!finite || !(smin >= 0.0f)) return make_uint4(entry, 0x7c00fc00u, 0x7c00fc00u, 0u);
+    return make_uint4(entry, half_down(xmin) | (half_up(xmax) << 16), half_down(ymin) | (half_up(ymax) << 16),
+                      __float_as_uint(smin));
+}
+
+// True when no slot of the page can pass the gate for the observed point: the
+// distance to the box is <= |fx - x_lm| for every slot, the margins use the
+// box's largest |x|, and s_min <= s, and every fp32 operation below is
+// monotone, so the value compared is <= gate_reject_fast's value for each slot.
+__device__ __forceinline__ bool page_reject(const uint4 &d, float fx, float fy, float fe, float gate2f) {
+    const float xmin = half_lo(d.y), xmax = half_hi(d.y), ymin = half_lo(d.z), ymax = half_hi(d.z);
+    const float Dx = fmaxf(fmaxf(xmin - fx, fx - xmax), 0.0f);
+    const float Dy = fmaxf(fmaxf(ymin - fy, fy - ymax), 0.0f);
+    const float Cx = fmaxf(fabsf(xmin), fabsf(xmax)) * 2.3841858e-7f;
+    const float Cy = fmaxf(fabsf(ymin), fabsf(ymax)) * 2.3841858e-7f;
+    const float lx = fmaxf(fmaf(Dx, 0.99999976f, -(fe + Cx)), 0.0f);
+    const float ly = fmaxf(fmaf(Dy, 0.99999976f, -(fe + Cy)), 0.0f);
+    return __uint_as_float(d.w) * fmaf(lx, lx, ly * ly) > gate2f;
+}
+
+// EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line: it
+// runs a few times per particle and scan, and inlined at k_update's three call
+// sites it would inflate the kernel's register footprint.
+struct EkfOut {
+    Slot s;
+    double lik;
+    int singular;
+};
+
+// Arguments and result by value, so that the call passes everything in VGPRs
+// (a Slot& would live in scratch memory, and a scratch store ahead of the
+// caller's next global load makes that load's wait cover the store too).
+static __device__ __noinline__ EkfOut ekf_step(Slot s, double px, double py, double pyaw, double md,
+                                              double mb, double r00, double r01, double r10, double r11) {
     const double dx = s.mx - px, dy = s.my - py;
     const double q = dx * dx + dy * dy;          // reference: pow(dx, 2) + pow(dy, 2)
     const double r = sqrt(q);
     const double ang = atan2(dy, dx) - pyaw;
-    const double nu0 = m.d - r;
-    const double nu1 = pymod((m.b - ang) + kPi, kTwoPi) - kPi;
+    const double nu0 = md - r;
+    const double nu1 = pymod((mb - ang) + kPi, kTwoPi) - kPi;
     const M2 H{dx / r, dy / r, -dy / q, dx / q};
     const M2 Ht = tr2(H);
     M2 S = mm2(mm2(H, s.P), Ht);
-    S.a00 += R.a00; S.a01 += R.a01; S.a10 += R.a10; S.a11 += R.a11;
+    S.a00 += r00; S.a01 += r01; S.a10 += r10; S.a11 += r11;
     M2 Si;
-    if (!inv2(S, Si)) {
-        singular = true;
-        return 0.0;
-    }
+    if (!inv2(S, Si)) return EkfOut{s, 0.0, 1};
     const M2 K = mm2(mm2(s.P, Ht), Si);
     const double kn0 = fma(K.a00, nu0, K.a01 * nu1);
     const double kn1 = fma(K.a10, nu0, K.a11 * nu1);
     const M2 KH = mm2(K, H);
     const M2 IKH{1.0 - KH.a00, 0.0 - KH.a01, 0.0 - KH.a10, 1.0 - KH.a11};
     const M2 Pn = mm2(IKH, s.P);
-    s.mx = s.mx + kn0;
-    s.my = s.my + kn1;
-    s.P = Pn;
+    EkfOut o;
+    o.s.mx = s.mx + kn0;
+    o.s.my = s.my + kn1;
+    o.s.P = Pn;
     // scipy: eigh on the lower triangle; closed form of log|S| and nu^T S^-1 nu.
     const double a = S.a00, b = S.a10, c = S.a11;
     const double det = a * c - b * b;
     const double maha = (c * nu0 * nu0 - 2.0 * b * nu0 * nu1 + a * nu1 * nu1) / det;
-    return exp(-0.5 * (2.0 * kLog2Pi + log(det) + maha));
+    o.lik = exp(-0.5 * (2.0 * kLog2Pi + log(det) + maha));
+    o.singular = 0;
+    return o;
+}
+
+// Updates `s` in place and returns the scipy multivariate_normal.pdf value.
+__device__ __forceinline__ double ekf_update(Slot &s, double px, double py, double pyaw, const Meas &m,
+                                             const M2 &R, bool &singular) {
+    const EkfOut o = ekf_step(s, px, py, pyaw, m.d, m.b, R.a00, R.a01, R.a10, R.a11);
+    if (o.singular) {
+        singular = true;
+        return 0.0;
+    }
+    s = o.s;
+    return o.lik;
 }
 
 // ------------------------------------------------------------- Philox4x32-10

@@ -18,11 +18,16 @@ constexpr int kMaxCand = 16;         // candidate slots listed per particle and 
 // A page holds 8 consecutive slots of a map:
 //   [0, 128)     8 x float4 gate mirror (x, y, s, 0)           -- read every scan
 //   [128, 512)   8 x 48 B fp64 slot (x, y, P00, P01, P10, P11)  -- read on candidates
-// Pages live in one pool (page id p at pool + 512 p).  A map is a row of page ids
-// in the page table pt[row][particle]; bit 31 of an entry says the map owns the
-// page (no other page-table entry refers to it) and may write it in place;
-// otherwise the first write copies the page (copy-on-write).  Resampling shares
-// pages between a source and its copies instead of copying maps.
+// Pages live in one pool (page id p at pool + 512 p).  A map is a row of page
+// descriptors in the page table pt[row][particle] (uint4):
+//   .x  page id; bit 31 says the map owns the page (no other entry refers to
+//       it) and may write it in place, otherwise the first write copies the page
+//       (copy-on-write).  Resampling shares pages instead of copying maps.
+//   .y  fp16 (min, max) of the page's mirror x, rounded outward
+//   .z  fp16 (min, max) of the page's mirror y, rounded outward
+//   .w  fp32 smallest mirror s of the page (0: never reject)
+// The summary lets the candidate stream reject a whole page with one test that
+// is never less conservative than the slot tests it replaces (page_reject).
 constexpr int kPageBytes = 512;
 constexpr int kMirrorBytes = 128;
 constexpr int kSlotBytes = 48;
@@ -94,7 +99,7 @@ struct MeasPack {
 // The maps of one particle buffer: page pool + page table.
 struct MapRef {
     char *pool;              // page id p at pool + p * kPageBytes
-    uint32_t *pt;            // [rows][n] page ids (| kOwned)
+    uint4 *pt;               // [rows][n] page descriptors
     int64_t n;               // row stride (local particles)
     int32_t rows;            // rows allocated
 };
@@ -176,7 +181,8 @@ struct ResampleParams {
     double *ox, *oy, *oyaw, *ow;
     int32_t *ocnt;
     MapRef map;              // current page table
-    uint32_t *opt;           // next page table [rows][n]
+    uint4 *opt;              // next page table [rows][n]
+    uint4 *rdesc;            // [nrecv][rows] descriptors of received pages
     PageAlloc alloc;         // pages for received particles: record r, row k -> base + r*rows + k
     int32_t *rank_d;         // [n] rank among packed records
     int32_t *rank_e;         // [n] packed slot offset
@@ -213,6 +219,9 @@ hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
                          int32_t rows_each, int32_t *cnt, hipStream_t s);
+// page summaries of rows [0, ceil(cnt/8)) of particles first .. first+count-1
+hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count,
+                           hipStream_t s);
 hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm_cap,
                          MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s);

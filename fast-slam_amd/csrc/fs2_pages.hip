@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kBlock) void k_mark(const MapRef map, const int32_t
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= map.n) return;
     const int rows = (cnt[i] + kPageSlots - 1) / kPageSlots;
-    for (int r = 0; r < rows; ++r) mark[*pt_entry(map, r, i) & kIdMask] = epoch;
+    for (int r = 0; r < rows; ++r) mark[pt_entry(map, r, i)->x & kIdMask] = epoch;
 }
 
 __device__ __forceinline__ int wave_incl_scan_int(int v) {

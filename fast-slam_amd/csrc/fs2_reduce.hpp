@@ -102,17 +102,19 @@ __device__ int block_max_i(int v, int *lds) {
 
 // ------------------------------------------------------------- map access ---
 
+typedef int v4i __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ char *page_ptr(char *pool, uint32_t e) {
     return pool + (int64_t)(e & kIdMask) * kPageBytes;
 }
 
-__device__ __forceinline__ uint32_t *pt_entry(const MapRef &m, int row, int64_t i) {
+__device__ __forceinline__ uint4 *pt_entry(const MapRef &m, int row, int64_t i) {
     return m.pt + (int64_t)row * m.n + i;
 }
 
 // Page of slot j of particle i (read access).
 __device__ __forceinline__ char *page_of(const MapRef &m, int j, int64_t i) {
-    return page_ptr(m.pool, *pt_entry(m, j / kPageSlots, i));
+    return page_ptr(m.pool, pt_entry(m, j / kPageSlots, i)->x);
 }
 
 __device__ __forceinline__ float4 load_mirror(const char *page, int j) {
@@ -137,15 +139,20 @@ __device__ __forceinline__ uint32_t take_page(const PageAlloc &a, int64_t n, int
 // private copy of a shared one (copy-on-write; the page table is updated).
 __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t i,
                                                const PageAlloc &a, int &t, unsigned &cow) {
-    uint32_t *pe = pt_entry(m, row, i);
-    const uint32_t e = *pe;
+    uint4 *pe = pt_entry(m, row, i);
+    const uint32_t e = pe->x;
     if (e & kOwned) return page_ptr(m.pool, e);
     const uint32_t id = take_page(a, m.n, i, t);
-    const int4 *src = reinterpret_cast<const int4 *>(page_ptr(m.pool, e));
-    int4 *dst = reinterpret_cast<int4 *>(page_ptr(m.pool, id));
-#pragma unroll 8
-    for (int q = 0; q < kPageBytes / 16; ++q) dst[q] = src[q];
-    *pe = id | kOwned;
+    const v4i *src = reinterpret_cast<const v4i *>(page_ptr(m.pool, e));
+    v4i *dst = reinterpret_cast<v4i *>(page_ptr(m.pool, id));
+    for (int q0 = 0; q0 < kPageBytes / 16; q0 += 8) {
+        v4i v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[q0 + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dst[q0 + u] = v[u];
+    }
+    pe->x = id | kOwned;       // same content: the summary stays valid
     ++cow;
     return reinterpret_cast<char *>(dst);
 }
@@ -154,17 +161,46 @@ __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t
 __device__ __forceinline__ char *fresh_page(const MapRef &m, int row, int64_t i, const PageAlloc &a,
                                             int &t) {
     const uint32_t id = take_page(a, m.n, i, t);
-    *pt_entry(m, row, i) = id | kOwned;
+    pt_entry(m, row, i)->x = id | kOwned;      // summary refreshed by the caller
     return page_ptr(m.pool, id);
 }
 
 // Every slot write keeps the fp32 gate mirror in step with the fp64 slot.
-__device__ __forceinline__ void store_slot(char *page, int j, const Slot &s) {
+__device__ __forceinline__ float4 store_slot(char *page, int j, const Slot &s) {
     double2 *q = reinterpret_cast<double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
     q[0] = make_double2(s.mx, s.my);
     q[1] = make_double2(s.P.a00, s.P.a01);
     q[2] = make_double2(s.P.a10, s.P.a11);
-    reinterpret_cast<float4 *>(page)[j & (kPageSlots - 1)] = mirror_of(s);
+    const float4 mv = mirror_of(s);
+    reinterpret_cast<float4 *>(page)[j & (kPageSlots - 1)] = mv;
+    return mv;
+}
+
+// Page summary after slot j (mirror mv) of particle i was written: the first
+// slot appended to a fresh page starts a new summary, otherwise the box grows to include mv and s_min
+// takes min(s_min, s).  The result covers every slot now in the page (it may
+// also cover values since replaced: still conservative).
+__device__ __forceinline__ void note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
+    uint4 *pe = pt_entry(m, j / kPageSlots, i);
+    uint4 d = *pe;
+    if (fresh) {
+        d = describe_page(d.x, &mv, 1);
+    } else if (!(isfinite(mv.x) && isfinite(mv.y))) {
+        d = describe_page(d.x, &mv, 0);
+    } else {
+        d.y = half_down(fminf(half_lo(d.y), mv.x)) | (half_up(fmaxf(half_hi(d.y), mv.x)) << 16);
+        d.z = half_down(fminf(half_lo(d.z), mv.y)) | (half_up(fmaxf(half_hi(d.z), mv.y)) << 16);
+        d.w = __float_as_uint(fminf(__uint_as_float(d.w), mv.z));
+    }
+    *pe = d;
+}
+
+// Recompute the summary of page `row` of particle i from its mirrors (map size c).
+__device__ __forceinline__ void refresh_summary(const MapRef &m, int row, int64_t i, int c) {
+    uint4 *pe = pt_entry(m, row, i);
+    const uint32_t e = pe->x;
+    const float4 *mir = reinterpret_cast<const float4 *>(page_ptr(m.pool, e));
+    *pe = describe_page(e, mir, min(kPageSlots, c - row * kPageSlots));
 }
 
 // Gate decisions this close to the threshold could depend on ulp-level

@@ -480,6 +480,12 @@ __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, 
             int4 *pg = reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[j / kPageSlots]) + kMirrorBytes);
             pg[(j % kPageSlots) * 3 + (q - 3 * j)] = sf[q];
         }
+        __syncthreads();
+        // summaries of the new pages, from the payload's mirrors
+        const float4 *mir = reinterpret_cast<const float4 *>(sm);
+        for (int k = threadIdx.x; k * kPageSlots < h.cnt; k += kBlock)
+            P.rdesc[(int64_t)r * P.map.rows + k] =
+                describe_page(ids[k], mir + k * kPageSlots, min(kPageSlots, h.cnt - k * kPageSlots));
         if (threadIdx.x == 0) pages += (h.cnt + kPageSlots - 1) / kPageSlots;
     }
     const unsigned long long b = block_sum_u64<kBlock>(pages, lds_u);
@@ -512,8 +518,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             c = P.cnt[s];
             const int64_t lo = max((int64_t)P.mlo[s], P.a), hi = min((int64_t)P.mhi[s], P.a + n - 1);
             const uint32_t keep = (hi == lo) ? 0xffffffffu : kIdMask;
-            for (int k = 0; k * kPageSlots < c; ++k)
-                P.opt[(int64_t)k * n + m] = *pt_entry(P.map, k, s) & keep;
+            for (int k = 0; k * kPageSlots < c; ++k) {
+                uint4 e = *pt_entry(P.map, k, s);
+                e.x &= keep;
+                P.opt[(int64_t)k * n + m] = e;
+            }
         } else {
             const int r = -s - 1;
             const int p = peer_of(P, r);
@@ -524,8 +533,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             w = h.w;
             c = h.cnt;
             const uint32_t own = (h.out_hi == h.out_lo) ? kOwned : 0u;
-            const uint32_t *ids = P.alloc.freel + P.alloc.base + (int64_t)r * P.map.rows;
-            for (int k = 0; k * kPageSlots < c; ++k) P.opt[(int64_t)k * n + m] = ids[k] | own;
+            const uint4 *rd = P.rdesc + (int64_t)r * P.map.rows;
+            for (int k = 0; k * kPageSlots < c; ++k) {
+                uint4 e = rd[k];
+                e.x |= own;
+                P.opt[(int64_t)k * n + m] = e;
+            }
         }
         P.ocnt[m] = c;
         P.ow[m] = w;

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const bool live = i < n;
     const int c = live ? P.cnt[i] : 0;
     const MapRef map = P.map;
-    const uint32_t *ptrow = map.pt + (live ? i : 0);
+    const uint4 *ptrow = map.pt + (live ? i : 0);
     const int rlast = map.rows - 1;
     // the list lives in registers until the walk ends: 16-bit slot indices, four
     // per 64-bit word (a store inside the walk would serialise the prefetch,
@@ -58,33 +58,33 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     int nc = 0;
     unsigned visited = 0, groups = 0;
 
-    // Group g = page g of the map.  Loads are branch-free (a load under a
-    // per-slot branch gets a vmcnt(0) of its own and the prefetch is lost): a
-    // lane past the end of its map reads page 0 and discards it.  Pipeline: the
-    // page-table entry of group g+2 and the mirrors of group g+1 are in flight
-    // while group g is tested.
-    auto page_at = [&](int g, uint32_t e) -> const char * {
-        return page_ptr(map.pool, (g * kPageSlots < c) ? e : 0u);
-    };
-    float4 cur[kScanGroup], nxt[kScanGroup];
-    uint32_t e1 = ptrow[(int64_t)min(1, rlast) * n];
-    {
-        const char *pg = page_at(0, ptrow[0]);
-#pragma unroll
-        for (int u = 0; u < kScanGroup; ++u) cur[u] = load_mirror(pg, u);
-    }
+    // Page g: its descriptor is tested against every measurement first (the
+    // next descriptor already in flight); only pages it cannot reject have their
+    // 8 mirrors loaded, and the wave loads them together (lanes without an open
+    // page read page 0, which stays in cache, and discard it).
+    uint4 d1 = ptrow[0];
     for (int g = 0; __any(g * kPageSlots < c); ++g) {
         const int j0 = g * kPageSlots;
-        const uint32_t e2 = ptrow[(int64_t)min(g + 2, rlast) * n];
-        const char *npg = page_at(g + 1, e1);
+        const uint4 d = d1;
+        d1 = ptrow[(int64_t)min(g + 1, rlast) * n];
+        bool open = false;
+        if (j0 < c) {
+            ++groups;
 #pragma unroll
-        for (int u = 0; u < kScanGroup; ++u) nxt[u] = load_mirror(npg, u);
-        if (j0 < c) ++groups;
+            for (int k = 0; k < MAXM; ++k)
+                if (k < P.m) open |= !page_reject(d, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f);
+        }
+        if (!__any(open)) continue;
+        const char *pg = page_ptr(map.pool, open ? d.x : 0u);
+        float4 mir[kScanGroup];
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
+        if (!open) continue;
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) {
             if (j0 + u < c) {
                 ++visited;
-                const float4 mv = cur[u];
+                const float4 mv = mir[u];
                 const float cx = fabsf(mv.x) * 2.3841858e-7f;   // 2^-22 |x_lm|
                 const float cy = fabsf(mv.y) * 2.3841858e-7f;
                 bool hit = false;
@@ -102,9 +102,6 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                 }
             }
         }
-#pragma unroll
-        for (int u = 0; u < kScanGroup; ++u) cur[u] = nxt[u];
-        e1 = e2;
     }
     if (live) {
         P.ncand[i] = nc;
@@ -143,6 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ Meas s_ms[MAXM];                 // this pass's measurements
     __shared__ double s_lik[MAXM][kBlock];      // per (measurement, lane) likelihood
     __shared__ int s_idx[MAXM][kBlock];         // per (measurement, lane) association
+    __shared__ uint2 s_cow[kBlock / 64][64 * (MAXM + 1)];   // per wave: (shared page, copy)
 
     const int tid = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
@@ -166,6 +164,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     const int64_t il = live ? i : 0;
     int nalloc = 0;                  // pages taken from this pass's reservation
     unsigned cow = 0, fresh = 0;
+    uint64_t mods = 0;               // existing slots modified in phase A (16 bits each)
+    int nmod = 0;
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
         const double nz = P.noise ? P.noise[i]
@@ -243,8 +243,92 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (!ok) todo = 0u;
         }
         if (mod) {
-            store_slot(writable_page(map, j / kPageSlots, il, P.alloc, nalloc, cow), j, s);
+            // written back in phase B; only the slot index is kept
+            mods |= (uint64_t)j << (16 * nmod);
+            ++nmod;
             ++written;
+        }
+    }
+
+    // ---- phase B: every store of this pass.  Stores come last because vmcnt
+    // counts loads and stores in issue order: a store ahead of a load makes the
+    // wait for that load wait for the store as well. ----
+
+    uint32_t modpage[MAXM];          // page of each modified slot, once owned
+    // (B1) own every page this lane will write: the modified slots' pages and the
+    // page the first append lands in (later appends start fresh pages).  The
+    // wave lists its shared pages in LDS and copies them together, 16 pages (8
+    // independent 16-byte loads per lane) per batch: a copy loop with one load
+    // per iteration would pay a full memory latency per page.
+    {
+        const int lane = tid & 63, wid = tid >> 6;
+        const int nrows = nmod + ((pend != 0u && c % kPageSlots != 0) ? 1 : 0);
+        int T = 0;                    // pages listed by the wave so far
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) modpage[t] = 0u;
+#pragma unroll
+        for (int t = 0; t < MAXM + 1; ++t) {
+            bool task = false;
+            uint32_t src = 0, dst = 0;
+            if (t < nrows) {
+                const int r = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) / kPageSlots : c / kPageSlots;
+                uint4 *pe = pt_entry(map, r, il);
+                const uint32_t e = pe->x;
+                uint32_t id = e & kIdMask;
+                if (!(e & kOwned)) {   // a later row of this lane on the same page now reads owned
+                    task = true;
+                    src = id;
+                    dst = take_page(P.alloc, n, il, nalloc);
+                    pe->x = dst | kOwned;
+                    id = dst;
+                    ++cow;
+                }
+#pragma unroll
+                for (int u = 0; u < MAXM; ++u)
+                    if (u == t) modpage[u] = id;
+            }
+            const uint64_t bm = __ballot(task);
+            if (task) s_cow[wid][T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
+            T += __popcll(bm);
+        }
+        __syncthreads();
+        const int off = (lane & 31) * 16;
+        for (int base = 0; base < T; base += 16) {
+            v4i v[8];                 // clang vector type: HIP's int4 struct defeats SROA here
+            uint32_t dst[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint2 tk = s_cow[wid][min(base + 2 * u + (lane >> 5), T - 1)];
+                dst[u] = tk.y;
+                v[u] = *reinterpret_cast<const v4i *>(page_ptr(map.pool, tk.x) + off);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, dst[u]) + off) = v[u];
+        }
+        __threadfence_block();        // copies land before the slot stores below
+    }
+
+    // (B2) modified slots: the EKF updates of phase A replayed on the original slot
+    // in measurement order (bit-identical), then stored.  All reloads are issued
+    // first (branch-free: missing entries read slot 0 of page 0 and are unused).
+    {
+        Slot sl[MAXM];
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) {
+            const int j = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) : 0;
+            sl[t] = load_slot(page_ptr(map.pool, modpage[t]), j);
+        }
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) {
+            if (t < nmod) {
+                const int j = (int)((mods >> (16 * t)) & 0xffffu);
+                Slot s = sl[t];
+                bool dummy = false;
+#pragma unroll
+                for (int k = 0; k < MAXM; ++k)
+                    if (s_idx[k][tid] == j) (void)ekf_update(s, px, py, pyaw, s_ms[k], R, dummy);
+                note_write(map, j, il, store_slot(page_ptr(map.pool, modpage[t]), j, s), false);
+            }
         }
     }
 
@@ -274,7 +358,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             const int jh = c + hit;
             Slot s = load_slot(page_of(map, jh, il), jh);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
-            store_slot(writable_page(map, jh / kPageSlots, il, P.alloc, nalloc, cow), jh, s);
+            note_write(map, jh, il, store_slot(writable_page(map, jh / kPageSlots, il, P.alloc, nalloc, cow), jh, s),
+                       false);
             s_idx[k][tid] = c + hit;
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
@@ -288,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             } else {
                 pg = writable_page(map, ja / kPageSlots, il, P.alloc, nalloc, cow);
             }
-            store_slot(pg, ja, s);
+            note_write(map, ja, il, store_slot(pg, ja, s), ja % kPageSlots == 0);
             s_idx[k][tid] = -1;
             ++nap;
             ++appends;
@@ -467,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         if (j >= c) continue;
         const int row = j / kPageSlots;
         const uint32_t id = alloc.freel[alloc.base + p * rows_each + row];
-        if (j % kPageSlots == 0) *pt_entry(map, row, first + p) = id | kOwned;
+        if (j % kPageSlots == 0) pt_entry(map, row, first + p)->x = id | kOwned;
         const double *s = stage + e * 6;
         store_slot(page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}});
     }
@@ -488,6 +573,18 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
     }
 }
 
+__global__ __launch_bounds__(kBlock) void k_describe(MapRef map, const int32_t *cnt, int64_t first,
+                                                     int64_t count) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t total = count * map.rows;
+    for (int64_t e = t; e < total; e += (int64_t)gridDim.x * kBlock) {
+        const int64_t p = first + e % count;      // consecutive lanes: consecutive particles
+        const int row = (int)(e / count);
+        const int c = cnt[p];
+        if (row * kPageSlots < c) refresh_summary(map, row, p, c);
+    }
+}
+
 static unsigned grid_for(int64_t total) {
     int64_t g = (total + kBlock - 1) / kBlock;
     if (g > 8192) g = 8192;
@@ -499,6 +596,13 @@ hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t 
                          int32_t rows_each, int32_t *cnt, hipStream_t s) {
     hipLaunchKernelGGL(k_import, dim3(grid_for(count * lm_cap)), dim3(kBlock), 0, s, stage,
                        cnt_stage, first, count, lm_cap, map, alloc, rows_each, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_describe, dim3(grid_for(count * map.rows)), dim3(kBlock), 0, s, map, cnt, first,
+                       count);
     return hipGetLastError();
 }
 

@@ -418,3 +418,35 @@ def test_page_sharing_long_run(fs):
     assert np.allclose(lmg, o.lm, rtol=RTOL, atol=1e-12)
     assert np.allclose(wg, o.w, rtol=RTOL, atol=1e-300)
     f.close()
+
+
+def test_page_summary_extreme_coordinates(fs):
+    """Page summaries store fp16 boxes rounded outward: maps far beyond fp16 range
+    (|x| ~ 1e5), near its limit (6.5e4) and at tiny scales (1e-6) must give the same
+    associations and state with and without the filter."""
+    N, L = 1024, 40
+    rng = np.random.default_rng(31)
+    for scale in (1e5, 6.55e4, 1e-6):
+        lm = np.zeros((N, L, 6))
+        base = rng.uniform(-1, 1, (L, 2)) * scale
+        lm[:, :, 0:2] = base + rng.normal(0, 0.02 * scale, (N, L, 2))
+        lm[:, :, 2] = lm[:, :, 5] = (0.1 * scale) ** 2
+        ms = np.array([[np.hypot(*base[k]) * 1.001, np.arctan2(base[k, 1], base[k, 0])]
+                       for k in (3, 17, 29)] + [[scale * 3.0, 0.5]])
+        x = rng.normal(0, 0.01 * scale, N)
+        y = rng.normal(0, 0.01 * scale, N)
+        yaw = rng.normal(0, 0.01, N)
+        fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False)
+              for g in (True, False)]
+        for f in fl:
+            f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+        for sc in range(3):
+            nz = rng.normal(0, 0.0055, N)
+            out = [f.step(0.0, 0.03, ms, None, nz, 0.3 / N) for f in fl]
+            assert np.array_equal(fl[0].associations(), fl[1].associations()), (scale, sc)
+            assert np.array_equal(out[0][0], out[1][0])
+        s0, s1 = fl[0].get_state(lm_cap=L + 16), fl[1].get_state(lm_cap=L + 16)
+        for a, b in zip(s0, s1):
+            assert np.array_equal(a, b, equal_nan=True)
+        for f in fl:
+            f.close()
