@@ -634,7 +634,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     }
     // normalise (:161-175), local prefix of the normalised weights, this rank's record
     HIP_TRY(h, launch_normalize(rp, s));
-    HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    // sharded ranks need their prefix end in the record; one GPU needs the
+    // prefix only when the rule fires (computed below, kernels exit otherwise)
+    if (G > 1) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
     HIP_TRY(h, launch_finalize(rp, s));
     if (G > 1) {
         rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
@@ -642,6 +644,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     }
     // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183)
     HIP_TRY(h, launch_global_finalize(rp, s));
+    if (G == 1) {
+        rs.lazy = 1;
+        HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    }
     if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[2], s));
 
     // ---- low-variance resample (:177-199); on one GPU the kernels exit unless the

@@ -174,6 +174,7 @@ struct ResampleParams {
     double *c;               // local inclusive prefix [n]
     double *bsum;            // block sums (prefix)
     int32_t nblk;            // 1024-element blocks
+    int32_t lazy;            // prefix kernels run only when the resample rule fired
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
     const double *x, *y, *yaw;

@@ -205,6 +205,7 @@ __device__ __forceinline__ int wave_incl_scan_i(int v) {
 
 // Sequential running sum, the reference's order (fast_slam_2.py:184-193).
 __global__ __launch_bounds__(1) void k_scan_seq(const ResampleParams P) {
+    if (P.lazy && !P.stats->resampled) return;
     double c = 0.0;
     for (int64_t i = 0; i < P.n; ++i) {
         c = (i == 0) ? P.w[0] : c + P.w[i];
@@ -215,6 +216,7 @@ __global__ __launch_bounds__(1) void k_scan_seq(const ResampleParams P) {
 
 __global__ __launch_bounds__(kBlock) void k_scan_local(const ResampleParams P) {
     __shared__ double lds[kBlock / 64];
+    if (P.lazy && !P.stats->resampled) return;
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
     double v[kScanPer];
     double run = 0.0;
@@ -239,16 +241,29 @@ __global__ __launch_bounds__(kBlock) void k_scan_local(const ResampleParams P) {
     if (threadIdx.x == kBlock - 1) P.bsum[blockIdx.x] = off + v[kScanPer - 1];
 }
 
-__global__ __launch_bounds__(1) void k_scan_blocks(const ResampleParams P) {
-    double acc = 0.0;
-    for (int b = 0; b < P.nblk; ++b) {
+// exclusive scan of the block sums: 1024 threads, each a contiguous run of blocks
+__global__ __launch_bounds__(1024) void k_scan_blocks(const ResampleParams P) {
+    __shared__ double lds[1024 / 64];
+    if (P.lazy && !P.stats->resampled) return;
+    const int per = (P.nblk + 1023) / 1024;
+    const int b0 = threadIdx.x * per, b1 = min(P.nblk, b0 + per);
+    double run = 0.0;
+    for (int b = b0; b < b1; ++b) run += P.bsum[b];
+    const double incl = wave_incl_scan(run);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 63) lds[wid] = incl;
+    __syncthreads();
+    double off = incl - run;
+    for (int k = 0; k < wid; ++k) off += lds[k];
+    for (int b = b0; b < b1; ++b) {
         const double t = P.bsum[b];
-        P.bsum[b] = acc;    // exclusive offset
-        acc += t;
+        P.bsum[b] = off;
+        off += t;
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_scan_add(const ResampleParams P) {
+    if (P.lazy && !P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < P.n) {
         const double v = P.c[i] + P.bsum[i / kScanBlock];
@@ -264,7 +279,7 @@ hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s)
         hipLaunchKernelGGL(k_scan_seq, dim3(1), dim3(1), 0, s, p);
     } else {
         hipLaunchKernelGGL(k_scan_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1), 0, s, p);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, p);
         hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(kBlock), 0, s, p);
     }
     return hipGetLastError();
@@ -276,8 +291,18 @@ __device__ __forceinline__ double u_of(double u0, int64_t m, int64_t N) {
     return u0 + (double)m * (1.0 / (double)N);      // fast_slam_2.py:189, as written
 }
 
-// first output m in [0, N] with u_m > v
+// first output m in [0, N] with u_m > v.  u_m is non-decreasing in m (the
+// rounded product and sum are monotone), so the answer is unique: start from
+// the real-arithmetic estimate and step to it (a step or two at most, bounded
+// by a binary search fallback).
 __device__ __forceinline__ int64_t first_above(double v, double u0, int64_t N) {
+    const double est = (v - u0) * (double)N;
+    int64_t m = (est < 0.0) ? 0 : (est >= (double)N ? N : (int64_t)est + 1);
+    for (int it = 0; it < 8; ++it) {
+        if (m > 0 && u_of(u0, m - 1, N) > v) --m;
+        else if (m < N && !(u_of(u0, m, N) > v)) ++m;
+        else return m;
+    }
     int64_t lo = 0, hi = N;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
@@ -518,10 +543,19 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             c = P.cnt[s];
             const int64_t lo = max((int64_t)P.mlo[s], P.a), hi = min((int64_t)P.mhi[s], P.a + n - 1);
             const uint32_t keep = (hi == lo) ? 0xffffffffu : kIdMask;
-            for (int k = 0; k * kPageSlots < c; ++k) {
-                uint4 e = *pt_entry(P.map, k, s);
-                e.x &= keep;
-                P.opt[(int64_t)k * n + m] = e;
+            const int rows = (c + kPageSlots - 1) / kPageSlots;
+            // 8 independent loads in flight per lane (one per iteration would pay a
+            // full memory latency per row)
+            for (int k0 = 0; k0 < rows; k0 += 8) {
+                uint4 e[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) e[u] = *pt_entry(P.map, min(k0 + u, rows - 1), s);
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (k0 + u < rows) {
+                        e[u].x &= keep;
+                        P.opt[(int64_t)(k0 + u) * n + m] = e[u];
+                    }
             }
         } else {
             const int r = -s - 1;
