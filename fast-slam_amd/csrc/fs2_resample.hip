@@ -313,26 +313,36 @@ __device__ __forceinline__ int64_t first_above(double v, double u0, int64_t N) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
+    __shared__ int lds_i[kBlock / 64];
     if (!P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= P.n) return;
-    const double u0 = P.stats->u0, off = P.stats->offset;
-    const int64_t g = P.a + i;
-    const double cur = (P.a == 0) ? P.c[i] : off + P.c[i];
-    int64_t lo;
-    if (g == 0) lo = 0;
-    else {
-        const double prev = (i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1]);
-        lo = first_above(prev, u0, P.N);
+    int omin = INT32_MAX, omax = -1;
+    if (i < P.n) {
+        const double u0 = P.stats->u0, off = P.stats->offset;
+        const int64_t g = P.a + i;
+        const double cur = (P.a == 0) ? P.c[i] : off + P.c[i];
+        int64_t lo;
+        if (g == 0) lo = 0;
+        else {
+            const double prev = (i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1]);
+            lo = first_above(prev, u0, P.N);
+        }
+        const int64_t hi = (g == P.N - 1) ? P.N - 1 : first_above(cur, u0, P.N) - 1;
+        P.mlo[i] = (int32_t)lo;
+        P.mhi[i] = (int32_t)hi;
+        const int64_t llo = max(lo, P.a), lhi = min(hi, P.a + P.n - 1);
+        for (int64_t m = llo; m <= lhi; ++m) P.out_src[m - P.a] = (int32_t)i;
+        if (lo <= hi) {
+            omin = (int)lo;
+            omax = (int)hi;
+        }
     }
-    const int64_t hi = (g == P.N - 1) ? P.N - 1 : first_above(cur, u0, P.N) - 1;
-    P.mlo[i] = (int32_t)lo;
-    P.mhi[i] = (int32_t)hi;
-    const int64_t llo = max(lo, P.a), lhi = min(hi, P.a + P.n - 1);
-    for (int64_t m = llo; m <= lhi; ++m) P.out_src[m - P.a] = (int32_t)i;
-    if (lo <= hi) {
-        atomicMin(&P.stats->out_min, (int32_t)lo);
-        atomicMax(&P.stats->out_max, (int32_t)hi);
+    // smallest / largest output served by this rank (one atomic per block)
+    const int bmax = block_max_i<kBlock>(omax, lds_i);
+    const int bmin = -block_max_i<kBlock>(omin == INT32_MAX ? INT32_MIN + 1 : -omin, lds_i);
+    if (threadIdx.x == 0 && bmax >= 0) {
+        atomicMin(&P.stats->out_min, bmin);
+        atomicMax(&P.stats->out_max, bmax);
     }
 }
 
