@@ -119,6 +119,20 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
 }
 
+// Slot of a lane's p-th candidate: the listed ones, then (list overflow or no
+// filter) every slot from jf on; -1 past the end.  A pure function of p, so the
+// candidate loop keeps no mutable state outside registers.
+static __device__ __forceinline__ int cand_at(int p, int ncl, int jf, int c, uint64_t w0, uint64_t w1,
+                                              uint64_t w2, uint64_t w3) {
+    if (p < ncl) {
+        const int wq = p >> 2;
+        const uint64_t wsel = wq == 0 ? w0 : (wq == 1 ? w1 : (wq == 2 ? w2 : w3));
+        return (int)((wsel >> (16 * (p & 3))) & 0xffffu);
+    }
+    const int j = jf + (p - ncl);
+    return j < c ? j : -1;
+}
+
 // ------------------------------------------------------------ k_update ------
 //
 // One lane per particle: move, then the exact association + EKF over the
@@ -196,23 +210,29 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         ncl = min(nc, kMaxCand);
         jf = nc > kMaxCand ? (int)(P.cand[(int64_t)(kMaxCand / 4 - 1) * n + i] >> 48) + 1 : c;
     }
-    int q = 0;
-    uint64_t word = 0;
-    while (pend) {
-        int j;
-        if (q < ncl) {
-            if ((q & 3) == 0) word = P.cand[(int64_t)(q >> 2) * n + i];
-            j = (int)(word & 0xffffu);
-            word >>= 16;
-            ++q;
-        } else if (jf < c) {
-            j = jf++;
-            if (!P.filter) ++visited;
-        } else {
-            break;
-        }
-        const char *page = page_of(map, j, il);
-        Slot s = load_slot(page, j);
+    // Candidates in slot order.  While slot j0 is tested, the slot of the next
+    // candidate (its page-table entry arrived one step earlier) and the entry of
+    // the one after are in flight; every load is branch-free (a missing
+    // candidate reads slot 0 of page 0 and is never used).
+    static_assert(kMaxCand == 16, "four list words");
+    const uint64_t w0 = P.cand[il], w1 = P.cand[n + il], w2 = P.cand[2 * n + il], w3 = P.cand[3 * n + il];
+    int p = 0;                       // candidates taken so far
+    int j0 = cand_at(0, ncl, jf, c, w0, w1, w2, w3);
+    int j1 = cand_at(1, ncl, jf, c, w0, w1, w2, w3);
+    if (pend == 0u) j0 = -1;
+    uint32_t e1 = pt_entry(map, (j1 >= 0 ? j1 : 0) / kPageSlots, il)->x;
+    Slot s0 = load_slot(page_ptr(map.pool, j0 >= 0 ? pt_entry(map, j0 / kPageSlots, il)->x : 0u), j0 >= 0 ? j0 : 0);
+    while (j0 >= 0 && pend != 0u) {
+        const int j2 = cand_at(p + 2, ncl, jf, c, w0, w1, w2, w3);
+        const uint32_t e2 = pt_entry(map, (j2 >= 0 ? j2 : 0) / kPageSlots, il)->x;
+        const Slot s1 = load_slot(page_ptr(map.pool, j1 >= 0 ? e1 : 0u), j1 >= 0 ? j1 : 0);
+        const int j = j0;
+        Slot s = s0;
+        ++p;
+        j0 = j1;
+        s0 = s1;
+        j1 = j2;
+        e1 = e2;
         ++candidates;
         bool mod = false;
         M2 I;
@@ -249,6 +269,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             ++written;
         }
     }
+
+    if (!P.filter) visited += (unsigned)max(0, p - ncl);
 
     // ---- phase B: every store of this pass.  Stores come last because vmcnt
     // counts loads and stores in issue order: a store ahead of a load makes the
