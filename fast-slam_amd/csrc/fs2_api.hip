@@ -431,7 +431,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     h->recvbuf.assign(G, nullptr);
     h->sendcap.assign(G, 0);
     h->recvcap.assign(G, 0);
-    if (G > 1) {
+    if (G > 1 || cfg->sharded_path) {
         rc = (cfg->comm_mode == FS2_COMM_LOCAL)
                  ? fs2comm::create_local(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
                  : fs2comm::create_rccl(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err);
@@ -487,7 +487,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     const int cur = h->cur;
     hipStream_t s = h->stream;
     const int G = h->cfg.world_size;
-    const bool seq = h->sequential() && G == 1;   // sharded sums are parallel by nature
+    const bool sh = h->tp != nullptr;             // sharded path (G > 1, or forced for testing)
+    const bool seq = h->sequential() && !sh;      // sharded sums are parallel by nature
     const bool prof = h->profiling;
 
     if (noise) {
@@ -598,7 +599,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.world = G;
     rp.rank = h->cfg.rank;
     rp.rec = h->rec;
-    rp.recs = (G > 1) ? h->recs : h->rec;
+    rp.recs = sh ? h->recs : h->rec;
     rp.totals = h->totals;
 
     const int nxt = 1 - cur;
@@ -627,7 +628,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
 
     // weight total over all ranks (fast_slam_2.py:166)
     HIP_TRY(h, launch_wsum(rp, s));
-    if (G > 1) {
+    if (sh) {
         rc = h->tp->allgather(&h->stats_dev->total, h->totals, sizeof(double), s, &h->err);
         if (rc) return rc;
         HIP_TRY(h, launch_global_total(rp, s));
@@ -636,15 +637,15 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     HIP_TRY(h, launch_normalize(rp, s));
     // sharded ranks need their prefix end in the record; one GPU needs the
     // prefix only when the rule fires (computed below, kernels exit otherwise)
-    if (G > 1) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
     HIP_TRY(h, launch_finalize(rp, s));
-    if (G > 1) {
+    if (sh) {
         rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
         if (rc) return rc;
     }
     // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183)
     HIP_TRY(h, launch_global_finalize(rp, s));
-    if (G == 1) {
+    if (!sh) {
         rs.lazy = 1;
         HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
     }
@@ -653,7 +654,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // ---- low-variance resample (:177-199); on one GPU the kernels exit unless the
     // rule fired, sharded ranks learn the decision first (sizes of the transfers) ----
     bool run_resample = true;
-    if (G > 1) {
+    if (sh) {
         HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
         HIP_TRY(h, hipStreamSynchronize(s));
         run_resample = h->stats_host->resampled != 0;
@@ -661,7 +662,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     if (run_resample) {
         HIP_TRY(h, hipMemsetAsync(h->out_src, 0, sizeof(int32_t) * std::max<int64_t>(h->n, 1), s));
         HIP_TRY(h, launch_resample_ranges(rs, s));
-        if (G > 1) {
+        if (sh) {
             rc = exchange_particles(h, rs);
             if (rc) return rc;
             // fresh pages for the received maps: record r, row k -> base + r * rows + k
@@ -680,7 +681,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             rs.rdesc = h->rdesc;
         }
         HIP_TRY(h, launch_resample_apply(rs, s));
-        if (G > 1) {
+        if (sh) {
             rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
             if (rc) return rc;
         }

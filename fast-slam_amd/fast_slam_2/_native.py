@@ -51,7 +51,7 @@ class fs2_config(C.Structure):
         ("world_size", C.c_int32),
         ("comm_id", C.c_uint8 * 128),
         ("comm_mode", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("sharded_path", C.c_int32),
     ]
 
 

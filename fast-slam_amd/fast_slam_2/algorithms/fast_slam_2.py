@@ -36,7 +36,7 @@ class FastSLAM2:
                  seed: int | None = None, reduce: str = "auto", record_assoc: bool = False,
                  landmark_capacity: int = 64, rank: int = 0, world_size: int = 1,
                  comm_id: bytes | None = None, verbose: bool = True, gate_filter: bool = True,
-                 comm_mode: str = "rccl"):
+                 comm_mode: str = "rccl", sharded_path: bool = False):
         lib = nat.load()
         cfg = nat.default_config()
         cfg.num_particles = int(config.NUM_PARTICLES if num_particles is None else num_particles)
@@ -58,6 +58,7 @@ class FastSLAM2:
         if comm_id is not None:
             C.memmove(cfg.comm_id, comm_id, 128)
         cfg.comm_mode = {"rccl": nat.FS2_COMM_RCCL, "local": nat.FS2_COMM_LOCAL}[comm_mode]
+        cfg.sharded_path = 1 if sharded_path else 0
         if rng not in ("numpy", "device"):
             raise ValueError("rng must be 'numpy' or 'device'")
         self._rng = rng

@@ -76,7 +76,8 @@ typedef struct fs2_config {
     int32_t world_size;             /* number of ranks; 1 = single GPU */
     uint8_t comm_id[128];           /* ncclUniqueId from fs2_comm_unique_id (world_size > 1) */
     int32_t comm_mode;              /* FS2_COMM_* */
-    int32_t reserved0;
+    int32_t sharded_path;           /* 1: run the sharded path (transport, collectives) even
+                                       with world_size 1 -- tests the transport on one GPU */
 } fs2_config;
 
 typedef struct fs2_iter_stats {

@@ -96,3 +96,42 @@ def test_sharded_matches_single(G, N, L):
     assert resamples >= 2
     for h in shards + [single]:
         h.close()
+
+
+@pytest.mark.parametrize("mode", ["rccl", "local"])
+def test_sharded_path_one_rank(mode):
+    """The sharded path with world_size 1 (sharded_path=True): the transport is
+    created and every collective runs (RCCL: ncclCommInitRank, ncclAllGather, an
+    empty grouped send/recv), so the RCCL transport is exercised on a one-GPU box.
+    Results equal a plain handle."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from fast_slam_2 import _native as nat
+    from gpu_util import configure
+    configure()
+    N, L = 5000, 30
+    wl = syn.Workload(N, L, seed=41)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    lm[:, :, 2] = lm[:, :, 5] = 0.01
+    key = nat.comm_unique_id() if mode == "rccl" else os.urandom(128)
+    hs = [fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=3, landmark_capacity=L + 40,
+                                verbose=False, **kw)
+          for kw in ({}, dict(sharded_path=True, comm_mode=mode, comm_id=key))]
+    for h in hs:
+        h.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    resamples = 0
+    for s in range(6):
+        rot, tr = syn.odometry(s)
+        ms = wl.measurements(s)
+        (p0, s0), (p1, s1) = [h.step(rot, tr, ms) for h in hs]
+        assert s0.resampled == s1.resampled and s0.best_index == s1.best_index, s
+        assert np.allclose(p0, p1, rtol=1e-12, atol=1e-15), s
+        assert np.array_equal(hs[0].associations(), hs[1].associations()), s
+        resamples += s0.resampled
+    a, b = hs[0].get_state(lm_cap=L + 40), hs[1].get_state(lm_cap=L + 40)
+    for u, v in zip(a, b):
+        assert np.allclose(u, v, rtol=1e-12, atol=1e-15)
+    assert resamples >= 1
+    for h in hs:
+        h.close()
