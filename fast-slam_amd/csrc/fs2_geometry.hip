@@ -16,14 +16,69 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ------------------------------------------------------------------- ICP ---
 //
 // One workgroup per alignment; the target cloud and the moving source cloud
-// live in LDS for the whole loop; nearest neighbours by brute force with
-// broadcast LDS reads (every lane reads the same target point), lowest index
-// on exact ties; centroids / cross-covariance / mean distance by fixed-order
+// live in LDS for the whole loop.  Nearest neighbours (icp.py:36, KDTree query)
+// through a uniform grid over the target cloud, built once in LDS: each source
+// point searches rings of cells outward until the best distance found is
+// provably below the distance to any cell not yet searched, so the result is
+// the exact fp64 nearest neighbour, lowest index on exact ties, as brute force
+// would give.  Centroids / cross-covariance / mean distance by fixed-order
 // wave + LDS reductions; rotation by the closed-form 2-D Kabsch angle, which
 // equals the reference's SVD + reflection fix (icp.py:76-85).
 
 constexpr int kIcpMaxP = 1024;
 constexpr int kIcpThreads = 1024;
+constexpr int kIcpGrid = 32;                 // cells per axis
+
+struct IcpGrid {
+    double x0, y0, hx, hy, ihx, ihy, slack;
+};
+
+__device__ __forceinline__ int icp_cell(double v, double v0, double ih) {
+    const double c = (v - v0) * ih;
+    return !(c >= 0.0) ? 0 : (c >= (double)(kIcpGrid - 1) ? kIcpGrid - 1 : (int)c);   // NaN -> 0
+}
+
+// exact nearest target of p: (index, squared distance)
+__device__ __forceinline__ void icp_nearest(const double2 p, const IcpGrid &g, const int *cstart,
+                                            const int16_t *cidx, const double2 *tgt, int &bj,
+                                            double &best) {
+    const int cx = icp_cell(p.x, g.x0, g.ihx), cy = icp_cell(p.y, g.y0, g.ihy);
+    best = INFINITY;
+    bj = INT32_MAX;
+    for (int r = 0; r < kIcpGrid; ++r) {
+        for (int j = max(cy - r, 0); j <= min(cy + r, kIcpGrid - 1); ++j) {
+            const bool edge_row = (j == cy - r) || (j == cy + r);
+            const int step = (edge_row || r == 0) ? 1 : 2 * r;
+            for (int i = cx - r; i <= cx + r; i += step) {
+                if (i < 0 || i >= kIcpGrid) continue;
+                const int cell = j * kIcpGrid + i;
+                for (int q = cstart[cell]; q < cstart[cell + 1]; ++q) {
+                    const int t = cidx[q];
+                    const double2 tp = tgt[t];
+                    const double dx = p.x - tp.x, dy = p.y - tp.y;
+                    const double d2 = dx * dx + dy * dy;
+                    if (d2 < best || (d2 == best && t < bj)) {
+                        best = d2;
+                        bj = t;
+                    }
+                }
+            }
+        }
+        // distance from p to the cells outside the searched block (those that exist)
+        double bound = INFINITY;
+        if (cx + r < kIcpGrid - 1) bound = fmin(bound, g.x0 + (cx + r + 1) * g.hx - p.x);
+        if (cx - r > 0) bound = fmin(bound, p.x - (g.x0 + (cx - r) * g.hx));
+        if (cy + r < kIcpGrid - 1) bound = fmin(bound, g.y0 + (cy + r + 1) * g.hy - p.y);
+        if (cy - r > 0) bound = fmin(bound, p.y - (g.y0 + (cy - r) * g.hy));
+        if (bound == INFINITY) break;                       // every cell searched
+        bound -= g.slack;                                   // cell assignment rounding
+        if (bound > 0.0 && best < bound * bound * (1.0 - 1e-12)) break;
+    }
+    if (bj == INT32_MAX) {          // no comparable target (NaN point): brute force keeps index 0
+        bj = 0;
+        best = INFINITY;
+    }
+}
 
 template <int NT>
 __device__ void block_sum5(double v[5], double *lds) {
@@ -56,6 +111,10 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
     __shared__ double red[5 * 16];
     __shared__ double s_R[4], s_t[2];
     __shared__ int s_stop;
+    __shared__ int s_cstart[kIcpGrid * kIcpGrid + 1];
+    __shared__ int s_cfill[kIcpGrid * kIcpGrid];
+    __shared__ int16_t s_cidx[kIcpMaxP];
+    __shared__ IcpGrid s_g;
 
     const int b = blockIdx.x;
     const double2 *src = reinterpret_cast<const double2 *>(src_all) + (int64_t)b * P;
@@ -65,23 +124,74 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
     double Rt[4] = {1.0, 0.0, 0.0, 1.0}, tt[2] = {0.0, 0.0};
     double prev = INFINITY;
     int it = 0;
+    // ---- grid over the target cloud (fixed for the whole alignment) ----
+    for (int k = threadIdx.x; k < kIcpGrid * kIcpGrid; k += kIcpThreads) s_cfill[k] = 0;
+    __syncthreads();
+    {
+        double v[5] = {INFINITY, INFINITY, INFINITY, INFINITY, 0.0};   // min x, min y, -max x, -max y
+        for (int k = threadIdx.x; k < nt; k += kIcpThreads) {
+            const double2 tp = s_tgt[k];
+            v[0] = fmin(v[0], tp.x); v[1] = fmin(v[1], tp.y);
+            v[2] = fmin(v[2], -tp.x); v[3] = fmin(v[3], -tp.y);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            for (int o = 32; o > 0; o >>= 1) v[q] = fmin(v[q], __shfl_xor(v[q], o, 64));
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (lane == 0)
+            for (int q = 0; q < 4; ++q) red[q * 16 + wid] = v[q];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double m[4];
+            for (int q = 0; q < 4; ++q) {
+                m[q] = red[q * 16];
+                for (int k = 1; k < kIcpThreads / 64; ++k) m[q] = fmin(m[q], red[q * 16 + k]);
+            }
+            IcpGrid g;
+            const bool ok = isfinite(m[0]) && isfinite(m[1]) && isfinite(m[2]) && isfinite(m[3]);
+            g.x0 = ok ? m[0] : 0.0;
+            g.y0 = ok ? m[1] : 0.0;
+            const double wx = ok ? -m[2] - m[0] : 0.0, wy = ok ? -m[3] - m[1] : 0.0;
+            g.hx = wx > 0.0 ? wx / kIcpGrid : 1.0;
+            g.hy = wy > 0.0 ? wy / kIcpGrid : 1.0;
+            g.ihx = 1.0 / g.hx;
+            g.ihy = 1.0 / g.hy;
+            // a target may sit a few ulps on the other side of its cell's edge
+            g.slack = 1e-9 * (fabs(g.x0) + fabs(g.y0) + wx + wy) + 1e-300;
+            if (!ok) g.hx = g.hy = INFINITY;               // non-finite input: one cell
+            s_g = g;
+        }
+        __syncthreads();
+    }
+    const IcpGrid grid = s_g;
+    for (int k = threadIdx.x; k < nt; k += kIcpThreads) {
+        const double2 tp = s_tgt[k];
+        atomicAdd(&s_cfill[icp_cell(tp.y, grid.y0, grid.ihy) * kIcpGrid + icp_cell(tp.x, grid.x0, grid.ihx)], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int k = 0; k < kIcpGrid * kIcpGrid; ++k) {
+            s_cstart[k] = run;
+            run += s_cfill[k];
+            s_cfill[k] = s_cstart[k];
+        }
+        s_cstart[kIcpGrid * kIcpGrid] = run;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nt; k += kIcpThreads) {
+        const double2 tp = s_tgt[k];
+        const int cell = icp_cell(tp.y, grid.y0, grid.ihy) * kIcpGrid + icp_cell(tp.x, grid.x0, grid.ihx);
+        s_cidx[atomicAdd(&s_cfill[cell], 1)] = (int16_t)k;
+    }
     __syncthreads();
     while (it < max_iter) {
         ++it;
         // nearest neighbours
         for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k];
-            double best = INFINITY;
-            int bj = 0;
-            for (int j = 0; j < nt; ++j) {
-                const double2 tp = s_tgt[j];
-                const double dx = sp.x - tp.x, dy = sp.y - tp.y;
-                const double d2 = dx * dx + dy * dy;
-                if (d2 < best) {
-                    best = d2;
-                    bj = j;
-                }
-            }
+            double best;
+            int bj;
+            icp_nearest(s_src[k], grid, s_cstart, s_cidx, s_tgt, bj, best);
             s_nn[k] = bj;
             s_dist[k] = sqrt(best);
         }

@@ -450,3 +450,30 @@ def test_page_summary_extreme_coordinates(fs):
             assert np.array_equal(a, b, equal_nan=True)
         for f in fl:
             f.close()
+
+
+def test_icp_grid_search_matches_brute_force(fs):
+    """The grid nearest-neighbour search is exact: clustered clouds, duplicated
+    target points (exact ties -> lowest index), sources far outside the target
+    box and a degenerate (collinear) target cloud give the oracle's brute-force
+    ICP result."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(77)
+    cases = []
+    tgt = rng.normal(0, 1, (600, 2)) * [8, 3]
+    tgt[::7] = tgt[3]                                   # exact duplicates
+    src = tgt[rng.permutation(600)[:500]] + rng.normal(0, 0.05, (500, 2))
+    cases.append((src, tgt))
+    cl = np.concatenate([rng.normal(c, 0.2, (120, 2)) for c in ([0, 0], [10, 2], [-5, 7])])
+    cases.append((cl[::-1] * 1.01 + [0.3, -0.2], cl))
+    far = rng.normal(0, 1, (256, 2))
+    for sh in ([9.0, 0.0], [0.0, 12.0], [20.0, 20.0]):  # sources outside the target box
+        cases.append((far + sh, far))
+    line = np.stack([np.linspace(-5, 5, 300), np.zeros(300)], 1)
+    cases.append((line + [0.01, 0.2], line))            # zero-height box
+    for k, (s, t) in enumerate(cases):
+        R, tt, it = fs.ICP.get_transformation_ex(s, t)
+        Ro, to, ito = orc.icp(s, t)
+        assert it == ito, k
+        assert np.allclose(R, Ro, atol=1e-9), k
+        assert np.allclose(tt, to, atol=1e-9 * max(1.0, np.abs(to).max())), k
