@@ -211,16 +211,19 @@ def main():
     if rank == 0:
         launches = max(prof["update_launches"], 1)
         upd_ms = prof["update_ms"] / launches
-        # dominant kernel: the candidate stream (k_candidates) reads every slot's
-        # mirror; without the gate filter the exact kernel streams the fp64 slots
+        # per-kernel split of the update pass (HIP events around k_candidates on the
+        # library's stream; k_update is the rest of the pass)
+        kern = {}
         if prof["filter_launches"] > 0:
-            kernel = "k_candidates"
-            ms_launch = prof["filter_ms"] / prof["filter_launches"]
-            bytes_launch = prof["filter_bytes"] / prof["filter_launches"]
+            fl = prof["filter_launches"]
+            kern["k_candidates"] = (prof["filter_ms"] / fl, prof["filter_bytes"] / fl)
+            kern["k_update"] = ((prof["update_ms"] - prof["filter_ms"]) / fl,
+                                (prof["update_bytes"] - prof["filter_bytes"]) / fl)
         else:
-            kernel = "k_update"
-            ms_launch = upd_ms
-            bytes_launch = prof["update_bytes"] / launches
+            kern["k_update"] = (upd_ms, prof["update_bytes"] / launches)
+        # the roofline line is for the dominant (longest) kernel
+        kernel = max(kern, key=lambda k: kern[k][0])
+        ms_launch, bytes_launch = kern[kernel]
         achieved = bytes_launch / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -252,6 +255,10 @@ def main():
             "cpu_baseline": cpu,
             "extra": {"scan_device_ms": prof["scan_ms"] / max(prof["scans"], 1),
                       "update_pass_ms": upd_ms,
+                      "kernels": {k: {"ms_per_launch": v[0], "bytes_per_launch": v[1],
+                                      "achieved_GBs": v[1] / (v[0] * 1e-3) / 1e9 if v[0] > 0 else 0.0,
+                                      "hbm_traffic_per_launch": pmc_traffic(cfg["name"], k)}
+                                  for k, v in kern.items()},
                       "update_pass_bytes": prof["update_bytes"] / launches,
                       "reduce_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resample_ms_total": prof["resample_ms"],

@@ -59,14 +59,15 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     unsigned visited = 0, groups = 0;
 
     // Page g: its descriptor is tested against every measurement first (the
-    // next descriptor already in flight); only pages it cannot reject have their
+    // next two descriptors already in flight); only pages it cannot reject have their
     // 8 mirrors loaded, and the wave loads them together (lanes without an open
     // page read page 0, which stays in cache, and discard it).
-    uint4 d1 = ptrow[0];
+    uint4 d1 = ptrow[0], d2 = ptrow[(int64_t)min(1, rlast) * n];
     for (int g = 0; __any(g * kPageSlots < c); ++g) {
         const int j0 = g * kPageSlots;
         const uint4 d = d1;
-        d1 = ptrow[(int64_t)min(g + 1, rlast) * n];
+        d1 = d2;
+        d2 = ptrow[(int64_t)min(g + 2, rlast) * n];
         bool open = false;
         if (j0 < c) {
             ++groups;
