@@ -1090,6 +1090,16 @@ int fs2_mahalanobis(int32_t device, const double *a, const double *b, const doub
     return FS2_OK;
 }
 
+#ifdef FS2_PHASE_TIMING
+// timing builds only (not in include/fs2.h): summed per-wave s_memtime cycles of
+// the k_update phases since the last reset
+int fs2_debug_phase_times(uint64_t out[8], int32_t reset) {
+    return fs2::debug_phase_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess
+               ? FS2_OK
+               : FS2_ERR_HIP;
+}
+#endif
+
 int fs2_comm_unique_id(uint8_t out[128]) {
     if (!out) return set_err(nullptr, FS2_ERR_ARG, "null argument");
     std::string err;

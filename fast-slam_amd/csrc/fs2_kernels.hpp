@@ -217,6 +217,9 @@ hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t 
 hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s);
 hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 
+#ifdef FS2_PHASE_TIMING
+hipError_t debug_phase_times(unsigned long long out[8], int reset);
+#endif
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
                          int32_t rows_each, int32_t *cnt, hipStream_t s);

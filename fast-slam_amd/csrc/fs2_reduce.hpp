@@ -180,19 +180,18 @@ __device__ __forceinline__ float4 store_slot(char *page, int j, const Slot &s) {
 // slot appended to a fresh page starts a new summary, otherwise the box grows to include mv and s_min
 // takes min(s_min, s).  The result covers every slot now in the page (it may
 // also cover values since replaced: still conservative).
+__device__ __forceinline__ uint4 merge_summary(uint4 d, const float4 &mv) {
+    if (!(isfinite(mv.x) && isfinite(mv.y))) return describe_page(d.x, &mv, 0);
+    d.y = half_down(fminf(half_lo(d.y), mv.x)) | (half_up(fmaxf(half_hi(d.y), mv.x)) << 16);
+    d.z = half_down(fminf(half_lo(d.z), mv.y)) | (half_up(fmaxf(half_hi(d.z), mv.y)) << 16);
+    d.w = __float_as_uint(fminf(__uint_as_float(d.w), mv.z));
+    return d;
+}
+
 __device__ __forceinline__ void note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
     uint4 *pe = pt_entry(m, j / kPageSlots, i);
-    uint4 d = *pe;
-    if (fresh) {
-        d = describe_page(d.x, &mv, 1);
-    } else if (!(isfinite(mv.x) && isfinite(mv.y))) {
-        d = describe_page(d.x, &mv, 0);
-    } else {
-        d.y = half_down(fminf(half_lo(d.y), mv.x)) | (half_up(fmaxf(half_hi(d.y), mv.x)) << 16);
-        d.z = half_down(fminf(half_lo(d.z), mv.y)) | (half_up(fmaxf(half_hi(d.z), mv.y)) << 16);
-        d.w = __float_as_uint(fminf(__uint_as_float(d.w), mv.z));
-    }
-    *pe = d;
+    const uint4 d = *pe;
+    *pe = fresh ? describe_page(d.x, &mv, 1) : merge_summary(d, mv);
 }
 
 // Recompute the summary of page `row` of particle i from its mirrors (map size c).

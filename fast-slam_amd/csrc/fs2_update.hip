@@ -23,6 +23,20 @@
 
 namespace fs2 {
 
+// Optional per-phase wave timing of k_update (build with -DFS2_PHASE_TIMING;
+// read back with fs2_debug_phase_times).  Compiled out otherwise.
+#ifdef FS2_PHASE_TIMING
+__device__ unsigned long long g_phase[8];
+#define FS2_PHASE(k)                                                                         \
+    do {                                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                           \
+        if ((threadIdx.x & 63) == 0 && (k) > 0) atomicAdd(&g_phase[(k) - 1], t_ - ph_last);   \
+        ph_last = t_;                                                                        \
+    } while (0)
+#else
+#define FS2_PHASE(k) do { } while (0)
+#endif
+
 // ------------------------------------------------------- k_candidates ------
 //
 // Streaming half of the association (fast_slam_2.py:95-106 first-match search).
@@ -157,6 +171,9 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ int s_idx[MAXM][kBlock];         // per (measurement, lane) association
     __shared__ uint2 s_cow[kBlock / 64][64 * (MAXM + 1)];   // per wave: (shared page, copy)
 
+#ifdef FS2_PHASE_TIMING
+    unsigned long long ph_last = 0;
+#endif
     const int tid = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
     const bool live = i < P.n;
@@ -181,6 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     unsigned cow = 0, fresh = 0;
     uint64_t mods = 0;               // existing slots modified in phase A (16 bits each)
     int nmod = 0;
+    FS2_PHASE(0);
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
         const double nz = P.noise ? P.noise[i]
@@ -204,6 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     bool singular = false;
     const double gate2 = P.gate2;
 
+    FS2_PHASE(1);
     // ---- exact pass over the candidate slots (association + EKF) ----
     int ncl = 0, jf = 0;
     if (live && P.filter) {
@@ -273,74 +292,106 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     if (!P.filter) visited += (unsigned)max(0, p - ncl);
 
+    FS2_PHASE(2);
     // ---- phase B: every store of this pass.  Stores come last because vmcnt
     // counts loads and stores in issue order: a store ahead of a load makes the
     // wait for that load wait for the store as well. ----
 
-    uint32_t modpage[MAXM];          // page of each modified slot, once owned
-    // (B1) own every page this lane will write: the modified slots' pages and the
-    // page the first append lands in (later appends start fresh pages).  The
-    // wave lists its shared pages in LDS and copies them together, 16 pages (8
-    // independent 16-byte loads per lane) per batch: a copy loop with one load
-    // per iteration would pay a full memory latency per page.
+    // Rows this lane writes before the appends: the modified slots' rows, then the
+    // row the first append lands in when it is partly filled (later appends start
+    // fresh pages).  Their descriptors and this pass's reserved free pages are
+    // loaded together, before any store.
+    constexpr int NR = MAXM + 1;
+    const int nrows = nmod + ((pend != 0u && c % kPageSlots != 0) ? 1 : 0);
+    int rrow[NR];
+    uint4 rdesc[NR];
+    int canon[NR];                   // first entry with the same row
+#pragma unroll
+    for (int t = 0; t < NR; ++t) {
+        rrow[t] = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) / kPageSlots
+                             : (t == nmod && t < nrows ? c / kPageSlots : 0);
+        rdesc[t] = *pt_entry(map, rrow[t], il);
+    }
+    uint32_t fpage[MAXM];
+#pragma unroll
+    for (int t = 0; t < MAXM; ++t) fpage[t] = P.alloc.freel[P.alloc.base + (int64_t)t * n + il];
+
+    // (B1) own those pages.  The wave lists its shared pages in LDS and copies
+    // them together, 16 pages per batch (8 independent 16-byte loads per lane),
+    // the loads of the next batch issued before the stores of this one.
     {
         const int lane = tid & 63, wid = tid >> 6;
-        const int nrows = nmod + ((pend != 0u && c % kPageSlots != 0) ? 1 : 0);
         int T = 0;                    // pages listed by the wave so far
 #pragma unroll
-        for (int t = 0; t < MAXM; ++t) modpage[t] = 0u;
-#pragma unroll
-        for (int t = 0; t < MAXM + 1; ++t) {
+        for (int t = 0; t < NR; ++t) {
             bool task = false;
             uint32_t src = 0, dst = 0;
-            if (t < nrows) {
-                const int r = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) / kPageSlots : c / kPageSlots;
-                uint4 *pe = pt_entry(map, r, il);
-                const uint32_t e = pe->x;
-                uint32_t id = e & kIdMask;
-                if (!(e & kOwned)) {   // a later row of this lane on the same page now reads owned
-                    task = true;
-                    src = id;
-                    dst = take_page(P.alloc, n, il, nalloc);
-                    pe->x = dst | kOwned;
-                    id = dst;
-                    ++cow;
-                }
+            canon[t] = t;
+#pragma unroll
+            for (int u = 0; u < t; ++u)
+                if (canon[t] == t && u < nrows && rrow[u] == rrow[t]) canon[t] = u;
+            if (t < nrows && canon[t] == t && !(rdesc[t].x & kOwned)) {
+                task = true;
+                src = rdesc[t].x & kIdMask;
 #pragma unroll
                 for (int u = 0; u < MAXM; ++u)
-                    if (u == t) modpage[u] = id;
+                    if (u == nalloc) dst = fpage[u];
+                ++nalloc;
+                rdesc[t].x = dst | kOwned;
+                ++cow;
             }
             const uint64_t bm = __ballot(task);
             if (task) s_cow[wid][T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
             T += __popcll(bm);
         }
+#pragma unroll
+        for (int t = 0; t < NR; ++t)
+            if (t < nrows && canon[t] == t) pt_entry(map, rrow[t], il)->x = rdesc[t].x;
         __syncthreads();
         const int off = (lane & 31) * 16;
-        for (int base = 0; base < T; base += 16) {
-            v4i v[8];                 // clang vector type: HIP's int4 struct defeats SROA here
-            uint32_t dst[8];
+        v4i va[8], vb[8];             // clang vector type: HIP's int4 struct defeats SROA here
+        uint32_t da[8], db[8];
+        auto load_batch = [&](int base, v4i *v, uint32_t *d) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const uint2 tk = s_cow[wid][min(base + 2 * u + (lane >> 5), T - 1)];
-                dst[u] = tk.y;
+                d[u] = tk.y;
                 v[u] = *reinterpret_cast<const v4i *>(page_ptr(map.pool, tk.x) + off);
             }
+        };
+        auto store_batch = [&](const v4i *v, const uint32_t *d) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, dst[u]) + off) = v[u];
+            for (int u = 0; u < 8; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
+        };
+        if (T > 0) load_batch(0, va, da);
+        for (int base = 0; base < T; base += 32) {
+            if (base + 16 < T) load_batch(base + 16, vb, db);
+            store_batch(va, da);
+            if (base + 16 >= T) break;
+            if (base + 32 < T) load_batch(base + 32, va, da);
+            store_batch(vb, db);
         }
         __threadfence_block();        // copies land before the slot stores below
     }
 
+    FS2_PHASE(3);
     // (B2) modified slots: the EKF updates of phase A replayed on the original slot
-    // in measurement order (bit-identical), then stored.  All reloads are issued
-    // first (branch-free: missing entries read slot 0 of page 0 and are unused).
+    // in measurement order (bit-identical) and stored; then the row summaries
+    // are read once, merged and written back.
     {
         Slot sl[MAXM];
+        uint32_t pid[MAXM];
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
             const int j = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) : 0;
-            sl[t] = load_slot(page_ptr(map.pool, modpage[t]), j);
+            uint32_t id = 0;
+#pragma unroll
+            for (int u = 0; u < NR; ++u)
+                if (u == canon[t]) id = rdesc[u].x;
+            pid[t] = t < nmod ? id : 0u;
+            sl[t] = load_slot(page_ptr(map.pool, pid[t]), j);
         }
+        float4 mv[MAXM];
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
             if (t < nmod) {
@@ -350,11 +401,24 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
                 for (int k = 0; k < MAXM; ++k)
                     if (s_idx[k][tid] == j) (void)ekf_update(s, px, py, pyaw, s_ms[k], R, dummy);
-                note_write(map, j, il, store_slot(page_ptr(map.pool, modpage[t]), j, s), false);
+                mv[t] = store_slot(page_ptr(map.pool, pid[t]), j, s);
+            }
+        }
+        // summaries: rows in first-occurrence order, each merged with all its slots
+#pragma unroll
+        for (int t = 0; t < MAXM; ++t) {
+            if (t < nmod && canon[t] == t) {
+                uint4 *pe = pt_entry(map, rrow[t], il);
+                uint4 d = *pe;
+#pragma unroll
+                for (int u = t; u < MAXM; ++u)
+                    if (u < nmod && canon[u] == t) d = merge_summary(d, mv[u]);
+                *pe = d;
             }
         }
     }
 
+    FS2_PHASE(4);
     // ---- measurements that matched nothing: appended slots, in order ----
     int nap = 0;
     while (pend) {
@@ -405,6 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
     c += nap;
 
+    FS2_PHASE(5);
     // likelihoods in measurement order (fast_slam_2.py:159)
     unsigned hits = 0;
 #pragma unroll
@@ -427,6 +492,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         P.cnt[i] = c;
     }
 
+    FS2_PHASE(6);
     // ---- block statistics ----
     const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
     const unsigned long long bc = block_sum_u64<kBlock>(candidates, lds_u);
@@ -655,5 +721,16 @@ hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kBlock), 0, s, p, n);
     return hipGetLastError();
 }
+
+#ifdef FS2_PHASE_TIMING
+hipError_t debug_phase_times(unsigned long long out[8], int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
+    }
+    return e;
+}
+#endif
 
 }  // namespace fs2
