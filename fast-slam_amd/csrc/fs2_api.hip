@@ -841,6 +841,45 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
     return FS2_OK;
 }
 
+int fs2_update_known_landmarks(fs2_handle *h, double eps, double min_fraction, double *centres, int64_t cap,
+                               int64_t *n_clusters) {
+    if (!h || !n_clusters || (cap > 0 && !centres) || !(eps > 0.0))
+        return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_update_known_landmarks: bad arguments");
+    if (h->cfg.world_size > 1)
+        return set_err(&h->err, FS2_ERR_STATE, "update_known_landmarks needs every particle on one rank");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    hipStream_t s = h->stream;
+    HIP_TRY(h, hipStreamSynchronize(s));
+    double2 *pts = nullptr;
+    int64_t np = 0;
+    HIP_TRY(h, gather_map_points(h->map(), h->cnt[h->cur], h->n, &pts, &np, s));
+    // min_samples = int(len(all) / len(particles) * 0.7) (landmark_utils.py:131-132)
+    const double avg = (double)np / (double)h->n_global;
+    const double ms = avg * min_fraction;
+    if (!(ms >= 1.0)) {
+        (void)hipFree(pts);
+        *n_clusters = -1;
+        return FS2_OK;
+    }
+    int32_t status = 0;
+    int64_t K = 0;
+    double *dcent = nullptr;
+    hipError_t e = hipMalloc(&dcent, sizeof(double) * 2 * std::max<int64_t>(cap, 1));
+    if (e == hipSuccess)
+        e = cluster_points(pts, np, eps, (int64_t)ms, dcent, cap, &K, nullptr, &status, s);
+    if (e == hipSuccess && K <= cap && K > 0)
+        e = hipMemcpy(centres, dcent, sizeof(double) * 2 * K, hipMemcpyDeviceToHost);
+    (void)hipFree(pts);
+    (void)hipFree(dcent);
+    if (e != hipSuccess) return set_err(&h->err, FS2_ERR_HIP, "update_known_landmarks: %s", hipGetErrorString(e));
+    if (status == 1) return set_err(&h->err, FS2_ERR_ARG, "Input contains NaN or infinity");
+    if (status == 2) return set_err(&h->err, FS2_ERR_ARG, "landmark coordinates span too many eps-cells");
+    *n_clusters = K;
+    if (K > cap) return set_err(&h->err, FS2_ERR_ARG, "%lld clusters, centre buffer holds %lld", (long long)K,
+                                (long long)cap);
+    return FS2_OK;
+}
+
 int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double *y, double *yaw,
                   double *w, int32_t *cnt, double *lm, int32_t lm_cap, int32_t where) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
@@ -1099,6 +1138,36 @@ int fs2_debug_phase_times(uint64_t out[8], int32_t reset) {
                : FS2_ERR_HIP;
 }
 #endif
+
+int fs2_cluster_points(int32_t device, const double *points, int64_t n, double eps, int64_t min_samples,
+                       double *centres, int64_t cap, int64_t *n_clusters, int32_t *labels, int32_t where) {
+    if (n <= 0 || !points || !n_clusters || !(eps > 0.0) || min_samples < 1 || cap < 0 || (cap > 0 && !centres))
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_cluster_points: bad arguments (n > 0, eps > 0, min_samples >= 1)");
+    if (n > (int64_t)INT32_MAX) return set_err(nullptr, FS2_ERR_ARG, "fs2_cluster_points: more than 2^31 points");
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 16, &sc);
+    if (rc) return rc;
+    const double2 *dp = reinterpret_cast<const double2 *>(points);
+    double2 *own = nullptr;
+    if (where != FS2_DEVICE) {
+        SHIP(hipMalloc(&own, sizeof(double2) * n));
+        SHIP(hipMemcpyAsync(own, points, sizeof(double2) * n, hipMemcpyHostToDevice, sc->stream));
+        dp = own;
+    }
+    int32_t status = 0;
+    int64_t K = 0;
+    hipError_t e = cluster_points(dp, n, eps, min_samples, cap > 0 ? centres : nullptr, cap, &K, labels, &status,
+                                  sc->stream);
+    if (own) (void)hipFree(own);
+    if (e != hipSuccess) return set_err(nullptr, FS2_ERR_HIP, "fs2_cluster_points: %s", hipGetErrorString(e));
+    if (status == 1) return set_err(nullptr, FS2_ERR_ARG, "Input contains NaN or infinity");
+    if (status == 2) return set_err(nullptr, FS2_ERR_ARG, "point coordinates span too many eps-cells");
+    *n_clusters = K;
+    if (K > cap) return set_err(nullptr, FS2_ERR_ARG, "%lld clusters, centre buffer holds %lld", (long long)K,
+                                (long long)cap);
+    return FS2_OK;
+}
 
 int fs2_comm_unique_id(uint8_t out[128]) {
     if (!out) return set_err(nullptr, FS2_ERR_ARG, "null argument");

@@ -239,6 +239,14 @@ hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t
                           hipStream_t s);
 int64_t collect_blocks(int64_t npool);
 
+// known-landmark clustering (fs2_cluster.hip).  status: 0 ok, 1 non-finite input,
+// 2 coordinate span too large.
+hipError_t cluster_points(const double2 *pts, int64_t n, double eps, int64_t min_samples, double *centres_out,
+                          int64_t centres_cap, int64_t *nclusters, int32_t *labels_out, int32_t *status,
+                          hipStream_t s);
+hipError_t gather_map_points(MapRef map, const int32_t *cnt, int64_t n, double2 **pts_out, int64_t *npts,
+                             hipStream_t s);
+
 hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt,
                       int32_t n_tgt, int32_t max_iter, double thr, double *R, double *t,
                       int32_t *iters, hipStream_t s);

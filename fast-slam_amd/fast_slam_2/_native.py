@@ -139,6 +139,10 @@ SIGNATURES = [
     ("fs2_gaussian_taps", C.c_int32, [C.c_double, C.c_double, _dp, C.c_int32]),
     ("fs2_associate", C.c_int, [C.c_int32, _dp, _dp, C.c_int32, C.c_double, _ip]),
     ("fs2_mahalanobis", C.c_int, [C.c_int32, _dp, _dp, _dp, C.c_int32, _dp]),
+    ("fs2_cluster_points", C.c_int, [C.c_int32, _vp, C.c_int64, C.c_double, C.c_int64, _vp, C.c_int64,
+                                     C.POINTER(C.c_int64), _vp, C.c_int32]),
+    ("fs2_update_known_landmarks", C.c_int, [_H, C.c_double, C.c_double, _dp, C.c_int64,
+                                             C.POINTER(C.c_int64)]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
 ]
 

@@ -16,6 +16,7 @@ instead (no host work per particle; used by bench.py).
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -168,20 +169,27 @@ class FastSLAM2:
         self._particles = None
 
     @property
-    def particles(self) -> list[Particle]:
-        """Host snapshot of this rank's particles (reference attribute `particles`)."""
+    def particles(self) -> "ParticleView":
+        """This rank's particles (reference attribute `particles`), materialised lazily in
+        chunks; LandmarkUtils.update_known_landmarks given this view clusters on the device."""
         if self._particles is None:
-            x, y, yaw, w, cnt, lm = self.get_state()
-            out = []
-            for i in range(self.n_local):
-                p = Particle.__new__(Particle)
-                p.x, p.y, p.yaw, p.weight = float(x[i]), float(y[i]), float(yaw[i]), float(w[i])
-                p.landmarks = [Landmark(float(lm[i, j, 0]), float(lm[i, j, 1]),
-                                        lm[i, j, 2:6].reshape(2, 2).copy())
-                               for j in range(int(cnt[i]))]
-                out.append(p)
-            self._particles = out
+            self._particles = ParticleView(self)
         return self._particles
+
+    def cluster_landmarks(self, eps: float = 0.5, min_fraction: float = 0.7):
+        """Centres [K][2] of DBSCAN over every particle's landmarks, on the device
+        (update_known_landmarks, landmark_utils.py:120-144); None when min_samples < 1."""
+        cap = 256
+        while True:
+            cen = np.empty((cap, 2))
+            k = C.c_int64()
+            rc = self._lib.fs2_update_known_landmarks(self._h, float(eps), float(min_fraction),
+                                                      nat.dptr(cen), cap, C.byref(k))
+            if rc == nat.FS2_ERR_ARG and k.value > cap:
+                cap = int(k.value)
+                continue
+            nat.check(rc, self._h)
+            return None if k.value < 0 else cen[:k.value].copy()
 
     @particles.setter
     def particles(self, plist: list[Particle]):
@@ -227,3 +235,43 @@ class FastSLAM2:
             self.close()
         except Exception:
             pass
+
+
+class ParticleView(Sequence):
+    """Lazy, read-only sequence of Particle objects over a FastSLAM2's device state
+    (downloaded 4096 particles at a time on first access)."""
+
+    _CHUNK = 4096
+
+    def __init__(self, filt: FastSLAM2):
+        self._filter = filt
+        self._n = filt.n_local
+        self._chunks: dict[int, list[Particle]] = {}
+
+    def __len__(self):
+        return self._n
+
+    def _chunk(self, c: int) -> list[Particle]:
+        if c not in self._chunks:
+            first = c * self._CHUNK
+            count = min(self._CHUNK, self._n - first)
+            x, y, yaw, w, cnt, lm = self._filter.get_state(first, count)
+            out = []
+            for i in range(count):
+                p = Particle.__new__(Particle)
+                p.x, p.y, p.yaw, p.weight = float(x[i]), float(y[i]), float(yaw[i]), float(w[i])
+                p.landmarks = [Landmark(float(lm[i, j, 0]), float(lm[i, j, 1]),
+                                        lm[i, j, 2:6].reshape(2, 2).copy())
+                               for j in range(int(cnt[i]))]
+                out.append(p)
+            self._chunks[c] = out
+        return self._chunks[c]
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError("particle index out of range")
+        return self._chunk(i // self._CHUNK)[i % self._CHUNK]

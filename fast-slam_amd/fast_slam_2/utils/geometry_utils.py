@@ -1,6 +1,7 @@
 """Geometry helpers (reference: fast_slam_2/utils/geometry_utils.py)."""
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import numpy as np
@@ -34,6 +35,29 @@ class GeometryUtils:
 
     @staticmethod
     def cluster_points(point_lists, eps: float, min_samples: int):
-        raise NotImplementedError(
-            "GeometryUtils.cluster_points (DBSCAN, geometry_utils.py:26-62) is outside the "
-            "particle-update hot path (SURVEY.md §8f, NEXT)")
+        """DBSCAN(eps, min_samples) + cluster centres (geometry_utils.py:26-62) on the GPU:
+        exact sklearn labels, centres as numpy means, in label order."""
+        pts = nat.f64(np.asarray(point_lists, dtype=np.float64).reshape(-1, 2))
+        centres, _ = GeometryUtils.dbscan(pts, eps, min_samples, labels=False)
+        return [c for c in centres]
+
+    @staticmethod
+    def dbscan(points, eps: float, min_samples: int, labels: bool = True):
+        """(centres [K][2], labels [n] or None) of sklearn DBSCAN(eps, min_samples)."""
+        pts = nat.f64(np.asarray(points, dtype=np.float64).reshape(-1, 2))
+        if len(pts) == 0:
+            raise ValueError("Found array with 0 sample(s) (shape=(0, 2)) while a minimum of 1 is required")
+        lib = nat.load()
+        lab = np.empty(len(pts), dtype=np.int32) if labels else None
+        cap = 64
+        while True:
+            cen = np.empty((cap, 2))
+            k = C.c_int64()
+            rc = lib.fs2_cluster_points(GeometryUtils.device, nat.ptr(pts), len(pts), float(eps),
+                                        int(min_samples), nat.ptr(cen), cap, C.byref(k), nat.ptr(lab),
+                                        nat.FS2_HOST)
+            if rc == nat.FS2_ERR_ARG and k.value > cap:
+                cap = int(k.value)
+                continue
+            nat.check(rc)
+            return cen[:k.value].copy(), lab

@@ -39,6 +39,20 @@ class LandmarkUtils:
 
     @staticmethod
     def update_known_landmarks(particles):
-        raise NotImplementedError(
-            "update_known_landmarks (DBSCAN visualisation, landmark_utils.py:120-144) is outside "
-            "the particle-update hot path (SURVEY.md §8f, NEXT)")
+        """Known landmarks = DBSCAN(eps 0.5, min_samples int(0.7 * average map size)) centres
+        over every particle's landmarks (landmark_utils.py:120-144).  Given
+        FastSLAM2.particles, the clustering runs on the device-resident maps."""
+        from ..models.landmark import Landmark
+        fs = getattr(particles, "_filter", None)
+        if fs is not None:
+            cen = fs.cluster_landmarks(eps=0.5, min_fraction=0.7)
+            if cen is None:
+                return
+        else:
+            pts = [(lm.x, lm.y) for p in particles for lm in p.landmarks]
+            min_samples = int(len(pts) / len(particles) * 0.7)
+            if min_samples < 1:
+                return
+            from .geometry_utils import GeometryUtils
+            cen = GeometryUtils.cluster_points(pts, eps=0.5, min_samples=min_samples)
+        LandmarkUtils.known_landmarks = [Landmark(float(c[0]), float(c[1])) for c in cen]

@@ -221,6 +221,26 @@ int fs2_mahalanobis(int32_t device, const double *a, const double *b, const doub
 
 /* ---------------------------------------------------------- multi-GPU ---- */
 
+/* Replaces GeometryUtils.cluster_points (utils/geometry_utils.py:26-62), i.e.
+ * sklearn DBSCAN(eps, min_samples) over n points (x, y) followed by the centre
+ * (numpy mean) of every cluster, clusters in sklearn's label order.  Exact:
+ * labels equal sklearn's (border points to the lowest-numbered cluster in reach).
+ * centres is [cap][2]; K > cap sets *n_clusters = K and fails with FS2_ERR_ARG.
+ * labels (nullable) receives n labels, -1 = noise.  where: FS2_HOST / FS2_DEVICE
+ * for points, centres and labels.  Non-finite input fails (sklearn raises). */
+int fs2_cluster_points(int32_t device, const double *points, int64_t n, double eps,
+                       int64_t min_samples, double *centres, int64_t cap, int64_t *n_clusters,
+                       int32_t *labels, int32_t where);
+
+/* Replaces LandmarkUtils.update_known_landmarks (utils/landmark_utils.py:120-144)
+ * for the particles held by the handle, without moving them off the device: every
+ * landmark (x, y) in (particle, slot) order, min_samples = int(total / N *
+ * min_fraction) (reference: 0.7), DBSCAN eps (reference: 0.5), centres in label
+ * order into centres[cap][2] (host).  *n_clusters = -1 when min_samples < 1 (the
+ * reference returns without updating).  Single-rank handles only. */
+int fs2_update_known_landmarks(fs2_handle *h, double eps, double min_fraction, double *centres,
+                               int64_t cap, int64_t *n_clusters);
+
 /* ncclUniqueId for fs2_config.comm_id (call on rank 0, broadcast to all ranks). */
 int fs2_comm_unique_id(uint8_t out[128]);
 
