@@ -2,23 +2,26 @@
 
 Same public names as cy-rae/fast-slam's `fast_slam_2` package
 (fast_slam_2/__init__.py:5-22).  The particle update, ICP, LineFilter and the
-association / Mahalanobis helpers run in libfs2.so (HIP, gfx950).  Robot,
-EvaluationUtils, HoughTransformation and Serializer are simulator- or
-front-end-bound and outside this build's scope.
+association / Mahalanobis helpers and the known-landmark clustering
+(update_known_landmarks / cluster_points) run in libfs2.so (HIP, gfx950);
+Serializer writes the viewer's JSON from one device download.  Robot,
+EvaluationUtils and HoughTransformation are simulator- or front-end-bound and
+outside this build's scope.
 """
 from .algorithms.fast_slam_2 import FastSLAM2
 from .algorithms.icp import ICP
 from .algorithms.line_filter import LineFilter
 from .models.directed_point import DirectedPoint
+from .models.evaluation_results import EvaluationResults
 from .models.landmark import Landmark
 from .models.measurement import Measurement
 from .models.particle import Particle
 from .models.point import Point
 from .utils.geometry_utils import GeometryUtils
 from .utils.landmark_utils import LandmarkUtils
+from .utils.serializer import Serializer
 
-_OUT_OF_SCOPE = {"Robot", "EvaluationUtils", "HoughTransformation", "Serializer",
-                 "EvaluationResults"}
+_OUT_OF_SCOPE = {"Robot", "EvaluationUtils", "HoughTransformation"}
 
 
 def __getattr__(name):
@@ -28,5 +31,5 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
-__all__ = ["FastSLAM2", "ICP", "LineFilter", "DirectedPoint", "Landmark", "Measurement",
-           "Particle", "Point", "GeometryUtils", "LandmarkUtils"]
+__all__ = ["FastSLAM2", "ICP", "LineFilter", "DirectedPoint", "EvaluationResults", "Landmark",
+           "Measurement", "Particle", "Point", "GeometryUtils", "LandmarkUtils", "Serializer"]

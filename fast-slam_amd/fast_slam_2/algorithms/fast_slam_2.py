@@ -176,6 +176,13 @@ class FastSLAM2:
             self._particles = ParticleView(self)
         return self._particles
 
+    def poses(self):
+        """(x, y, yaw) arrays of this rank's particles (one structure-of-arrays download)."""
+        x, y, yaw = (np.empty(self.n_local) for _ in range(3))
+        nat.check(self._lib.fs2_get_state(self._h, 0, self.n_local, nat.ptr(x), nat.ptr(y), nat.ptr(yaw),
+                                          None, None, None, 0, nat.FS2_HOST), self._h)
+        return x, y, yaw
+
     def cluster_landmarks(self, eps: float = 0.5, min_fraction: float = 0.7):
         """Centres [K][2] of DBSCAN over every particle's landmarks, on the device
         (update_known_landmarks, landmark_utils.py:120-144); None when min_samples < 1."""

@@ -85,3 +85,28 @@ def test_cluster_bad_input():
         GeometryUtils.dbscan(np.array([[0.0, np.nan], [1.0, 1.0]]), 0.5, 1)
     with pytest.raises(ValueError):
         GeometryUtils.dbscan(np.zeros((0, 2)), 0.5, 1)
+
+
+def test_serializer_from_device_view():
+    """Serializer given FastSLAM2.particles (one device download) writes the same text
+    as the reference's per-object json.dump."""
+    import json
+    import fast_slam_2
+    from fast_slam_2 import DirectedPoint, EvaluationResults, Point, Serializer
+    from gpu_util import configure
+    configure()
+    N = 3000
+    rng = np.random.default_rng(8)
+    f = fast_slam_2.FastSLAM2(N, verbose=False)
+    f.set_state(rng.normal(0, 3, N), rng.normal(0, 3, N), rng.uniform(-3, 3, N), np.full(N, 1.0 / N))
+    est, act = DirectedPoint(0.5, 0.25, 0.1), DirectedPoint(0.0, 0.0, 0.0)
+    lms = [Point(1.0, 2.0)]
+    res = EvaluationResults("t", 0.0, 0.0, 0.0, 0.0, 0.0)
+    x, y, yaw, *_ = f.get_state()
+    want = json.dumps({"estimated_robot_pos": est.to_dict(), "actual_robot_pos": act.to_dict(),
+                       "particles": [{"x": float(a), "y": float(b), "yaw": float(c)}
+                                     for a, b, c in zip(x, y, yaw)],
+                       "landmarks": [lm.to_dict() for lm in lms], "results": res.to_dict()}, indent=4)
+    assert Serializer.to_json(est, act, f.particles, lms, res) == want
+    assert len(f.particles) == N and f.particles[N - 1].yaw == yaw[N - 1]
+    f.close()
