@@ -135,3 +135,51 @@ def test_sharded_path_one_rank(mode):
     assert resamples >= 1
     for h in hs:
         h.close()
+
+
+def test_sharded_long_run_with_collections():
+    """30 scans, 3 ranks, small initial capacity: maps grow past several page rows,
+    resampling moves shared pages across shards and every rank's pool is collected
+    more than once; each scan equals the single-handle run."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    configure()
+    G, N, L = 3, 4500, 12
+    wl = syn.Workload(N, L, seed=77)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    lm[:, :, 2] = lm[:, :, 5] = 0.01
+    w = np.full(N, 1.0 / N)
+    cnt = np.full(N, L, np.int32)
+    single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=11, landmark_capacity=16,
+                                   verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    key = os.urandom(128)
+    shards = [fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=11, landmark_capacity=16,
+                                    rank=g, world_size=G, comm_id=key, comm_mode="local", verbose=False)
+              for g in range(G)]
+    for h in shards:
+        a, b = h.first_global, h.first_global + h.n_local
+        h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+    resamples = 0
+    for s in range(30):
+        rot, tr = syn.odometry(s)
+        ms = wl.measurements(s)
+        pose1, st1 = single.step(rot, tr, ms)
+        outs = _step_all(shards, rot, tr, ms)
+        for pose, st in outs:
+            assert st.resampled == st1.resampled and st.best_index == st1.best_index, s
+            assert np.allclose(pose, pose1, rtol=1e-9, atol=1e-12), s
+        assert np.array_equal(single.associations(),
+                              np.concatenate([h.associations() for h in shards], axis=1)), s
+        resamples += st1.resampled
+    cap = L + 30 * 4
+    s1 = single.get_state(lm_cap=cap)
+    sg = _gather(shards, cap)
+    assert np.array_equal(s1[4], sg[4])
+    assert np.allclose(s1[5], sg[5], rtol=1e-9, atol=1e-12)
+    assert resamples >= 5
+    assert max(h.last_stats.collections for h in shards) >= 2
+    for h in shards + [single]:
+        h.close()
