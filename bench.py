@@ -86,28 +86,42 @@ def populate(f, n_local, L, seed, rank):
 
 
 def cpu_baseline(L, P, budget_s, seed):
-    """The C oracle (oracle/fs2_oracle.c, reference semantics, 1 thread) on a sample."""
+    """The C oracle (oracle/fs2_oracle.c, reference semantics) on a sample of the
+    workload: with every host thread OpenMP gives it (the reference's NUM_THREAD
+    particle pool), and with one thread."""
     import fs2_synthetic as syn
     from oracle import oracle as orc
-    n = 6000
-    wl = syn.Workload(n, L, seed)
-    x, y, yaw = wl.poses()
-    o = orc.OracleFilter(n, L + 4 * 61)
-    o.set_state(x, y, yaw, np.full(n, 1.0 / n), np.full(n, L), wl.maps())
-    rng = np.random.default_rng(seed)
-    t_work, scans = 0.0, 0
-    while t_work < budget_s and scans < 60:
-        rot, tr = syn.odometry(scans)
-        ms = wl.measurements(scans)
-        nz = rng.normal(0, 0.001 if rot else 0.0055, n)
-        u0 = rng.uniform(0, 1.0 / n)
-        t0 = time.perf_counter()
-        o.iterate(rot, tr, ms, nz, u0)
-        t_work += time.perf_counter() - t0
-        scans += 1
-    return dict(value=n * scans / t_work, unit="particle-updates/s", cores=1, kind="port",
-                sample=f"{n} particles x {L} landmarks, M=4, {scans} scans "
-                       f"(C oracle, reference semantics, 1 thread, {t_work:.1f} s)")
+
+    def run(n, threads, budget):
+        orc.set_threads(threads)
+        wl = syn.Workload(n, L, seed)
+        x, y, yaw = wl.poses()
+        o = orc.OracleFilter(n, L + 4 * 61)
+        o.set_state(x, y, yaw, np.full(n, 1.0 / n), np.full(n, L), wl.maps())
+        rng = np.random.default_rng(seed)
+        t_work, scans = 0.0, 0
+        while t_work < budget and scans < 60:
+            rot, tr = syn.odometry(scans)
+            ms = wl.measurements(scans)
+            nz = rng.normal(0, 0.001 if rot else 0.0055, n)
+            u0 = rng.uniform(0, 1.0 / n)
+            t0 = time.perf_counter()
+            o.iterate(rot, tr, ms, nz, u0)
+            t_work += time.perf_counter() - t0
+            scans += 1
+        del o
+        return n * scans / t_work, scans, t_work
+
+    threads = orc.threads()
+    one, s1, t1 = run(6000, 1, budget_s / 2)
+    n = 6000 * max(1, min(threads, 32))
+    many, sm, tm = run(n, threads, budget_s / 2)
+    orc.set_threads(threads)
+    return dict(value=many, unit="particle-updates/s", cores=threads, kind="port",
+                single_thread_value=one,
+                sample=f"{n} particles x {L} landmarks, M=4, {sm} scans on {threads} OpenMP threads "
+                       f"({tm:.1f} s); 1 thread: 6000 particles, {s1} scans ({t1:.1f} s); "
+                       f"C oracle, reference semantics")
 
 
 def pmc_traffic(workload, kernel):

@@ -78,6 +78,15 @@ def _f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
 
 
+def threads():
+    """OpenMP worker threads of the oracle's particle loops (OMP_NUM_THREADS)."""
+    return int(lib().orc_threads())
+
+
+def set_threads(n):
+    lib().orc_set_threads(int(n))
+
+
 def pymod(a, b):
     return lib().orc_pymod(a, b)
 
