@@ -219,10 +219,16 @@ __global__ __launch_bounds__(kBlock) void k_cl_cellcore(const int32_t *cstart, c
     if (lane == 0) first_core[c] = found;
 }
 
+// Device-scope loads: a plain load may hit a stale line in this CU's L1 while
+// other CUs hook roots in L2 (the CAS below always sees the L2 value).
+__device__ __forceinline__ int uf_load(int32_t *parent, int x) {
+    return __hip_atomic_load(parent + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ int uf_find(int32_t *parent, int x) {
-    int p = parent[x];
+    int p = uf_load(parent, x);
     while (p != x) {
-        const int gp = parent[p];
+        const int gp = uf_load(parent, p);
         if (gp != p) parent[x] = gp;    // path halving (benign race)
         x = p;
         p = gp;
@@ -276,21 +282,26 @@ __global__ __launch_bounds__(kBlock) void k_cl_union(const double2 *pts, const u
     if (joined) uf_union(parent, a, b);
 }
 
-__global__ __launch_bounds__(kBlock) void k_cl_roots(int32_t *parent, const int32_t *first_core, const uint32_t *sidx,
-                                                     int32_t C, uint32_t *comp_min) {
+// Read-only find into a separate array: a compressing find here would race with
+// the other threads' path halving (a halving store landing after parent[c] = root
+// leaves parent[c] at a non-root ancestor).
+__global__ __launch_bounds__(kBlock) void k_cl_roots(const int32_t *parent, const int32_t *first_core,
+                                                     const uint32_t *sidx, int32_t C, int32_t *root,
+                                                     uint32_t *comp_min) {
     const int c = (int)((int64_t)blockIdx.x * kBlock + threadIdx.x);
     if (c >= C) return;
-    const int r = uf_find(parent, c);
-    parent[c] = r;                    // full compression: parent[] names the root from here on
+    int r = c;
+    while (parent[r] != r) r = parent[r];
+    root[c] = r;
     if (first_core[c] >= 0) atomicMin(&comp_min[r], sidx[first_core[c]]);
 }
 
 // roots with cores -> (comp_min, root) pairs for the numbering sort
-__global__ __launch_bounds__(kBlock) void k_cl_rootlist(const int32_t *parent, const uint32_t *comp_min, int32_t C,
+__global__ __launch_bounds__(kBlock) void k_cl_rootlist(const int32_t *root, const uint32_t *comp_min, int32_t C,
                                                         uint32_t *rkey, int32_t *rval, int32_t *nroots) {
     const int c = (int)((int64_t)blockIdx.x * kBlock + threadIdx.x);
     if (c >= C) return;
-    if (parent[c] == c && comp_min[c] != 0xffffffffu) {
+    if (root[c] == c && comp_min[c] != 0xffffffffu) {
         const int s = atomicAdd(nroots, 1);
         rkey[s] = comp_min[c];
         rval[s] = c;
@@ -303,11 +314,11 @@ __global__ __launch_bounds__(kBlock) void k_cl_number(const int32_t *sorted_root
 }
 
 // cell label: the label of its component if it has core points, else -1
-__global__ __launch_bounds__(kBlock) void k_cl_celllabel(const int32_t *parent, const int32_t *first_core,
+__global__ __launch_bounds__(kBlock) void k_cl_celllabel(const int32_t *root, const int32_t *first_core,
                                                          const int32_t *root_label, int32_t C, int32_t *clabel) {
     const int c = (int)((int64_t)blockIdx.x * kBlock + threadIdx.x);
     if (c >= C) return;
-    clabel[c] = first_core[c] >= 0 ? root_label[parent[c]] : -1;
+    clabel[c] = first_core[c] >= 0 ? root_label[root[c]] : -1;
 }
 
 // ---- 6. labels: core -> its cluster; border -> lowest cluster in reach ----
@@ -489,7 +500,7 @@ hipError_t cluster_points(const double2 *pts, int64_t n, double eps, int64_t min
     int32_t C = 0;
     CL_TRY(hipMemcpyAsync(&C, cid + n - 1, 4, hipMemcpyDeviceToHost, s));
     CL_TRY(hipStreamSynchronize(s));
-    int32_t *cstart, *nbr, *first_core, *parent, *clabel, *root_label, *rval, *srval, *nroots;
+    int32_t *cstart, *nbr, *first_core, *parent, *root, *clabel, *root_label, *rval, *srval, *nroots;
     uint64_t *ckey;
     double4 *cbox;
     uint32_t *comp_min, *rkey, *srkey;
@@ -501,6 +512,7 @@ hipError_t cluster_points(const double2 *pts, int64_t n, double eps, int64_t min
     CL_TRY(sc.get(&core, n));
     CL_TRY(sc.get(&first_core, C));
     CL_TRY(sc.get(&parent, C));
+    CL_TRY(sc.get(&root, C));
     CL_TRY(sc.get(&comp_min, C));
     CL_TRY(sc.get(&clabel, C));
     CL_TRY(sc.get(&root_label, C));
@@ -521,8 +533,9 @@ hipError_t cluster_points(const double2 *pts, int64_t n, double eps, int64_t min
     CL_TRY(hipMemsetAsync(nroots, 0, 4, s));
     hipLaunchKernelGGL(k_cl_union, dim3(cl_grid((int64_t)C * kNbr)), dim3(kBlock), 0, s, pts, sidx, cstart, cbox, nbr,
                        first_core, core, C, g, parent);
-    hipLaunchKernelGGL(k_cl_roots, dim3(cl_grid(C)), dim3(kBlock), 0, s, parent, first_core, sidx, C, comp_min);
-    hipLaunchKernelGGL(k_cl_rootlist, dim3(cl_grid(C)), dim3(kBlock), 0, s, parent, comp_min, C, rkey, rval, nroots);
+    hipLaunchKernelGGL(k_cl_roots, dim3(cl_grid(C)), dim3(kBlock), 0, s, parent, first_core, sidx, C, root,
+                       comp_min);
+    hipLaunchKernelGGL(k_cl_rootlist, dim3(cl_grid(C)), dim3(kBlock), 0, s, root, comp_min, C, rkey, rval, nroots);
     int32_t K = 0;
     CL_TRY(hipMemcpyAsync(&K, nroots, 4, hipMemcpyDeviceToHost, s));
     CL_TRY(hipStreamSynchronize(s));
@@ -534,7 +547,7 @@ hipError_t cluster_points(const double2 *pts, int64_t n, double eps, int64_t min
         CL_TRY(rocprim::radix_sort_pairs(rtmp, rb, rkey, srkey, rval, srval, (size_t)K, 0, 32, s));
         hipLaunchKernelGGL(k_cl_number, dim3(cl_grid(K)), dim3(kBlock), 0, s, srval, K, root_label);
     }
-    hipLaunchKernelGGL(k_cl_celllabel, dim3(cl_grid(C)), dim3(kBlock), 0, s, parent, first_core, root_label, C,
+    hipLaunchKernelGGL(k_cl_celllabel, dim3(cl_grid(C)), dim3(kBlock), 0, s, root, first_core, root_label, C,
                        clabel);
     int32_t *labels;
     CL_TRY(sc.get(&labels, n));

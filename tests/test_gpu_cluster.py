@@ -73,6 +73,8 @@ def test_cluster_points_vs_sklearn_random():
         lab_ref = sk.DBSCAN(eps=0.5, min_samples=ms).fit(pts).labels_
         cen, lab = GeometryUtils.dbscan(pts, 0.5, ms)
         assert np.array_equal(lab, lab_ref), trial
+        for rep in range(4):      # the union-find is concurrent: results must not vary
+            assert np.array_equal(GeometryUtils.dbscan(pts, 0.5, ms)[1], lab_ref), (trial, rep)
         K = lab_ref.max() + 1
         for c in range(K):
             m = pts[lab_ref == c]
