@@ -197,3 +197,36 @@ def corner_measurements(pose, scan: int, seed: int = 0, noise: float = 0.02,
         ly += rng.normal(0.0, noise)
         rows.append(encode(lx, ly))
     return np.array(rows, dtype=np.float64).reshape(-1, 2)
+
+
+# --------------------------------------------------------------- front-end ---
+# Scenes for LandmarkUtils.get_measurements_to_landmarks (landmark_utils.py:21-89):
+# closed polygons (walls), ray-cast like Robot.scan_environment (robot.py:32-58):
+# beams outside [min_range, max_range] are dropped.
+
+L_ROOM = np.array([[-6.0, -4.0], [6.0, -4.0], [6.0, 1.0], [2.0, 1.0], [2.0, 5.0], [-6.0, 5.0]])
+BOX_ROOM = np.array([[-ROOM[0] / 2, -ROOM[1] / 2], [ROOM[0] / 2, -ROOM[1] / 2],
+                     [ROOM[0] / 2, ROOM[1] / 2], [-ROOM[0] / 2, ROOM[1] / 2]])
+
+
+def polygon_scan(vertices: np.ndarray, pose: tuple[float, float, float], P: int = 180,
+                 rng: np.random.Generator | None = None, noise: float = RANGE_NOISE,
+                 min_range: float = 0.1, max_range: float = 10.0) -> np.ndarray:
+    """Robot-frame points (x, y) of a P-beam scan over -90..90 deg of a polygon."""
+    px, py, pyaw = pose
+    ang = beam_angles(P)
+    dx, dy = np.cos(ang + pyaw), np.sin(ang + pyaw)
+    v0 = np.asarray(vertices, dtype=np.float64)
+    v1 = np.roll(v0, -1, axis=0)
+    ex, ey = (v1 - v0)[:, 0], (v1 - v0)[:, 1]
+    wx, wy = v0[:, 0] - px, v0[:, 1] - py
+    den = dx[:, None] * ey[None, :] - dy[:, None] * ex[None, :]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = (wx[None, :] * ey[None, :] - wy[None, :] * ex[None, :]) / den
+        u = (wx[None, :] * dy[:, None] - wy[None, :] * dx[:, None]) / den
+    ok = (np.abs(den) > 1e-12) & (t > 0) & (u >= 0) & (u <= 1)
+    r = np.where(ok, t, np.inf).min(axis=1)
+    if rng is not None and noise > 0:
+        r = r + rng.normal(0.0, noise, size=P)
+    keep = (r >= min_range) & (r <= max_range)
+    return np.column_stack((r[keep] * np.cos(ang[keep]), r[keep] * np.sin(ang[keep])))

@@ -30,8 +30,9 @@ class OrcState(C.Structure):
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "fs2_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("fs2_oracle.c", "fs2_frontend_oracle.c", "Makefile")]
+    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(s)
+                                                    for s in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -66,6 +67,26 @@ def lib():
         L.orc_correlate_reflect.argtypes = [_dp, C.c_int64, C.c_int64, _dp, C.c_int32, _dp]
         L.orc_gauss_pdf2.restype = C.c_double
         L.orc_gauss_pdf2.argtypes = [_dp, _dp]
+        _fp = C.POINTER(C.c_float)
+        L.orc_np_sinf.restype = C.c_float
+        L.orc_np_sinf.argtypes = [C.c_float]
+        L.orc_np_cosf.restype = C.c_float
+        L.orc_np_cosf.argtypes = [C.c_float]
+        L.orc_fe_geom.argtypes = [_dp, C.c_int, _lp]
+        L.orc_fe_raster.argtypes = [_dp, C.c_int, _lp, C.POINTER(C.c_uint8)]
+        L.orc_fe_trig.argtypes = [C.c_int, C.c_float, _fp, _fp]
+        L.orc_fe_hough.restype = C.c_int
+        L.orc_fe_hough.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int, _fp, C.c_int]
+        L.orc_fe_intersections.restype = C.c_int
+        L.orc_fe_intersections.argtypes = [_fp, C.c_int, C.c_int64, C.c_int64, _fp, C.c_int]
+        L.orc_fe_back.argtypes = [_fp, C.c_int, C.c_int64, C.c_int64, C.c_int, _dp]
+        L.orc_fe_cluster1.restype = C.c_int
+        L.orc_fe_cluster1.argtypes = [_dp, C.c_int, C.c_double, C.c_int, _dp]
+        L.orc_fe_corners.restype = C.c_int
+        L.orc_fe_corners.argtypes = [_dp, C.c_int, _dp, C.c_int, C.c_double, _dp]
+        L.orc_fe_measure.argtypes = [_dp, C.c_int, C.c_int, _dp]
+        L.orc_fe_extract.restype = C.c_int
+        L.orc_fe_extract.argtypes = [_dp, C.c_int, _dp, C.c_int32, C.c_int, _dp, C.c_int, _ip]
         _lib = L
     return _lib
 
@@ -181,6 +202,103 @@ def line_filter(points, sigma=0.1):
         lib().orc_correlate_reflect(_p(src), len(src), 1, _p(wts), r, _p(dst))
         out[:, col] = dst
     return out
+
+
+# ------------------------------------------------------------- front-end ---
+# LandmarkUtils.get_measurements_to_landmarks (landmark_utils.py:21-89) and
+# HoughTransformation (hough_transformation.py:14-145), fs2_frontend_oracle.c.
+
+def _f32p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def np_sinf(x):
+    return np.float32(lib().orc_np_sinf(float(np.float32(x))))
+
+
+def np_cosf(x):
+    return np.float32(lib().orc_np_cosf(float(np.float32(x))))
+
+
+def fe_geom(points):
+    pts = _f64(points)
+    g = np.zeros(4, np.int64)
+    lib().orc_fe_geom(_p(pts), len(pts), _p(g, _lp))
+    return [int(v) for v in g]
+
+
+def fe_image(points):
+    """The uint8 image HoughTransformation.__create_hough_transformation_image draws."""
+    pts = _f64(points)
+    g = np.array(fe_geom(pts), np.int64)
+    img = np.zeros((int(g[3]), int(g[2])), np.uint8)
+    lib().orc_fe_raster(_p(pts), len(pts), _p(g, _lp), img.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return img, [int(v) for v in g]
+
+
+def fe_hough(img, threshold=80):
+    """cv2.HoughLines(img, 1, np.pi / 180, threshold): float32 [K][2] (rho, theta)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    ip = img.ctypes.data_as(C.POINTER(C.c_uint8))
+    K = lib().orc_fe_hough(ip, w, h, threshold, None, 0)
+    lines = np.zeros((K, 2), np.float32)
+    if K:
+        lib().orc_fe_hough(ip, w, h, threshold, _f32p(lines), K)
+    return lines
+
+
+def fe_intersections(lines, width, height):
+    lines = np.ascontiguousarray(lines, dtype=np.float32).reshape(-1, 2)
+    K = len(lines)
+    n = lib().orc_fe_intersections(_f32p(lines), K, width, height, None, 0)
+    out = np.zeros((n, 2), np.float32)
+    if n:
+        lib().orc_fe_intersections(_f32p(lines), K, width, height, _f32p(out), n)
+    return out
+
+
+def fe_back(isect, off_x, off_y, legacy=False):
+    isect = np.ascontiguousarray(isect, dtype=np.float32).reshape(-1, 2)
+    out = np.zeros((len(isect), 2))
+    lib().orc_fe_back(_f32p(isect), len(isect), off_x, off_y, int(legacy), _p(out))
+    return out
+
+
+def fe_cluster1(points, eps=0.5, legacy=False):
+    pts = _f64(points).reshape(-1, 2)
+    out = np.zeros((max(len(pts), 1), 2))
+    K = lib().orc_fe_cluster1(_p(pts), len(pts), eps, int(legacy), _p(out))
+    return out[:K]
+
+
+def fe_corners(centres, scan, threshold=0.1):
+    c = _f64(centres).reshape(-1, 2)
+    sc = _f64(scan).reshape(-1, 2)
+    out = np.zeros((max(len(c), 1), 2))
+    m = lib().orc_fe_corners(_p(c), len(c), _p(sc), len(sc), threshold, _p(out))
+    return out[:m]
+
+
+def fe_measure(corners, legacy=False):
+    c = _f64(corners).reshape(-1, 2)
+    out = np.zeros((len(c), 2))
+    lib().orc_fe_measure(_p(c), len(c), int(legacy), _p(out))
+    return out
+
+
+def fe_extract(points, sigma=0.1, legacy=False):
+    """Measurements (distance, angle) [M][2] and counts (lines, intersections,
+    clusters, corners) for one scan."""
+    pts = _f64(points).reshape(-1, 2)
+    wts, r = gaussian_weights(sigma)
+    cap = 4096
+    out = np.zeros((cap, 2))
+    counts = np.zeros(4, np.int32)
+    m = lib().orc_fe_extract(_p(pts), len(pts), _p(wts), r, int(legacy), _p(out), cap, _p(counts, _ip))
+    if m < 0:
+        raise MemoryError("front-end oracle allocation failed")
+    return out[:min(m, cap)].copy(), counts
 
 
 class OracleFilter:
