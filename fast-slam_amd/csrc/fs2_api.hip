@@ -14,6 +14,7 @@
 
 #include "../../include/fs2.h"
 #include "fs2_comm.hpp"
+#include "fs2_frontend.hpp"
 #include "fs2_kernels.hpp"
 
 using namespace fs2;
@@ -1166,6 +1167,100 @@ int fs2_cluster_points(int32_t device, const double *points, int64_t n, double e
     *n_clusters = K;
     if (K > cap) return set_err(nullptr, FS2_ERR_ARG, "%lld clusters, centre buffer holds %lld", (long long)K,
                                 (long long)cap);
+    return FS2_OK;
+}
+
+// fs2_frontend: the batched device pipeline (fs2_frontend.hip) up to the corners;
+// the corners' (distance, angle) (GeometryUtils.calculate_distance_and_angle,
+// geometry_utils.py:65-74: math.sqrt(x ** 2 + y ** 2), math.atan2(y, x)) on the
+// host with the C library's powf / pow / atan2 -- the functions numpy's scalar
+// power and math.atan2 call -- so the measurements fed to fs2_iterate are the
+// reference's bits.  Called through volatile pointers so that the compiler
+// cannot rewrite pow(x, 2) as x * x (which differs in the last bit at times).
+static float (*volatile g_powf)(float, float) = powf;
+static double (*volatile g_pow)(double, double) = pow;
+
+int fs2_frontend(int32_t device, int32_t B, const int64_t *offsets, const double *points, int32_t where,
+                 const double *taps, int32_t radius, int32_t legacy, fs2_frontend_out *out) {
+    if (B < 0 || !offsets || !taps || radius < 0 || !out || !out->counts || out->cap < 0 ||
+        (legacy != 0 && legacy != 1))
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_frontend: bad arguments");
+    if (B == 0) return FS2_OK;
+    if (offsets[0] != 0) return set_err(nullptr, FS2_ERR_ARG, "fs2_frontend: offsets[0] must be 0");
+    for (int32_t b = 0; b < B; ++b)
+        if (offsets[b + 1] < offsets[b]) return set_err(nullptr, FS2_ERR_ARG, "fs2_frontend: offsets decrease");
+    if (offsets[B] > 0 && !points) return set_err(nullptr, FS2_ERR_ARG, "fs2_frontend: null points");
+    if (offsets[B] >= ((int64_t)1 << 31) / 13)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_frontend: too many points in one call");
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 16, &sc);
+    if (rc) return rc;
+    static FeWorkspace ws[64];
+    FeArgs a;
+    a.B = B;
+    a.offs = offsets;
+    a.points = points;
+    a.points_on_device = where == FS2_DEVICE;
+    a.taps = taps;
+    a.radius = radius;
+    a.legacy = legacy;
+    a.cap = out->cap;
+    FeHostOut o;
+    o.lines = out->lines;
+    o.intersections = out->intersections;
+    o.clusters = out->clusters;
+    std::vector<double> corners;
+    const bool want_corners = out->corners || out->measurements;
+    if (want_corners) {
+        corners.resize((size_t)B * std::max(out->cap, 1) * 2);
+        o.corners = corners.data();
+    }
+    hipError_t e = frontend_run(ws[device], a, o, sc->stream);
+    if (e != hipSuccess) return set_err(nullptr, FS2_ERR_HIP, "fs2_frontend: %s", hipGetErrorString(e));
+    for (int32_t b = 0; b < B; ++b) {
+        switch (o.status[b]) {
+        case kFeOk: break;
+        case kFeEmpty: return set_err(nullptr, FS2_ERR_ARG, "scan %d has no points (zero-size array)", b);
+        case kFeNonFinite: return set_err(nullptr, FS2_ERR_ARG, "scan %d has non-finite points", b);
+        case kFeTooLarge:
+            return set_err(nullptr, FS2_ERR_ARG, "scan %d spans more than %d px of Hough image", b, kFeMaxRow / 2 - 1);
+        default: return set_err(nullptr, FS2_ERR_ARG, "scan %d has more than %d Hough lines", b, kFeMaxLines);
+        }
+    }
+    std::memcpy(out->counts, o.counts.data(), sizeof(int32_t) * 4 * B);
+    const int cap = out->cap;
+    for (int32_t b = 0; b < B; ++b) {
+        const int32_t *c = out->counts + 4 * b;
+        if ((out->lines && c[0] > cap) || (out->intersections && c[1] > cap) || (out->clusters && c[2] > cap) ||
+            (want_corners && c[3] > cap))
+            return set_err(nullptr, FS2_ERR_ARG, "scan %d: counts (%d, %d, %d, %d) exceed cap %d", b, c[0], c[1], c[2],
+                           c[3], cap);
+    }
+    if (want_corners) {
+        for (int32_t b = 0; b < B; ++b) {
+            const int32_t m = out->counts[4 * b + 3];
+            for (int32_t k = 0; k < m; ++k) {
+                const size_t r = ((size_t)b * cap + k) * 2;
+                const double x = corners[r], y = corners[r + 1];
+                if (out->corners) {
+                    out->corners[r] = x;
+                    out->corners[r + 1] = y;
+                }
+                if (out->measurements) {
+                    double d;
+                    if (legacy) {
+                        d = std::sqrt(g_pow(x, 2.0) + g_pow(y, 2.0));
+                    } else {
+                        const float s = g_powf((float)x, 2.0f) + g_powf((float)y, 2.0f);
+                        d = std::sqrt((double)s);
+                    }
+                    out->measurements[r] = d;
+                    out->measurements[r + 1] = std::atan2(y, x);
+                }
+            }
+        }
+    }
     return FS2_OK;
 }
 

@@ -4,11 +4,13 @@ Same public names as cy-rae/fast-slam's `fast_slam_2` package
 (fast_slam_2/__init__.py:5-22).  The particle update, ICP, LineFilter and the
 association / Mahalanobis helpers and the known-landmark clustering
 (update_known_landmarks / cluster_points) run in libfs2.so (HIP, gfx950);
-Serializer writes the viewer's JSON from one device download.  Robot,
-EvaluationUtils and HoughTransformation are simulator- or front-end-bound and
-outside this build's scope.
+Serializer writes the viewer's JSON from one device download; the landmark
+front-end (LandmarkUtils.get_measurements_to_landmarks, HoughTransformation)
+runs batched on the device too.  Robot and EvaluationUtils are simulator-bound
+(HAL) and outside this build's scope.
 """
 from .algorithms.fast_slam_2 import FastSLAM2
+from .algorithms.hough_transformation import HoughTransformation
 from .algorithms.icp import ICP
 from .algorithms.line_filter import LineFilter
 from .models.directed_point import DirectedPoint
@@ -21,15 +23,15 @@ from .utils.geometry_utils import GeometryUtils
 from .utils.landmark_utils import LandmarkUtils
 from .utils.serializer import Serializer
 
-_OUT_OF_SCOPE = {"Robot", "EvaluationUtils", "HoughTransformation"}
+_OUT_OF_SCOPE = {"Robot", "EvaluationUtils"}
 
 
 def __getattr__(name):
     if name in _OUT_OF_SCOPE:
-        raise ImportError(f"fast_slam_2.{name} is outside the particle-update hot path this "
-                          f"build replaces (simulator/front-end bound; SURVEY.md §2, §8f)")
+        raise ImportError(f"fast_slam_2.{name} drives the JdeRobot simulator (HAL), which this "
+                          f"build does not replace (SURVEY.md §2)")
     raise AttributeError(name)
 
 
-__all__ = ["FastSLAM2", "ICP", "LineFilter", "DirectedPoint", "EvaluationResults", "Landmark",
+__all__ = ["FastSLAM2", "HoughTransformation", "ICP", "LineFilter", "DirectedPoint", "EvaluationResults", "Landmark",
            "Measurement", "Particle", "Point", "GeometryUtils", "LandmarkUtils", "Serializer"]

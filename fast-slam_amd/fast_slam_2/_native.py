@@ -100,6 +100,12 @@ class fs2_profile(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class fs2_frontend_out(C.Structure):
+    _fields_ = [("cap", C.c_int32), ("lines", C.c_void_p), ("intersections", C.c_void_p),
+                ("clusters", C.c_void_p), ("corners", C.c_void_p), ("measurements", C.c_void_p),
+                ("counts", C.c_void_p)]
+
+
 class FS2Error(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"libfs2 error {code}: {msg}")
@@ -143,6 +149,8 @@ SIGNATURES = [
                                      C.POINTER(C.c_int64), _vp, C.c_int32]),
     ("fs2_update_known_landmarks", C.c_int, [_H, C.c_double, C.c_double, _dp, C.c_int64,
                                              C.POINTER(C.c_int64)]),
+    ("fs2_frontend", C.c_int, [C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _dp, C.c_int32, C.c_int32,
+                               C.POINTER(fs2_frontend_out)]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
 ]
 

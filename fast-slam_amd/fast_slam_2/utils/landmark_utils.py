@@ -1,4 +1,6 @@
-"""Landmark association (reference: fast_slam_2/utils/landmark_utils.py:92-117)."""
+"""LandmarkUtils (reference: fast_slam_2/utils/landmark_utils.py): front-end
+(get_measurements_to_landmarks, :21-89), association (:92-117) and known-landmark
+clustering (:120-144), all on the GPU."""
 from __future__ import annotations
 
 import ctypes as C
@@ -33,9 +35,29 @@ class LandmarkUtils:
 
     @staticmethod
     def get_measurements_to_landmarks(scanned_points):
-        raise NotImplementedError(
-            "landmark extraction (Hough + DBSCAN front-end, landmark_utils.py:21-89) is outside "
-            "the particle-update hot path (SURVEY.md §8f, NEXT)")
+        """Measurements (distance, angle) to the corners observed in a scan
+        (landmark_utils.py:21-36): LineFilter, Hough intersections, DBSCAN(0.5, 1)
+        centres and the 0.1 m corner test on the GPU (fs2_frontend)."""
+        from ..models.measurement import Measurement
+        m = LandmarkUtils.get_measurements_batch([scanned_points])[0]
+        return [Measurement(float(d), float(a)) for d, a in m]
+
+    @staticmethod
+    def get_measurements_batch(scans, sigma: float = 0.1):
+        """Batched form: one [M_b][2] (distance, angle) array per scan, all scans in
+        one device pass."""
+        from ..algorithms import _frontend
+        return _frontend.run(scans, sigma=sigma, want=("measurements",))["measurements"]
+
+    @staticmethod
+    def get_observed_landmarks(scanned_points):
+        """Corners as Landmark objects (landmark_utils.py:39-64); coordinates are numpy
+        float32 scalars (float64 with config.FRONTEND_NUMPY1_PROMOTION) as in the reference."""
+        from ..algorithms import _frontend
+        from ..models.landmark import Landmark
+        c = _frontend.run([scanned_points], want=("corners",))["corners"][0]
+        t = np.float64 if config.FRONTEND_NUMPY1_PROMOTION else np.float32
+        return [Landmark(t(x), t(y)) for x, y in c]
 
     @staticmethod
     def update_known_landmarks(particles):

@@ -241,6 +241,39 @@ int fs2_cluster_points(int32_t device, const double *points, int64_t n, double e
 int fs2_update_known_landmarks(fs2_handle *h, double eps, double min_fraction, double *centres,
                                int64_t cap, int64_t *n_clusters);
 
+/* ------------------------------------------- landmark front-end (§8f 1) ---- */
+
+/* Outputs of fs2_frontend; every array is [B][cap][2] on the host and may be
+ * NULL except counts.  Rows past a scan's count are left undefined. */
+typedef struct fs2_frontend_out {
+    int32_t cap;             /* rows per scan of each non-NULL array below */
+    float *lines;            /* (rho, theta) in cv2.HoughLines order (hough_transformation.py:25) */
+    double *intersections;   /* HoughTransformation.detect_line_intersections (hough_transformation.py:14-41) */
+    double *clusters;        /* GeometryUtils.cluster_points(intersections, 0.5, 1) (landmark_utils.py:54-59) */
+    double *corners;         /* LandmarkUtils.get_observed_landmarks (landmark_utils.py:39-64): (x, y) */
+    double *measurements;    /* LandmarkUtils.get_measurements_to_landmarks (landmark_utils.py:21-36):
+                                (distance, angle) = GeometryUtils.calculate_distance_and_angle */
+    int32_t *counts;         /* [B][4]: lines, intersections, clusters, corners (required) */
+} fs2_frontend_out;
+
+/* Replaces LandmarkUtils.get_measurements_to_landmarks (utils/landmark_utils.py:21-89)
+ * with LineFilter.filter (algorithms/line_filter.py:12-21), HoughTransformation
+ * (algorithms/hough_transformation.py:14-145: image at 100 px/m, padding 20,
+ * filled radius-2 circles, cv2.HoughLines(img, 1, pi/180, 80), pairwise
+ * intersections of lines >= 45 deg apart), DBSCAN(eps 0.5, min_samples 1) means
+ * and the 0.1 m corner test, for B scans in one call.  Scan b is points
+ * [offsets[b], offsets[b+1]) of points[][2] (x, y); offsets: host, B + 1 entries.
+ * taps/radius: the LineFilter Gaussian (fs2_gaussian_taps; sigma 0.1 gives the
+ * identity, radius 0).  legacy = 0 follows numpy >= 2 scalar promotion (float32
+ * intersections, centres and corners; what the fixtures pin), 1 numpy 1.x
+ * (float64 from the back-conversion on).  where: FS2_HOST / FS2_DEVICE for points.
+ * FS2_ERR_ARG for an empty or non-finite scan (the reference raises ValueError),
+ * an image over 20000 px in width + height, more than 4096 Hough lines in a
+ * scan, or a count above out->cap for a requested array (counts still filled). */
+int fs2_frontend(int32_t device, int32_t B, const int64_t *offsets, const double *points,
+                 int32_t where, const double *taps, int32_t radius, int32_t legacy,
+                 fs2_frontend_out *out);
+
 /* ncclUniqueId for fs2_config.comm_id (call on rank 0, broadcast to all ranks). */
 int fs2_comm_unique_id(uint8_t out[128]);
 

@@ -22,7 +22,8 @@ def main():
         f.write("# durations in microseconds; names shortened\n")
         f.write(f"{'kernel':60s} {'calls':>6s} {'total_us':>12s} {'avg_us':>11s} {'pct':>6s}\n")
         for name, calls, tot, avg, pct in rows:
-            short = name.split("(")[0][:60] if name.startswith(("fs2", "void fs2")) else name[:60]
+            short = name.replace("(anonymous namespace)::", "")
+            short = short.split("(")[0][:60] if short.startswith(("fs2", "void fs2")) else short[:60]
             f.write(f"{short:60s} {calls:6d} {tot:12.1f} {avg:11.1f} {pct:6.2f}\n")
     print(open(out).read())
 

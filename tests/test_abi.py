@@ -36,7 +36,8 @@ def test_struct_layout_matches_header():
     from fast_slam_2 import _native
     src = open(os.path.join(REPO, "include", "fs2.h")).read()
     for cname, py in [("fs2_config", _native.fs2_config), ("fs2_iter_stats", _native.fs2_iter_stats),
-                      ("fs2_profile", _native.fs2_profile)]:
+                      ("fs2_profile", _native.fs2_profile),
+                      ("fs2_frontend_out", _native.fs2_frontend_out)]:
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []
@@ -46,7 +47,7 @@ def test_struct_layout_matches_header():
                 continue
             names = decl.split(None, 1)[1]
             for nm in names.split(","):
-                fields.append(re.sub(r"\[.*\]", "", nm).strip())
+                fields.append(re.sub(r"\[.*\]", "", nm).strip().lstrip("*"))
         assert [f for f, _ in py._fields_] == fields, cname
 
 
