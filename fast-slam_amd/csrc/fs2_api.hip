@@ -82,6 +82,16 @@ struct fs2_handle {
     int32_t *bcnt = nullptr;               // sweep block counts
     int64_t *nfree_dev = nullptr;
     uint64_t collections = 0;
+    // slot records (fs2_kernels.hpp): pool, free list, marks (collected with the pages)
+    char *rpool = nullptr;
+    int64_t nrecs = 0;
+    uint32_t *rfreel = nullptr;
+    int64_t rnfree = 0, rcursor = 0;
+    uint8_t *rmark = nullptr;
+    uint8_t repoch = 0;
+    int32_t *rbcnt = nullptr;
+    int64_t *rnfree_dev = nullptr;
+    int64_t s_recv = 0;                    // slots received by the last resample
     int32_t *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
     int cap = 0, max_cap = kMaxSlots;
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
@@ -112,7 +122,7 @@ struct fs2_handle {
     std::vector<size_t> sendcap, recvcap;
     int32_t n_recv = 0;                             // particles received by the last resample
 
-    MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows}; }
+    MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
     bool sequential() const {
         const int mode = cfg.reduce_mode;
@@ -144,8 +154,9 @@ static int grow_rows(fs2_handle *h, int need_slots) {
 }
 
 // Collect the page pool: every page the current page table does not refer to
-// becomes free (fs2_pages.hip); the reservation cursor restarts.
-static int collect(fs2_handle *h) {
+// becomes free (fs2_pages.hip); the reservation cursor restarts.  With
+// `records`, the record pool is collected from the same marks as well.
+static int collect(fs2_handle *h, bool records) {
     hipStream_t s = h->stream;
     if (h->epoch == 255) {
         HIP_TRY(h, hipMemsetAsync(h->mark, 0, (size_t)h->npool, s));
@@ -155,6 +166,17 @@ static int collect(fs2_handle *h) {
     HIP_TRY(h, launch_collect(h->map(), h->cnt[h->cur], h->npool, h->mark, h->epoch, h->bcnt, h->freel,
                               h->nfree_dev, s));
     HIP_TRY(h, hipMemcpyAsync(&h->nfree, h->nfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (records && h->nrecs > 0) {
+        if (h->repoch == 255) {
+            HIP_TRY(h, hipMemsetAsync(h->rmark, 0, (size_t)h->nrecs, s));
+            h->repoch = 0;
+        }
+        h->repoch += 1;
+        HIP_TRY(h, launch_collect_records(h->pool, h->npool, h->mark, h->epoch, h->nrecs, h->rmark, h->repoch,
+                                          h->rbcnt, h->rfreel, h->rnfree_dev, s));
+        HIP_TRY(h, hipMemcpyAsync(&h->rnfree, h->rnfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        h->rcursor = 0;
+    }
     HIP_TRY(h, hipStreamSynchronize(s));
     h->cursor = 0;
     h->collections += 1;
@@ -185,14 +207,42 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
     h->bcnt = nullptr;
     HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int32_t) * (size_t)collect_blocks(pages)));
     h->npool = pages;
-    return collect(h);
+    return collect(h, false);
+}
+
+// Record pool of `n` records (existing records keep their ids), free list, marks.
+static int grow_recs(fs2_handle *h, int64_t n) {
+    if (n <= h->nrecs) return FS2_OK;
+    if (n > (int64_t)0xfffffffell * 16)
+        return set_err(&h->err, FS2_ERR_OOM, "record pool of %lld records exceeds the id space", (long long)n);
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    char *rp = nullptr;
+    HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
+    if (h->rpool) HIP_TRY(h, hipMemcpy(rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
+    hipFree(h->rpool);
+    h->rpool = rp;
+    uint8_t *mark = nullptr;
+    HIP_TRY(h, hipMalloc(&mark, (size_t)n));
+    HIP_TRY(h, hipMemset(mark, 0, (size_t)n));
+    hipFree(h->rmark);
+    h->rmark = mark;
+    h->repoch = 0;
+    hipFree(h->rfreel);
+    h->rfreel = nullptr;
+    HIP_TRY(h, hipMalloc(&h->rfreel, sizeof(uint32_t) * (size_t)n));
+    hipFree(h->rbcnt);
+    h->rbcnt = nullptr;
+    HIP_TRY(h, hipMalloc(&h->rbcnt, sizeof(int32_t) * (size_t)collect_blocks(n)));
+    h->nrecs = n;
+    return collect(h, true);
 }
 
 // Reserve `need` free pages (collecting, then growing the pool, when short);
-// returns the reservation's first index into freel.
+// returns the reservation's first index into freel.  A launch that needs both
+// reserves its records first: a record collection restarts the page cursor.
 static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
     if (h->cursor + need > h->nfree) {
-        int rc = collect(h);
+        int rc = collect(h, false);
         if (rc) return rc;
         if (need > h->nfree) {
             const int64_t live = h->npool - h->nfree;
@@ -203,6 +253,22 @@ static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
     out->freel = h->freel;
     out->base = h->cursor;
     h->cursor += need;
+    return FS2_OK;
+}
+
+static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
+    if (h->rcursor + need > h->rnfree) {
+        int rc = collect(h, true);
+        if (rc) return rc;
+        if (need > h->rnfree) {
+            const int64_t live = h->nrecs - h->rnfree;
+            rc = grow_recs(h, std::max(h->nrecs + h->nrecs / 2, live + 2 * need));
+            if (rc) return rc;
+        }
+    }
+    out->rfreel = h->rfreel;
+    out->rbase = h->rcursor;
+    h->rcursor += need;
     return FS2_OK;
 }
 
@@ -258,6 +324,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     std::vector<fs2comm::Xfer> sends, recvs;
     rs.npeers = 0;
     int32_t kbase = 0;
+    int64_t sbase = 0;
     for (int q = 0; q < G; ++q) {
         if (q == R) continue;
         if (row[2 * q])
@@ -272,11 +339,14 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         pp.pay = h->recvbuf[q] + K * 64;
         pp.K = (int32_t)K;
         pp.kbase = kbase;
+        pp.sbase = sbase;
         kbase += (int32_t)K;
+        sbase += S;
     }
     rc = h->tp->exchange(sends, recvs, s, &h->err);
     if (rc) return rc;
     h->n_recv = kbase;
+    h->s_recv = sbase;
     return FS2_OK;
 }
 
@@ -321,6 +391,7 @@ static void free_handle(fs2_handle *h) {
     }
     hipFree(h->rdesc);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
+    hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
@@ -387,10 +458,11 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= alloc((void **)&h->cnt[s], n * 4) == hipSuccess;
     }
     ok &= alloc((void **)&h->nfree_dev, sizeof(int64_t)) == hipSuccess;
+    ok &= alloc((void **)&h->rnfree_dev, sizeof(int64_t)) == hipSuccess;
     ok &= alloc((void **)&h->mlo, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->out_src, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->cand, n * 2 * kMaxCand) == hipSuccess;
+    ok &= alloc((void **)&h->cand, n * 8 * kMaxCand) == hipSuccess;
     ok &= alloc((void **)&h->ncand, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
     ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
@@ -425,8 +497,11 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     }
     int rc = grow_rows(h, std::max(cfg->landmark_capacity, 1));
     if (rc) return fail(rc);
-    // pool: twice the initial maps plus room for a few scans of new pages
+    // pool: twice the initial maps plus room for a few scans of new pages;
+    // records: the initial maps plus room for many scans of writes
     rc = grow_pool(h, n * h->rows * 2 + 8 * n + 1024);
+    if (rc) return fail(rc);
+    rc = grow_recs(h, n * h->cap + n * h->cap / 4 + 64 * n + 1024);
     if (rc) return fail(rc);
     h->sendbuf.assign(G, nullptr);
     h->recvbuf.assign(G, nullptr);
@@ -561,6 +636,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
                                       std::fabs(oy - (double)up.meas.fy[k]));
             up.meas.fe[k] = std::isfinite(e) ? std::nextafter((float)e, INFINITY) : INFINITY;
         }
+        rc = reserve_recs(h, (int64_t)up.m * h->n, &up.alloc);
+        if (rc) return rc;
         rc = reserve_pages(h, (int64_t)up.m * h->n, &up.alloc);
         if (rc) return rc;
         up.map = h->map();
@@ -666,7 +743,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         if (sh) {
             rc = exchange_particles(h, rs);
             if (rc) return rc;
-            // fresh pages for the received maps: record r, row k -> base + r * rows + k
+            // fresh records and pages for the received maps: record r, row k ->
+            // page base + r * rows + k; slot q -> record rbase + peer sbase + soff + q
+            rc = reserve_recs(h, h->s_recv, &rs.alloc);
+            if (rc) return rc;
             rc = reserve_pages(h, (int64_t)h->n_recv * h->rows, &rs.alloc);
             if (rc) return rc;
             rs.map = h->map();
@@ -726,7 +806,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 16ull * st.groups +
                                                           16ull * st.words + 8ull * (uint64_t)h->n * passes
                                                     : 0ull) +
-                                52ull * st.candidates + 64ull * st.written + fixed_bytes +
+                                48ull * st.candidates + 64ull * st.written + fixed_bytes +
                                 2ull * kPageBytes * st.cow_pages + 8ull * (uint64_t)h->nblocks();
         if (st.resampled)
             // page-table rows (read + write 4 B per page of every output) + scalar
@@ -827,6 +907,8 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             hipError_t e = hipMemcpy(stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
             if (e == hipSuccess) e = hipMemcpy(cstage, hc.data() + o, sizeof(int32_t) * k, hipMemcpyHostToDevice);
             PageAlloc pa{};
+            rc2 = reserve_recs(h, k * std::max(1, lm_cap), &pa);
+            if (rc2) break;
             rc2 = reserve_pages(h, k * rows_each, &pa);
             if (rc2) break;
             if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], s);

@@ -591,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_cl_gather_maps(MapRef map, const int
     const char *pg = page_of(map, j0, i);
     double2 *o = out + off[i];
     for (int j = j0; j < min(c, j0 + kPageSlots); ++j) {
-        const Slot sl = load_slot(pg, j);
+        const Slot sl = load_slot(map, pg, j);
         o[j] = make_double2(sl.mx, sl.my);
     }
 }

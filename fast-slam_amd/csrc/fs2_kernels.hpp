@@ -13,12 +13,14 @@ constexpr int kMaxSlots = 4096;      // landmark slots per particle max
 constexpr int kMaxRows = kMaxSlots / kPageSlots;   // page-table rows max
 constexpr int kMaxM = 4;             // measurements fused into one map pass
 constexpr int kScanGroup = kPageSlots;   // slots whose mirrors a lane loads per step (128 B)
-constexpr int kMaxCand = 16;         // candidate slots listed per particle and pass
+constexpr int kMaxCand = 8;          // candidate slots listed per particle and pass
 
-// A page holds 8 consecutive slots of a map:
-//   [0, 128)     8 x float4 gate mirror (x, y, s, 0)           -- read every scan
-//   [128, 512)   8 x 48 B fp64 slot (x, y, P00, P01, P10, P11)  -- read on candidates
-// Pages live in one pool (page id p at pool + 512 p).  A map is a row of page
+// A page holds 8 consecutive slots of a map as their gate mirrors, one 128-byte
+// line: 8 x {float x, float y, float s, uint32 rec}.  rec names the slot's fp64
+// record (x, y, P00, P01, P10, P11; 48 B) in the record pool.  Records are
+// immutable and shared like pages: a slot write stores a new record and points
+// the (private) page's mirror at it, so copy-on-write moves 128 B, not the slots.
+// Pages live in one pool (page id p at pool + 128 p).  A map is a row of page
 // descriptors in the page table pt[row][particle] (uint4):
 //   .x  page id; bit 31 says the map owns the page (no other entry refers to
 //       it) and may write it in place, otherwise the first write copies the page
@@ -28,9 +30,8 @@ constexpr int kMaxCand = 16;         // candidate slots listed per particle and 
 //   .w  fp32 smallest mirror s of the page (0: never reject)
 // The summary lets the candidate stream reject a whole page with one test that
 // is never less conservative than the slot tests it replaces (page_reject).
-constexpr int kPageBytes = 512;
-constexpr int kMirrorBytes = 128;
-constexpr int kSlotBytes = 48;
+constexpr int kPageBytes = 128;
+constexpr int kRecBytes = 48;
 constexpr uint32_t kOwned = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7fffffffu;
 
@@ -48,7 +49,7 @@ struct DevStats {
     int32_t error_flags;
     int32_t pad1;
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
-    unsigned long long words;    // candidate list words (4 slots each) written by k_candidates
+    unsigned long long words;    // candidate list entries (8 B: slot, record) written by k_candidates
     unsigned long long cow_pages;    // pages copied before their first write (shared)
     unsigned long long new_pages;    // fresh pages (appends, received particles)
     unsigned long long groups;       // page groups streamed by k_candidates
@@ -88,6 +89,7 @@ struct RecvPeer {
     const char *pay;         // payload base
     int32_t K;               // records from this peer
     int32_t kbase;           // index of its first record among all received
+    int64_t sbase;           // index of its first slot among all received slots
 };
 
 struct MeasPack {
@@ -102,14 +104,17 @@ struct MapRef {
     uint4 *pt;               // [rows][n] page descriptors
     int64_t n;               // row stride (local particles)
     int32_t rows;            // rows allocated
+    char *recs;              // record r at recs + r * kRecBytes
 };
 
-// Free pages reserved for one launch: lane i's t-th new page is
-// freel[base + t * n + i] (coalesced across lanes; unused ones return at the
-// next collection).
+// Free pages and records reserved for one launch: lane i's t-th new page is
+// freel[base + t * n + i], its t-th new record rfreel[rbase + t * n + i]
+// (coalesced across lanes; unused ones return at the next collection).
 struct PageAlloc {
     const uint32_t *freel;
     int64_t base;
+    const uint32_t *rfreel;
+    int64_t rbase;
 };
 
 struct UpdateParams {
@@ -130,7 +135,7 @@ struct UpdateParams {
     float gate2f;            // gate2 rounded up to fp32 (mirror test)
     int32_t filter;          // use the fp32 gate mirror
     PageAlloc alloc;         // up to m new pages per lane (copy-on-write, appends)
-    uint64_t *cand;          // [kMaxCand/4][n] candidate slots, four 16-bit per word
+    uint64_t *cand;          // [kMaxCand][n] candidates: record id << 16 | slot
     int32_t *ncand;          // [n] candidates found (> kMaxCand: list truncated)
     double R[4];
     double init_cov[4];
@@ -184,7 +189,8 @@ struct ResampleParams {
     MapRef map;              // current page table
     uint4 *opt;              // next page table [rows][n]
     uint4 *rdesc;            // [nrecv][rows] descriptors of received pages
-    PageAlloc alloc;         // pages for received particles: record r, row k -> base + r*rows + k
+    PageAlloc alloc;         // received particle r: row k -> page base + r*rows + k,
+                             // slot q -> record rbase + peer sbase + soff + q
     int32_t *rank_d;         // [n] rank among packed records
     int32_t *rank_e;         // [n] packed slot offset
     int32_t *iblk;           // [2 * nblk] per-block counts -> offsets
@@ -220,6 +226,8 @@ hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset);
 #endif
+// particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
+// alloc.rbase + p * lm_cap + j
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
                          int32_t rows_each, int32_t *cnt, hipStream_t s);
@@ -237,6 +245,11 @@ hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s);
 hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark,
                           uint8_t epoch, int32_t *bcnt, uint32_t *freel, int64_t *nfree_dev,
                           hipStream_t s);
+// after launch_collect with the same (mark, epoch): mark every record a live page
+// refers to, then list every unmarked record of [0, nrecs) in rfreel
+hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,
+                                  int64_t nrecs, uint8_t *rmark, uint8_t repoch, int32_t *rbcnt,
+                                  uint32_t *rfreel, int64_t *rnfree_dev, hipStream_t s);
 int64_t collect_blocks(int64_t npool);
 
 // known-landmark clustering (fs2_cluster.hip).  status: 0 ok, 1 non-finite input,

@@ -13,6 +13,13 @@
 //   k_sweep_count free pages per 4096-page block
 //   k_sweep_scan  exclusive scan of the block counts (one workgroup)
 //   k_sweep_write free page ids, in id order, into freel
+//
+// Slot records (fs2_kernels.hpp) are collected the same way, less often (the
+// record pool is sized for many scans of writes): after the page mark, every
+// marked page marks the records its 8 mirrors name (k_mark_recs), and the same
+// sweep lists the unmarked records.  A mirror past the map's end (in the last,
+// partly filled page) may name a stale record; it is marked too, which only
+// keeps that record out of the free list until the slot is overwritten.
 #include "fs2_reduce.hpp"
 
 namespace fs2 {
@@ -119,6 +126,31 @@ __global__ __launch_bounds__(kBlock) void k_sweep_write(const uint8_t *mark, int
         bits &= bits - 1u;
         freel[pos++] = (uint32_t)(id0 + e);
     }
+}
+
+// one lane per (page, slot) of the pool: 8 consecutive lanes read one 128-byte page
+__global__ __launch_bounds__(kBlock) void k_mark_recs(const char *pool, int64_t npool, const uint8_t *mark,
+                                                      uint8_t epoch, int64_t nrecs, uint8_t *rmark,
+                                                      uint8_t repoch) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t id = t / kPageSlots;
+    if (id >= npool || mark[id] != epoch) return;
+    const uint32_t r = mirror_rec(load_mirror(pool + id * kPageBytes, (int)(t % kPageSlots)));
+    if ((int64_t)r < nrecs) rmark[r] = repoch;
+}
+
+hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,
+                                  int64_t nrecs, uint8_t *rmark, uint8_t repoch, int32_t *rbcnt,
+                                  uint32_t *rfreel, int64_t *rnfree_dev, hipStream_t s) {
+    const int64_t nb = collect_blocks(nrecs);
+    const int64_t lanes = npool * kPageSlots;
+    if (lanes > 0)
+        hipLaunchKernelGGL(k_mark_recs, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, pool,
+                           npool, mark, epoch, nrecs, rmark, repoch);
+    hipLaunchKernelGGL(k_sweep_count, dim3((unsigned)nb), dim3(kBlock), 0, s, rmark, nrecs, repoch, rbcnt);
+    hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, rbcnt, nb, rnfree_dev);
+    hipLaunchKernelGGL(k_sweep_write, dim3((unsigned)nb), dim3(kBlock), 0, s, rmark, nrecs, repoch, rbcnt, rfreel);
+    return hipGetLastError();
 }
 
 hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark, uint8_t epoch,

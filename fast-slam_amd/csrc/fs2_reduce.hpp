@@ -121,22 +121,42 @@ __device__ __forceinline__ float4 load_mirror(const char *page, int j) {
     return reinterpret_cast<const float4 *>(page)[j & (kPageSlots - 1)];
 }
 
-__device__ __forceinline__ Slot load_slot(const char *page, int j) {
-    const double2 *q =
-        reinterpret_cast<const double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
+__device__ __forceinline__ uint32_t mirror_rec(const float4 &m) { return __float_as_uint(m.w); }
+
+// fp64 record r (x, y, P00, P01, P10, P11).
+__device__ __forceinline__ Slot load_rec(const char *recs, uint32_t r) {
+    const double2 *q = reinterpret_cast<const double2 *>(recs + (int64_t)r * kRecBytes);
     const double2 a = q[0], b = q[1], c = q[2];
     return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
 }
 
-// Next reserved free page of lane i (t counts the lane's allocations).
+__device__ __forceinline__ void store_rec(char *recs, uint32_t r, const Slot &s) {
+    double2 *q = reinterpret_cast<double2 *>(recs + (int64_t)r * kRecBytes);
+    q[0] = make_double2(s.mx, s.my);
+    q[1] = make_double2(s.P.a00, s.P.a01);
+    q[2] = make_double2(s.P.a10, s.P.a11);
+}
+
+// Slot j of a page: its mirror names the record.
+__device__ __forceinline__ Slot load_slot(const MapRef &m, const char *page, int j) {
+    return load_rec(m.recs, mirror_rec(load_mirror(page, j)));
+}
+
+// Next reserved free page / record of lane i (t counts the lane's allocations).
 __device__ __forceinline__ uint32_t take_page(const PageAlloc &a, int64_t n, int64_t i, int &t) {
     const uint32_t id = a.freel[a.base + (int64_t)t * n + i];
     ++t;
     return id;
 }
 
+__device__ __forceinline__ uint32_t take_rec(const PageAlloc &a, int64_t n, int64_t i, int &t) {
+    const uint32_t id = a.rfreel[a.rbase + (int64_t)t * n + i];
+    ++t;
+    return id;
+}
+
 // Page of row `row` of particle i that this lane may write: its own page, or a
-// private copy of a shared one (copy-on-write; the page table is updated).
+// private copy of a shared one (copy-on-write: 128 B; the page table is updated).
 __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t i,
                                                const PageAlloc &a, int &t, unsigned &cow) {
     uint4 *pe = pt_entry(m, row, i);
@@ -145,13 +165,11 @@ __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t
     const uint32_t id = take_page(a, m.n, i, t);
     const v4i *src = reinterpret_cast<const v4i *>(page_ptr(m.pool, e));
     v4i *dst = reinterpret_cast<v4i *>(page_ptr(m.pool, id));
-    for (int q0 = 0; q0 < kPageBytes / 16; q0 += 8) {
-        v4i v[8];
+    v4i v[kPageBytes / 16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = src[q0 + u];
+    for (int u = 0; u < kPageBytes / 16; ++u) v[u] = src[u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dst[q0 + u] = v[u];
-    }
+    for (int u = 0; u < kPageBytes / 16; ++u) dst[u] = v[u];
     pe->x = id | kOwned;       // same content: the summary stays valid
     ++cow;
     return reinterpret_cast<char *>(dst);
@@ -165,13 +183,12 @@ __device__ __forceinline__ char *fresh_page(const MapRef &m, int row, int64_t i,
     return page_ptr(m.pool, id);
 }
 
-// Every slot write keeps the fp32 gate mirror in step with the fp64 slot.
-__device__ __forceinline__ float4 store_slot(char *page, int j, const Slot &s) {
-    double2 *q = reinterpret_cast<double2 *>(page + kMirrorBytes + (j & (kPageSlots - 1)) * kSlotBytes);
-    q[0] = make_double2(s.mx, s.my);
-    q[1] = make_double2(s.P.a00, s.P.a01);
-    q[2] = make_double2(s.P.a10, s.P.a11);
-    const float4 mv = mirror_of(s);
+// Every slot write stores the fp64 record r and the slot's mirror (fp32 gate
+// shadow + r) in the page.
+__device__ __forceinline__ float4 store_slot(const MapRef &m, char *page, int j, const Slot &s, uint32_t r) {
+    store_rec(m.recs, r, s);
+    float4 mv = mirror_of(s);
+    mv.w = __uint_as_float(r);
     reinterpret_cast<float4 *>(page)[j & (kPageSlots - 1)] = mv;
     return mv;
 }

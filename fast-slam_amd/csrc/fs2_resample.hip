@@ -452,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P)
     P.shdr[k] = h;
 }
 
-// one workgroup per record: pages -> packed (cnt x 16 B mirrors, cnt x 48 B slots)
+// one workgroup per record: pages + records -> packed (cnt x 16 B mirrors, cnt x 48 B slots)
 __global__ __launch_bounds__(kBlock) void k_pack_payload(const ResampleParams P, int32_t nrec) {
     if (!P.stats->resampled) return;
     for (int k = blockIdx.x; k < nrec; k += gridDim.x) {
@@ -464,8 +464,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_payload(const ResampleParams P,
             dm[q] = reinterpret_cast<const int4 *>(page_of(P.map, q, i))[q % kPageSlots];
         for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
             const int j = q / 3;
-            const int4 *pg = reinterpret_cast<const int4 *>(page_of(P.map, j, i) + kMirrorBytes);
-            df[q] = pg[(j % kPageSlots) * 3 + (q - 3 * j)];
+            const uint32_t r = mirror_rec(load_mirror(page_of(P.map, j, i), j));
+            df[q] = reinterpret_cast<const int4 *>(P.map.recs + (int64_t)r * kRecBytes)[q - 3 * j];
         }
     }
 }
@@ -496,8 +496,9 @@ __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P,
     for (int64_t m = h.out_lo; m <= h.out_hi; ++m) P.out_src[m - P.a] = -(k + 1);
 }
 
-// Received particles' maps into fresh pages: record r, row k takes reserved page
-// alloc.base + r * rows + k (one workgroup per record).
+// Received particles' maps into fresh pages and records: record r, row k takes
+// reserved page alloc.base + r * rows + k, its slot q reserved record
+// alloc.rbase + (peer's sbase) + soff + q (one workgroup per received particle).
 __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, int32_t nrecv) {
     __shared__ unsigned long long lds_u[kBlock / 64];
     if (!P.stats->resampled) return;
@@ -508,12 +509,15 @@ __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, 
         const int4 *sm = reinterpret_cast<const int4 *>(P.peers[p].pay + (int64_t)h.soff * 64);
         const int4 *sf = sm + h.cnt;
         const uint32_t *ids = P.alloc.freel + P.alloc.base + (int64_t)r * P.map.rows;
-        for (int q = threadIdx.x; q < h.cnt; q += kBlock)
-            reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[q / kPageSlots]))[q % kPageSlots] = sm[q];
+        const uint32_t *rids = P.alloc.rfreel + P.alloc.rbase + P.peers[p].sbase + h.soff;
+        for (int q = threadIdx.x; q < h.cnt; q += kBlock) {
+            int4 m = sm[q];
+            m.w = (int)rids[q];       // the sender's record id, replaced by the local one
+            reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[q / kPageSlots]))[q % kPageSlots] = m;
+        }
         for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
             const int j = q / 3;
-            int4 *pg = reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[j / kPageSlots]) + kMirrorBytes);
-            pg[(j % kPageSlots) * 3 + (q - 3 * j)] = sf[q];
+            reinterpret_cast<int4 *>(P.map.recs + (int64_t)rids[j] * kRecBytes)[q - 3 * j] = sf[q];
         }
         __syncthreads();
         // summaries of the new pages, from the payload's mirrors

@@ -3,10 +3,11 @@
 //
 // Layout in HBM (see fs2_kernels.hpp and DESIGN.md):
 //   particle scalars x/y/yaw/w (fp64) and cnt (int32) in logical particle order;
-//   landmark maps in 512-byte pages of 8 slots (128 B of fp32 gate mirrors, then
-//   384 B of fp64 slots) in one pool; particle i's map is row i of the page
-//   table pt[row][i]; pages are shared after resampling and copied on first
-//   write (fs2_kernels.hpp).
+//   landmark maps in 128-byte pages of 8 fp32 gate mirrors, each naming the
+//   slot's 48-byte fp64 record in a record pool; particle i's map is row i of
+//   the page table pt[row][i]; pages and records are shared after resampling,
+//   a page is copied on its first write and a written slot gets a new record
+//   (fs2_kernels.hpp).
 //
 // Kernels
 //   k_candidates    streaming fp32 gate-mirror pass listing each particle's
@@ -41,11 +42,12 @@ __device__ unsigned long long g_phase[8];
 //
 // Streaming half of the association (fast_slam_2.py:95-106 first-match search).
 // One lane per particle walks its whole map reading only the 16-byte fp32 gate
-// mirrors (128 contiguous bytes = one cache line per lane and group of 8 slots,
+// mirrors (one 128-byte page = one cache line per lane and group of 8 slots,
 // the next group in flight while this one is tested) and lists, in slot order,
 // every slot the mirror cannot rule out for at least one measurement of the
-// pass.  No fp64, no calls: the kernel stays small enough for full occupancy,
-// which is what an HBM stream needs.
+// pass, with the slot's record id (so k_update reads the record directly).  No
+// fp64, no calls: the kernel stays small enough for full occupancy, which is
+// what an HBM stream needs.
 //
 // Exactness: measurement k can only match slot j in the state slot j had when
 // the first measurement matching it arrived, and that first match sees slot j
@@ -57,6 +59,7 @@ __device__ unsigned long long g_phase[8];
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ unsigned long long lds_u[kBlock / 64];
+    __shared__ uint64_t s_list[kMaxCand][kBlock];
     const int tid = threadIdx.x;
     const int64_t n = P.n;
     const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
@@ -65,10 +68,9 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const MapRef map = P.map;
     const uint4 *ptrow = map.pt + (live ? i : 0);
     const int rlast = map.rows - 1;
-    // the list lives in registers until the walk ends: 16-bit slot indices, four
-    // per 64-bit word (a store inside the walk would serialise the prefetch,
-    // since vmcnt counts loads and stores in issue order)
-    uint64_t cw[kMaxCand / 4] = {};
+    // the list lives in LDS until the walk ends: (record id << 16 | slot) per
+    // entry (a global store inside the walk would serialise the prefetch, since
+    // vmcnt counts loads and stores in issue order)
     int nc = 0;
     unsigned visited = 0, groups = 0;
 
@@ -109,10 +111,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                         hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
                                                  P.gate2f);
                 if (hit) {
-                    const uint64_t v = (uint64_t)(j0 + u) << (16 * (nc & 3));
-#pragma unroll
-                    for (int q = 0; q < kMaxCand / 4; ++q)
-                        cw[q] |= ((nc >> 2) == q) ? v : 0ull;
+                    if (nc < kMaxCand) s_list[nc][tid] = ((uint64_t)mirror_rec(mv) << 16) | (uint64_t)(j0 + u);
                     ++nc;
                 }
             }
@@ -121,11 +120,11 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     if (live) {
         P.ncand[i] = nc;
 #pragma unroll
-        for (int q = 0; q < kMaxCand / 4; ++q)
-            if (4 * q < nc) P.cand[(int64_t)q * n + i] = cw[q];
+        for (int q = 0; q < kMaxCand; ++q)
+            if (q < nc) P.cand[(int64_t)q * n + i] = s_list[q][tid];
     }
     const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
-    const unsigned long long bl = block_sum_u64<kBlock>((unsigned)(min(nc, kMaxCand) + 3) / 4, lds_u);
+    const unsigned long long bl = block_sum_u64<kBlock>((unsigned)min(nc, kMaxCand), lds_u);
     const unsigned long long bg = block_sum_u64<kBlock>(groups, lds_u);
     if (tid == 0) {
         atomicAdd(&P.stats->visited, bv);
@@ -134,18 +133,13 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
 }
 
-// Slot of a lane's p-th candidate: the listed ones, then (list overflow or no
-// filter) every slot from jf on; -1 past the end.  A pure function of p, so the
-// candidate loop keeps no mutable state outside registers.
-static __device__ __forceinline__ int cand_at(int p, int ncl, int jf, int c, uint64_t w0, uint64_t w1,
-                                              uint64_t w2, uint64_t w3) {
-    if (p < ncl) {
-        const int wq = p >> 2;
-        const uint64_t wsel = wq == 0 ? w0 : (wq == 1 ? w1 : (wq == 2 ? w2 : w3));
-        return (int)((wsel >> (16 * (p & 3))) & 0xffffu);
-    }
-    const int j = jf + (p - ncl);
-    return j < c ? j : -1;
+template <int K>
+static __device__ __forceinline__ uint32_t sel_u32(int t, const uint32_t (&a)[K]) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+        if (t == q) v = a[q];
+    return v;
 }
 
 // ------------------------------------------------------------ k_update ------
@@ -195,9 +189,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     const MapRef map = P.map;
     const int64_t il = live ? i : 0;
     int nalloc = 0;                  // pages taken from this pass's reservation
+    int nrec = 0;                    // records taken from this pass's reservation
     unsigned cow = 0, fresh = 0;
     uint64_t mods = 0;               // existing slots modified in phase A (16 bits each)
+    uint32_t orec[MAXM];             // their records before this pass
     int nmod = 0;
+#pragma unroll
+    for (int t = 0; t < MAXM; ++t) orec[t] = 0u;
     FS2_PHASE(0);
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
@@ -228,31 +226,11 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     if (live && P.filter) {
         const int nc = P.ncand[i];
         ncl = min(nc, kMaxCand);
-        jf = nc > kMaxCand ? (int)(P.cand[(int64_t)(kMaxCand / 4 - 1) * n + i] >> 48) + 1 : c;
+        jf = nc > kMaxCand ? (int)(P.cand[(int64_t)(kMaxCand - 1) * n + i] & 0xffffu) + 1 : c;
     }
-    // Candidates in slot order.  While slot j0 is tested, the slot of the next
-    // candidate (its page-table entry arrived one step earlier) and the entry of
-    // the one after are in flight; every load is branch-free (a missing
-    // candidate reads slot 0 of page 0 and is never used).
-    static_assert(kMaxCand == 16, "four list words");
-    const uint64_t w0 = P.cand[il], w1 = P.cand[n + il], w2 = P.cand[2 * n + il], w3 = P.cand[3 * n + il];
-    int p = 0;                       // candidates taken so far
-    int j0 = cand_at(0, ncl, jf, c, w0, w1, w2, w3);
-    int j1 = cand_at(1, ncl, jf, c, w0, w1, w2, w3);
-    if (pend == 0u) j0 = -1;
-    uint32_t e1 = pt_entry(map, (j1 >= 0 ? j1 : 0) / kPageSlots, il)->x;
-    Slot s0 = load_slot(page_ptr(map.pool, j0 >= 0 ? pt_entry(map, j0 / kPageSlots, il)->x : 0u), j0 >= 0 ? j0 : 0);
-    while (j0 >= 0 && pend != 0u) {
-        const int j2 = cand_at(p + 2, ncl, jf, c, w0, w1, w2, w3);
-        const uint32_t e2 = pt_entry(map, (j2 >= 0 ? j2 : 0) / kPageSlots, il)->x;
-        const Slot s1 = load_slot(page_ptr(map.pool, j1 >= 0 ? e1 : 0u), j1 >= 0 ? j1 : 0);
-        const int j = j0;
-        Slot s = s0;
-        ++p;
-        j0 = j1;
-        s0 = s1;
-        j1 = j2;
-        e1 = e2;
+
+    // slot j (record rec, value s): test the pending measurements in order, EKF on a match
+    auto visit = [&](int j, uint32_t rec, Slot s) {
         ++candidates;
         bool mod = false;
         M2 I;
@@ -283,14 +261,41 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (!ok) todo = 0u;
         }
         if (mod) {
-            // written back in phase B; only the slot index is kept
+            // written back in phase B; only the slot index and its record are kept
             mods |= (uint64_t)j << (16 * nmod);
+#pragma unroll
+            for (int t = 0; t < MAXM; ++t)
+                if (t == nmod) orec[t] = rec;
             ++nmod;
             ++written;
         }
-    }
+    };
 
-    if (!P.filter) visited += (unsigned)max(0, p - ncl);
+    // Listed candidates in slot order; the list names their records, so while
+    // one is tested the next one's record and the entry after it are in flight
+    // (every load is branch-free: a missing entry reads entry 0 and record 0,
+    // which are never used).
+    {
+        const int nl = (pend != 0u) ? ncl : 0;
+        auto entry = [&](int p) -> uint64_t { return P.cand[(int64_t)(p < nl ? p : 0) * n + il]; };
+        auto rec_of = [&](int p, uint64_t e) -> uint32_t { return p < nl ? (uint32_t)(e >> 16) : 0u; };
+        uint64_t e0 = entry(0), e1 = entry(1);
+        Slot s0 = load_rec(map.recs, rec_of(0, e0));
+        for (int p = 0; p < nl && pend != 0u; ++p) {
+            const uint64_t e2 = entry(p + 2);
+            const Slot s1 = load_rec(map.recs, rec_of(p + 1, e1));
+            visit((int)(e0 & 0xffffu), (uint32_t)(e0 >> 16), s0);
+            e0 = e1;
+            s0 = s1;
+            e1 = e2;
+        }
+    }
+    // Past an overflowing list (or without the filter): every slot from jf on.
+    for (int j = jf; j < c && pend != 0u; ++j) {
+        const uint32_t r = mirror_rec(load_mirror(page_of(map, j, il), j));
+        if (!P.filter) ++visited;
+        visit(j, r, load_rec(map.recs, r));
+    }
 
     FS2_PHASE(2);
     // ---- phase B: every store of this pass.  Stores come last because vmcnt
@@ -299,8 +304,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     // Rows this lane writes before the appends: the modified slots' rows, then the
     // row the first append lands in when it is partly filled (later appends start
-    // fresh pages).  Their descriptors and this pass's reserved free pages are
-    // loaded together, before any store.
+    // fresh pages).  Their descriptors and this pass's reserved free pages and
+    // records are loaded together, before any store.
     constexpr int NR = MAXM + 1;
     const int nrows = nmod + ((pend != 0u && c % kPageSlots != 0) ? 1 : 0);
     int rrow[NR];
@@ -312,13 +317,18 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                              : (t == nmod && t < nrows ? c / kPageSlots : 0);
         rdesc[t] = *pt_entry(map, rrow[t], il);
     }
-    uint32_t fpage[MAXM];
+    uint32_t fpage[MAXM], frec[MAXM];
 #pragma unroll
-    for (int t = 0; t < MAXM; ++t) fpage[t] = P.alloc.freel[P.alloc.base + (int64_t)t * n + il];
+    for (int t = 0; t < MAXM; ++t) {
+        // the pass reserved m pages and m records per lane
+        fpage[t] = t < P.m ? P.alloc.freel[P.alloc.base + (int64_t)t * n + il] : 0u;
+        frec[t] = t < P.m ? P.alloc.rfreel[P.alloc.rbase + (int64_t)t * n + il] : 0u;
+    }
 
     // (B1) own those pages.  The wave lists its shared pages in LDS and copies
-    // them together, 16 pages per batch (8 independent 16-byte loads per lane),
-    // the loads of the next batch issued before the stores of this one.
+    // them together, 8 lanes per 128-byte page and 64 pages per batch (8
+    // independent 16-byte loads per lane), the loads of the next batch issued
+    // before the stores of this one.
     {
         const int lane = tid & 63, wid = tid >> 6;
         int T = 0;                    // pages listed by the wave so far
@@ -333,9 +343,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (t < nrows && canon[t] == t && !(rdesc[t].x & kOwned)) {
                 task = true;
                 src = rdesc[t].x & kIdMask;
-#pragma unroll
-                for (int u = 0; u < MAXM; ++u)
-                    if (u == nalloc) dst = fpage[u];
+                dst = sel_u32(nalloc, fpage);
                 ++nalloc;
                 rdesc[t].x = dst | kOwned;
                 ++cow;
@@ -348,13 +356,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         for (int t = 0; t < NR; ++t)
             if (t < nrows && canon[t] == t) pt_entry(map, rrow[t], il)->x = rdesc[t].x;
         __syncthreads();
-        const int off = (lane & 31) * 16;
+        const int off = (lane & 7) * 16;
         v4i va[8], vb[8];             // clang vector type: HIP's int4 struct defeats SROA here
         uint32_t da[8], db[8];
         auto load_batch = [&](int base, v4i *v, uint32_t *d) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const uint2 tk = s_cow[wid][min(base + 2 * u + (lane >> 5), T - 1)];
+                const uint2 tk = s_cow[wid][min(base + 8 * u + (lane >> 3), T - 1)];
                 d[u] = tk.y;
                 v[u] = *reinterpret_cast<const v4i *>(page_ptr(map.pool, tk.x) + off);
             }
@@ -364,46 +372,42 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             for (int u = 0; u < 8; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
         };
         if (T > 0) load_batch(0, va, da);
-        for (int base = 0; base < T; base += 32) {
-            if (base + 16 < T) load_batch(base + 16, vb, db);
+        for (int base = 0; base < T; base += 128) {
+            if (base + 64 < T) load_batch(base + 64, vb, db);
             store_batch(va, da);
-            if (base + 16 >= T) break;
-            if (base + 32 < T) load_batch(base + 32, va, da);
+            if (base + 64 >= T) break;
+            if (base + 128 < T) load_batch(base + 128, va, da);
             store_batch(vb, db);
         }
         __threadfence_block();        // copies land before the slot stores below
     }
 
     FS2_PHASE(3);
-    // (B2) modified slots: the EKF updates of phase A replayed on the original slot
-    // in measurement order (bit-identical) and stored; then the row summaries
-    // are read once, merged and written back.
+    // (B2) modified slots: the EKF updates of phase A replayed on the slot's
+    // record in measurement order (bit-identical), stored as a new record; then
+    // the row summaries are read once, merged and written back.
     {
-        Slot sl[MAXM];
-        uint32_t pid[MAXM];
+        Slot sl[MAXM];               // records of the modified slots before this pass
 #pragma unroll
-        for (int t = 0; t < MAXM; ++t) {
-            const int j = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) : 0;
-            uint32_t id = 0;
-#pragma unroll
-            for (int u = 0; u < NR; ++u)
-                if (u == canon[t]) id = rdesc[u].x;
-            pid[t] = t < nmod ? id : 0u;
-            sl[t] = load_slot(page_ptr(map.pool, pid[t]), j);
-        }
+        for (int t = 0; t < MAXM; ++t) sl[t] = load_rec(map.recs, t < nmod ? orec[t] : 0u);
         float4 mv[MAXM];
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
             if (t < nmod) {
                 const int j = (int)((mods >> (16 * t)) & 0xffffu);
+                uint32_t id = 0;
+#pragma unroll
+                for (int u = 0; u < NR; ++u)
+                    if (u == canon[t]) id = rdesc[u].x;
                 Slot s = sl[t];
                 bool dummy = false;
 #pragma unroll
                 for (int k = 0; k < MAXM; ++k)
                     if (s_idx[k][tid] == j) (void)ekf_update(s, px, py, pyaw, s_ms[k], R, dummy);
-                mv[t] = store_slot(page_ptr(map.pool, pid[t]), j, s);
+                mv[t] = store_slot(map, page_ptr(map.pool, id), j, s, frec[t]);
             }
         }
+        nrec = nmod;
         // summaries: rows in first-occurrence order, each merged with all its slots
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
@@ -427,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         const Meas mk = s_ms[k];
         int hit = -1;
         for (int a = 0; a < nap; ++a) {
-            const Slot s = load_slot(page_of(map, c + a, il), c + a);
+            const Slot s = load_slot(map, page_of(map, c + a, il), c + a);
             ++candidates;
             M2 I;
             if (!inv2(s.P, I)) {
@@ -442,11 +446,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             }
         }
         if (hit >= 0) {
+            // a slot appended by this pass: page and record are this lane's own
             const int jh = c + hit;
-            Slot s = load_slot(page_of(map, jh, il), jh);
+            char *pg = writable_page(map, jh / kPageSlots, il, P.alloc, nalloc, cow);
+            const uint32_t r = mirror_rec(load_mirror(pg, jh));
+            Slot s = load_rec(map.recs, r);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
-            note_write(map, jh, il, store_slot(writable_page(map, jh / kPageSlots, il, P.alloc, nalloc, cow), jh, s),
-                       false);
+            note_write(map, jh, il, store_slot(map, pg, jh, s, r), false);
             s_idx[k][tid] = c + hit;
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
@@ -460,7 +466,9 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             } else {
                 pg = writable_page(map, ja / kPageSlots, il, P.alloc, nalloc, cow);
             }
-            note_write(map, ja, il, store_slot(pg, ja, s), ja % kPageSlots == 0);
+            const uint32_t r = sel_u32(nrec, frec);
+            ++nrec;
+            note_write(map, ja, il, store_slot(map, pg, ja, s, r), ja % kPageSlots == 0);
             s_idx[k][tid] = -1;
             ++nap;
             ++appends;
@@ -625,8 +633,9 @@ hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
 // ------------------------------------------------------ state import/export --
 
 // stage: [count][lm_cap][6] -> maps of particles first .. first+count-1, written
-// into fresh pages (row k of particle p takes reserved page p * rows_each + k);
-// the pages they replace are reclaimed by the next collection.
+// into fresh pages and records (row k of particle p takes reserved page
+// p * rows_each + k, slot j reserved record p * lm_cap + j); the pages and
+// records they replace are reclaimed by the next collection.
 __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const int32_t *cnt_stage,
                                                    int64_t first, int64_t count, int32_t lm_cap,
                                                    MapRef map, PageAlloc alloc, int32_t rows_each,
@@ -643,7 +652,8 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         const uint32_t id = alloc.freel[alloc.base + p * rows_each + row];
         if (j % kPageSlots == 0) pt_entry(map, row, first + p)->x = id | kOwned;
         const double *s = stage + e * 6;
-        store_slot(page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}});
+        store_slot(map, page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}},
+                   alloc.rfreel[alloc.rbase + e]);
     }
 }
 
@@ -655,7 +665,7 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
         const int64_t p = e / lm_cap;
         const int j = (int)(e % lm_cap);
         if (j >= cnt[first + p]) continue;
-        const Slot s = load_slot(page_of(map, j, first + p), j);
+        const Slot s = load_slot(map, page_of(map, j, first + p), j);
         double *d = stage + e * 6;
         d[0] = s.mx; d[1] = s.my;
         d[2] = s.P.a00; d[3] = s.P.a01; d[4] = s.P.a10; d[5] = s.P.a11;
