@@ -95,6 +95,7 @@ struct fs2_handle {
     int32_t *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
     int cap = 0, max_cap = kMaxSlots;
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
+    unsigned long long *cpart = nullptr;   // update-pass block counters [kNumCounters][nblocks]
     int64_t *part_best_i = nullptr;
     int32_t *part_maxcnt = nullptr;
     double *cbuf = nullptr, *bsum = nullptr;
@@ -398,7 +399,7 @@ static void free_handle(fs2_handle *h) {
     for (char *b : h->sendbuf) hipFree(b);
     for (char *b : h->recvbuf) hipFree(b);
     hipFree(h->cand); hipFree(h->ncand);
-    hipFree(h->wpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
+    hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
     if (h->stats_host) hipHostFree(h->stats_host);
@@ -473,6 +474,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 4) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->cpart, nb * 8 * kNumCounters) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_i, nb * 8) == hipSuccess;
@@ -486,6 +488,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= hipHostMalloc((void **)&h->noise_pin, n * 8, 0) == hipSuccess;
     ok &= hipHostMalloc((void **)&h->u0_pin, 8, 0) == hipSuccess;
     if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
+    if (hipMemsetAsync(h->cpart, 0, nb * 8 * kNumCounters, h->stream) != hipSuccess)
+        return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     // Particle.__init__: (0, 0, 0), weight 1/NUM_PARTICLES, empty map (particle.py:11-20)
     for (int s = 0; s < 2; ++s) {
         if (hipMemsetAsync(h->x[s], 0, n * 8, h->stream) != hipSuccess ||
@@ -609,6 +613,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
     up.assoc = h->cfg.record_assoc ? h->assoc_dev : nullptr;
     up.wpart = h->wpart;
+    up.cpart = h->cpart;
     up.stats = h->stats_dev;
     int passes = 0;
     uint64_t fixed_bytes = 0;
@@ -662,6 +667,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.cnt = h->cnt[cur];
     rp.x = h->x[cur]; rp.y = h->y[cur]; rp.yaw = h->yaw[cur];
     rp.wpart = h->wpart;
+    rp.cpart = h->cpart;
     rp.nwpart = (int32_t)h->nblocks();
     rp.part_sq = h->part_sq;
     rp.part_best_w = h->part_best_w;

@@ -87,6 +87,45 @@ __device__ void block_argmax(double &v, int64_t &i, double *ldv, int64_t *ldi) {
     for (int k = 1; k < NT / 64; ++k) argmax_combine(v, i, ldv[k], ldi[k]);
 }
 
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// The counters of this workgroup (NV per lane: counters FIRST .. FIRST+NV-1)
+// added into its column of cpart ([kNumCounters][gridDim.x]) and, when
+// wsum != nullptr, its deterministic weight sum (block_sum's tree) stored to
+// *wsum: one LDS exchange, one barrier.
+template <int NT, int FIRST, int NV>
+__device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpart, double w, double *wsum) {
+    __shared__ unsigned s_c[NT / 64][NV];
+    __shared__ double s_w[NT / 64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned r[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) r[k] = wave_sum_u32(v[k]);
+    const double ws = wave_sum(w);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) s_c[wid][k] = r[k];
+        s_w[wid] = ws;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int q = 0; q < NT / 64; ++q) t += s_c[q][threadIdx.x];
+        if (t) cpart[(int64_t)(FIRST + threadIdx.x) * gridDim.x + blockIdx.x] += t;
+    }
+    if (wsum && threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < NT / 64; ++q) t += s_w[q];
+        *wsum = t;
+    }
+}
+
 template <int NT>
 __device__ int block_max_i(int v, int *lds) {
     v = wave_max_i(v);

@@ -58,7 +58,6 @@ __device__ unsigned long long g_phase[8];
 // and k_update resumes with an exact scan after the last stored one.
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
-    __shared__ unsigned long long lds_u[kBlock / 64];
     __shared__ uint64_t s_list[kMaxCand][kBlock];
     const int tid = threadIdx.x;
     const int64_t n = P.n;
@@ -123,14 +122,8 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         for (int q = 0; q < kMaxCand; ++q)
             if (q < nc) P.cand[(int64_t)q * n + i] = s_list[q][tid];
     }
-    const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
-    const unsigned long long bl = block_sum_u64<kBlock>((unsigned)min(nc, kMaxCand), lds_u);
-    const unsigned long long bg = block_sum_u64<kBlock>(groups, lds_u);
-    if (tid == 0) {
-        atomicAdd(&P.stats->visited, bv);
-        atomicAdd(&P.stats->words, bl);
-        atomicAdd(&P.stats->groups, bg);
-    }
+    const unsigned cv[3] = {(unsigned)min(nc, kMaxCand), groups, visited};   // kCWords, kCGroups, kCVisited
+    block_counters<kBlock, kCWords, 3>(cv, P.cpart, 0.0, nullptr);
 }
 
 template <int K>
@@ -157,13 +150,11 @@ static __device__ __forceinline__ uint32_t sel_u32(int t, const uint32_t (&a)[K]
 // (or past an overflowing candidate list) every slot takes the exact path.
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
-    __shared__ double lds_d[kBlock / 64];
-    __shared__ unsigned long long lds_u[kBlock / 64];
-    __shared__ int lds_i[kBlock / 64];
     __shared__ Meas s_ms[MAXM];                 // this pass's measurements
     __shared__ double s_lik[MAXM][kBlock];      // per (measurement, lane) likelihood
     __shared__ int s_idx[MAXM][kBlock];         // per (measurement, lane) association
     __shared__ uint2 s_cow[kBlock / 64][64 * (MAXM + 1)];   // per wave: (shared page, copy)
+    __shared__ float4 s_mv[MAXM][kBlock];       // new mirrors of the slots phase A modified
 
 #ifdef FS2_PHASE_TIMING
     unsigned long long ph_last = 0;
@@ -192,10 +183,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     int nrec = 0;                    // records taken from this pass's reservation
     unsigned cow = 0, fresh = 0;
     uint64_t mods = 0;               // existing slots modified in phase A (16 bits each)
-    uint32_t orec[MAXM];             // their records before this pass
     int nmod = 0;
+    // this pass's reserved records (m per lane): phase A stores modified slots into them
+    uint32_t frec[MAXM];
 #pragma unroll
-    for (int t = 0; t < MAXM; ++t) orec[t] = 0u;
+    for (int t = 0; t < MAXM; ++t) {
+        frec[t] = (live && t < P.m) ? P.alloc.rfreel[P.alloc.rbase + (int64_t)t * n + i] : 0u;
+    }
     FS2_PHASE(0);
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
@@ -230,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
 
     // slot j (record rec, value s): test the pending measurements in order, EKF on a match
-    auto visit = [&](int j, uint32_t rec, Slot s) {
+    auto visit = [&](int j, Slot s) {
         ++candidates;
         bool mod = false;
         M2 I;
@@ -261,11 +255,15 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (!ok) todo = 0u;
         }
         if (mod) {
-            // written back in phase B; only the slot index and its record are kept
+            // final: every measurement matching slot j was applied above.  Its new
+            // record is private, so it is stored now; the mirror naming it goes
+            // into the page in phase B (after the page is owned).
+            const uint32_t r = sel_u32(nmod, frec);
+            store_rec(map.recs, r, s);
+            float4 m = mirror_of(s);
+            m.w = __uint_as_float(r);
+            s_mv[nmod][tid] = m;
             mods |= (uint64_t)j << (16 * nmod);
-#pragma unroll
-            for (int t = 0; t < MAXM; ++t)
-                if (t == nmod) orec[t] = rec;
             ++nmod;
             ++written;
         }
@@ -284,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         for (int p = 0; p < nl && pend != 0u; ++p) {
             const uint64_t e2 = entry(p + 2);
             const Slot s1 = load_rec(map.recs, rec_of(p + 1, e1));
-            visit((int)(e0 & 0xffffu), (uint32_t)(e0 >> 16), s0);
+            visit((int)(e0 & 0xffffu), s0);
             e0 = e1;
             s0 = s1;
             e1 = e2;
@@ -294,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     for (int j = jf; j < c && pend != 0u; ++j) {
         const uint32_t r = mirror_rec(load_mirror(page_of(map, j, il), j));
         if (!P.filter) ++visited;
-        visit(j, r, load_rec(map.recs, r));
+        visit(j, load_rec(map.recs, r));
     }
 
     FS2_PHASE(2);
@@ -317,13 +315,10 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                              : (t == nmod && t < nrows ? c / kPageSlots : 0);
         rdesc[t] = *pt_entry(map, rrow[t], il);
     }
-    uint32_t fpage[MAXM], frec[MAXM];
+    uint32_t fpage[MAXM];
 #pragma unroll
-    for (int t = 0; t < MAXM; ++t) {
-        // the pass reserved m pages and m records per lane
+    for (int t = 0; t < MAXM; ++t)     // the pass reserved m pages per lane
         fpage[t] = t < P.m ? P.alloc.freel[P.alloc.base + (int64_t)t * n + il] : 0u;
-        frec[t] = t < P.m ? P.alloc.rfreel[P.alloc.rbase + (int64_t)t * n + il] : 0u;
-    }
 
     // (B1) own those pages.  The wave lists its shared pages in LDS and copies
     // them together, 8 lanes per 128-byte page and 64 pages per batch (8
@@ -355,10 +350,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
         for (int t = 0; t < NR; ++t)
             if (t < nrows && canon[t] == t) pt_entry(map, rrow[t], il)->x = rdesc[t].x;
-        __syncthreads();
+        // the task list is per wave: a wave-level barrier orders its LDS writes and reads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int off = (lane & 7) * 16;
-        v4i va[8], vb[8];             // clang vector type: HIP's int4 struct defeats SROA here
-        uint32_t da[8], db[8];
+        v4i va[8];                    // clang vector type: HIP's int4 struct defeats SROA here
+        uint32_t da[8];
         auto load_batch = [&](int base, v4i *v, uint32_t *d) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -371,26 +369,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
         };
-        if (T > 0) load_batch(0, va, da);
-        for (int base = 0; base < T; base += 128) {
-            if (base + 64 < T) load_batch(base + 64, vb, db);
+        for (int base = 0; base < T; base += 64) {
+            load_batch(base, va, da);
             store_batch(va, da);
-            if (base + 64 >= T) break;
-            if (base + 128 < T) load_batch(base + 128, va, da);
-            store_batch(vb, db);
         }
         __threadfence_block();        // copies land before the slot stores below
     }
 
     FS2_PHASE(3);
-    // (B2) modified slots: the EKF updates of phase A replayed on the slot's
-    // record in measurement order (bit-identical), stored as a new record; then
-    // the row summaries are read once, merged and written back.
+    // (B2) modified slots: their mirrors (computed in phase A) into the owned
+    // pages; then the row summaries are read once, merged and written back.
     {
-        Slot sl[MAXM];               // records of the modified slots before this pass
-#pragma unroll
-        for (int t = 0; t < MAXM; ++t) sl[t] = load_rec(map.recs, t < nmod ? orec[t] : 0u);
-        float4 mv[MAXM];
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
             if (t < nmod) {
@@ -399,12 +388,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
                 for (int u = 0; u < NR; ++u)
                     if (u == canon[t]) id = rdesc[u].x;
-                Slot s = sl[t];
-                bool dummy = false;
-#pragma unroll
-                for (int k = 0; k < MAXM; ++k)
-                    if (s_idx[k][tid] == j) (void)ekf_update(s, px, py, pyaw, s_ms[k], R, dummy);
-                mv[t] = store_slot(map, page_ptr(map.pool, id), j, s, frec[t]);
+                reinterpret_cast<float4 *>(page_ptr(map.pool, id))[j & (kPageSlots - 1)] = s_mv[t][tid];
             }
         }
         nrec = nmod;
@@ -412,26 +396,40 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
             if (t < nmod && canon[t] == t) {
-                uint4 *pe = pt_entry(map, rrow[t], il);
-                uint4 d = *pe;
+                uint4 d = rdesc[t];      // loaded before B1, .x now the owned page
 #pragma unroll
                 for (int u = t; u < MAXM; ++u)
-                    if (u < nmod && canon[u] == t) d = merge_summary(d, mv[u]);
-                *pe = d;
+                    if (u < nmod && canon[u] == t) d = merge_summary(d, s_mv[u][tid]);
+                *pt_entry(map, rrow[t], il) = d;
+                rdesc[t] = d;
             }
         }
     }
 
     FS2_PHASE(4);
-    // ---- measurements that matched nothing: appended slots, in order ----
+    // ---- measurements that matched nothing: appended slots, in order.  The
+    // descriptor of the row being appended into stays in registers (ad) and is
+    // stored when the appends leave the row. ----
     int nap = 0;
+    int arow = -1;
+    uint4 ad = make_uint4(0u, 0u, 0u, 0u);
+    if (pend != 0u && c % kPageSlots != 0) {
+        // the partly filled last row: owned by B1, summary merged if a modified slot shares it
+        arow = c / kPageSlots;
+#pragma unroll
+        for (int u = 0; u < NR; ++u)
+            if (u == canon[nmod]) ad = rdesc[u];
+    }
+    auto page_at = [&](int j) -> char * {
+        return (j / kPageSlots == arow) ? page_ptr(map.pool, ad.x) : page_of(map, j, il);
+    };
     while (pend) {
         const int k = __builtin_ctz(pend);
         pend &= pend - 1u;
         const Meas mk = s_ms[k];
         int hit = -1;
         for (int a = 0; a < nap; ++a) {
-            const Slot s = load_slot(map, page_of(map, c + a, il), c + a);
+            const Slot s = load_slot(map, page_at(c + a), c + a);
             ++candidates;
             M2 I;
             if (!inv2(s.P, I)) {
@@ -446,35 +444,40 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             }
         }
         if (hit >= 0) {
-            // a slot appended by this pass: page and record are this lane's own
+            // a slot appended by this pass: page (owned) and record are this lane's own
             const int jh = c + hit;
-            char *pg = writable_page(map, jh / kPageSlots, il, P.alloc, nalloc, cow);
+            char *pg = page_at(jh);
             const uint32_t r = mirror_rec(load_mirror(pg, jh));
             Slot s = load_rec(map.recs, r);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
-            note_write(map, jh, il, store_slot(map, pg, jh, s, r), false);
+            const float4 mv = store_slot(map, pg, jh, s, r);
+            if (jh / kPageSlots == arow) ad = merge_summary(ad, mv);
+            else note_write(map, jh, il, mv, false);
             s_idx[k][tid] = c + hit;
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
             const Slot s{px + mk.d * cos(pyaw + mk.b), py + mk.d * sin(pyaw + mk.b),
                          M2{P.init_cov[0], P.init_cov[1], P.init_cov[2], P.init_cov[3]}};
             const int ja = c + nap;
-            char *pg;
-            if (ja % kPageSlots == 0) {
-                pg = fresh_page(map, ja / kPageSlots, il, P.alloc, nalloc);
-                ++fresh;
-            } else {
-                pg = writable_page(map, ja / kPageSlots, il, P.alloc, nalloc, cow);
-            }
             const uint32_t r = sel_u32(nrec, frec);
             ++nrec;
-            note_write(map, ja, il, store_slot(map, pg, ja, s, r), ja % kPageSlots == 0);
+            if (ja % kPageSlots == 0) {
+                if (arow >= 0) *pt_entry(map, arow, il) = ad;     // leaving that row
+                const uint32_t id = take_page(P.alloc, map.n, il, nalloc);
+                arow = ja / kPageSlots;
+                const float4 mv = store_slot(map, page_ptr(map.pool, id), ja, s, r);
+                ad = describe_page(id | kOwned, &mv, 1);
+                ++fresh;
+            } else {
+                ad = merge_summary(ad, store_slot(map, page_ptr(map.pool, ad.x), ja, s, r));
+            }
             s_idx[k][tid] = -1;
             ++nap;
             ++appends;
         }
         ++written;
     }
+    if (arow >= 0) *pt_entry(map, arow, il) = ad;
     c += nap;
 
     FS2_PHASE(5);
@@ -501,35 +504,9 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
 
     FS2_PHASE(6);
-    // ---- block statistics ----
-    const unsigned long long bv = block_sum_u64<kBlock>(visited, lds_u);
-    const unsigned long long bc = block_sum_u64<kBlock>(candidates, lds_u);
-    const unsigned long long bw = block_sum_u64<kBlock>(written, lds_u);
-    const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
-    const unsigned long long bap = block_sum_u64<kBlock>(appends, lds_u);
-    const unsigned long long bh = block_sum_u64<kBlock>(hits, lds_u);
-    const unsigned long long bcow = block_sum_u64<kBlock>(cow, lds_u);
-    const unsigned long long bnew = block_sum_u64<kBlock>(fresh, lds_u);
-    const int anysing = __syncthreads_or(singular ? 1 : 0);
-    if (P.last_pass) {
-        const double ws = block_sum<kBlock>(live ? w : 0.0, lds_d);
-        const int mc = block_max_i<kBlock>(live ? c : 0, lds_i);
-        if (tid == 0) {
-            P.wpart[blockIdx.x] = ws;
-            atomicMax(&P.stats->max_count, mc);
-        }
-    }
-    if (tid == 0) {
-        atomicAdd(&P.stats->visited, bv);
-        atomicAdd(&P.stats->candidates, bc);
-        atomicAdd(&P.stats->written, bw);
-        atomicAdd(&P.stats->ambiguous, ba);
-        atomicAdd(&P.stats->appends, bap);
-        atomicAdd(&P.stats->hits, bh);
-        if (bcow) atomicAdd(&P.stats->cow_pages, bcow);
-        if (bnew) atomicAdd(&P.stats->new_pages, bnew);
-        if (anysing) atomicOr(&P.stats->error_flags, 1);
-    }
+    // ---- block statistics (kCVisited .. kCSingular) and the weight partial ----
+    const unsigned cv[9] = {visited, candidates, written, amb, appends, hits, cow, fresh, singular ? 1u : 0u};
+    block_counters<kBlock, kCVisited, 9>(cv, P.cpart, live ? w : 0.0, P.last_pass ? P.wpart + blockIdx.x : nullptr);
 }
 
 hipError_t launch_candidates(const UpdateParams &p, hipStream_t s) {
@@ -573,8 +550,42 @@ __device__ double pairwise_sq(const double *a, int64_t n) {
 }
 
 // Weight total. Sequential mode: Python builtin sum in particle order.
+__device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k) {
+    switch (k) {
+        case kCWords: return &st->words;
+        case kCGroups: return &st->groups;
+        case kCVisited: return &st->visited;
+        case kCCandidates: return &st->candidates;
+        case kCWritten: return &st->written;
+        case kCAmbiguous: return &st->ambiguous;
+        case kCAppends: return &st->appends;
+        case kCHits: return &st->hits;
+        case kCCow: return &st->cow_pages;
+        default: return &st->new_pages;
+    }
+}
+
+// Weight total (Python builtin sum in particle order in sequential mode) and the
+// update pass's block counters folded into the scan statistics (partials reset).
 __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
     __shared__ double lds[16];
+    __shared__ unsigned long long lds_u[16];
+    for (int k = 0; k < kNumCounters; ++k) {
+        unsigned long long v = 0;
+        unsigned long long *col = P.cpart + (int64_t)k * P.nwpart;
+        for (int b = threadIdx.x; b < P.nwpart; b += 1024) {
+            v += col[b];
+            col[b] = 0;
+        }
+        v = block_sum_u64<1024>(v, lds_u);
+        if (threadIdx.x == 0) {
+            if (k == kCSingular) {
+                if (v) P.stats->error_flags |= 1;
+            } else {
+                *counter_field(P.stats, k) += v;
+            }
+        }
+    }
     if (P.sequential) {
         if (threadIdx.x == 0) {
             double t = 0.0;
