@@ -77,25 +77,19 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     // next two descriptors already in flight); only pages it cannot reject have their
     // 8 mirrors loaded, and the wave loads them together (lanes without an open
     // page read page 0, which stays in cache, and discard it).
-    uint4 d1 = ptrow[0], d2 = ptrow[(int64_t)min(1, rlast) * n];
-    for (int g = 0; __any(g * kPageSlots < c); ++g) {
-        const int j0 = g * kPageSlots;
-        const uint4 d = d1;
-        d1 = d2;
-        d2 = ptrow[(int64_t)min(g + 2, rlast) * n];
-        bool open = false;
-        if (j0 < c) {
-            ++groups;
+    // measurements whose gate page g (descriptor d) cannot rule out
+    auto open_mask = [&](const uint4 &d, int g) -> unsigned {
+        unsigned om = 0u;
+        if (g * kPageSlots < c) {
 #pragma unroll
             for (int k = 0; k < MAXM; ++k)
-                if (k < P.m) open |= !page_reject(d, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f);
+                if (k < P.m && !page_reject(d, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f)) om |= 1u << k;
         }
-        if (!__any(open)) continue;
-        const char *pg = page_ptr(map.pool, open ? d.x : 0u);
-        float4 mir[kScanGroup];
-#pragma unroll
-        for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
-        if (!open) continue;
+        return om;
+    };
+    // slots of open page g (mirrors mir) tested against the measurements of om only
+    auto test_page = [&](const float4 *mir, int g, unsigned om) {
+        const int j0 = g * kPageSlots;
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) {
             if (j0 + u < c) {
@@ -106,7 +100,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                 bool hit = false;
 #pragma unroll
                 for (int k = 0; k < MAXM; ++k)
-                    if (k < P.m)
+                    if ((om >> k) & 1u)
                         hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
                                                  P.gate2f);
                 if (hit) {
@@ -115,6 +109,20 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                 }
             }
         }
+    };
+    uint4 d1 = ptrow[0], d2 = ptrow[(int64_t)min(1, rlast) * n];
+    for (int g = 0; __any(g * kPageSlots < c); ++g) {
+        const uint4 d = d1;
+        d1 = d2;
+        d2 = ptrow[(int64_t)min(g + 2, rlast) * n];
+        if (g * kPageSlots < c) ++groups;
+        const unsigned om = open_mask(d, g);
+        if (!__any(om)) continue;
+        const char *pg = page_ptr(map.pool, om ? d.x : 0u);
+        float4 mir[kScanGroup];
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
+        if (om) test_page(mir, g, om);
     }
     if (live) {
         P.ncand[i] = nc;
