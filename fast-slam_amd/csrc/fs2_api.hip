@@ -744,7 +744,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         run_resample = h->stats_host->resampled != 0;
     }
     if (run_resample) {
-        HIP_TRY(h, hipMemsetAsync(h->out_src, 0, sizeof(int32_t) * std::max<int64_t>(h->n, 1), s));
+        // every local output is written below: the output ranges of the local
+        // sources (k_ranges) and of the received ones (k_scatter_recv) partition them
         HIP_TRY(h, launch_resample_ranges(rs, s));
         if (sh) {
             rc = exchange_particles(h, rs);

@@ -35,9 +35,9 @@ constexpr int kRecBytes = 48;
 constexpr uint32_t kOwned = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7fffffffu;
 
-// Counters of the update pass, kept per workgroup (cpart[counter][block],
-// accumulated over the passes of a scan) and folded into DevStats by k_wsum:
-// no same-address atomics on the hot kernels.
+// Counters of the update pass, kept per workgroup (cpart[counter][block]: the
+// first pass of a scan stores them, later passes add) and folded into DevStats
+// by k_wsum: no same-address atomics on the hot kernels.
 // k_candidates adds [kCWords, kCVisited], k_update [kCVisited, kCSingular].
 enum : int {
     kCWords, kCGroups, kCVisited, kCCandidates, kCWritten, kCAmbiguous, kCAppends, kCHits, kCCow, kCNew,
@@ -150,7 +150,7 @@ struct UpdateParams {
     double init_cov[4];
     int32_t *assoc;          // [M][n] or null
     double *wpart;           // [gridDim.x] block partial sums of w (last pass)
-    unsigned long long *cpart;   // [kNumCounters][gridDim.x] block counters (+=)
+    unsigned long long *cpart;   // [kNumCounters][gridDim.x] block counters
     DevStats *stats;
     MeasPack meas;
 };
@@ -164,7 +164,7 @@ struct ReduceParams {
     const double *x, *y, *yaw;
     const double *wpart;     // update partials
     int32_t nwpart;
-    unsigned long long *cpart;   // update counters [kNumCounters][nwpart], reset by k_wsum
+    unsigned long long *cpart;   // update counters [kNumCounters][nwpart]
     double *part_sq;         // normalise partials: sum w'^2
     double *part_best_w;
     int64_t *part_best_i;

@@ -94,11 +94,12 @@ __device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
 }
 
 // The counters of this workgroup (NV per lane: counters FIRST .. FIRST+NV-1)
-// added into its column of cpart ([kNumCounters][gridDim.x]) and, when
-// wsum != nullptr, its deterministic weight sum (block_sum's tree) stored to
-// *wsum: one LDS exchange, one barrier.
+// stored (bit k of `assign` set) or added into its column of cpart
+// ([kNumCounters][gridDim.x]) and, when wsum != nullptr, its deterministic
+// weight sum (block_sum's tree) stored to *wsum: one LDS exchange, one barrier.
 template <int NT, int FIRST, int NV>
-__device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpart, double w, double *wsum) {
+__device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpart, unsigned assign, double w,
+                               double *wsum) {
     __shared__ unsigned s_c[NT / 64][NV];
     __shared__ double s_w[NT / 64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -116,7 +117,9 @@ __device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpar
         unsigned long long t = 0;
 #pragma unroll
         for (int q = 0; q < NT / 64; ++q) t += s_c[q][threadIdx.x];
-        if (t) cpart[(int64_t)(FIRST + threadIdx.x) * gridDim.x + blockIdx.x] += t;
+        unsigned long long *e = cpart + (int64_t)(FIRST + threadIdx.x) * gridDim.x + blockIdx.x;
+        if ((assign >> (FIRST + threadIdx.x)) & 1u) *e = t;
+        else if (t) *e += t;
     }
     if (wsum && threadIdx.x == 0) {
         double t = 0.0;

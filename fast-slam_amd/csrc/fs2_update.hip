@@ -131,7 +131,8 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             if (q < nc) P.cand[(int64_t)q * n + i] = s_list[q][tid];
     }
     const unsigned cv[3] = {(unsigned)min(nc, kMaxCand), groups, visited};   // kCWords, kCGroups, kCVisited
-    block_counters<kBlock, kCWords, 3>(cv, P.cpart, 0.0, nullptr);
+    // the first pass of a scan stores its counters, later passes add
+    block_counters<kBlock, kCWords, 3>(cv, P.cpart, P.k0 == 0 ? 0xffffffffu : 0u, 0.0, nullptr);
 }
 
 template <int K>
@@ -512,9 +513,15 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
 
     FS2_PHASE(6);
-    // ---- block statistics (kCVisited .. kCSingular) and the weight partial ----
-    const unsigned cv[9] = {visited, candidates, written, amb, appends, hits, cow, fresh, singular ? 1u : 0u};
-    block_counters<kBlock, kCVisited, 9>(cv, P.cpart, live ? w : 0.0, P.last_pass ? P.wpart + blockIdx.x : nullptr);
+    // ---- block statistics (every counter) and the weight partial.  The first
+    // pass stores, except the counters k_candidates already stored for it ----
+    const unsigned cv[kNumCounters] = {0u, 0u, visited, candidates, written, amb, appends, hits, cow, fresh,
+                                       singular ? 1u : 0u};
+    const unsigned assign = P.k0 != 0 ? 0u
+                                       : (P.filter ? ~((1u << kCWords) | (1u << kCGroups) | (1u << kCVisited))
+                                                   : 0xffffffffu);
+    block_counters<kBlock, 0, kNumCounters>(cv, P.cpart, assign, live ? w : 0.0,
+                                            P.last_pass ? P.wpart + blockIdx.x : nullptr);
 }
 
 hipError_t launch_candidates(const UpdateParams &p, hipStream_t s) {
@@ -574,23 +581,33 @@ __device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k
 }
 
 // Weight total (Python builtin sum in particle order in sequential mode) and the
-// update pass's block counters folded into the scan statistics (partials reset).
+// update pass's block counters folded into the scan statistics.
 __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
     __shared__ double lds[16];
-    __shared__ unsigned long long lds_u[16];
-    for (int k = 0; k < kNumCounters; ++k) {
-        unsigned long long v = 0;
-        unsigned long long *col = P.cpart + (int64_t)k * P.nwpart;
+    __shared__ unsigned long long s_c[16][kNumCounters];
+    {
+        // every counter column at once: independent loads, one LDS exchange
+        unsigned long long v[kNumCounters] = {};
         for (int b = threadIdx.x; b < P.nwpart; b += 1024) {
-            v += col[b];
-            col[b] = 0;
+#pragma unroll
+            for (int k = 0; k < kNumCounters; ++k) v[k] += P.cpart[(int64_t)k * P.nwpart + b];
         }
-        v = block_sum_u64<1024>(v, lds_u);
-        if (threadIdx.x == 0) {
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < kNumCounters; ++k) {
+            v[k] = wave_sum_u64(v[k]);
+            if (lane == 0) s_c[wid][k] = v[k];
+        }
+        __syncthreads();
+        if (threadIdx.x < kNumCounters) {
+            const int k = threadIdx.x;
+            unsigned long long t = 0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t += s_c[q][k];
             if (k == kCSingular) {
-                if (v) P.stats->error_flags |= 1;
-            } else {
-                *counter_field(P.stats, k) += v;
+                if (t) atomicOr(&P.stats->error_flags, 1);
+            } else if (t) {
+                atomicAdd(counter_field(P.stats, k), t);
             }
         }
     }
