@@ -71,8 +71,12 @@ struct fs2_handle {
     // landmark pages (fs2_kernels.hpp): pool, page tables A/B, free list
     char *pool = nullptr;
     int64_t npool = 0;                     // pages in the pool
-    uint4 *pt[2] = {};                     // [rows][n] page descriptors (A/B across resamples)
-    uint4 *rdesc = nullptr;                // descriptors of received pages [n_recv][rows]
+    Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
+    Desc *rdesc = nullptr;                 // descriptors of received pages [n_recv][rows]
+    SumFrame frame{-127.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
+    float ext_seen = 0.0f;                 // largest |x|, |y| imported so far
+    float *slb = nullptr;                  // device: lower bound on every nonzero mirror s
+    uint32_t *ext_dev = nullptr;           // device: import extent (float bits)
     size_t rdesc_cap = 0;
     int rows = 0;                          // page-table rows allocated
     uint32_t *freel = nullptr;             // free page ids [0, nfree)
@@ -123,7 +127,7 @@ struct fs2_handle {
     std::vector<size_t> sendcap, recvcap;
     int32_t n_recv = 0;                             // particles received by the last resample
 
-    MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool}; }
+    MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
     bool sequential() const {
         const int mode = cfg.reduce_mode;
@@ -140,10 +144,10 @@ static int grow_rows(fs2_handle *h, int need_slots) {
         return set_err(&h->err, FS2_ERR_CAPACITY, "map needs %d landmark slots, limit is %d",
                        need_slots, h->max_cap);
     const int rows = (need_slots + kPageSlots - 1) / kPageSlots;
-    const size_t row_bytes = sizeof(uint4) * (size_t)std::max<int64_t>(h->n, 1);
+    const size_t row_bytes = sizeof(Desc) * (size_t)std::max<int64_t>(h->n, 1);
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     for (int b = 0; b < 2; ++b) {
-        uint4 *p = nullptr;
+        Desc *p = nullptr;
         HIP_TRY(h, hipMalloc(&p, row_bytes * rows));
         if (h->pt[b] && b == h->cur) HIP_TRY(h, hipMemcpy(p, h->pt[b], row_bytes * h->rows, hipMemcpyDeviceToDevice));
         hipFree(h->pt[b]);
@@ -393,6 +397,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->rdesc);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
+    hipFree(h->slb); hipFree(h->ext_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
@@ -460,6 +465,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     }
     ok &= alloc((void **)&h->nfree_dev, sizeof(int64_t)) == hipSuccess;
     ok &= alloc((void **)&h->rnfree_dev, sizeof(int64_t)) == hipSuccess;
+    ok &= alloc((void **)&h->slb, sizeof(float)) == hipSuccess;
+    ok &= alloc((void **)&h->ext_dev, sizeof(uint32_t)) == hipSuccess;
     ok &= alloc((void **)&h->mlo, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->out_src, n * 4) == hipSuccess;
@@ -488,7 +495,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= hipHostMalloc((void **)&h->noise_pin, n * 8, 0) == hipSuccess;
     ok &= hipHostMalloc((void **)&h->u0_pin, 8, 0) == hipSuccess;
     if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
-    if (hipMemsetAsync(h->cpart, 0, nb * 8 * kNumCounters, h->stream) != hipSuccess)
+    if (hipMemsetAsync(h->cpart, 0, nb * 8 * kNumCounters, h->stream) != hipSuccess ||
+        hipMemsetD32Async((hipDeviceptr_t)h->slb, 0x7f7fffff, 1, h->stream) != hipSuccess)   // FLT_MAX: no mirror yet
         return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     // Particle.__init__: (0, 0, 0), weight 1/NUM_PARTICLES, empty map (particle.py:11-20)
     for (int s = 0; s < 2; ++s) {
@@ -757,7 +765,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             rc = reserve_pages(h, (int64_t)h->n_recv * h->rows, &rs.alloc);
             if (rc) return rc;
             rs.map = h->map();
-            const size_t rbytes = sizeof(uint4) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
+            const size_t rbytes = sizeof(Desc) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
             if (rbytes > h->rdesc_cap) {
                 HIP_TRY(h, hipStreamSynchronize(s));
                 hipFree(h->rdesc);
@@ -795,9 +803,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             hipEventElapsedTime(&f, h->ev.e[4], h->ev.e[5]);
             h->prof.filter_launches += 1;
             h->prof.filter_ms += f;
-            // one 16 B descriptor per page, the mirrors of the pages it could not
-            // reject, cnt read + count written (8 B per particle), list words
-            h->prof.filter_bytes += 16ull * st.visited + 16ull * st.groups + 8ull * (uint64_t)h->n +
+            // one 8 B descriptor per page, the mirrors of the pages it could not
+            // reject, cnt read + count written (8 B per particle), list entries
+            h->prof.filter_bytes += 16ull * st.visited + sizeof(Desc) * st.groups + 8ull * (uint64_t)h->n +
                                     8ull * st.words;
         }
         h->prof.scans += 1;
@@ -806,19 +814,19 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         h->prof.reduce_ms += b;
         h->prof.resample_ms += c;
         h->prof.scan_ms += a + b + c;
-        // mirror reads (16 B) per visited slot when filtering, fp64 slot reads (48 B) per
-        // candidate, full slot writes (48 B + 16 B mirror)
-        // + candidate list words written and read back (8 B each) and their counts,
-        // + page-table entry per page group and per exact slot read, page copies
-        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + 16ull * st.groups +
+        // mirror reads (16 B) per visited slot when filtering, record reads (48 B) per
+        // candidate, slot writes (48 B record + 16 B mirror) and the descriptor of the
+        // written row (read + write), candidate list entries written and read back
+        // (8 B each) and their counts, a descriptor per page group, page copies
+        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + sizeof(Desc) * st.groups +
                                                           16ull * st.words + 8ull * (uint64_t)h->n * passes
                                                     : 0ull) +
-                                48ull * st.candidates + 64ull * st.written + fixed_bytes +
+                                48ull * st.candidates + (64ull + 2ull * sizeof(Desc)) * st.written + fixed_bytes +
                                 2ull * kPageBytes * st.cow_pages + 8ull * (uint64_t)h->nblocks();
         if (st.resampled)
             // page-table rows (read + write 4 B per page of every output) + scalar
             // gather + plan arrays; received maps (64 B per slot)
-            h->prof.resample_bytes += 8ull * (st.resample_slots / kPageSlots) + 2ull * 36ull * (uint64_t)h->n +
+            h->prof.resample_bytes += 2ull * sizeof(Desc) * (st.resample_slots / kPageSlots) + 2ull * 36ull * (uint64_t)h->n +
                                       40ull * (uint64_t)h->n;
     }
     if (out_pose) {
@@ -906,6 +914,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / per);
         double *stage = nullptr;
         int32_t *cstage = nullptr;
+        HIP_TRY(h, hipMemsetAsync(h->ext_dev, 0, sizeof(uint32_t), s));
         HIP_TRY(h, hipMalloc(&stage, (size_t)std::min(chunk, count) * per));
         HIP_TRY(h, hipMalloc(&cstage, sizeof(int32_t) * std::min(chunk, count)));
         int rc2 = FS2_OK;
@@ -918,7 +927,8 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             if (rc2) break;
             rc2 = reserve_pages(h, k * rows_each, &pa);
             if (rc2) break;
-            if (e == hipSuccess) e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], s);
+            if (e == hipSuccess)
+                e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], h->ext_dev, s);
             if (e == hipSuccess) e = launch_describe(h->map(), h->cnt[c], first + o, k, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
@@ -926,6 +936,19 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         hipFree(stage);
         hipFree(cstage);
         if (rc2) return rc2;
+        // the summary grid covers every imported landmark with room to spare; when it
+        // grows, every descriptor is re-encoded on the new grid
+        uint32_t eb = 0;
+        HIP_TRY(h, hipMemcpy(&eb, h->ext_dev, sizeof eb, hipMemcpyDeviceToHost));
+        float ext = 0.0f;
+        std::memcpy(&ext, &eb, sizeof ext);
+        h->ext_seen = std::max(h->ext_seen, ext);
+        float cell = 1.0f / 64.0f;
+        while (127.0f * cell < 1.25f * h->ext_seen && cell < 65536.0f) cell *= 2.0f;
+        if (cell != h->frame.cell) {
+            h->frame = SumFrame{-127.0f * cell, cell};
+            HIP_TRY(h, launch_describe(h->map(), h->cnt[c], 0, h->n, s));
+        }
     }
     HIP_TRY(h, hipStreamSynchronize(s));
     return FS2_OK;

@@ -140,54 +140,6 @@ __device__ __forceinline__ bool gate_reject_fast(const float4 &m, float cx, floa
     return m.z * fmaf(lx, lx, ly * ly) > gate2f;
 }
 
-// ---- page summaries (fs2_kernels.hpp) ----
-
-// fp16 bits of the largest half <= v (finite v).
-__device__ __forceinline__ uint32_t half_down(float v) {
-    uint32_t b = __half_as_ushort(__float2half_rn(v));
-    if (__half2float(__ushort_as_half((unsigned short)b)) > v)
-        b = (b & 0x8000u) ? b + 1u : (b == 0u ? 0x8001u : b - 1u);
-    return b;
-}
-// fp16 bits of the smallest half >= v.
-__device__ __forceinline__ uint32_t half_up(float v) { return half_down(-v) ^ 0x8000u; }
-
-__device__ __forceinline__ float half_lo(uint32_t w) { return __half2float(__ushort_as_half((unsigned short)(w & 0xffffu))); }
-__device__ __forceinline__ float half_hi(uint32_t w) { return __half2float(__ushort_as_half((unsigned short)(w >> 16))); }
-
-// Summary of the first nvalid mirrors of a page (descriptor .y .z .w).
-__device__ __forceinline__ uint4 describe_page(uint32_t entry, const float4 *mir, int nvalid) {
-    float xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY, smin = INFINITY;
-    bool finite = nvalid > 0;
-    for (int u = 0; u < nvalid; ++u) {
-        const float4 m = mir[u];
-        finite &= isfinite(m.x) && isfinite(m.y);
-        xmin = fminf(xmin, m.x);
-        xmax = fmaxf(xmax, m.x);
-        ymin = fminf(ymin, m.y);
-        ymax = fmaxf(ymax, m.y);
-        smin = fminf(smin, m.z);
-    }
-    if (!finite || !(smin >= 0.0f)) return make_uint4(entry, 0x7c00fc00u, 0x7c00fc00u, 0u);
-    return make_uint4(entry, half_down(xmin) | (half_up(xmax) << 16), half_down(ymin) | (half_up(ymax) << 16),
-                      __float_as_uint(smin));
-}
-
-// True when no slot of the page can pass the gate for the observed point: the
-// distance to the box is <= |fx - x_lm| for every slot, the margins use the
-// box's largest |x|, and s_min <= s, and every fp32 operation below is
-// monotone, so the value compared is <= gate_reject_fast's value for each slot.
-__device__ __forceinline__ bool page_reject(const uint4 &d, float fx, float fy, float fe, float gate2f) {
-    const float xmin = half_lo(d.y), xmax = half_hi(d.y), ymin = half_lo(d.z), ymax = half_hi(d.z);
-    const float Dx = fmaxf(fmaxf(xmin - fx, fx - xmax), 0.0f);
-    const float Dy = fmaxf(fmaxf(ymin - fy, fy - ymax), 0.0f);
-    const float Cx = fmaxf(fabsf(xmin), fabsf(xmax)) * 2.3841858e-7f;
-    const float Cy = fmaxf(fabsf(ymin), fabsf(ymax)) * 2.3841858e-7f;
-    const float lx = fmaxf(fmaf(Dx, 0.99999976f, -(fe + Cx)), 0.0f);
-    const float ly = fmaxf(fmaf(Dy, 0.99999976f, -(fe + Cy)), 0.0f);
-    return __uint_as_float(d.w) * fmaf(lx, lx, ly * ly) > gate2f;
-}
-
 // EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line: it
 // runs a few times per particle and scan, and inlined at k_update's three call
 // sites it would inflate the kernel's register footprint.

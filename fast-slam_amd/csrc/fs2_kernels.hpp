@@ -20,20 +20,30 @@ constexpr int kMaxCand = 8;          // candidate slots listed per particle and 
 // record (x, y, P00, P01, P10, P11; 48 B) in the record pool.  Records are
 // immutable and shared like pages: a slot write stores a new record and points
 // the (private) page's mirror at it, so copy-on-write moves 128 B, not the slots.
-// Pages live in one pool (page id p at pool + 128 p).  A map is a row of page
-// descriptors in the page table pt[row][particle] (uint4):
+// Pages live in one pool (page id p at pool + 128 p).  A map is a row of 8-byte
+// page descriptors in the page table pt[row][particle] (Desc = uint2):
 //   .x  page id; bit 31 says the map owns the page (no other entry refers to
 //       it) and may write it in place, otherwise the first write copies the page
 //       (copy-on-write).  Resampling shares pages instead of copying maps.
-//   .y  fp16 (min, max) of the page's mirror x, rounded outward
-//   .z  fp16 (min, max) of the page's mirror y, rounded outward
-//   .w  fp32 smallest mirror s of the page (0: never reject)
-// The summary lets the candidate stream reject a whole page with one test that
-// is never less conservative than the slot tests it replaces (page_reject).
+//   .y  the page's bounding box on the handle's summary grid, rounded outward:
+//       four 8-bit cell codes (x lo, x hi, y lo, y hi; SumFrame).
+// With the handle-wide lower bound slb on every nonzero mirror s, the summary
+// lets the candidate stream reject a whole page with one test that is never
+// less conservative than the slot tests it replaces (page_reject); a page with
+// an s = 0 slot gets an unbounded box (never rejected).
 constexpr int kPageBytes = 128;
 constexpr int kRecBytes = 48;
 constexpr uint32_t kOwned = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7fffffffu;
+typedef uint2 Desc;
+
+// Summary grid: box bound codes c in [0, 255]; lo(c) = org + (c - 1) cell (c = 0:
+// unbounded), hi(c) = org + c cell (c = 255: unbounded).  cell is a power of two
+// and org a multiple of it, so every bound is exact in fp32.
+struct SumFrame {
+    float org, cell;
+};
+constexpr uint32_t kSumOpen = 0xff00ff00u;   // unbounded box: never rejected
 
 // Counters of the update pass, kept per workgroup (cpart[counter][block]: the
 // first pass of a scan stores them, later passes add) and folded into DevStats
@@ -110,10 +120,12 @@ struct MeasPack {
 // The maps of one particle buffer: page pool + page table.
 struct MapRef {
     char *pool;              // page id p at pool + p * kPageBytes
-    uint4 *pt;               // [rows][n] page descriptors
+    Desc *pt;                // [rows][n] page descriptors
     int64_t n;               // row stride (local particles)
     int32_t rows;            // rows allocated
     char *recs;              // record r at recs + r * kRecBytes
+    SumFrame frame;          // summary grid of the descriptors
+    float *slb;              // lower bound on every nonzero mirror s (lowered by every write)
 };
 
 // Free pages and records reserved for one launch: lane i's t-th new page is
@@ -198,8 +210,8 @@ struct ResampleParams {
     double *ox, *oy, *oyaw, *ow;
     int32_t *ocnt;
     MapRef map;              // current page table
-    uint4 *opt;              // next page table [rows][n]
-    uint4 *rdesc;            // [nrecv][rows] descriptors of received pages
+    Desc *opt;               // next page table [rows][n]
+    Desc *rdesc;             // [nrecv][rows] descriptors of received pages
     PageAlloc alloc;         // received particle r: row k -> page base + r*rows + k,
                              // slot q -> record rbase + peer sbase + soff + q
     int32_t *rank_d;         // [n] rank among packed records
@@ -239,9 +251,11 @@ hipError_t debug_phase_times(unsigned long long out[8], int reset);
 #endif
 // particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
 // alloc.rbase + p * lm_cap + j
+// (ext: atomicMax of the float bits of the largest finite |x|, |y| imported; slb
+// lowered to the smallest nonzero mirror s)
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
-                         int32_t rows_each, int32_t *cnt, hipStream_t s);
+                         int32_t rows_each, int32_t *cnt, uint32_t *ext, hipStream_t s);
 // page summaries of rows [0, ceil(cnt/8)) of particles first .. first+count-1
 hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count,
                            hipStream_t s);

@@ -150,7 +150,7 @@ __device__ __forceinline__ char *page_ptr(char *pool, uint32_t e) {
     return pool + (int64_t)(e & kIdMask) * kPageBytes;
 }
 
-__device__ __forceinline__ uint4 *pt_entry(const MapRef &m, int row, int64_t i) {
+__device__ __forceinline__ Desc *pt_entry(const MapRef &m, int row, int64_t i) {
     return m.pt + (int64_t)row * m.n + i;
 }
 
@@ -201,7 +201,7 @@ __device__ __forceinline__ uint32_t take_rec(const PageAlloc &a, int64_t n, int6
 // private copy of a shared one (copy-on-write: 128 B; the page table is updated).
 __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t i,
                                                const PageAlloc &a, int &t, unsigned &cow) {
-    uint4 *pe = pt_entry(m, row, i);
+    Desc *pe = pt_entry(m, row, i);
     const uint32_t e = pe->x;
     if (e & kOwned) return page_ptr(m.pool, e);
     const uint32_t id = take_page(a, m.n, i, t);
@@ -235,30 +235,98 @@ __device__ __forceinline__ float4 store_slot(const MapRef &m, char *page, int j,
     return mv;
 }
 
-// Page summary after slot j (mirror mv) of particle i was written: the first
-// slot appended to a fresh page starts a new summary, otherwise the box grows to include mv and s_min
-// takes min(s_min, s).  The result covers every slot now in the page (it may
-// also cover values since replaced: still conservative).
-__device__ __forceinline__ uint4 merge_summary(uint4 d, const float4 &mv) {
-    if (!(isfinite(mv.x) && isfinite(mv.y))) return describe_page(d.x, &mv, 0);
-    d.y = half_down(fminf(half_lo(d.y), mv.x)) | (half_up(fmaxf(half_hi(d.y), mv.x)) << 16);
-    d.z = half_down(fminf(half_lo(d.z), mv.y)) | (half_up(fmaxf(half_hi(d.z), mv.y)) << 16);
-    d.w = __float_as_uint(fminf(__uint_as_float(d.w), mv.z));
+// ---- page summaries (fs2_kernels.hpp) ----
+
+// Code of the largest grid bound <= v (0: unbounded) / of the smallest >= v (255).
+__device__ __forceinline__ uint32_t sum_lo(const SumFrame &f, float v) {
+    const double k = floor(((double)v - (double)f.org) / (double)f.cell);
+    if (!(k >= 0.0)) return 0u;
+    return (uint32_t)fmin(k, 254.0) + 1u;
+}
+__device__ __forceinline__ uint32_t sum_hi(const SumFrame &f, float v) {
+    const double k = ceil(((double)v - (double)f.org) / (double)f.cell);
+    if (!(k <= 254.0)) return 255u;
+    return (uint32_t)fmax(k, 0.0);
+}
+__device__ __forceinline__ float sum_lo_val(const SumFrame &f, uint32_t c) {
+    return c == 0u ? -INFINITY : fmaf((float)(c - 1u), f.cell, f.org);
+}
+__device__ __forceinline__ float sum_hi_val(const SumFrame &f, uint32_t c) {
+    return c == 255u ? INFINITY : fmaf((float)c, f.cell, f.org);
+}
+
+// Summary of the first nvalid mirrors of a page: their box on the grid, or the
+// unbounded box when a mirror is not finite or has s = 0 (never reject).
+__device__ __forceinline__ Desc describe_page(uint32_t entry, const float4 *mir, int nvalid, const SumFrame &f) {
+    float xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY, smin = INFINITY;
+    bool finite = nvalid > 0;
+    for (int u = 0; u < nvalid; ++u) {
+        const float4 m = mir[u];
+        finite &= isfinite(m.x) && isfinite(m.y);
+        xmin = fminf(xmin, m.x);
+        xmax = fmaxf(xmax, m.x);
+        ymin = fminf(ymin, m.y);
+        ymax = fmaxf(ymax, m.y);
+        smin = fminf(smin, m.z);
+    }
+    if (!finite || !(smin > 0.0f)) return make_uint2(entry, kSumOpen);
+    return make_uint2(entry, sum_lo(f, xmin) | (sum_hi(f, xmax) << 8) | (sum_lo(f, ymin) << 16) |
+                                 (sum_hi(f, ymax) << 24));
+}
+
+// Summary after a slot (mirror mv) was written: the box grows to include mv (it
+// may also cover values since replaced: still conservative).
+__device__ __forceinline__ Desc merge_summary(Desc d, const float4 &mv, const SumFrame &f) {
+    if (!(isfinite(mv.x) && isfinite(mv.y)) || !(mv.z > 0.0f)) {
+        d.y = kSumOpen;
+        return d;
+    }
+    const uint32_t xl = min(d.y & 0xffu, sum_lo(f, mv.x)), xh = max((d.y >> 8) & 0xffu, sum_hi(f, mv.x));
+    const uint32_t yl = min((d.y >> 16) & 0xffu, sum_lo(f, mv.y)), yh = max(d.y >> 24, sum_hi(f, mv.y));
+    d.y = xl | (xh << 8) | (yl << 16) | (yh << 24);
     return d;
 }
 
+// True when no slot of the page can pass the gate for the observed point: the
+// distance to the box is <= |fx - x_lm| for every slot, the margins use the
+// box's largest |x|, and slb <= s of every slot (a slot with s = 0 opened the
+// box), and every fp32 operation below is monotone, so the value compared is
+// <= gate_reject_fast's value for each slot.
+__device__ __forceinline__ bool page_reject(uint32_t sum, const SumFrame &f, float slb, float fx, float fy,
+                                            float fe, float gate2f) {
+    const float xmin = sum_lo_val(f, sum & 0xffu), xmax = sum_hi_val(f, (sum >> 8) & 0xffu);
+    const float ymin = sum_lo_val(f, (sum >> 16) & 0xffu), ymax = sum_hi_val(f, sum >> 24);
+    const float Dx = fmaxf(fmaxf(xmin - fx, fx - xmax), 0.0f);
+    const float Dy = fmaxf(fmaxf(ymin - fy, fy - ymax), 0.0f);
+    const float Cx = fmaxf(fabsf(xmin), fabsf(xmax)) * 2.3841858e-7f;
+    const float Cy = fmaxf(fabsf(ymin), fabsf(ymax)) * 2.3841858e-7f;
+    const float lx = fmaxf(fmaf(Dx, 0.99999976f, -(fe + Cx)), 0.0f);
+    const float ly = fmaxf(fmaf(Dy, 0.99999976f, -(fe + Cy)), 0.0f);
+    return slb * fmaf(lx, lx, ly * ly) > gate2f;
+}
+
 __device__ __forceinline__ void note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
-    uint4 *pe = pt_entry(m, j / kPageSlots, i);
-    const uint4 d = *pe;
-    *pe = fresh ? describe_page(d.x, &mv, 1) : merge_summary(d, mv);
+    Desc *pe = pt_entry(m, j / kPageSlots, i);
+    const Desc d = *pe;
+    *pe = fresh ? describe_page(d.x, &mv, 1, m.frame) : merge_summary(d, mv, m.frame);
 }
 
 // Recompute the summary of page `row` of particle i from its mirrors (map size c).
 __device__ __forceinline__ void refresh_summary(const MapRef &m, int row, int64_t i, int c) {
-    uint4 *pe = pt_entry(m, row, i);
+    Desc *pe = pt_entry(m, row, i);
     const uint32_t e = pe->x;
     const float4 *mir = reinterpret_cast<const float4 *>(page_ptr(m.pool, e));
-    *pe = describe_page(e, mir, min(kPageSlots, c - row * kPageSlots));
+    *pe = describe_page(e, mir, min(kPageSlots, c - row * kPageSlots), m.frame);
+}
+
+// slb lowered to the smallest positive s the wave's lanes pass (+inf: none); at
+// most one atomic per wave, and only when it lowers the bound.  Call with the
+// whole wave converged.
+__device__ __forceinline__ void lower_slb(float *slb, float s) {
+    float v = (s > 0.0f) ? s : INFINITY;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0 && v < *slb) atomicMin(reinterpret_cast<unsigned *>(slb), __float_as_uint(v));
 }
 
 // Gate decisions this close to the threshold could depend on ulp-level

@@ -503,6 +503,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, 
     __shared__ unsigned long long lds_u[kBlock / 64];
     if (!P.stats->resampled) return;
     unsigned long long pages = 0;
+    float smin = INFINITY;           // smallest positive s received (slb)
     for (int r = blockIdx.x; r < nrecv; r += gridDim.x) {
         const int p = peer_of(P, r);
         const PackHeader &h = P.peers[p].hdr[r - P.peers[p].kbase];
@@ -524,11 +525,13 @@ __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, 
         const float4 *mir = reinterpret_cast<const float4 *>(sm);
         for (int k = threadIdx.x; k * kPageSlots < h.cnt; k += kBlock)
             P.rdesc[(int64_t)r * P.map.rows + k] =
-                describe_page(ids[k], mir + k * kPageSlots, min(kPageSlots, h.cnt - k * kPageSlots));
+                describe_page(ids[k], mir + k * kPageSlots, min(kPageSlots, h.cnt - k * kPageSlots), P.map.frame);
+        for (int q = threadIdx.x; q < h.cnt; q += kBlock) smin = fminf(smin, mir[q].z > 0.0f ? mir[q].z : INFINITY);
         if (threadIdx.x == 0) pages += (h.cnt + kPageSlots - 1) / kPageSlots;
     }
     const unsigned long long b = block_sum_u64<kBlock>(pages, lds_u);
     if (threadIdx.x == 0 && b) atomicAdd(&P.stats->new_pages, b);
+    lower_slb(P.map.slb, smin);
 }
 
 // Outputs take their source's scalars and page-table row (fast_slam_2.py:196
@@ -561,7 +564,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             // 8 independent loads in flight per lane (one per iteration would pay a
             // full memory latency per row)
             for (int k0 = 0; k0 < rows; k0 += 8) {
-                uint4 e[8];
+                Desc e[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) e[u] = *pt_entry(P.map, min(k0 + u, rows - 1), s);
 #pragma unroll
@@ -581,9 +584,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             w = h.w;
             c = h.cnt;
             const uint32_t own = (h.out_hi == h.out_lo) ? kOwned : 0u;
-            const uint4 *rd = P.rdesc + (int64_t)r * P.map.rows;
+            const Desc *rd = P.rdesc + (int64_t)r * P.map.rows;
             for (int k = 0; k * kPageSlots < c; ++k) {
-                uint4 e = rd[k];
+                Desc e = rd[k];
                 e.x |= own;
                 P.opt[(int64_t)k * n + m] = e;
             }

@@ -65,7 +65,8 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const bool live = i < n;
     const int c = live ? P.cnt[i] : 0;
     const MapRef map = P.map;
-    const uint4 *ptrow = map.pt + (live ? i : 0);
+    const Desc *ptrow = map.pt + (live ? i : 0);
+    const float slb = *map.slb;
     const int rlast = map.rows - 1;
     // the list lives in LDS until the walk ends: (record id << 16 | slot) per
     // entry (a global store inside the walk would serialise the prefetch, since
@@ -78,12 +79,14 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     // 8 mirrors loaded, and the wave loads them together (lanes without an open
     // page read page 0, which stays in cache, and discard it).
     // measurements whose gate page g (descriptor d) cannot rule out
-    auto open_mask = [&](const uint4 &d, int g) -> unsigned {
+    auto open_mask = [&](const Desc &d, int g) -> unsigned {
         unsigned om = 0u;
         if (g * kPageSlots < c) {
 #pragma unroll
             for (int k = 0; k < MAXM; ++k)
-                if (k < P.m && !page_reject(d, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f)) om |= 1u << k;
+                if (k < P.m && !page_reject(d.y, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
+                                            P.gate2f))
+                    om |= 1u << k;
         }
         return om;
     };
@@ -110,9 +113,9 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             }
         }
     };
-    uint4 d1 = ptrow[0], d2 = ptrow[(int64_t)min(1, rlast) * n];
+    Desc d1 = ptrow[0], d2 = ptrow[(int64_t)min(1, rlast) * n];
     for (int g = 0; __any(g * kPageSlots < c); ++g) {
-        const uint4 d = d1;
+        const Desc d = d1;
         d1 = d2;
         d2 = ptrow[(int64_t)min(g + 2, rlast) * n];
         if (g * kPageSlots < c) ++groups;
@@ -191,6 +194,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     int nalloc = 0;                  // pages taken from this pass's reservation
     int nrec = 0;                    // records taken from this pass's reservation
     unsigned cow = 0, fresh = 0;
+    float smin_w = INFINITY;         // smallest positive s of the mirrors this lane writes (slb)
     uint64_t mods = 0;               // existing slots modified in phase A (16 bits each)
     int nmod = 0;
     // this pass's reserved records (m per lane): phase A stores modified slots into them
@@ -271,6 +275,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             store_rec(map.recs, r, s);
             float4 m = mirror_of(s);
             m.w = __uint_as_float(r);
+            smin_w = fminf(smin_w, m.z > 0.0f ? m.z : INFINITY);
             s_mv[nmod][tid] = m;
             mods |= (uint64_t)j << (16 * nmod);
             ++nmod;
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     constexpr int NR = MAXM + 1;
     const int nrows = nmod + ((pend != 0u && c % kPageSlots != 0) ? 1 : 0);
     int rrow[NR];
-    uint4 rdesc[NR];
+    Desc rdesc[NR];
     int canon[NR];                   // first entry with the same row
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
@@ -405,10 +410,10 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
             if (t < nmod && canon[t] == t) {
-                uint4 d = rdesc[t];      // loaded before B1, .x now the owned page
+                Desc d = rdesc[t];       // loaded before B1, .x now the owned page
 #pragma unroll
                 for (int u = t; u < MAXM; ++u)
-                    if (u < nmod && canon[u] == t) d = merge_summary(d, s_mv[u][tid]);
+                    if (u < nmod && canon[u] == t) d = merge_summary(d, s_mv[u][tid], map.frame);
                 *pt_entry(map, rrow[t], il) = d;
                 rdesc[t] = d;
             }
@@ -421,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     // stored when the appends leave the row. ----
     int nap = 0;
     int arow = -1;
-    uint4 ad = make_uint4(0u, 0u, 0u, 0u);
+    Desc ad = make_uint2(0u, 0u);
     if (pend != 0u && c % kPageSlots != 0) {
         // the partly filled last row: owned by B1, summary merged if a modified slot shares it
         arow = c / kPageSlots;
@@ -460,7 +465,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             Slot s = load_rec(map.recs, r);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
             const float4 mv = store_slot(map, pg, jh, s, r);
-            if (jh / kPageSlots == arow) ad = merge_summary(ad, mv);
+            smin_w = fminf(smin_w, mv.z > 0.0f ? mv.z : INFINITY);
+            if (jh / kPageSlots == arow) ad = merge_summary(ad, mv, map.frame);
             else note_write(map, jh, il, mv, false);
             s_idx[k][tid] = c + hit;
         } else {
@@ -475,10 +481,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 const uint32_t id = take_page(P.alloc, map.n, il, nalloc);
                 arow = ja / kPageSlots;
                 const float4 mv = store_slot(map, page_ptr(map.pool, id), ja, s, r);
-                ad = describe_page(id | kOwned, &mv, 1);
+                smin_w = fminf(smin_w, mv.z > 0.0f ? mv.z : INFINITY);
+                ad = describe_page(id | kOwned, &mv, 1, map.frame);
                 ++fresh;
             } else {
-                ad = merge_summary(ad, store_slot(map, page_ptr(map.pool, ad.x), ja, s, r));
+                const float4 mv = store_slot(map, page_ptr(map.pool, ad.x), ja, s, r);
+                smin_w = fminf(smin_w, mv.z > 0.0f ? mv.z : INFINITY);
+                ad = merge_summary(ad, mv, map.frame);
             }
             s_idx[k][tid] = -1;
             ++nap;
@@ -522,6 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                                                    : 0xffffffffu);
     block_counters<kBlock, 0, kNumCounters>(cv, P.cpart, assign, live ? w : 0.0,
                                             P.last_pass ? P.wpart + blockIdx.x : nullptr);
+    lower_slb(map.slb, smin_w);
 }
 
 hipError_t launch_candidates(const UpdateParams &p, hipStream_t s) {
@@ -675,9 +685,10 @@ hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
 __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const int32_t *cnt_stage,
                                                    int64_t first, int64_t count, int32_t lm_cap,
                                                    MapRef map, PageAlloc alloc, int32_t rows_each,
-                                                   int32_t *cnt) {
+                                                   int32_t *cnt, uint32_t *ext) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t total = count * lm_cap;
+    float smin = INFINITY, amax = 0.0f;
     for (int64_t e = t; e < total; e += (int64_t)gridDim.x * kBlock) {
         const int64_t p = e / lm_cap;
         const int j = (int)(e % lm_cap);
@@ -688,9 +699,16 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         const uint32_t id = alloc.freel[alloc.base + p * rows_each + row];
         if (j % kPageSlots == 0) pt_entry(map, row, first + p)->x = id | kOwned;
         const double *s = stage + e * 6;
-        store_slot(map, page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}},
-                   alloc.rfreel[alloc.rbase + e]);
+        const float4 mv = store_slot(map, page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}},
+                                     alloc.rfreel[alloc.rbase + e]);
+        smin = fminf(smin, mv.z > 0.0f ? mv.z : INFINITY);
+        if (isfinite(mv.x)) amax = fmaxf(amax, fabsf(mv.x));
+        if (isfinite(mv.y)) amax = fmaxf(amax, fabsf(mv.y));
     }
+    lower_slb(map.slb, smin);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    if ((threadIdx.x & 63) == 0 && amax > 0.0f) atomicMax(ext, __float_as_uint(amax));
 }
 
 __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first, int64_t count,
@@ -728,9 +746,9 @@ static unsigned grid_for(int64_t total) {
 
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
-                         int32_t rows_each, int32_t *cnt, hipStream_t s) {
+                         int32_t rows_each, int32_t *cnt, uint32_t *ext, hipStream_t s) {
     hipLaunchKernelGGL(k_import, dim3(grid_for(count * lm_cap)), dim3(kBlock), 0, s, stage,
-                       cnt_stage, first, count, lm_cap, map, alloc, rows_each, cnt);
+                       cnt_stage, first, count, lm_cap, map, alloc, rows_each, cnt, ext);
     return hipGetLastError();
 }
 
