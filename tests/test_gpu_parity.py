@@ -421,9 +421,10 @@ def test_page_sharing_long_run(fs):
 
 
 def test_page_summary_extreme_coordinates(fs):
-    """Page summaries store fp16 boxes rounded outward: maps far beyond fp16 range
-    (|x| ~ 1e5), near its limit (6.5e4) and at tiny scales (1e-6) must give the same
-    associations and state with and without the filter."""
+    """Page summaries store boxes on a power-of-two grid fitted to the imported
+    maps, rounded outward: maps at |x| ~ 1e5, 6.5e4 and at tiny scales (1e-6, below
+    the finest grid cell) must give the same associations and state with and
+    without the filter."""
     N, L = 1024, 40
     rng = np.random.default_rng(31)
     for scale in (1e5, 6.55e4, 1e-6):
@@ -450,6 +451,51 @@ def test_page_summary_extreme_coordinates(fs):
             assert np.array_equal(a, b, equal_nan=True)
         for f in fl:
             f.close()
+
+
+def test_summary_grid_growth_and_saturation(fs):
+    """The summary grid is fitted to the first import (a 10 m map: 1/8 m cells),
+    grows when a later import reaches 600 m (every descriptor re-encoded), and
+    landmarks appended 5 km away saturate the grid (unbounded boxes).  With and
+    without the filter, and against the oracle: identical associations and state."""
+    from oracle import oracle as orc
+    N, L = 512, 24
+    rng = np.random.default_rng(57)
+    lm = np.zeros((N, L, 6))
+    base = rng.uniform(-5, 5, (L, 2))
+    lm[:, :, 0:2] = base + rng.normal(0, 0.02, (N, L, 2))
+    lm[:, :, 2] = lm[:, :, 5] = 0.01
+    x, y, yaw = (rng.normal(0, s_, N) for s_ in (0.02, 0.02, 0.01))
+    far = lm[N // 2:].copy()
+    far[:, :, 0:2] *= 120.0                     # second import: extent ~600 m
+    cap = L + 40
+    fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False,
+                       landmark_capacity=cap) for g in (True, False)]
+    o = orc.OracleFilter(N, cap)
+    full = np.concatenate([lm[:N // 2], far])
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), full)
+    for f in fl:
+        f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+        f.set_state(cnt=np.full(N - N // 2, L, np.int32), lm=far, first=N // 2)
+    for sc in range(4):
+        ks = rng.choice(L, 2, replace=False)
+        ms = np.array([[np.hypot(*base[k]) * 1.01, np.arctan2(base[k, 1], base[k, 0])] for k in ks] +
+                      [[5000.0 + 10.0 * sc, 0.3 * sc], [5000.0 + 10.0 * sc, 0.3 * sc + 0.001]])
+        nz = rng.normal(0, 0.0055, N)
+        u0 = 0.37 / N
+        out = [f.step(0.0, 0.03, ms, None, nz, u0) for f in fl]
+        opose, oassoc, _, _ = o.iterate(0.0, 0.03, ms, nz, u0)
+        assert np.array_equal(fl[0].associations(), fl[1].associations()), sc
+        assert np.array_equal(fl[0].associations(), oassoc), sc
+        assert np.array_equal(out[0][0], out[1][0]), sc
+        assert np.allclose(out[0][0], opose, rtol=1e-9, atol=1e-12), sc
+    s0, s1 = fl[0].get_state(lm_cap=cap), fl[1].get_state(lm_cap=cap)
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(s0[4], o.cnt)
+    assert np.allclose(s0[5], o.lm, rtol=1e-9, atol=1e-12)
+    for f in fl:
+        f.close()
 
 
 def test_icp_grid_search_matches_brute_force(fs):
