@@ -31,23 +31,30 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+    """defines / out: an A/B variant (-D flags) written to `out` instead of libfs2.so."""
+    lib = out or LIB
+    if not force and not defines and out is None and not _stale():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value",
-           "-I", os.path.join(ROCM, "include"),
+           "-I", os.path.join(ROCM, "include"), *defines,
            *[os.path.join(CSRC, s) for s in SOURCES],
-           "-o", LIB + ".tmp", "-L", os.path.join(ROCM, "lib"), "-lrccl",
+           "-o", lib + ".tmp", "-L", os.path.join(ROCM, "lib"), "-lrccl",
            "-Wl,-rpath," + os.path.join(ROCM, "lib")]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python build.py [--force] [--variant TAG -DNAME=V ...]  (variant -> lib/libfs2_TAG.so)
+    args = sys.argv[1:]
+    tag = args[args.index("--variant") + 1] if "--variant" in args else None
+    defs = [a for a in args if a.startswith("-D")]
+    out = os.path.join(LIB_DIR, f"libfs2_{tag}.so") if tag else None
+    print(build(force="--force" in args, verbose=True, defines=defs, out=out))

@@ -305,6 +305,57 @@ __device__ __forceinline__ bool page_reject(uint32_t sum, const SumFrame &f, flo
     return slb * fmaf(lx, lx, ly * ly) > gate2f;
 }
 
+// ---- measurement bands: the cheap pre-tests of the candidate stream ----
+//
+// For measurement (fx, fy, fe) every slot with mirror s >= slb > 0 and finite
+// fp32 coordinates whose true distance to fx in x alone is D >= Rx is rejected
+// by gate_reject_fast, whatever its y:
+//   |fl(fx - x)| >= D (1 - 2^-24),  fl(fe + cx) <= (fe + (|fx| + D) 2^-22)(1 + 2^-24),
+//   so lx >= D (1 - 6e-7) - (fe + 2^-22 |fx|)(1 + 1e-7) >= L (1 + 1.9e-5)
+// with Rx = (L (1 + 1e-5) + fe (1 + 1e-5) + 1e-6 |fx|)(1 + 1e-5), L = sqrt(gate2f / slb);
+// then s * fma(lx, lx, ly^2) >= slb lx^2 (1 - 2^-24)^2 > gate2f.  Likewise in y.
+// A page summary box lying entirely beyond fx + Rx or fx - Rx holds only such
+// slots (a bounded box has finite mirrors with s > 0; kSumOpen is never outside),
+// so the page is rejected for that measurement from its 8-bit codes alone;
+// a slot is rejected when |fl(fx - x)| >= float(Rx) rounded up (finite, s > 0).
+// Every margin only widens the band, so no slot the slot test keeps is dropped.
+struct Band {
+    uint32_t cx, cy;   // (a | b << 8): box outside iff low code > a or high code < b
+    float rx, ry;      // slot outside iff s > 0 and finite |fx - x| >= rx (or the same in y)
+};
+
+__device__ __forceinline__ Band band_none() { return Band{0xffu, 0xffu, INFINITY, INFINITY}; }
+
+// code thresholds of the band [f - R, f + R] on the summary grid: a box with
+// lo(xl) >= f + R (xl >= A) or hi(xh) <= f - R (xh <= B) is outside
+__device__ inline uint32_t band_codes(double f, double R, const SumFrame &fr) {
+    const double cell = fr.cell, org = fr.org;
+    if (!(isfinite(R) && isfinite(f) && cell > 0.0)) return 0xffu;   // never outside
+    const double ta = (f + R - org) / cell + 1.0 + 1e-6;   // lo(c) = org + (c - 1) cell >= f + R
+    const double tb = (f - R - org) / cell - 1e-6;         // hi(c) = org + c cell <= f - R
+    const double A = fmin(fmax(ceil(ta), 1.0), 256.0);     // 256: never (codes <= 255)
+    const double B = fmin(fmax(floor(tb), -1.0), 254.0);   // -1: never; 255 is unbounded
+    return (uint32_t)(A - 1.0) | ((uint32_t)(B + 1.0) << 8);
+}
+
+__device__ inline Band gate_band(float fx, float fy, float fe, float slb, float gate2f, const SumFrame &fr) {
+    const double L = sqrt((double)gate2f / (double)slb);
+    const double base = L * (1.0 + 1e-5) + (double)fe * (1.0 + 1e-5);
+    const double Rx = (base + fabs((double)fx) * 1e-6) * (1.0 + 1e-5);
+    const double Ry = (base + fabs((double)fy) * 1e-6) * (1.0 + 1e-5);
+    Band b;
+    b.cx = band_codes(fx, Rx, fr);
+    b.cy = band_codes(fy, Ry, fr);
+    b.rx = (isfinite(Rx) && isfinite(fx)) ? __double2float_ru(Rx * (1.0 + 0x1p-20)) : INFINITY;
+    b.ry = (isfinite(Ry) && isfinite(fy)) ? __double2float_ru(Ry * (1.0 + 0x1p-20)) : INFINITY;
+    return b;
+}
+
+__device__ __forceinline__ bool slot_outside_band(const float4 &m, float fx, float fy, float rx, float ry) {
+    const float ax = fabsf(fx - m.x), ay = fabsf(fy - m.y);
+    return m.z > 0.0f && ((ax >= rx && ax < INFINITY) || (ay >= ry && ay < INFINITY));
+}
+
 __device__ __forceinline__ void note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
     Desc *pe = pt_entry(m, j / kPageSlots, i);
     const Desc d = *pe;

@@ -56,9 +56,25 @@ __device__ unsigned long long g_phase[8];
 // can therefore never match and are never modified; k_update visits exactly the
 // listed ones.  A list longer than kMaxCand stores its first kMaxCand entries
 // and k_update resumes with an exact scan after the last stored one.
+// A/B knobs (profiles/r01_v13_ab_k_candidates.txt): deeper descriptor prefetch,
+// the Euclidean box test on pages that pass the bands, and the band pre-test
+// on slots of open pages all measured slower than the defaults (more SGPRs,
+// fewer waves, divergent branches for little rejection gained).
+#ifndef FS2_DESC_AHEAD
+#define FS2_DESC_AHEAD 2
+#endif
+#ifndef FS2_PAGE_REFINE
+#define FS2_PAGE_REFINE 0
+#endif
+#ifndef FS2_SLOT_BAND
+#define FS2_SLOT_BAND 0
+#endif
+constexpr int kDescAhead = FS2_DESC_AHEAD;   // page descriptors a lane keeps in flight
+
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ uint64_t s_list[kMaxCand][kBlock];
+    __shared__ Band s_band[MAXM];
     const int tid = threadIdx.x;
     const int64_t n = P.n;
     const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
@@ -68,25 +84,58 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const Desc *ptrow = map.pt + (live ? i : 0);
     const float slb = *map.slb;
     const int rlast = map.rows - 1;
+    // Each measurement's band (gate_band): a page whose box, or a slot whose
+    // mirror, lies beyond it in x or in y is rejected by integer / one-compare
+    // tests; computed once per workgroup, kept in scalar registers.
+    if (tid < MAXM) {
+        Band b = band_none();
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+            if (tid == k && k < P.m)
+                b = gate_band(P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], slb, P.gate2f, map.frame);
+        s_band[tid] = b;
+    }
+    __syncthreads();
+    uint32_t bc[MAXM];               // (x a, x b, y a, y b) code thresholds, one byte each
+    float rx[MAXM], ry[MAXM];
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k) {
+        bc[k] = __builtin_amdgcn_readfirstlane(s_band[k].cx | (s_band[k].cy << 16));
+        rx[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_band[k].rx)));
+        ry[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_band[k].ry)));
+    }
     // the list lives in LDS until the walk ends: (record id << 16 | slot) per
     // entry (a global store inside the walk would serialise the prefetch, since
     // vmcnt counts loads and stores in issue order)
     int nc = 0;
     unsigned visited = 0, groups = 0;
 
-    // Page g: its descriptor is tested against every measurement first (the
-    // next two descriptors already in flight); only pages it cannot reject have their
+    // Page g: its descriptor's box codes are tested against every measurement's
+    // band first (integer compares; the next descriptors already in flight);
+    // only pages outside no band have their
     // 8 mirrors loaded, and the wave loads them together (lanes without an open
     // page read page 0, which stays in cache, and discard it).
     // measurements whose gate page g (descriptor d) cannot rule out
     auto open_mask = [&](const Desc &d, int g) -> unsigned {
         unsigned om = 0u;
         if (g * kPageSlots < c) {
+            const uint32_t s = d.y;
+            const uint32_t xl = s & 0xffu, xh = (s >> 8) & 0xffu, yl = (s >> 16) & 0xffu, yh = s >> 24;
 #pragma unroll
             for (int k = 0; k < MAXM; ++k)
-                if (k < P.m && !page_reject(d.y, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
-                                            P.gate2f))
+                if (k < P.m && xl <= (bc[k] & 0xffu) && xh >= ((bc[k] >> 8) & 0xffu) &&
+                    yl <= ((bc[k] >> 16) & 0xffu) && yh >= (bc[k] >> 24))
                     om |= 1u << k;
+#if FS2_PAGE_REFINE
+            // the box survived the bands: the full (Euclidean) box test
+            if (om) {
+#pragma unroll
+                for (int k = 0; k < MAXM; ++k)
+                    if (((om >> k) & 1u) &&
+                        page_reject(s, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
+                        om &= ~(1u << k);
+            }
+#endif
         }
         return om;
     };
@@ -102,10 +151,15 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                 const float cy = fabsf(mv.y) * 2.3841858e-7f;
                 bool hit = false;
 #pragma unroll
-                for (int k = 0; k < MAXM; ++k)
-                    if ((om >> k) & 1u)
+                for (int k = 0; k < MAXM; ++k) {
+                    if ((om >> k) & 1u) {
+#if FS2_SLOT_BAND
+                        if (slot_outside_band(mv, P.meas.fx[k], P.meas.fy[k], rx[k], ry[k])) continue;
+#endif
                         hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
                                                  P.gate2f);
+                    }
+                }
                 if (hit) {
                     if (nc < kMaxCand) s_list[nc][tid] = ((uint64_t)mirror_rec(mv) << 16) | (uint64_t)(j0 + u);
                     ++nc;
@@ -113,11 +167,14 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             }
         }
     };
-    Desc d1 = ptrow[0], d2 = ptrow[(int64_t)min(1, rlast) * n];
+    Desc dq[kDescAhead];             // descriptors of pages g .. g + kDescAhead - 1 in flight
+#pragma unroll
+    for (int q = 0; q < kDescAhead; ++q) dq[q] = ptrow[(int64_t)min(q, rlast) * n];
     for (int g = 0; __any(g * kPageSlots < c); ++g) {
-        const Desc d = d1;
-        d1 = d2;
-        d2 = ptrow[(int64_t)min(g + 2, rlast) * n];
+        const Desc d = dq[0];
+#pragma unroll
+        for (int q = 0; q + 1 < kDescAhead; ++q) dq[q] = dq[q + 1];
+        dq[kDescAhead - 1] = ptrow[(int64_t)min(g + kDescAhead, rlast) * n];
         if (g * kPageSlots < c) ++groups;
         const unsigned om = open_mask(d, g);
         if (!__any(om)) continue;

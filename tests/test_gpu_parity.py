@@ -523,3 +523,51 @@ def test_icp_grid_search_matches_brute_force(fs):
         assert it == ito, k
         assert np.allclose(R, Ro, atol=1e-9), k
         assert np.allclose(tt, to, atol=1e-9 * max(1.0, np.abs(to).max())), k
+
+
+def test_gate_band_boundaries(fs):
+    """The measurement bands of the candidate stream (integer page pre-test on the
+    summary codes, one-compare slot pre-test) only drop what the slot test drops:
+    pages of landmarks just inside / just outside the gate radius along +-x, +-y
+    and the diagonals, at three scales, give the same associations and state with
+    and without the filter, and the oracle's."""
+    from oracle import oracle as orc
+    N = 1024
+    rng = np.random.default_rng(91)
+    eps = (-1e-7, 1e-7, 3e-6, 3e-5, 1e-4, 1e-3, 1e-2, 0.3)      # 8 per page
+    dirs = [(1, 0), (-1, 0), (0, 1), (0, -1), (0.6, 0.8), (-0.8, 0.6)]
+    for scale in (1.0, 40.0, 1e-3):
+        sig = 0.1 * scale
+        r = 8.0 * sig                                   # MAXIMUM_LANDMARK_DISTANCE 8, cov sig^2 I
+        obs = np.array([[3.1, 2.2], [-1.7, 4.4], [0.35, -2.9]]) * scale
+        base = np.array([o + np.array(d) * r * (1.0 + e) for o in obs for d in dirs for e in eps])
+        L = len(base)                                    # 144 landmarks, 18 pages
+        lm = np.zeros((N, L, 6))
+        lm[:, :, 0:2] = base + rng.normal(0, sig * 1e-9, (N, L, 2))
+        lm[:, :, 2] = lm[:, :, 5] = sig * sig
+        x, y, yaw = (rng.normal(0, s_ * scale, N) for s_ in (1e-3, 1e-3, 1e-3))
+        cap = L + 16
+        fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False,
+                           landmark_capacity=cap) for g in (True, False)]
+        for f in fl:
+            f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+        o = orc.OracleFilter(N, cap)
+        o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+        for sc in range(3):
+            ob = obs[[(sc + k) % 3 for k in range(3)]] + rng.normal(0, sig * 1e-9, (3, 2))
+            ob = np.concatenate([ob, [[9.0 * scale, -9.0 * scale]]])
+            ms = np.stack([np.hypot(ob[:, 0], ob[:, 1]), np.arctan2(ob[:, 1], ob[:, 0])], 1)
+            nz = rng.normal(0, 0.0055 * scale, N)
+            u0 = 0.41 / N
+            out = [f.step(0.0, 0.03 * scale, ms, ob, nz, u0) for f in fl]
+            opose, oassoc, _, _ = o.iterate(0.0, 0.03 * scale, ms, nz, u0, observed=ob)
+            assert np.array_equal(fl[0].associations(), fl[1].associations()), (scale, sc)
+            assert np.array_equal(fl[0].associations(), oassoc), (scale, sc)
+            assert np.array_equal(out[0][0], out[1][0]), (scale, sc)
+            assert out[0][1].candidates < out[1][1].candidates
+        s0, s1 = fl[0].get_state(lm_cap=cap), fl[1].get_state(lm_cap=cap)
+        for a, b in zip(s0, s1):
+            assert np.array_equal(a, b, equal_nan=True)
+        assert np.array_equal(s0[4], o.cnt)
+        for f in fl:
+            f.close()
