@@ -83,7 +83,7 @@ struct fs2_handle {
     int64_t nfree = 0, cursor = 0;         // free pages listed / reserved since the last collection
     uint8_t *mark = nullptr;               // collection marks, one byte per page
     uint8_t epoch = 0;
-    int32_t *bcnt = nullptr;               // sweep block counts
+    int64_t *bcnt = nullptr;               // sweep block counts -> offsets
     int64_t *nfree_dev = nullptr;
     uint64_t collections = 0;
     // slot records (fs2_kernels.hpp): pool, free list, marks (collected with the pages)
@@ -93,7 +93,7 @@ struct fs2_handle {
     int64_t rnfree = 0, rcursor = 0;
     uint8_t *rmark = nullptr;
     uint8_t repoch = 0;
-    int32_t *rbcnt = nullptr;
+    int64_t *rbcnt = nullptr;
     int64_t *rnfree_dev = nullptr;
     int64_t s_recv = 0;                    // slots received by the last resample
     int32_t *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
@@ -210,7 +210,7 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
     HIP_TRY(h, hipMalloc(&h->freel, sizeof(uint32_t) * (size_t)pages));
     hipFree(h->bcnt);
     h->bcnt = nullptr;
-    HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int32_t) * (size_t)collect_blocks(pages)));
+    HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int64_t) * (size_t)collect_blocks(pages)));
     h->npool = pages;
     return collect(h, false);
 }
@@ -237,7 +237,7 @@ static int grow_recs(fs2_handle *h, int64_t n) {
     HIP_TRY(h, hipMalloc(&h->rfreel, sizeof(uint32_t) * (size_t)n));
     hipFree(h->rbcnt);
     h->rbcnt = nullptr;
-    HIP_TRY(h, hipMalloc(&h->rbcnt, sizeof(int32_t) * (size_t)collect_blocks(n)));
+    HIP_TRY(h, hipMalloc(&h->rbcnt, sizeof(int64_t) * (size_t)collect_blocks(n)));
     h->nrecs = n;
     return collect(h, true);
 }
@@ -601,6 +601,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // ---- fused update passes (move in the first) ----
     UpdateParams up{};
     up.n = h->n;
+    up.nblk = h->nblocks();
+    up.blk0 = 0;
+    up.blk1 = up.nblk;
     up.gidx0 = h->first;
     up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
     up.map = h->map();

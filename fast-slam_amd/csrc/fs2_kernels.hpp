@@ -140,6 +140,8 @@ struct PageAlloc {
 
 struct UpdateParams {
     int64_t n;               // local particles
+    int64_t blk0, blk1;      // workgroups [blk0, blk1) of kBlock particles in this launch
+    int64_t nblk;            // workgroups of the whole pass (column stride of cpart)
     int64_t gidx0;           // global index of local particle 0
     double *x, *y, *yaw, *w;
     int32_t *cnt;
@@ -161,8 +163,8 @@ struct UpdateParams {
     double R[4];
     double init_cov[4];
     int32_t *assoc;          // [M][n] or null
-    double *wpart;           // [gridDim.x] block partial sums of w (last pass)
-    unsigned long long *cpart;   // [kNumCounters][gridDim.x] block counters
+    double *wpart;           // [nblk] block partial sums of w (last pass)
+    unsigned long long *cpart;   // [kNumCounters][nblk] block counters
     DevStats *stats;
     MeasPack meas;
 };
@@ -268,12 +270,12 @@ hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s);
 // of `map`, then list every unmarked page of [0, npool) in freel; nfree_dev
 // receives the count.
 hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark,
-                          uint8_t epoch, int32_t *bcnt, uint32_t *freel, int64_t *nfree_dev,
+                          uint8_t epoch, int64_t *bcnt, uint32_t *freel, int64_t *nfree_dev,
                           hipStream_t s);
 // after launch_collect with the same (mark, epoch): mark every record a live page
 // refers to, then list every unmarked record of [0, nrecs) in rfreel
 hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,
-                                  int64_t nrecs, uint8_t *rmark, uint8_t repoch, int32_t *rbcnt,
+                                  int64_t nrecs, uint8_t *rmark, uint8_t repoch, int64_t *rbcnt,
                                   uint32_t *rfreel, int64_t *rnfree_dev, hipStream_t s);
 int64_t collect_blocks(int64_t npool);
 

@@ -12,7 +12,7 @@
 //   k_mark        one lane per particle, one byte store per page of its map
 //   k_sweep_count free pages per 4096-page block
 //   k_sweep_scan  exclusive scan of the block counts (one workgroup)
-//   k_sweep_write free page ids, in id order, into freel
+//   k_sweep_write free page ids, in id order, into freel (staged in LDS, stored contiguously)
 //
 // Slot records (fs2_kernels.hpp) are collected the same way, less often (the
 // record pool is sized for many scans of writes): after the page mark, every
@@ -29,12 +29,22 @@ constexpr int kSweepBlock = kBlock * kSweepPer;      // page ids per workgroup
 
 int64_t collect_blocks(int64_t npool) { return (npool + kSweepBlock - 1) / kSweepBlock; }
 
+// One lane per particle; its page-table entries are loaded 8 at a time (a mark
+// store may alias them, so one load per iteration would pay a full memory
+// latency per row).
 __global__ __launch_bounds__(kBlock) void k_mark(const MapRef map, const int32_t *cnt, uint8_t *mark,
                                                  uint8_t epoch) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= map.n) return;
     const int rows = (cnt[i] + kPageSlots - 1) / kPageSlots;
-    for (int r = 0; r < rows; ++r) mark[pt_entry(map, r, i)->x & kIdMask] = epoch;
+    for (int r0 = 0; r0 < rows; r0 += 8) {
+        uint32_t e[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) e[u] = pt_entry(map, min(r0 + u, rows - 1), i)->x;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (r0 + u < rows) mark[e[u] & kIdMask] = epoch;
+    }
 }
 
 __device__ __forceinline__ int wave_incl_scan_int(int v) {
@@ -63,19 +73,28 @@ __device__ __forceinline__ int block_excl_scan(int v, int *lds, int *tot) {
     return off + inc - v;
 }
 
+// free ids among the kSweepPer consecutive ids from id0 (bit e: id0 + e), from
+// one 16-byte load of their marks; ids past npool are not free
 __device__ __forceinline__ unsigned free_bits(const uint8_t *mark, int64_t npool, uint8_t epoch,
                                               int64_t id0) {
     unsigned bits = 0;
+    if (id0 + kSweepPer <= npool) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(mark + id0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int e = 0; e < kSweepPer; ++e) {
-        const int64_t id = id0 + e;
-        if (id < npool && mark[id] != epoch) bits |= 1u << e;
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (((w[q] >> (8 * b)) & 0xffu) != epoch) bits |= 1u << (4 * q + b);
+    } else {
+        for (int e = 0; e < kSweepPer; ++e)
+            if (id0 + e < npool && mark[id0 + e] != epoch) bits |= 1u << e;
     }
     return bits;
 }
 
 __global__ __launch_bounds__(kBlock) void k_sweep_count(const uint8_t *mark, int64_t npool, uint8_t epoch,
-                                                        int32_t *bcnt) {
+                                                        int64_t *bcnt) {
     __shared__ int lds[kBlock / 64];
     const int64_t id0 = (int64_t)blockIdx.x * kSweepBlock + (int64_t)threadIdx.x * kSweepPer;
     const int f = __popc(free_bits(mark, npool, epoch, id0));
@@ -84,12 +103,19 @@ __global__ __launch_bounds__(kBlock) void k_sweep_count(const uint8_t *mark, int
     if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(1024) void k_sweep_scan(int32_t *bcnt, int64_t nb, int64_t *nfree) {
+// exclusive scan of the block counts in place; *nfree = total.  Each thread
+// owns a contiguous run of blocks, read 4 at a time.
+__global__ __launch_bounds__(1024) void k_sweep_scan(int64_t *bcnt, int64_t nb, int64_t *nfree) {
     __shared__ int64_t lds[1024 / 64];
     const int64_t per = (nb + 1023) / 1024;
-    const int64_t b0 = threadIdx.x * per;
+    const int64_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
     int64_t s = 0;
-    for (int64_t k = b0; k < min(nb, b0 + per); ++k) s += bcnt[k];
+    for (int64_t k = b0; k < b1; k += 4) {
+        int64_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = (k + u < b1) ? bcnt[k + u] : 0;
+        s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
     // inclusive scan of the per-thread sums
     int64_t v = s;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -106,26 +132,32 @@ __global__ __launch_bounds__(1024) void k_sweep_scan(int32_t *bcnt, int64_t nb, 
         tot += lds[k];
     }
     int64_t run = off + v - s;
-    for (int64_t k = b0; k < min(nb, b0 + per); ++k) {
-        const int32_t c = bcnt[k];
-        bcnt[k] = (int32_t)run;
+    for (int64_t k = b0; k < b1; ++k) {
+        const int64_t c = bcnt[k];
+        bcnt[k] = run;
         run += c;
     }
     if (threadIdx.x == 0) *nfree = tot;
 }
 
+// The workgroup's free ids, in id order, staged in LDS and stored contiguously
+// (a lane storing its own run of ids would scatter 4-byte stores).
 __global__ __launch_bounds__(kBlock) void k_sweep_write(const uint8_t *mark, int64_t npool, uint8_t epoch,
-                                                        const int32_t *bcnt, uint32_t *freel) {
+                                                        const int64_t *bcnt, uint32_t *freel) {
     __shared__ int lds[kBlock / 64];
+    __shared__ uint32_t s_ids[kSweepBlock];
     const int64_t id0 = (int64_t)blockIdx.x * kSweepBlock + (int64_t)threadIdx.x * kSweepPer;
     unsigned bits = free_bits(mark, npool, epoch, id0);
     int tot;
-    int pos = bcnt[blockIdx.x] + block_excl_scan(__popc(bits), lds, &tot);
+    int pos = block_excl_scan(__popc(bits), lds, &tot);
     while (bits) {
         const int e = __builtin_ctz(bits);
         bits &= bits - 1u;
-        freel[pos++] = (uint32_t)(id0 + e);
+        s_ids[pos++] = (uint32_t)(id0 + e);
     }
+    __syncthreads();
+    uint32_t *dst = freel + bcnt[blockIdx.x];
+    for (int j = threadIdx.x; j < tot; j += kBlock) dst[j] = s_ids[j];
 }
 
 // one lane per (page, slot) of the pool: 8 consecutive lanes read one 128-byte page
@@ -140,7 +172,7 @@ __global__ __launch_bounds__(kBlock) void k_mark_recs(const char *pool, int64_t 
 }
 
 hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,
-                                  int64_t nrecs, uint8_t *rmark, uint8_t repoch, int32_t *rbcnt,
+                                  int64_t nrecs, uint8_t *rmark, uint8_t repoch, int64_t *rbcnt,
                                   uint32_t *rfreel, int64_t *rnfree_dev, hipStream_t s) {
     const int64_t nb = collect_blocks(nrecs);
     const int64_t lanes = npool * kPageSlots;
@@ -154,7 +186,7 @@ hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t
 }
 
 hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark, uint8_t epoch,
-                          int32_t *bcnt, uint32_t *freel, int64_t *nfree_dev, hipStream_t s) {
+                          int64_t *bcnt, uint32_t *freel, int64_t *nfree_dev, hipStream_t s) {
     const int64_t nb = collect_blocks(npool);
     if (map.n > 0)
         hipLaunchKernelGGL(k_mark, dim3((unsigned)((map.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, map,

@@ -95,11 +95,11 @@ __device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
 
 // The counters of this workgroup (NV per lane: counters FIRST .. FIRST+NV-1)
 // stored (bit k of `assign` set) or added into its column of cpart
-// ([kNumCounters][gridDim.x]) and, when wsum != nullptr, its deterministic
+// ([kNumCounters][nb], column b) and, when wsum != nullptr, its deterministic
 // weight sum (block_sum's tree) stored to *wsum: one LDS exchange, one barrier.
 template <int NT, int FIRST, int NV>
-__device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpart, unsigned assign, double w,
-                               double *wsum) {
+__device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpart, int64_t nb, int64_t b,
+                               unsigned assign, double w, double *wsum) {
     __shared__ unsigned s_c[NT / 64][NV];
     __shared__ double s_w[NT / 64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -117,7 +117,7 @@ __device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpar
         unsigned long long t = 0;
 #pragma unroll
         for (int q = 0; q < NT / 64; ++q) t += s_c[q][threadIdx.x];
-        unsigned long long *e = cpart + (int64_t)(FIRST + threadIdx.x) * gridDim.x + blockIdx.x;
+        unsigned long long *e = cpart + (int64_t)(FIRST + threadIdx.x) * nb + b;
         if ((assign >> (FIRST + threadIdx.x)) & 1u) *e = t;
         else if (t) *e += t;
     }

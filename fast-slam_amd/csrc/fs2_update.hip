@@ -77,7 +77,8 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ Band s_band[MAXM];
     const int tid = threadIdx.x;
     const int64_t n = P.n;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
+    const int64_t blk = P.blk0 + blockIdx.x;   // this launch may cover a chunk of the blocks
+    const int64_t i = blk * kBlock + tid;
     const bool live = i < n;
     const int c = live ? P.cnt[i] : 0;
     const MapRef map = P.map;
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
     const unsigned cv[3] = {(unsigned)min(nc, kMaxCand), groups, visited};   // kCWords, kCGroups, kCVisited
     // the first pass of a scan stores its counters, later passes add
-    block_counters<kBlock, kCWords, 3>(cv, P.cpart, P.k0 == 0 ? 0xffffffffu : 0u, 0.0, nullptr);
+    block_counters<kBlock, kCWords, 3>(cv, P.cpart, P.nblk, blk, P.k0 == 0 ? 0xffffffffu : 0u, 0.0, nullptr);
 }
 
 template <int K>
@@ -229,7 +230,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     unsigned long long ph_last = 0;
 #endif
     const int tid = threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + tid;
+    const int64_t blk = P.blk0 + blockIdx.x;
+    const int64_t i = blk * kBlock + tid;
     const bool live = i < P.n;
     const int64_t n = P.n;
     if (tid < MAXM) s_ms[tid] = Meas{P.meas.d[tid], P.meas.b[tid], P.meas.ox[tid], P.meas.oy[tid]};
@@ -586,20 +588,20 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     const unsigned assign = P.k0 != 0 ? 0u
                                        : (P.filter ? ~((1u << kCWords) | (1u << kCGroups) | (1u << kCVisited))
                                                    : 0xffffffffu);
-    block_counters<kBlock, 0, kNumCounters>(cv, P.cpart, assign, live ? w : 0.0,
-                                            P.last_pass ? P.wpart + blockIdx.x : nullptr);
+    block_counters<kBlock, 0, kNumCounters>(cv, P.cpart, P.nblk, blk, assign, live ? w : 0.0,
+                                            P.last_pass ? P.wpart + blk : nullptr);
     lower_slb(map.slb, smin_w);
 }
 
 hipError_t launch_candidates(const UpdateParams &p, hipStream_t s) {
-    const unsigned grid = (unsigned)((p.n + kBlock - 1) / kBlock);
+    const unsigned grid = (unsigned)(p.blk1 - p.blk0);
     if (grid == 0 || !p.filter) return hipSuccess;
     hipLaunchKernelGGL(k_candidates<kMaxM>, dim3(grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_update(const UpdateParams &p, hipStream_t s) {
-    const unsigned grid = (unsigned)((p.n + kBlock - 1) / kBlock);
+    const unsigned grid = (unsigned)(p.blk1 - p.blk0);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_update<kMaxM>, dim3(grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
