@@ -274,8 +274,9 @@ def main():
                                       "hbm_traffic_per_launch": pmc_traffic(cfg["name"], k)}
                                   for k, v in kern.items()},
                       "update_pass_bytes": prof["update_bytes"] / launches,
-                      "reduce_ms": prof["reduce_ms"] / max(prof["scans"], 1),
-                      "resample_ms_total": prof["resample_ms"],
+                      # normalise / N_eff / estimate, the resample when it fires, the
+                      # stats publication: one event span per scan
+                      "reduce_and_resample_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resamples": resamples,
                       "resample_shared_slots": copied_slots,
                       "cow_pages_per_particle_scan": cow_pages / (f.n_local * args.steps),

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -54,9 +55,22 @@ double gate_to_q(double gate) {
     return q;
 }
 
+// Profiling: four events per scan (start, after k_candidates, after the update
+// pass, after publication), double-buffered and read at the next scan, so the
+// host never waits for them and only two markers sit between kernels.
+struct ProfScan {
+    bool pending = false;
+    int set = 0;
+    DevStats st{};
+    int passes = 0;
+    int m = 0;
+    uint64_t fixed_bytes = 0;
+};
 struct ProfEvents {
-    hipEvent_t e[6] = {};
+    hipEvent_t e[2][4] = {};
     bool ok = false;
+    int cur = 0;
+    ProfScan pend;
 };
 
 }  // namespace
@@ -104,6 +118,11 @@ struct fs2_handle {
     int32_t *part_maxcnt = nullptr;
     double *cbuf = nullptr, *bsum = nullptr;
     DevStats *stats_dev = nullptr, *stats_host = nullptr;
+    // end-of-scan publication (k_publish): stats + sequence flag in coherent host memory
+    DevStats *pub_stats = nullptr, *pub_stats_dev = nullptr;
+    unsigned long long *pub_flag = nullptr, *pub_flag_dev = nullptr;
+    unsigned long long pub_seq = 0;
+    bool stats_clean = false;              // stats_dev is zero (k_publish ran last)
     double *noise_dev = nullptr, *noise_pin = nullptr, *u0_dev = nullptr, *u0_pin = nullptr;
     int32_t *assoc_dev = nullptr;
     int64_t assoc_cap = 0;
@@ -408,10 +427,12 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
     if (h->stats_host) hipHostFree(h->stats_host);
+    if (h->pub_stats) hipHostFree(h->pub_stats);
     if (h->noise_pin) hipHostFree(h->noise_pin);
     if (h->u0_pin) hipHostFree(h->u0_pin);
     if (h->ev.ok)
-        for (auto &e : h->ev.e) hipEventDestroy(e);
+        for (auto &set : h->ev.e)
+            for (auto &e : set) hipEventDestroy(e);
     delete h->tp;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -492,6 +513,17 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
     ok &= hipHostMalloc((void **)&h->stats_host, sizeof(DevStats), 0) == hipSuccess;
+    // one coherent block: the published stats, then the flag on its own 64-byte line
+    ok &= hipHostMalloc((void **)&h->pub_stats, sizeof(DevStats) + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
+          hipSuccess;
+    if (ok) {
+        const size_t off = ((sizeof(DevStats) + 63) / 64) * 64;
+        h->pub_flag = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(h->pub_stats) + off);
+        *h->pub_flag = 0;
+        ok &= hipHostGetDevicePointer((void **)&h->pub_stats_dev, h->pub_stats, 0) == hipSuccess;
+        if (ok)
+            h->pub_flag_dev = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(h->pub_stats_dev) + off);
+    }
     ok &= hipHostMalloc((void **)&h->noise_pin, n * 8, 0) == hipSuccess;
     ok &= hipHostMalloc((void **)&h->u0_pin, 8, 0) == hipSuccess;
     if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
@@ -550,17 +582,83 @@ int fs2_synchronize(fs2_handle *h) {
 int fs2_set_profiling(fs2_handle *h, int32_t enable) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
     if (enable && !h->ev.ok) {
-        for (auto &e : h->ev.e) HIP_TRY(h, hipEventCreate(&e));
+        for (auto &set : h->ev.e)
+            for (auto &e : set) HIP_TRY(h, hipEventCreate(&e));
         h->ev.ok = true;
     }
+    h->ev.pend.pending = false;
     h->profiling = enable != 0;
     h->prof = fs2_profile{};
     return FS2_OK;
 }
 
-int fs2_get_profile(const fs2_handle *h, fs2_profile *out) {
-    if (!h || !out) return set_err(nullptr, FS2_ERR_ARG, "null argument");
+static int fold_profile(fs2_handle *h);
+
+int fs2_get_profile(const fs2_handle *hc, fs2_profile *out) {
+    if (!hc || !out) return set_err(nullptr, FS2_ERR_ARG, "null argument");
+    fs2_handle *h = const_cast<fs2_handle *>(hc);   // the last scan's events are folded in
+    const int rc = fold_profile(h);
+    if (rc) return rc;
     *out = h->prof;
+    return FS2_OK;
+}
+
+// Adds the pending profiled scan (ProfEvents) to h->prof.
+static int fold_profile(fs2_handle *h) {
+    ProfScan &p = h->ev.pend;
+    if (!p.pending) return FS2_OK;
+    p.pending = false;
+    hipEvent_t *E = h->ev.e[p.set];
+    HIP_TRY(h, hipEventSynchronize(E[3]));
+    const DevStats &st = p.st;
+    float a = 0, f = 0, r = 0;
+    HIP_TRY(h, hipEventElapsedTime(&a, E[0], E[2]));     // update pass(es)
+    HIP_TRY(h, hipEventElapsedTime(&r, E[2], E[3]));     // reduce, resample, publication
+    if (h->cfg.gate_filter && p.m <= kMaxM) {
+        // k_candidates (E[0] directly precedes it: the stats were zeroed by the
+        // previous scan's k_publish, or by a memset ahead of E[0])
+        HIP_TRY(h, hipEventElapsedTime(&f, E[0], E[1]));
+        h->prof.filter_launches += 1;
+        h->prof.filter_ms += f;
+        // one 8 B descriptor per page, the mirrors of the pages it could not
+        // reject, cnt read + count written (8 B per particle), list entries
+        h->prof.filter_bytes += 16ull * st.visited + sizeof(Desc) * st.groups + 8ull * (uint64_t)h->n +
+                                8ull * st.words;
+    }
+    h->prof.scans += 1;
+    h->prof.update_launches += p.passes;
+    h->prof.update_ms += a;
+    h->prof.reduce_ms += r;
+    h->prof.scan_ms += a + r;
+    // mirror reads (16 B) per visited slot when filtering, record reads (48 B) per
+    // candidate, slot writes (48 B record + 16 B mirror) and the descriptor of the
+    // written row (read + write), candidate list entries written and read back
+    // (8 B each) and their counts, a descriptor per page group, page copies
+    h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + sizeof(Desc) * st.groups +
+                                                      16ull * st.words + 8ull * (uint64_t)h->n * p.passes
+                                                : 0ull) +
+                            48ull * st.candidates + (64ull + 2ull * sizeof(Desc)) * st.written + p.fixed_bytes +
+                            2ull * kPageBytes * st.cow_pages + 8ull * (uint64_t)h->nblocks();
+    if (st.resampled)
+        // page-table rows (read + write per page of every output) + scalar gather +
+        // plan arrays
+        h->prof.resample_bytes += 2ull * sizeof(Desc) * (st.resample_slots / kPageSlots) +
+                                  2ull * 36ull * (uint64_t)h->n + 40ull * (uint64_t)h->n;
+    return FS2_OK;
+}
+
+// Wait for k_publish's flag: spin for up to 50 ms (a scan at config 3 takes
+// under 1 ms), then fall back to a stream sync, which also reports a fault.
+static int wait_flag(fs2_handle *h, unsigned long long seq) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+        if (__atomic_load_n(h->pub_flag, __ATOMIC_ACQUIRE) == seq) return FS2_OK;
+        if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+        __builtin_ia32_pause();
+    }
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (__atomic_load_n(h->pub_flag, __ATOMIC_ACQUIRE) != seq)
+        return set_err(&h->err, FS2_ERR_HIP, "scan statistics were not published");
     return FS2_OK;
 }
 
@@ -595,8 +693,12 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         HIP_TRY(h, hipMalloc(&h->assoc_dev, sizeof(int32_t) * (size_t)M * h->n));
         h->assoc_cap = (int64_t)M * h->n;
     }
-    HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
-    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[0], s));
+    // the last scan's k_publish zeroed the stats; anything else (first scan, an
+    // error return) leaves them to be cleared here
+    if (!h->stats_clean) HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
+    h->stats_clean = false;
+    hipEvent_t *E = h->ev.e[h->ev.cur];
+    if (prof) HIP_TRY(h, hipEventRecord(E[0], s));
 
     // ---- fused update passes (move in the first) ----
     UpdateParams up{};
@@ -657,9 +759,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         rc = reserve_pages(h, (int64_t)up.m * h->n, &up.alloc);
         if (rc) return rc;
         up.map = h->map();
-        if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(h->ev.e[4], s));
         HIP_TRY(h, launch_candidates(up, s));
-        if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(h->ev.e[5], s));
+        if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(E[1], s));
         HIP_TRY(h, launch_update(up, s));
         ++passes;
         // pose/weight/count read + weight/count write; pose write on the move pass
@@ -667,7 +768,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         if (up.do_move && noise) fixed_bytes += (uint64_t)h->n * 8;
         if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
     }
-    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[1], s));
+    if (prof) HIP_TRY(h, hipEventRecord(E[2], s));
 
     // ---- normalise, N_eff, estimate ----
     ReduceParams rp{};
@@ -744,7 +845,6 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         rs.lazy = 1;
         HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
     }
-    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[2], s));
 
     // ---- low-variance resample (:177-199); on one GPU the kernels exit unless the
     // rule fired, sharded ranks learn the decision first (sizes of the transfers) ----
@@ -786,51 +886,32 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         }
         HIP_TRY(h, launch_global_best(rp, s));
     }
-    if (prof) HIP_TRY(h, hipEventRecord(h->ev.e[3], s));
 
-    HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
-    HIP_TRY(h, hipStreamSynchronize(s));
-    const DevStats &st = *h->stats_host;
+    // publish the stats to host memory and spin on the flag: a stream sync's
+    // wake-up and a copy launch cost more than the whole reduction phase
+    const unsigned long long pseq = ++h->pub_seq;
+    HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
+    if (prof) HIP_TRY(h, hipEventRecord(E[3], s));
+    h->stats_clean = true;
+    rc = wait_flag(h, pseq);
+    if (rc) return rc;
+    const DevStats &st = *h->pub_stats;
     if (st.resampled) h->cur = nxt;
     h->cnt_upper = st.max_count;
     h->last_m = M;
     h->scan += 1;
     if (prof) {
-        float a = 0, b = 0, c = 0;
-        hipEventElapsedTime(&a, h->ev.e[0], h->ev.e[1]);
-        hipEventElapsedTime(&b, h->ev.e[1], h->ev.e[2]);
-        hipEventElapsedTime(&c, h->ev.e[2], h->ev.e[3]);
-        if (h->cfg.gate_filter && M <= kMaxM) {
-            // candidate stream: mirrors of every slot, the lists and their counts
-            float f = 0;
-            hipEventElapsedTime(&f, h->ev.e[4], h->ev.e[5]);
-            h->prof.filter_launches += 1;
-            h->prof.filter_ms += f;
-            // one 8 B descriptor per page, the mirrors of the pages it could not
-            // reject, cnt read + count written (8 B per particle), list entries
-            h->prof.filter_bytes += 16ull * st.visited + sizeof(Desc) * st.groups + 8ull * (uint64_t)h->n +
-                                    8ull * st.words;
-        }
-        h->prof.scans += 1;
-        h->prof.update_launches += passes;
-        h->prof.update_ms += a;
-        h->prof.reduce_ms += b;
-        h->prof.resample_ms += c;
-        h->prof.scan_ms += a + b + c;
-        // mirror reads (16 B) per visited slot when filtering, record reads (48 B) per
-        // candidate, slot writes (48 B record + 16 B mirror) and the descriptor of the
-        // written row (read + write), candidate list entries written and read back
-        // (8 B each) and their counts, a descriptor per page group, page copies
-        h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + sizeof(Desc) * st.groups +
-                                                          16ull * st.words + 8ull * (uint64_t)h->n * passes
-                                                    : 0ull) +
-                                48ull * st.candidates + (64ull + 2ull * sizeof(Desc)) * st.written + fixed_bytes +
-                                2ull * kPageBytes * st.cow_pages + 8ull * (uint64_t)h->nblocks();
-        if (st.resampled)
-            // page-table rows (read + write 4 B per page of every output) + scalar
-            // gather + plan arrays; received maps (64 B per slot)
-            h->prof.resample_bytes += 2ull * sizeof(Desc) * (st.resample_slots / kPageSlots) + 2ull * 36ull * (uint64_t)h->n +
-                                      40ull * (uint64_t)h->n;
+        // the previous profiled scan's events are complete (this scan ran after them)
+        rc = fold_profile(h);
+        if (rc) return rc;
+        ProfScan &p = h->ev.pend;
+        p.pending = true;
+        p.set = h->ev.cur;
+        p.st = st;
+        p.passes = passes;
+        p.m = M;
+        p.fixed_bytes = fixed_bytes;
+        h->ev.cur ^= 1;
     }
     if (out_pose) {
         out_pose[0] = st.pose[0];
@@ -869,6 +950,7 @@ int fs2_get_assoc(fs2_handle *h, int32_t *idx, int64_t capacity, int32_t *m_out)
     if (capacity < need) return set_err(&h->err, FS2_ERR_ARG, "assoc buffer too small (%lld < %lld)",
                                         (long long)capacity, (long long)need);
     if (m_out) *m_out = h->last_m;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
     if (need) HIP_TRY(h, hipMemcpy(idx, h->assoc_dev, sizeof(int32_t) * need, hipMemcpyDeviceToHost));
     return FS2_OK;
 }

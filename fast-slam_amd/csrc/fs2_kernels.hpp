@@ -247,6 +247,11 @@ hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t s);
 hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s);
 hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
+// End of a scan: the scan's DevStats into host memory (mapped, coherent), then
+// *flag = seq (system scope, after the stats), and the device copy zeroed for
+// the next scan.  The host spins on the flag instead of a stream sync.
+hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                          unsigned long long seq, hipStream_t s);
 
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset);

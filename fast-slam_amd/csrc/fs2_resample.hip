@@ -181,6 +181,28 @@ hipError_t launch_global_best(const ReduceParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(64) void k_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                                                unsigned long long seq) {
+    static_assert(sizeof(DevStats) % 8 == 0 && sizeof(DevStats) / 8 <= 64, "one word per lane");
+    constexpr int W = sizeof(DevStats) / 8;
+    const int t = threadIdx.x;
+    if (t < W) {
+        uint64_t *s = reinterpret_cast<uint64_t *>(stats);
+        const uint64_t v = s[t];
+        reinterpret_cast<uint64_t *>(host_stats)[t] = v;
+        s[t] = 0;                    // the next scan's counters start from zero
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                          unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, stats, host_stats, host_flag, seq);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ local prefix --
 
 __device__ __forceinline__ double wave_incl_scan(double v) {

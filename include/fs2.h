@@ -105,8 +105,9 @@ typedef struct fs2_profile {
     int64_t scans;              /* scans timed since profiling was enabled */
     int64_t update_launches;    /* update passes (candidate stream + exact kernel) */
     double update_ms;           /* summed device time of the update passes (HIP events) */
-    double reduce_ms;           /* normalise / N_eff / estimate kernels */
-    double resample_ms;         /* prefix + gather kernels (scans that resampled) */
+    double reduce_ms;           /* after the update pass: normalise / N_eff / estimate,
+                                   the resample when it fires, stats publication */
+    double resample_ms;         /* unused (0): folded into reduce_ms */
     double scan_ms;             /* summed device time of whole scans */
     uint64_t update_bytes;      /* algorithmic bytes moved by the update kernel */
     uint64_t resample_bytes;    /* algorithmic bytes moved by resample gathers */
