@@ -1,9 +1,10 @@
 """ICP scan matcher on the GPU (reference: fast_slam_2/algorithms/icp.py:13-90).
 
 One workgroup per alignment holds both clouds in LDS for the whole loop;
-nearest neighbours by brute force (lowest index on exact ties, matching a
-KD-tree query on non-degenerate clouds), rotation by the closed-form 2-D
-Kabsch angle (equal to the reference's SVD + reflection fix).
+exact nearest neighbours through a uniform grid over the target cloud (ring
+search with a conservative bound; lowest index on exact ties, as brute force
+and a KD-tree query on non-degenerate clouds give), rotation by the closed-form
+2-D Kabsch angle (equal to the reference's SVD + reflection fix).
 """
 from __future__ import annotations
 

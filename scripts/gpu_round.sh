@@ -16,10 +16,10 @@ if [[ $STAGE == all || $STAGE == tests ]]; then
   tail -1 gpurun_out/smoke.log
 fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
-  timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench.log; exit 4; }
+  timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench.log; exit 4; }
   tail -1 gpurun_out/bench.log
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof.log; exit 5; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof.log; exit 5; }
   python scripts/prof_summary.py gpurun_out/prof gpurun_out/prof_summary.txt "${PROF_TITLE:-}" > /dev/null && head -12 gpurun_out/prof_summary.txt
 fi
