@@ -839,8 +839,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
         if (rc) return rc;
     }
-    // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183)
-    HIP_TRY(h, launch_global_finalize(rp, s));
+    // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183); on
+    // one GPU k_finalize did this already
+    if (sh) HIP_TRY(h, launch_global_finalize(rp, s));
     if (!sh) {
         rs.lazy = 1;
         HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
@@ -879,18 +880,22 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             }
             rs.rdesc = h->rdesc;
         }
-        HIP_TRY(h, launch_resample_apply(rs, s));
+        HIP_TRY(h, launch_resample_apply(rs, sh, s));
         if (sh) {
             rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
             if (rc) return rc;
+            HIP_TRY(h, launch_global_best(rp, s));
         }
-        HIP_TRY(h, launch_global_best(rp, s));
     }
 
     // publish the stats to host memory and spin on the flag: a stream sync's
-    // wake-up and a copy launch cost more than the whole reduction phase
+    // wake-up and a copy launch cost more than the whole reduction phase (one
+    // GPU: together with the post-resample estimate, in one launch)
     const unsigned long long pseq = ++h->pub_seq;
-    HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
+    if (sh)
+        HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
+    else
+        HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
     if (prof) HIP_TRY(h, hipEventRecord(E[3], s));
     h->stats_clean = true;
     rc = wait_flag(h, pseq);

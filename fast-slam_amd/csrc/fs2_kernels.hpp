@@ -245,13 +245,18 @@ hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s);
 hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t s);
-hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s);
+// estimate: also this rank's post-resample record (k_estimate); one GPU leaves
+// it to launch_tail_single
+hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStream_t s);
 hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 // End of a scan: the scan's DevStats into host memory (mapped, coherent), then
 // *flag = seq (system scope, after the stats), and the device copy zeroed for
 // the next scan.  The host spins on the flag instead of a stream sync.
 hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
                           unsigned long long seq, hipStream_t s);
+// One GPU: k_estimate + k_global_best (when the resample fired) + k_publish.
+hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
+                              unsigned long long *host_flag, unsigned long long seq, hipStream_t s);
 
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset);

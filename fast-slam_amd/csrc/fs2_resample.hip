@@ -62,7 +62,10 @@ __device__ double pairwise_sq(const double *a, int64_t n) {
     return pairwise_sq(a, n2) + pairwise_sq(a + n2, n - n2);
 }
 
-// This rank's record: sum w'^2, first maximum, its pose, normalised total.
+__device__ void global_finalize_body(const ReduceParams &P);
+
+// This rank's record: sum w'^2, first maximum, its pose, normalised total (on
+// one GPU also the global decision, k_global_finalize's work).
 __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
@@ -102,6 +105,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
         r.t_local = P.stats->t_local;
         r.max_count = mc;
         *P.rec = r;
+        if (P.world == 1 && P.recs == P.rec) global_finalize_body(P);   // one GPU: no record exchange
     }
 }
 
@@ -112,7 +116,7 @@ hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
 
 // N_eff (fast_slam_2.py:212-223), the N_eff < N/2 rule (:62), the estimate
 // (:201-210), u0 (:183) and this rank's prefix offset, from all records.
-__global__ void k_global_finalize(const ReduceParams P) {
+__device__ void global_finalize_body(const ReduceParams &P) {
     DevStats *st = P.stats;
     double sq = P.recs[0].sumsq;
     double bv = P.recs[0].best_w;
@@ -148,15 +152,16 @@ __global__ void k_global_finalize(const ReduceParams P) {
                        : (1.0 / ng) * philox_uniform01(P.seed, P.scan | (1ull << 63), 0);
 }
 
+__global__ void k_global_finalize(const ReduceParams P) { global_finalize_body(P); }
+
 hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_global_finalize, dim3(1), dim3(1), 0, s, p);
     return hipGetLastError();
 }
 
 // Estimate after a resample: first maximum over all ranks' outputs.
-__global__ void k_global_best(const ReduceParams P) {
+__device__ void global_best_body(const ReduceParams &P) {
     DevStats *st = P.stats;
-    if (!st->resampled) return;
     double bv = P.recs[0].best_w;
     int64_t bi = P.recs[0].best_gidx;
     int gb = 0;
@@ -176,13 +181,17 @@ __global__ void k_global_best(const ReduceParams P) {
     st->pose[2] = P.recs[gb].pose[2];
 }
 
+__global__ void k_global_best(const ReduceParams P) {
+    if (P.stats->resampled) global_best_body(P);
+}
+
 hipError_t launch_global_best(const ReduceParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_global_best, dim3(1), dim3(1), 0, s, p);
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(64) void k_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
-                                                unsigned long long seq) {
+__device__ void publish_body(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                             unsigned long long seq) {
     static_assert(sizeof(DevStats) % 8 == 0 && sizeof(DevStats) / 8 <= 64, "one word per lane");
     constexpr int W = sizeof(DevStats) / 8;
     const int t = threadIdx.x;
@@ -195,6 +204,11 @@ __global__ __launch_bounds__(64) void k_publish(DevStats *stats, DevStats *host_
     __threadfence_system();
     __syncthreads();
     if (t == 0) __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                                                unsigned long long seq) {
+    publish_body(stats, host_stats, host_flag, seq);
 }
 
 hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
@@ -629,10 +643,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
 }
 
 // this rank's first maximum over its outputs -> record (post-resample estimate)
-__global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32_t nparts) {
+__device__ void estimate_body(const ResampleParams &P, int32_t nparts) {
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
-    if (!P.stats->resampled) return;
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
     for (int k = threadIdx.x; k < nparts; k += 1024) argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
@@ -650,7 +663,32 @@ __global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32
     }
 }
 
-hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s) {
+__global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32_t nparts) {
+    if (P.stats->resampled) estimate_body(P, nparts);
+}
+
+// One GPU, end of a scan: the estimate after a resample and the stats
+// publication (k_estimate + k_global_best + k_publish in one launch).
+__global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, const ReduceParams P, int32_t nparts,
+                                                     DevStats *host_stats, unsigned long long *host_flag,
+                                                     unsigned long long seq) {
+    if (R.stats->resampled) {
+        estimate_body(R, nparts);
+        __syncthreads();
+        if (threadIdx.x == 0) global_best_body(P);
+    }
+    __syncthreads();
+    publish_body(P.stats, host_stats, host_flag, seq);
+}
+
+hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
+                              unsigned long long *host_flag, unsigned long long seq, hipStream_t s) {
+    const int32_t nparts = (int32_t)((r.n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_tail_single, dim3(1), dim3(1024), 0, s, r, p, nparts, host_stats, host_flag, seq);
+    return hipGetLastError();
+}
+
+hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStream_t s) {
     const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
     if (g == 0) return hipSuccess;
     int32_t nrecv = 0;
@@ -660,7 +698,7 @@ hipError_t launch_resample_apply(const ResampleParams &p, hipStream_t s) {
         hipLaunchKernelGGL(k_unpack_recv, dim3(min(nrecv, 4096)), dim3(kBlock), 0, s, p, nrecv);
     }
     hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
+    if (estimate) hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
     return hipGetLastError();
 }
 
