@@ -87,7 +87,7 @@ struct fs2_handle {
     int64_t npool = 0;                     // pages in the pool
     Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
     Desc *rdesc = nullptr;                 // descriptors of received pages [n_recv][rows]
-    SumFrame frame{-127.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
+    SumFrame frame{-127.0f, 1.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
     float ext_seen = 0.0f;                 // largest |x|, |y| imported so far
     float *slb = nullptr;                  // device: lower bound on every nonzero mirror s
     uint32_t *ext_dev = nullptr;           // device: import extent (float bits)
@@ -1036,7 +1036,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         float cell = 1.0f / 64.0f;
         while (127.0f * cell < 1.25f * h->ext_seen && cell < 65536.0f) cell *= 2.0f;
         if (cell != h->frame.cell) {
-            h->frame = SumFrame{-127.0f * cell, cell};
+            h->frame = SumFrame{-127.0f * cell, cell, 1.0f / cell};
             HIP_TRY(h, launch_describe(h->map(), h->cnt[c], 0, h->n, s));
         }
     }

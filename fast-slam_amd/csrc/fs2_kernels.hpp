@@ -42,6 +42,7 @@ typedef uint2 Desc;
 // and org a multiple of it, so every bound is exact in fp32.
 struct SumFrame {
     float org, cell;
+    float icell;             // 1 / cell (exact: cell is a power of two)
 };
 constexpr uint32_t kSumOpen = 0xff00ff00u;   // unbounded box: never rejected
 

@@ -239,12 +239,12 @@ __device__ __forceinline__ float4 store_slot(const MapRef &m, char *page, int j,
 
 // Code of the largest grid bound <= v (0: unbounded) / of the smallest >= v (255).
 __device__ __forceinline__ uint32_t sum_lo(const SumFrame &f, float v) {
-    const double k = floor(((double)v - (double)f.org) / (double)f.cell);
+    const double k = floor(((double)v - (double)f.org) * (double)f.icell);   // = / cell, exactly
     if (!(k >= 0.0)) return 0u;
     return (uint32_t)fmin(k, 254.0) + 1u;
 }
 __device__ __forceinline__ uint32_t sum_hi(const SumFrame &f, float v) {
-    const double k = ceil(((double)v - (double)f.org) / (double)f.cell);
+    const double k = ceil(((double)v - (double)f.org) * (double)f.icell);
     if (!(k <= 254.0)) return 255u;
     return (uint32_t)fmax(k, 0.0);
 }

@@ -428,11 +428,12 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int off = (lane & 7) * 16;
-        v4i va[8];                    // clang vector type: HIP's int4 struct defeats SROA here
-        uint32_t da[8];
+        constexpr int CB = 8;         // pages per lane and batch (8 lanes per page)
+        v4i va[CB];                   // clang vector type: HIP's int4 struct defeats SROA here
+        uint32_t da[CB];
         auto load_batch = [&](int base, v4i *v, uint32_t *d) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < CB; ++u) {
                 const uint2 tk = s_cow[wid][min(base + 8 * u + (lane >> 3), T - 1)];
                 d[u] = tk.y;
                 v[u] = *reinterpret_cast<const v4i *>(page_ptr(map.pool, tk.x) + off);
@@ -440,9 +441,9 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         };
         auto store_batch = [&](const v4i *v, const uint32_t *d) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
+            for (int u = 0; u < CB; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
         };
-        for (int base = 0; base < T; base += 64) {
+        for (int base = 0; base < T; base += 8 * CB) {
             load_batch(base, va, da);
             store_batch(va, da);
         }
