@@ -1340,6 +1340,11 @@ int fs2_debug_phase_times(uint64_t out[8], int32_t reset) {
                ? FS2_OK
                : FS2_ERR_HIP;
 }
+extern "C" int fs2_debug_icp_phase_times(uint64_t out[4], int32_t reset) {
+    return fs2::debug_icp_phase_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess
+               ? FS2_OK
+               : FS2_ERR_HIP;
+}
 #endif
 
 int fs2_cluster_points(int32_t device, const double *points, int64_t n, double eps, int64_t min_samples,

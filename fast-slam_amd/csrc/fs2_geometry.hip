@@ -26,8 +26,35 @@ __device__ __forceinline__ double wave_sum(double v) {
 // equals the reference's SVD + reflection fix (icp.py:76-85).
 
 constexpr int kIcpMaxP = 1024;
-constexpr int kIcpThreads = 1024;
+#ifndef FS2_ICP_THREADS
+#define FS2_ICP_THREADS 1024
+#endif
+constexpr int kIcpThreads = FS2_ICP_THREADS;
 constexpr int kIcpGrid = 32;                 // cells per axis
+
+// Optional per-phase cycle counts of one alignment (build with -DFS2_PHASE_TIMING;
+// fs2_debug_icp_phase_times): NN search, centroid sums, covariance sums, update.
+#ifdef FS2_PHASE_TIMING
+__device__ unsigned long long g_icp_phase[4];
+#define ICP_T(k)                                                           \
+    do {                                                                   \
+        if (threadIdx.x == 0 && blockIdx.x == 0) {                         \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+            if ((k) > 0) g_icp_phase[(k) - 1] += t_ - t_last;              \
+            t_last = t_;                                                   \
+        }                                                                  \
+    } while (0)
+hipError_t debug_icp_phase_times(unsigned long long out[4], int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_phase), sizeof(unsigned long long) * 4);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[4] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_icp_phase), z, sizeof z);
+    }
+    return e;
+}
+#else
+#define ICP_T(k) do { } while (0)
+#endif
 
 struct IcpGrid {
     double x0, y0, hx, hy, ihx, ihy, slack;
@@ -38,9 +65,11 @@ __device__ __forceinline__ int icp_cell(double v, double v0, double ih) {
     return !(c >= 0.0) ? 0 : (c >= (double)(kIcpGrid - 1) ? kIcpGrid - 1 : (int)c);   // NaN -> 0
 }
 
-// exact nearest target of p: (index, squared distance)
+// exact nearest target of p: (index, squared distance).  tsort holds the
+// targets in cell order (tsort[q] = tgt[cidx[q]]), so a candidate costs one LDS
+// load; its index is read only when it improves or ties the best.
 __device__ __forceinline__ void icp_nearest(const double2 p, const IcpGrid &g, const int *cstart,
-                                            const int16_t *cidx, const double2 *tgt, int &bj,
+                                            const int16_t *cidx, const double2 *tsort, int &bj,
                                             double &best) {
     const int cx = icp_cell(p.x, g.x0, g.ihx), cy = icp_cell(p.y, g.y0, g.ihy);
     best = INFINITY;
@@ -53,13 +82,15 @@ __device__ __forceinline__ void icp_nearest(const double2 p, const IcpGrid &g, c
                 if (i < 0 || i >= kIcpGrid) continue;
                 const int cell = j * kIcpGrid + i;
                 for (int q = cstart[cell]; q < cstart[cell + 1]; ++q) {
-                    const int t = cidx[q];
-                    const double2 tp = tgt[t];
+                    const double2 tp = tsort[q];
                     const double dx = p.x - tp.x, dy = p.y - tp.y;
                     const double d2 = dx * dx + dy * dy;
-                    if (d2 < best || (d2 == best && t < bj)) {
-                        best = d2;
-                        bj = t;
+                    if (d2 <= best) {
+                        const int t = cidx[q];
+                        if (d2 < best || t < bj) {
+                            best = d2;
+                            bj = t;
+                        }
                     }
                 }
             }
@@ -106,14 +137,13 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
                                                      double *t_out, int32_t *iters_out) {
     __shared__ double2 s_src[kIcpMaxP];
     __shared__ double2 s_tgt[kIcpMaxP];
-    __shared__ int32_t s_nn[kIcpMaxP];
-    __shared__ double s_dist[kIcpMaxP];
     __shared__ double red[5 * 16];
     __shared__ double s_R[4], s_t[2];
     __shared__ int s_stop;
     __shared__ int s_cstart[kIcpGrid * kIcpGrid + 1];
     __shared__ int s_cfill[kIcpGrid * kIcpGrid];
     __shared__ int16_t s_cidx[kIcpMaxP];
+    __shared__ double2 s_tsort[kIcpMaxP];   // targets in cell order
     __shared__ IcpGrid s_g;
 
     const int b = blockIdx.x;
@@ -185,37 +215,85 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
         s_cidx[atomicAdd(&s_cfill[cell], 1)] = (int16_t)k;
     }
     __syncthreads();
+    for (int q = threadIdx.x; q < nt; q += kIcpThreads) s_tsort[q] = s_tgt[s_cidx[q]];
+    __syncthreads();
+#ifdef FS2_PHASE_TIMING
+    unsigned long long t_last = 0;
+#endif
+    // One source point per thread (P <= kIcpThreads).  The point's nearest
+    // neighbour and its centroid / covariance terms stay in registers, so an
+    // iteration needs three barriers: centroid partials, covariance partials,
+    // and thread 0's transform.  Sums follow the same fixed tree as block_sum5.
+    static_assert(kIcpMaxP <= kIcpThreads, "one source point per thread");
+    __shared__ double red2[5 * 16];
+    const int k = threadIdx.x, wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     while (it < max_iter) {
         ++it;
-        // nearest neighbours
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
+        ICP_T(0);
+        // nearest neighbour (icp.py:36) and the centroid terms
+        double v[5] = {0, 0, 0, 0, 0};
+        double2 sp = make_double2(0.0, 0.0), tp = make_double2(0.0, 0.0);
+        if (k < P) {
             double best;
             int bj;
-            icp_nearest(s_src[k], grid, s_cstart, s_cidx, s_tgt, bj, best);
-            s_nn[k] = bj;
-            s_dist[k] = sqrt(best);
+            sp = s_src[k];
+            icp_nearest(sp, grid, s_cstart, s_cidx, s_tsort, bj, best);
+            tp = s_tgt[bj];
+            v[0] = 0.0 + sp.x; v[1] = 0.0 + sp.y; v[2] = 0.0 + tp.x; v[3] = 0.0 + tp.y; v[4] = 0.0 + sqrt(best);
+        }
+        ICP_T(1);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) red[q * 16 + wid] = v[q];
         }
         __syncthreads();
-        // centroids and mean distance
-        double v[5] = {0, 0, 0, 0, 0};
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k], tp = s_tgt[s_nn[k]];
-            v[0] += sp.x; v[1] += sp.y; v[2] += tp.x; v[3] += tp.y; v[4] += s_dist[k];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < kIcpThreads / 64; ++w) t += red[q * 16 + w];
+            v[q] = t;
         }
-        block_sum5<kIcpThreads>(v, red);
         const double cs0 = v[0] / P, cs1 = v[1] / P, ct0 = v[2] / P, ct1 = v[3] / P;
         const double mean = v[4] / P;
-        // cross-covariance of the centred sets (icp.py:73)
-        double h[5] = {0, 0, 0, 0, 0};
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k], tp = s_tgt[s_nn[k]];
+        ICP_T(2);
+        // cross-covariance of the centred sets (icp.py:73), summed for thread 0
+        double h[4] = {0, 0, 0, 0};
+        if (k < P) {
             const double a0 = sp.x - cs0, a1 = sp.y - cs1, b0 = tp.x - ct0, b1 = tp.y - ct1;
-            h[0] += a0 * b0; h[1] += a0 * b1; h[2] += a1 * b0; h[3] += a1 * b1;
+            h[0] = 0.0 + a0 * b0; h[1] = 0.0 + a0 * b1; h[2] = 0.0 + a1 * b0; h[3] = 0.0 + a1 * b1;
         }
-        block_sum5<kIcpThreads>(h, red);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[q] = wave_sum(h[q]);
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red2[q * 16 + wid] = h[q];
+        }
+        __syncthreads();
         if (threadIdx.x == 0) {
-            const double th = atan2(h[1] - h[2], h[0] + h[3]);
-            const double c = cos(th), s = sin(th);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                double t = 0.0;
+#pragma unroll
+                for (int w = 0; w < kIcpThreads / 64; ++w) t += red2[q * 16 + w];
+                h[q] = t;
+            }
+            // rotation angle th = atan2(y, x) of the 2-D Kabsch solution: cos and
+            // sin directly as x / r, y / r (the trigonometric form only where r
+            // is 0 or not finite)
+            const double x = h[0] + h[3], y = h[1] - h[2];
+            const double r = sqrt(x * x + y * y);
+            double c, s;
+            if (r > 0.0 && r < INFINITY) {
+                c = x / r;
+                s = y / r;
+            } else {
+                const double th = atan2(y, x);
+                c = cos(th);
+                s = sin(th);
+            }
             const M2 Ri{c, -s, s, c};
             const double t0 = ct0 - fma(Ri.a00, cs0, Ri.a01 * cs1);
             const double t1 = ct1 - fma(Ri.a10, cs0, Ri.a11 * cs1);
@@ -224,11 +302,11 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
             s_stop = fabs(prev - mean) < thr ? 1 : 0;
         }
         __syncthreads();
+        ICP_T(3);
+        // every reader of red / red2 / s_R has passed the barrier above before
+        // the next iteration writes them (each thread moves only its own point)
         const double r00 = s_R[0], r01 = s_R[1], r10 = s_R[2], r11 = s_R[3], t0 = s_t[0], t1 = s_t[1];
-        for (int k = threadIdx.x; k < P; k += kIcpThreads) {
-            const double2 sp = s_src[k];
-            s_src[k] = make_double2(fma(sp.y, r01, sp.x * r00) + t0, fma(sp.y, r11, sp.x * r10) + t1);
-        }
+        if (k < P) s_src[k] = make_double2(fma(sp.y, r01, sp.x * r00) + t0, fma(sp.y, r11, sp.x * r10) + t1);
         const M2 Rn = mm2(M2{r00, r01, r10, r11}, M2{Rt[0], Rt[1], Rt[2], Rt[3]});
         Rt[0] = Rn.a00; Rt[1] = Rn.a01; Rt[2] = Rn.a10; Rt[3] = Rn.a11;
         const double nt0 = fma(r00, tt[0], r01 * tt[1]) + t0;
@@ -237,7 +315,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
         tt[1] = nt1;
         const int stop = s_stop;
         prev = mean;
-        __syncthreads();
+        ICP_T(4);
         if (stop) break;
     }
     if (threadIdx.x == 0) {

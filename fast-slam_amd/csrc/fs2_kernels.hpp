@@ -261,6 +261,7 @@ hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, De
 
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset);
+hipError_t debug_icp_phase_times(unsigned long long out[4], int reset);
 #endif
 // particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
 // alloc.rbase + p * lm_cap + j
