@@ -180,8 +180,9 @@ int fs2_get_profile(const fs2_handle *h, fs2_profile *out);
 
 /* ------------------------------------------------------ stateless helpers ---- */
 
-/* Replaces ICP.get_transformation (algorithms/icp.py:13-57): brute-force
- * nearest neighbour (lowest index on ties), closed-form 2-D Kabsch, stop when
+/* Replaces ICP.get_transformation (algorithms/icp.py:13-57): exact nearest
+ * neighbour (the brute-force / KD-tree result, lowest index on ties, through a
+ * uniform grid over the target cloud), closed-form 2-D Kabsch, stop when
  * |prev - mean NN distance| < threshold.  R: 2x2 row-major, t: 2. */
 int fs2_icp(int32_t device, const double *src, int32_t n_src, const double *tgt,
             int32_t n_tgt, int32_t max_iterations, double threshold, double R[4],
