@@ -13,6 +13,27 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// fp64 wave sum through DPP row shifts and row broadcasts (no LDS traffic):
+// lane 63 collects ((row 0 + row 1) + (row 2 + row 3)) of adjacent-first pair
+// sums, then every lane reads it.  A fixed tree, so the result is deterministic.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v += dpp_f64<0x111, 0xf>(v);     // row_shr:1
+    v += dpp_f64<0x112, 0xf>(v);     // row_shr:2
+    v += dpp_f64<0x114, 0xf>(v);     // row_shr:4
+    v += dpp_f64<0x118, 0xf>(v);     // row_shr:8  (lane 15 of each row: the row's sum)
+    v += dpp_f64<0x142, 0xa>(v);     // row_bcast:15 into rows 1 and 3
+    v += dpp_f64<0x143, 0xc>(v);     // row_bcast:31 into rows 2 and 3 (lane 63: the wave's sum)
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+    return __hiloint2double(hi, lo);
+}
+
 // ------------------------------------------------------------------- ICP ---
 //
 // One workgroup per alignment; the target cloud and the moving source cloud
@@ -243,7 +264,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
         }
         ICP_T(1);
 #pragma unroll
-        for (int q = 0; q < 5; ++q) v[q] = wave_sum(v[q]);
+        for (int q = 0; q < 5; ++q) v[q] = wave_sum_dpp(v[q]);
         if (lane == 0) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) red[q * 16 + wid] = v[q];
@@ -266,7 +287,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
             h[0] = 0.0 + a0 * b0; h[1] = 0.0 + a0 * b1; h[2] = 0.0 + a1 * b0; h[3] = 0.0 + a1 * b1;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) h[q] = wave_sum(h[q]);
+        for (int q = 0; q < 4; ++q) h[q] = wave_sum_dpp(h[q]);
         if (lane == 0) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) red2[q * 16 + wid] = h[q];
