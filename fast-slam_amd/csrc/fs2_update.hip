@@ -650,15 +650,22 @@ __device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k
     }
 }
 
-// Weight total (Python builtin sum in particle order in sequential mode) and the
-// update pass's block counters folded into the scan statistics.
+// Weight total (Python builtin sum in particle order in sequential mode) in
+// workgroup 0, and the update pass's block counters folded into the scan
+// statistics by workgroups 1 .. kWsumCounterBlocks, each over a slice of the
+// columns (atomics into DevStats: integer sums, order-free), in parallel.
+constexpr int kWsumCounterBlocks = 8;
+
 __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
     __shared__ double lds[16];
     __shared__ unsigned long long s_c[16][kNumCounters];
-    {
-        // every counter column at once: independent loads, one LDS exchange
+    if (blockIdx.x > 0) {
+        const int cb = blockIdx.x - 1;
+        const int per = (P.nwpart + kWsumCounterBlocks - 1) / kWsumCounterBlocks;
+        const int b0 = cb * per, b1 = min(P.nwpart, b0 + per);
+        // every counter column of the slice at once: independent loads, one LDS exchange
         unsigned long long v[kNumCounters] = {};
-        for (int b = threadIdx.x; b < P.nwpart; b += 1024) {
+        for (int b = b0 + threadIdx.x; b < b1; b += 1024) {
 #pragma unroll
             for (int k = 0; k < kNumCounters; ++k) v[k] += P.cpart[(int64_t)k * P.nwpart + b];
         }
@@ -680,6 +687,7 @@ __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
                 atomicAdd(counter_field(P.stats, k), t);
             }
         }
+        return;
     }
     if (P.sequential) {
         if (threadIdx.x == 0) {
@@ -696,14 +704,14 @@ __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
 }
 
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_wsum, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(k_wsum, dim3(1 + kWsumCounterBlocks), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
-    __shared__ double lds_d[kBlock / 64];
-    __shared__ int64_t lds_l[kBlock / 64];
-    __shared__ int lds_i[kBlock / 64];
+    __shared__ double s_sq[kBlock / 64], s_bv[kBlock / 64];
+    __shared__ int64_t s_bi[kBlock / 64];
+    __shared__ int s_mc[kBlock / 64];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool live = i < P.n;
     const double total = P.stats->total;
@@ -716,16 +724,36 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
         else w = (w < P.floor) ? w : w / total;
         P.w[i] = w;
     }
-    const double sq = block_sum<kBlock>(live ? w * w : 0.0, lds_d);
+    // block_sum / block_argmax / block_max_i (same trees) with one barrier
+    const double sq = wave_sum(live ? w * w : 0.0);
     double bv = live ? w : -INFINITY;
     int64_t bi = live ? i : INT64_MAX;
-    block_argmax<kBlock>(bv, bi, lds_d, lds_l);
-    const int mc = block_max_i<kBlock>(c, lds_i);
+    wave_argmax(bv, bi);
+    const int mc = wave_max_i(c);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        s_sq[wid] = sq;
+        s_bv[wid] = bv;
+        s_bi[wid] = bi;
+        s_mc[wid] = mc;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        P.part_sq[blockIdx.x] = sq;
-        P.part_best_w[blockIdx.x] = bv;
-        P.part_best_i[blockIdx.x] = bi;
-        P.part_maxcnt[blockIdx.x] = mc;
+        double t = 0.0;
+        double v = s_bv[0];
+        int64_t ix = s_bi[0];
+        int m = s_mc[0];
+#pragma unroll
+        for (int k = 0; k < kBlock / 64; ++k) t += s_sq[k];
+#pragma unroll
+        for (int k = 1; k < kBlock / 64; ++k) {
+            argmax_combine(v, ix, s_bv[k], s_bi[k]);
+            m = max(m, s_mc[k]);
+        }
+        P.part_sq[blockIdx.x] = t;
+        P.part_best_w[blockIdx.x] = v;
+        P.part_best_i[blockIdx.x] = ix;
+        P.part_maxcnt[blockIdx.x] = m;
     }
 }
 
