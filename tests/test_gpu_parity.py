@@ -571,3 +571,36 @@ def test_gate_band_boundaries(fs):
         assert np.array_equal(s0[4], o.cnt)
         for f in fl:
             f.close()
+
+
+def test_linalg_error_then_recover(fs):
+    """A singular landmark covariance raises numpy.linalg.LinAlgError, as the
+    reference's np.linalg.inv does (geometry_utils.py:21); after set_state the
+    next scans match the oracle, and their statistics start clean (the failed
+    scan's counters do not leak into the published stats)."""
+    import fs2_synthetic as syn
+    from oracle import oracle as orc
+    N, L = 512, 12
+    wl = syn.Workload(N, L, seed=8)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    bad = lm.copy()
+    bad[:, 3, 2:6] = 0.0                         # landmark 3 singular in every map
+    f = fs.FastSLAM2(N, reduce="parallel", record_assoc=True, verbose=False)
+    f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), bad)
+    rng = np.random.default_rng(3)
+    with pytest.raises(np.linalg.LinAlgError):   # the miss measurement scans every slot
+        f.step(0.0, 0.03, wl.measurements(0), None, rng.normal(0, 0.0055, N), 0.3 / N)
+    f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, L + 8)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    for s in range(2):
+        ms = wl.measurements(s + 1)
+        nz = rng.normal(0, 0.0055, N)
+        pose, st = f.step(0.0, 0.03, ms, None, nz, 0.3 / N)
+        opose, oassoc, _, _ = o.iterate(0.0, 0.03, ms, nz, 0.3 / N)
+        assert np.array_equal(f.associations(), oassoc), s
+        assert np.allclose(pose, opose, rtol=RTOL, atol=1e-12), s
+        assert st.appends == int((oassoc == -1).sum()), s
+        assert st.hits == int((oassoc >= 0).sum()), s
+    f.close()
