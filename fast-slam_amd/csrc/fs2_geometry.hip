@@ -168,19 +168,20 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
     __shared__ IcpGrid s_g;
 
     const int b = blockIdx.x;
+    const int nth = blockDim.x, nw = nth >> 6;   // launch_icp: one thread per source point, whole waves
     const double2 *src = reinterpret_cast<const double2 *>(src_all) + (int64_t)b * P;
     const double2 *tgt = reinterpret_cast<const double2 *>(tgt_all) + (int64_t)b * nt;
-    for (int k = threadIdx.x; k < P; k += kIcpThreads) s_src[k] = src[k];
-    for (int k = threadIdx.x; k < nt; k += kIcpThreads) s_tgt[k] = tgt[k];
+    for (int k = threadIdx.x; k < P; k += nth) s_src[k] = src[k];
+    for (int k = threadIdx.x; k < nt; k += nth) s_tgt[k] = tgt[k];
     double Rt[4] = {1.0, 0.0, 0.0, 1.0}, tt[2] = {0.0, 0.0};
     double prev = INFINITY;
     int it = 0;
     // ---- grid over the target cloud (fixed for the whole alignment) ----
-    for (int k = threadIdx.x; k < kIcpGrid * kIcpGrid; k += kIcpThreads) s_cfill[k] = 0;
+    for (int k = threadIdx.x; k < kIcpGrid * kIcpGrid; k += nth) s_cfill[k] = 0;
     __syncthreads();
     {
         double v[5] = {INFINITY, INFINITY, INFINITY, INFINITY, 0.0};   // min x, min y, -max x, -max y
-        for (int k = threadIdx.x; k < nt; k += kIcpThreads) {
+        for (int k = threadIdx.x; k < nt; k += nth) {
             const double2 tp = s_tgt[k];
             v[0] = fmin(v[0], tp.x); v[1] = fmin(v[1], tp.y);
             v[2] = fmin(v[2], -tp.x); v[3] = fmin(v[3], -tp.y);
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
             double m[4];
             for (int q = 0; q < 4; ++q) {
                 m[q] = red[q * 16];
-                for (int k = 1; k < kIcpThreads / 64; ++k) m[q] = fmin(m[q], red[q * 16 + k]);
+                for (int k = 1; k < nw; ++k) m[q] = fmin(m[q], red[q * 16 + k]);
             }
             IcpGrid g;
             const bool ok = isfinite(m[0]) && isfinite(m[1]) && isfinite(m[2]) && isfinite(m[3]);
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
         __syncthreads();
     }
     const IcpGrid grid = s_g;
-    for (int k = threadIdx.x; k < nt; k += kIcpThreads) {
+    for (int k = threadIdx.x; k < nt; k += nth) {
         const double2 tp = s_tgt[k];
         atomicAdd(&s_cfill[icp_cell(tp.y, grid.y0, grid.ihy) * kIcpGrid + icp_cell(tp.x, grid.x0, grid.ihx)], 1);
     }
@@ -230,23 +231,23 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
         s_cstart[kIcpGrid * kIcpGrid] = run;
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < nt; k += kIcpThreads) {
+    for (int k = threadIdx.x; k < nt; k += nth) {
         const double2 tp = s_tgt[k];
         const int cell = icp_cell(tp.y, grid.y0, grid.ihy) * kIcpGrid + icp_cell(tp.x, grid.x0, grid.ihx);
         s_cidx[atomicAdd(&s_cfill[cell], 1)] = (int16_t)k;
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < nt; q += kIcpThreads) s_tsort[q] = s_tgt[s_cidx[q]];
+    for (int q = threadIdx.x; q < nt; q += nth) s_tsort[q] = s_tgt[s_cidx[q]];
     __syncthreads();
 #ifdef FS2_PHASE_TIMING
     unsigned long long t_last = 0;
 #endif
-    // One source point per thread (P <= kIcpThreads).  The point's nearest
-    // neighbour and its centroid / covariance terms stay in registers, so an
-    // iteration needs three barriers: centroid partials, covariance partials,
-    // and thread 0's transform.  Sums follow the same fixed tree as block_sum5.
-    static_assert(kIcpMaxP <= kIcpThreads, "one source point per thread");
+    // One source point per thread (the block has ceil(P / 64) waves).  The
+    // point's nearest neighbour and its centroid / covariance terms stay in
+    // registers; the per-wave partials are added up once, by lanes of wave 0
+    // (one lane per sum), not by every thread.
     __shared__ double red2[5 * 16];
+    __shared__ double s_cen[5];
     const int k = threadIdx.x, wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     while (it < max_iter) {
         ++it;
@@ -270,15 +271,15 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
             for (int q = 0; q < 5; ++q) red[q * 16 + wid] = v[q];
         }
         __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
+        if (threadIdx.x < 5) {
+            const int q = threadIdx.x;
             double t = 0.0;
-#pragma unroll
-            for (int w = 0; w < kIcpThreads / 64; ++w) t += red[q * 16 + w];
-            v[q] = t;
+            for (int w = 0; w < nw; ++w) t += red[q * 16 + w];
+            s_cen[q] = t / P;
         }
-        const double cs0 = v[0] / P, cs1 = v[1] / P, ct0 = v[2] / P, ct1 = v[3] / P;
-        const double mean = v[4] / P;
+        __syncthreads();
+        const double cs0 = s_cen[0], cs1 = s_cen[1], ct0 = s_cen[2], ct1 = s_cen[3];
+        const double mean = s_cen[4];
         ICP_T(2);
         // cross-covariance of the centred sets (icp.py:73), summed for thread 0
         double h[4] = {0, 0, 0, 0};
@@ -293,14 +294,14 @@ __global__ __launch_bounds__(kIcpThreads) void k_icp(int32_t P, const double *sr
             for (int q = 0; q < 4; ++q) red2[q * 16 + wid] = h[q];
         }
         __syncthreads();
+        if (wid == 0) {
+            double t = 0.0;
+            if (lane < 4)
+                for (int w = 0; w < nw; ++w) t += red2[lane * 16 + w];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) h[q] = __shfl(t, q, 64);
+        }
         if (threadIdx.x == 0) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                double t = 0.0;
-#pragma unroll
-                for (int w = 0; w < kIcpThreads / 64; ++w) t += red2[q * 16 + w];
-                h[q] = t;
-            }
             // rotation angle th = atan2(y, x) of the 2-D Kabsch solution: cos and
             // sin directly as x / r, y / r (the trigonometric form only where r
             // is 0 or not finite)
@@ -351,7 +352,8 @@ hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt
                       int32_t max_iter, double thr, double *R, double *t, int32_t *iters,
                       hipStream_t s) {
     if (P > kIcpMaxP || n_tgt > kIcpMaxP) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_icp, dim3(B), dim3(kIcpThreads), 0, s, P, src, tgt, n_tgt, max_iter, thr,
+    const int nth = std::max(64, (P + 63) / 64 * 64);     // one thread per source point
+    hipLaunchKernelGGL(k_icp, dim3(B), dim3(nth), 0, s, P, src, tgt, n_tgt, max_iter, thr,
                        R, t, iters);
     return hipGetLastError();
 }
