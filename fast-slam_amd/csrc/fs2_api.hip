@@ -1229,6 +1229,110 @@ int fs2_icp(int32_t device, const double *src, int32_t n_src, const double *tgt,
     return FS2_OK;
 }
 
+}  // extern "C"
+
+// --------------------------------------------------------- pipelined ICP ---
+// fs2_icp_submit / fs2_icp_wait: the same alignment as fs2_icp, enqueued on a
+// per-device stream of its own, so that scan s+1's alignment (one workgroup)
+// runs beside scan s's filter update, which fills the rest of the GPU.  Each
+// ticket owns a slot: pinned host staging for the clouds and the result, device
+// buffers, and an event; the caller's arrays are copied at submit time.
+
+namespace {
+
+constexpr int kIcpSlots = 4;          // FS2_ICP_SLOTS in fs2.h
+constexpr size_t kIcpCloud = 1024 * 16;
+
+struct IcpSlot {
+    char *host = nullptr;             // pinned: src, tgt, out (R, t, iterations)
+    char *dev = nullptr;
+    hipEvent_t done = nullptr;
+    int64_t ticket = -1;              // outstanding ticket, -1 when free
+};
+
+struct IcpQueue {
+    hipStream_t stream = nullptr;
+    IcpSlot slot[kIcpSlots];
+    int64_t next = 0;
+};
+
+std::mutex g_icpq_mu;
+IcpQueue g_icpq[64];
+
+int icpq_get(int32_t device, IcpQueue **out) {
+    if (device < 0 || device >= 64) return set_err(nullptr, FS2_ERR_ARG, "bad device %d", device);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev)
+        return set_err(nullptr, FS2_ERR_HIP, "no HIP device %d (libfs2 has no CPU path)", device);
+    SHIP(hipSetDevice(device));
+    IcpQueue &q = g_icpq[device];
+    if (!q.stream) {
+        SHIP(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+        for (IcpSlot &s : q.slot) {
+            SHIP(hipHostMalloc((void **)&s.host, 2 * kIcpCloud + 64, hipHostMallocDefault));
+            SHIP(hipMalloc(&s.dev, 2 * kIcpCloud + 64));
+            SHIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        }
+    }
+    *out = &q;
+    return FS2_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fs2_icp_submit(int32_t device, const double *src, int32_t n_src, const double *tgt, int32_t n_tgt,
+                   int32_t max_iterations, double threshold, int64_t *ticket) {
+    if (n_src <= 0 || n_tgt <= 0 || n_src > 1024 || n_tgt > 1024 || !src || !tgt || !ticket)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_icp_submit: bad arguments (point counts must be 1..1024)");
+    std::lock_guard<std::mutex> lk(g_icpq_mu);
+    IcpQueue *q = nullptr;
+    int rc = icpq_get(device, &q);
+    if (rc) return rc;
+    IcpSlot &s = q->slot[q->next % kIcpSlots];
+    if (s.ticket >= 0)
+        return set_err(nullptr, FS2_ERR_STATE, "fs2_icp_submit: %d alignments already outstanding on device %d",
+                       kIcpSlots, device);
+    // the slot's previous alignment has been waited on, so its buffers are free
+    std::memcpy(s.host, src, (size_t)n_src * 16);
+    std::memcpy(s.host + kIcpCloud, tgt, (size_t)n_tgt * 16);
+    double *ds = (double *)s.dev, *dt = (double *)(s.dev + kIcpCloud);
+    double *dR = (double *)(s.dev + 2 * kIcpCloud), *dT = dR + 4;
+    int32_t *dI = (int32_t *)(dT + 2);
+    SHIP(hipMemcpyAsync(ds, s.host, (size_t)n_src * 16, hipMemcpyHostToDevice, q->stream));
+    SHIP(hipMemcpyAsync(dt, s.host + kIcpCloud, (size_t)n_tgt * 16, hipMemcpyHostToDevice, q->stream));
+    SHIP(launch_icp(1, n_src, ds, dt, n_tgt, max_iterations, threshold, dR, dT, dI, q->stream));
+    SHIP(hipMemcpyAsync(s.host + 2 * kIcpCloud, dR, 52, hipMemcpyDeviceToHost, q->stream));
+    SHIP(hipEventRecord(s.done, q->stream));
+    s.ticket = q->next++;
+    *ticket = s.ticket;
+    return FS2_OK;
+}
+
+int fs2_icp_wait(int32_t device, int64_t ticket, double R[4], double t[2], int32_t *iterations) {
+    if (!R || !t || ticket < 0) return set_err(nullptr, FS2_ERR_ARG, "fs2_icp_wait: bad arguments");
+    IcpSlot *s = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_icpq_mu);
+        if (device < 0 || device >= 64 || !g_icpq[device].stream)
+            return set_err(nullptr, FS2_ERR_STATE, "fs2_icp_wait: nothing submitted on device %d", device);
+        s = &g_icpq[device].slot[ticket % kIcpSlots];
+        if (s->ticket != ticket)
+            return set_err(nullptr, FS2_ERR_STATE, "fs2_icp_wait: ticket %lld is not outstanding",
+                           (long long)ticket);
+    }
+    SHIP(hipEventSynchronize(s->done));
+    const double *out = (const double *)(s->host + 2 * kIcpCloud);
+    std::memcpy(R, out, 32);
+    t[0] = out[4];
+    t[1] = out[5];
+    if (iterations) std::memcpy(iterations, out + 6, 4);
+    std::lock_guard<std::mutex> lk(g_icpq_mu);
+    s->ticket = -1;
+    return FS2_OK;
+}
+
 int fs2_best_fit_transform(int32_t device, const double *src, const double *tgt, int32_t n, double R[4],
                            double t[2]) {
     if (n <= 0 || !src || !tgt || !R || !t) return set_err(nullptr, FS2_ERR_ARG, "fs2_best_fit_transform: bad arguments");

@@ -138,6 +138,9 @@ SIGNATURES = [
     ("fs2_get_profile", C.c_int, [_H, C.POINTER(fs2_profile)]),
     ("fs2_icp", C.c_int, [C.c_int32, _dp, C.c_int32, _dp, C.c_int32, C.c_int32, C.c_double, _dp,
                           _dp, _ip]),
+    ("fs2_icp_submit", C.c_int, [C.c_int32, _dp, C.c_int32, _dp, C.c_int32, C.c_int32, C.c_double,
+                                 C.POINTER(C.c_int64)]),
+    ("fs2_icp_wait", C.c_int, [C.c_int32, C.c_int64, _dp, _dp, _ip]),
     ("fs2_icp_batched", C.c_int, [C.c_int32, C.c_int32, C.c_int32, _vp, _vp, C.c_int32,
                                   C.c_double, _vp, _vp, _vp, C.c_int32]),
     ("fs2_best_fit_transform", C.c_int, [C.c_int32, _dp, _dp, C.c_int32, _dp, _dp]),

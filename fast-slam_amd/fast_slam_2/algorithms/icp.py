@@ -39,6 +39,19 @@ class ICP:
         return R.reshape(2, 2), t, int(it.value)
 
     @staticmethod
+    def submit(source_points, target_points, max_iterations=100, threshold=1e-5) -> "IcpTicket":
+        """Enqueue get_transformation on the device's ICP stream and return at once;
+        ``.result()`` gives (R, t, iterations).  Lets the alignment of scan s+1 run
+        beside the filter update of scan s (fs2_icp_submit in include/fs2.h)."""
+        src = nat.f64(source_points, (-1, 2))
+        tgt = nat.f64(target_points, (-1, 2))
+        tk = C.c_int64()
+        nat.check(nat.load().fs2_icp_submit(ICP.device, nat.dptr(src), len(src), nat.dptr(tgt),
+                                            len(tgt), int(max_iterations), float(threshold),
+                                            C.byref(tk)))
+        return IcpTicket(ICP.device, tk.value)
+
+    @staticmethod
     def get_transformation_batched(sources, targets, max_iterations=100, threshold=1e-5):
         """B independent alignments: sources/targets [B][P][2] -> R [B][2][2], t [B][2], iters [B]."""
         src = nat.f64(sources)
@@ -61,3 +74,22 @@ class ICP:
         nat.check(nat.load().fs2_best_fit_transform(ICP.device, nat.dptr(src), nat.dptr(tgt),
                                                     len(src), nat.dptr(R), nat.dptr(t)))
         return R.reshape(2, 2), t
+
+
+class IcpTicket:
+    """An alignment enqueued by ICP.submit; result() waits for it once."""
+
+    def __init__(self, device, ticket):
+        self.device = device
+        self.ticket = ticket
+        self._out = None
+
+    def result(self):
+        if self._out is None:
+            R = np.empty(4)
+            t = np.empty(2)
+            it = C.c_int32()
+            nat.check(nat.load().fs2_icp_wait(self.device, self.ticket, nat.dptr(R), nat.dptr(t),
+                                              C.byref(it)))
+            self._out = (R.reshape(2, 2), t, int(it.value))
+        return self._out

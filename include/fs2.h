@@ -188,6 +188,18 @@ int fs2_icp(int32_t device, const double *src, int32_t n_src, const double *tgt,
             int32_t n_tgt, int32_t max_iterations, double threshold, double R[4],
             double t[2], int32_t *iterations);
 
+/* fs2_icp split in two for pipelining (Robot.get_transformation_icp,
+ * robot.py:108-120, aligns scan s+1 to scan s; the alignment of the next scan
+ * can run beside the filter update of this one): fs2_icp_submit copies the
+ * clouds and enqueues the alignment on the device's ICP stream; fs2_icp_wait
+ * blocks until ticket's alignment is done and returns fs2_icp's outputs.  At
+ * most FS2_ICP_SLOTS tickets may be outstanding per device (FS2_ERR_STATE
+ * beyond that, or for a ticket that is not outstanding). */
+#define FS2_ICP_SLOTS 4
+int fs2_icp_submit(int32_t device, const double *src, int32_t n_src, const double *tgt,
+                   int32_t n_tgt, int32_t max_iterations, double threshold, int64_t *ticket);
+int fs2_icp_wait(int32_t device, int64_t ticket, double R[4], double t[2], int32_t *iterations);
+
 /* B independent alignments of P points each (src/tgt [B][P][2]); R [B][4],
  * t [B][2], iterations [B] (nullable).  where: FS2_HOST or FS2_DEVICE. */
 int fs2_icp_batched(int32_t device, int32_t B, int32_t P, const double *src,

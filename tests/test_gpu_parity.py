@@ -111,6 +111,31 @@ def test_icp_batched_matches_single(fs):
         assert np.allclose(t[b], d["t"][k], atol=1e-10)
 
 
+def test_icp_submit_wait(fs):
+    """The pipelined form (fs2_icp_submit / fs2_icp_wait) returns the golden
+    alignments, out of order too; a fifth outstanding ticket and a ticket that
+    is not outstanding are refused."""
+    cases = list(_icp_cases())
+    for lo in range(0, len(cases), 4):
+        group = cases[lo:lo + 4]
+        tickets = [fs.ICP.submit(src, tgt) for _, src, tgt, _ in group]
+        # the caller's arrays may change once submit returns
+        for _, src, tgt, _ in group:
+            src[:] = np.nan
+            tgt[:] = np.nan
+        if len(group) == 4:
+            with pytest.raises(RuntimeError):
+                fs.ICP.submit(np.zeros((8, 2)), np.zeros((8, 2)))
+        for (k, _, _, d), tk in reversed(list(zip(group, tickets))):
+            R, t, it = tk.result()
+            assert it == d["iters"][k], (k, it)
+            assert np.allclose(R, d["R"][k], atol=1e-10)
+            assert np.allclose(t, d["t"][k], atol=1e-10)
+    from fast_slam_2 import _native as nat
+    R, t = np.empty(4), np.empty(2)
+    assert nat.load().fs2_icp_wait(0, tickets[0].ticket, nat.dptr(R), nat.dptr(t), None) == nat.FS2_ERR_STATE
+
+
 @pytest.mark.parametrize("name", SEQS)
 def test_sequence_golden(fs, name):
     from gpu_util import close, from_fixture
