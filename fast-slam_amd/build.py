@@ -51,6 +51,26 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     return lib
 
 
+HOOKS = os.path.join(LIB_DIR, "libfs2_hooks.so")
+
+
+def build_hooks(verbose: bool = False) -> str:
+    """libfs2_hooks.so: fs2_pages.hip alone with -DFS2_TEST_HOOKS (test entry points
+    of single kernels; the GPU tests load it beside libfs2.so)."""
+    src = os.path.join(CSRC, "fs2_pages.hip")
+    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")]
+    if os.path.exists(HOOKS) and os.path.getmtime(HOOKS) >= max(os.path.getmtime(d) for d in deps):
+        return HOOKS
+    cmd = [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+           "-shared", "-ffp-contract=off", "-DFS2_TEST_HOOKS", "-I", os.path.join(ROCM, "include"),
+           src, "-o", HOOKS + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(HOOKS + ".tmp", HOOKS)
+    return HOOKS
+
+
 if __name__ == "__main__":
     # python build.py [--force] [--variant TAG -DNAME=V ...]  (variant -> lib/libfs2_TAG.so)
     args = sys.argv[1:]
@@ -58,3 +78,5 @@ if __name__ == "__main__":
     defs = [a for a in args if a.startswith("-D")]
     out = os.path.join(LIB_DIR, f"libfs2_{tag}.so") if tag else None
     print(build(force="--force" in args, verbose=True, defines=defs, out=out))
+    if not tag:
+        print(build_hooks(verbose=True))

@@ -11,7 +11,7 @@
 //
 //   k_mark        one lane per particle, one byte store per page of its map
 //   k_sweep_count free pages per 4096-page block
-//   k_sweep_scan  exclusive scan of the block counts (one workgroup)
+//   k_sweep_scan  exclusive scan of the block counts (one workgroup, 8192-count tiles)
 //   k_sweep_write free page ids, in id order, into freel (staged in LDS, stored contiguously)
 //
 // Slot records (fs2_kernels.hpp) are collected the same way, less often (the
@@ -103,41 +103,48 @@ __global__ __launch_bounds__(kBlock) void k_sweep_count(const uint8_t *mark, int
     if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
 }
 
-// exclusive scan of the block counts in place; *nfree = total.  Each thread
-// owns a contiguous run of blocks, read 4 at a time.
+// exclusive scan of the block counts in place; *nfree = total.  Tiles of
+// 1024 x 8 counts: each thread loads 8 consecutive counts of the tile at once
+// (independent loads, one memory latency per tile), the workgroup scans their
+// sums, and a running carry joins the tiles.
+constexpr int kScanPer = 8;
 __global__ __launch_bounds__(1024) void k_sweep_scan(int64_t *bcnt, int64_t nb, int64_t *nfree) {
     __shared__ int64_t lds[1024 / 64];
-    const int64_t per = (nb + 1023) / 1024;
-    const int64_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
-    int64_t s = 0;
-    for (int64_t k = b0; k < b1; k += 4) {
-        int64_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = (k + u < b1) ? bcnt[k + u] : 0;
-        s += (v[0] + v[1]) + (v[2] + v[3]);
-    }
-    // inclusive scan of the per-thread sums
-    int64_t v = s;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t carry = 0;
+    for (int64_t base = 0; base < nb; base += 1024 * kScanPer) {
+        const int64_t b0 = base + (int64_t)threadIdx.x * kScanPer;
+        int64_t c[kScanPer];
+        int64_t s = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t o = __shfl_up(v, d, 64);
-        if (lane >= d) v += o;
+        for (int u = 0; u < kScanPer; ++u) {
+            c[u] = (b0 + u < nb) ? bcnt[b0 + u] : 0;
+            s += c[u];
+        }
+        // inclusive scan of the per-thread sums
+        int64_t v = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(v, d, 64);
+            if (lane >= d) v += o;
+        }
+        if (lane == 63) lds[wid] = v;
+        __syncthreads();
+        int64_t off = 0, tot = 0;
+        for (int k = 0; k < 1024 / 64; ++k) {
+            if (k < wid) off += lds[k];
+            tot += lds[k];
+        }
+        int64_t run = carry + off + v - s;
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) {
+            if (b0 + u < nb) bcnt[b0 + u] = run;
+            run += c[u];
+        }
+        carry += tot;
+        __syncthreads();                  // lds is rewritten by the next tile
     }
-    if (lane == 63) lds[wid] = v;
-    __syncthreads();
-    int64_t off = 0, tot = 0;
-    for (int k = 0; k < 1024 / 64; ++k) {
-        if (k < wid) off += lds[k];
-        tot += lds[k];
-    }
-    int64_t run = off + v - s;
-    for (int64_t k = b0; k < b1; ++k) {
-        const int64_t c = bcnt[k];
-        bcnt[k] = run;
-        run += c;
-    }
-    if (threadIdx.x == 0) *nfree = tot;
+    if (threadIdx.x == 0) *nfree = carry;
 }
 
 // The workgroup's free ids, in id order, staged in LDS and stored contiguously
@@ -198,3 +205,22 @@ hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t
 }
 
 }  // namespace fs2
+
+#ifdef FS2_TEST_HOOKS
+// Test hook (tests/test_gpu_parity.py, a separate libfs2_hooks.so built from this
+// file alone): k_sweep_scan on host counts, for block counts past one tile.
+extern "C" int fs2_debug_sweep_scan(int32_t device, int64_t *counts, int64_t nb, int64_t *total) {
+    if (hipSetDevice(device) != hipSuccess) return -2;
+    int64_t *d = nullptr;
+    if (hipMalloc(&d, sizeof(int64_t) * (size_t)(nb + 1)) != hipSuccess) return -3;
+    hipError_t e = hipMemcpy(d, counts, sizeof(int64_t) * (size_t)nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(fs2::k_sweep_scan, dim3(1), dim3(1024), 0, 0, d, nb, d + nb);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(counts, d, sizeof(int64_t) * (size_t)nb, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(total, d + nb, sizeof(int64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? 0 : -2;
+}
+#endif

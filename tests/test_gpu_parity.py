@@ -629,3 +629,21 @@ def test_linalg_error_then_recover(fs):
         assert st.appends == int((oassoc == -1).sum()), s
         assert st.hits == int((oassoc >= 0).sum()), s
     f.close()
+
+
+def test_sweep_scan_tiles(fs):
+    """k_sweep_scan (pool collection's exclusive scan of per-block free counts)
+    across its 8192-count tiles, through libfs2_hooks.so: equal to numpy."""
+    import ctypes as C
+    hooks = os.path.join(os.path.dirname(fs.__file__), "..", "lib", "libfs2_hooks.so")
+    lib = C.CDLL(os.path.abspath(hooks))
+    lib.fs2_debug_sweep_scan.argtypes = [C.c_int32, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+    rng = np.random.default_rng(11)
+    for nb in (1, 7, 1023, 8192, 8193, 34_700, 100_003):
+        cnt = rng.integers(0, 4097, nb).astype(np.int64)
+        cnt[rng.random(nb) < 0.1] = 0
+        out = cnt.copy()
+        tot = C.c_int64(-1)
+        assert lib.fs2_debug_sweep_scan(0, out.ctypes.data, nb, C.byref(tot)) == 0
+        assert tot.value == int(cnt.sum()), nb
+        assert np.array_equal(out, np.concatenate([[0], np.cumsum(cnt)[:-1]])), nb
