@@ -16,8 +16,8 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libfs2.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("FS2_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["fs2_api.hip", "fs2_update.hip", "fs2_resample.hip", "fs2_pages.hip", "fs2_cluster.hip", "fs2_geometry.hip",
-           "fs2_frontend.hip"]
+SOURCES = ["fs2_api.hip", "fs2_update.hip", "fs2_resample.hip", "fs2_exact.hip", "fs2_pages.hip", "fs2_cluster.hip",
+           "fs2_geometry.hip", "fs2_frontend.hip"]
 HEADERS = ["fs2_device.hpp", "fs2_kernels.hpp", "fs2_comm.hpp", "fs2_reduce.hpp", "fs2_frontend.hpp"]
 
 

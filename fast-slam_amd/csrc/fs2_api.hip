@@ -146,13 +146,42 @@ struct fs2_handle {
     std::vector<size_t> sendcap, recvcap;
     int32_t n_recv = 0;                             // particles received by the last resample
 
+    // exact-order reductions (fs2_exact.hip)
+    int32_t *uinfo = nullptr, *uord = nullptr, *seql = nullptr;
+    long long *udelta = nullptr;
+    unsigned long long *ug = nullptr;
+    double *sout = nullptr, *bpre = nullptr, *part_w = nullptr, *np_part = nullptr;
+
     MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
-    bool sequential() const {
+    // the reduction order in force (FS2_REDUCE_*, AUTO resolved)
+    int reduce() const {
         const int mode = cfg.reduce_mode;
-        if (mode == FS2_REDUCE_SEQUENTIAL) return true;
-        if (mode == FS2_REDUCE_PARALLEL) return false;
-        return n_global <= 4096;
+        if (tp) return mode == FS2_REDUCE_SEQUENTIAL ? FS2_REDUCE_SEQUENTIAL : FS2_REDUCE_PARALLEL;
+        if (mode != FS2_REDUCE_AUTO) return mode;
+        return n_global <= 4096 ? FS2_REDUCE_SEQUENTIAL : FS2_REDUCE_EXACT;
+    }
+    ChainParams chain(const double *a, const double *bsum, double *c, double *total, bool lazy) const {
+        ChainParams p{};
+        p.a = a;
+        p.n = n;
+        p.bsum = bsum;
+        p.bpre = bpre;
+        p.nb = (int32_t)nblocks();
+        p.lazy = lazy ? 1 : 0;
+        p.uinfo = uinfo;
+        p.udelta = udelta;
+        p.ug = ug;
+        p.uord = uord;
+        p.seql = seql;
+        p.sout = sout;
+        p.c = c;
+        p.total = total;
+        p.stats = stats_dev;
+        // recursive summation of n terms >= 0: |chain - exact| <= gamma_n exact; the
+        // block estimates add gamma_{n/256 + 30}; doubled, plus slack for the scaling
+        p.margin = std::ldexp(2.0 * (double)n + 8192.0, -53);
+        return p;
     }
 };
 
@@ -423,6 +452,8 @@ static void free_handle(fs2_handle *h) {
     for (char *b : h->sendbuf) hipFree(b);
     for (char *b : h->recvbuf) hipFree(b);
     hipFree(h->cand); hipFree(h->ncand);
+    hipFree(h->uinfo); hipFree(h->uord); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ug);
+    hipFree(h->sout); hipFree(h->bpre); hipFree(h->part_w); hipFree(h->np_part);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -510,6 +541,18 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->cbuf, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->bsum, nsb * 8) == hipSuccess;
     ok &= alloc((void **)&h->stats_dev, sizeof(DevStats)) == hipSuccess;
+    {
+        const int64_t nu = (n + 63) / 64;
+        ok &= alloc((void **)&h->uinfo, nu * 4) == hipSuccess;
+        ok &= alloc((void **)&h->uord, nu * 4) == hipSuccess;
+        ok &= alloc((void **)&h->seql, nu * 4) == hipSuccess;
+        ok &= alloc((void **)&h->udelta, nu * 8) == hipSuccess;
+        ok &= alloc((void **)&h->ug, nu * 8) == hipSuccess;
+        ok &= alloc((void **)&h->sout, nu * 8) == hipSuccess;
+        ok &= alloc((void **)&h->bpre, nb * 8) == hipSuccess;
+        ok &= alloc((void **)&h->part_w, nb * 8) == hipSuccess;
+        ok &= alloc((void **)&h->np_part, np_sumsq_chunks(n) * 8) == hipSuccess;
+    }
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
     ok &= hipHostMalloc((void **)&h->stats_host, sizeof(DevStats), 0) == hipSuccess;
@@ -674,7 +717,12 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     hipStream_t s = h->stream;
     const int G = h->cfg.world_size;
     const bool sh = h->tp != nullptr;             // sharded path (G > 1, or forced for testing)
-    const bool seq = h->sequential() && !sh;      // sharded sums are parallel by nature
+    const int red = h->reduce();
+    const bool seq = red == FS2_REDUCE_SEQUENTIAL && !sh;
+    const bool exact = red == FS2_REDUCE_EXACT;
+    // tree sums: |tree - reference| <= (2n + 64) 2^-53 of the value, for the
+    // total and hence for every normalised weight and prefix
+    const double flip_margin = (red == FS2_REDUCE_PARALLEL) ? std::ldexp(2.0 * (double)h->n_global + 64.0, -53) : 0.0;
     const bool prof = h->profiling;
 
     if (noise) {
@@ -788,6 +836,11 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.nparts = (int32_t)h->nblocks();
     rp.floor = h->cfg.weight_floor;
     rp.sequential = seq ? 1 : 0;
+    rp.exact = exact ? 1 : 0;
+    rp.np_part = h->np_part;
+    rp.n_np = (int32_t)np_sumsq_chunks(h->n);
+    rp.flip_margin = flip_margin;
+    rp.part_w = exact ? h->part_w : nullptr;
     rp.u0_host = u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
@@ -821,9 +874,12 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.part_best_i = h->part_best_i;
     rs.stats = h->stats_dev;
     rs.rec = h->rec;
+    rs.flip_margin = flip_margin;
 
     // weight total over all ranks (fast_slam_2.py:166)
     HIP_TRY(h, launch_wsum(rp, s));
+    // exact: Python's sum (in particle order) from the update pass's block sums
+    if (exact) HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false), s));
     if (sh) {
         rc = h->tp->allgather(&h->stats_dev->total, h->totals, sizeof(double), s, &h->err);
         if (rc) return rc;
@@ -831,6 +887,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     }
     // normalise (:161-175), local prefix of the normalised weights, this rank's record
     HIP_TRY(h, launch_normalize(rp, s));
+    if (exact) HIP_TRY(h, launch_np_sumsq(h->w[cur], h->n, h->np_part, nullptr, s));
     // sharded ranks need their prefix end in the record; one GPU needs the
     // prefix only when the rule fires (computed below, kernels exit otherwise)
     if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
@@ -844,7 +901,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     if (sh) HIP_TRY(h, launch_global_finalize(rp, s));
     if (!sh) {
         rs.lazy = 1;
-        HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+        if (exact)   // the resample's running sum (fast_slam_2.py:184-193), bit-exact
+            HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->part_w, h->cbuf, nullptr, true), s));
+        else
+            HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
     }
 
     // ---- low-variance resample (:177-199); on one GPU the kernels exit unless the
@@ -937,7 +997,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         stats->ambiguous = st.ambiguous;
         stats->resample_slots = st.resample_slots;
         stats->error_flags = st.error_flags;
-        stats->reserved = 0;
+        stats->reduce_ambiguous = (int32_t)std::min<unsigned long long>(st.reduce_amb, INT32_MAX);
         stats->cow_pages = st.cow_pages;
         stats->new_pages = st.new_pages;
         stats->collections = h->collections;

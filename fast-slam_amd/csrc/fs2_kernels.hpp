@@ -78,6 +78,8 @@ struct DevStats {
     int32_t out_min, out_max;   // smallest / largest output index served by a local particle
     int32_t n_recv;          // particles received from other ranks by the resample
     int32_t pad2;
+    unsigned long long reduce_amb;   // tree reductions: resample boundaries / the N_eff rule within
+                                     // the rounding bound of the reference's summation order
 };
 
 // Per-rank record all-gathered once per scan (and once more after a resample).
@@ -186,7 +188,12 @@ struct ReduceParams {
     int32_t *part_maxcnt;
     int32_t nparts;
     double floor;
-    int32_t sequential;
+    int32_t sequential;      // one lane, the reference's orders
+    int32_t exact;           // the reference's orders in parallel (fs2_exact.hip)
+    const double *np_part;   // exact: numpy chunk sums of w'^2 (k_np_sumsq)
+    int32_t n_np;            // their count
+    double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
+    double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
     uint64_t seed, scan;
     DevStats *stats;
@@ -206,6 +213,7 @@ struct ResampleParams {
     double *bsum;            // block sums (prefix)
     int32_t nblk;            // 1024-element blocks
     int32_t lazy;            // prefix kernels run only when the resample rule fired
+    double flip_margin;      // tree prefix: relative rounding bound counted in reduce_amb (0: off)
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
     const double *x, *y, *yaw;
@@ -232,6 +240,31 @@ struct ResampleParams {
     int32_t npeers;
     RecvPeer peers[kMaxRanks];
 };
+
+// The reference's sequential sum / running sum of a[0..n) (a >= 0), in parallel
+// and bit-exactly (fs2_exact.hip): s_0 = a_0, s_k = fl(s_{k-1} + a_k).
+struct ChainParams {
+    const double *a;
+    int64_t n;
+    const double *bsum;      // [nb] sums of 256-element blocks (any order: an estimate)
+    double *bpre;            // [nb] their exclusive prefix (written)
+    int32_t nb;
+    int32_t lazy;            // run only when stats->resampled
+    int32_t *uinfo;          // [nu] per 64-element unit: bit 0 serial, else (binade + 4096) << 1
+    long long *udelta;       // [nu] translation in ulps of the unit's binade
+    unsigned long long *ug;  // [nu] exclusive scan of udelta
+    int32_t *uord;           // [nu] ordinal of the last serial unit <= k
+    int32_t *seql;           // [nu] serial units in order
+    double *sout;            // [nu] chain value after each serial unit (by ordinal)
+    double *c;               // nullable: the chain's values (prefix mode)
+    double *total;           // nullable: the final value
+    const DevStats *stats;
+    double margin;           // relative bound on |estimate - chain| (doubled)
+};
+hipError_t launch_chain(const ChainParams &p, hipStream_t s);
+// numpy np.sum(w ** 2) chunk sums (8192-element buffers), added in order by the caller
+hipError_t launch_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy, hipStream_t s);
+int64_t np_sumsq_chunks(int64_t n);
 
 // ---- launch wrappers (defined in fs2_kernels.hip) ----
 hipError_t launch_candidates(const UpdateParams &p, hipStream_t s);

@@ -92,6 +92,11 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
                 s = (k == 0) ? p : s + p;
             }
             sq = s;
+        } else if (P.exact) {
+            // the same sums, each chunk's tree evaluated by k_np_sumsq
+            double s = 0.0;
+            for (int k = 0; k < P.n_np; ++k) s = (k == 0) ? P.np_part[0] : s + P.np_part[k];
+            sq = s;
         }
         RankRecord r{};
         r.sumsq = sq;
@@ -139,6 +144,9 @@ __device__ void global_finalize_body(const ReduceParams &P) {
     st->sumsq = sq;
     st->n_eff = ne;
     st->resampled = ne < ng / 2.0 ? 1 : 0;
+    // tree sums: a decision this close to the threshold may differ from the
+    // reference's summation order
+    if (P.flip_margin > 0.0 && fabs(ne - ng / 2.0) <= P.flip_margin * ng) st->reduce_amb += 1;
     st->max_count = max(st->max_count, P.recs[P.rank].max_count);
     st->best_index = bi;
     st->best_w = bv;
@@ -352,7 +360,9 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     __shared__ int lds_i[kBlock / 64];
     if (!P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    __shared__ unsigned long long lds_u[kBlock / 64];
     int omin = INT32_MAX, omax = -1;
+    unsigned amb = 0;
     if (i < P.n) {
         const double u0 = P.stats->u0, off = P.stats->offset;
         const int64_t g = P.a + i;
@@ -366,6 +376,14 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         const int64_t hi = (g == P.N - 1) ? P.N - 1 : first_above(cur, u0, P.N) - 1;
         P.mlo[i] = (int32_t)lo;
         P.mhi[i] = (int32_t)hi;
+        // tree prefix: a u_m within the rounding bound of this boundary might fall
+        // on the other side of the reference's sequential value
+        if (P.flip_margin > 0.0 && g != P.N - 1) {
+            const int64_t m1 = hi + 1;                  // first output with u > cur
+            const double tol = P.flip_margin * cur;
+            if ((m1 < P.N && u_of(u0, m1, P.N) - cur <= tol) || (m1 > 0 && cur - u_of(u0, m1 - 1, P.N) <= tol))
+                amb = 1;
+        }
         const int64_t llo = max(lo, P.a), lhi = min(hi, P.a + P.n - 1);
         for (int64_t m = llo; m <= lhi; ++m) P.out_src[m - P.a] = (int32_t)i;
         if (lo <= hi) {
@@ -379,6 +397,10 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     if (threadIdx.x == 0 && bmax >= 0) {
         atomicMin(&P.stats->out_min, bmin);
         atomicMax(&P.stats->out_max, bmax);
+    }
+    if (P.flip_margin > 0.0) {
+        const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
+        if (threadIdx.x == 0 && ba) atomicAdd(&P.stats->reduce_amb, ba);
     }
 }
 

@@ -610,30 +610,6 @@ hipError_t launch_update(const UpdateParams &p, hipStream_t s) {
 
 // ------------------------------------------------------- normalise & N_eff --
 
-// numpy pairwise summation of w[i]^2 (loops_utils.h.src) for the sequential mode.
-__device__ double pairwise_sq(const double *a, int64_t n) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int64_t i = 0; i < n; ++i) res += a[i] * a[i];
-        return res;
-    } else if (n <= 128) {
-        double r[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = a[k] * a[k];
-        int64_t i;
-        for (i = 8; i < n - (n % 8); i += 8) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) r[k] += a[i + k] * a[i + k];
-        }
-        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < n; ++i) res += a[i] * a[i];
-        return res;
-    }
-    int64_t n2 = n / 2;
-    n2 -= n2 % 8;
-    return pairwise_sq(a, n2) + pairwise_sq(a + n2, n - n2);
-}
-
 // Weight total. Sequential mode: Python builtin sum in particle order.
 __device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k) {
     switch (k) {
@@ -709,7 +685,7 @@ hipError_t launch_wsum(const ReduceParams &p, hipStream_t s) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
-    __shared__ double s_sq[kBlock / 64], s_bv[kBlock / 64];
+    __shared__ double s_sq[kBlock / 64], s_bv[kBlock / 64], s_w[kBlock / 64];
     __shared__ int64_t s_bi[kBlock / 64];
     __shared__ int s_mc[kBlock / 64];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -726,6 +702,7 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
     }
     // block_sum / block_argmax / block_max_i (same trees) with one barrier
     const double sq = wave_sum(live ? w * w : 0.0);
+    const double ws = P.part_w ? wave_sum(w) : 0.0;
     double bv = live ? w : -INFINITY;
     int64_t bi = live ? i : INT64_MAX;
     wave_argmax(bv, bi);
@@ -733,6 +710,7 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) {
         s_sq[wid] = sq;
+        s_w[wid] = ws;
         s_bv[wid] = bv;
         s_bi[wid] = bi;
         s_mc[wid] = mc;
@@ -751,6 +729,7 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
             m = max(m, s_mc[k]);
         }
         P.part_sq[blockIdx.x] = t;
+        if (P.part_w) P.part_w[blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);   // an estimate only
         P.part_best_w[blockIdx.x] = v;
         P.part_best_i[blockIdx.x] = ix;
         P.part_maxcnt[blockIdx.x] = m;

@@ -25,6 +25,7 @@ FS2_ERR_CAPACITY = -7
 FS2_REDUCE_AUTO = 0
 FS2_REDUCE_SEQUENTIAL = 1
 FS2_REDUCE_PARALLEL = 2
+FS2_REDUCE_EXACT = 3
 FS2_HOST = 0
 FS2_DEVICE = 1
 FS2_COMM_RCCL = 0
@@ -70,7 +71,7 @@ class fs2_iter_stats(C.Structure):
         ("ambiguous", C.c_uint64),
         ("resample_slots", C.c_uint64),
         ("error_flags", C.c_int32),
-        ("reserved", C.c_int32),
+        ("reduce_ambiguous", C.c_int32),
         ("cow_pages", C.c_uint64),
         ("new_pages", C.c_uint64),
         ("collections", C.c_uint64),
@@ -78,7 +79,7 @@ class fs2_iter_stats(C.Structure):
     ]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 class fs2_profile(C.Structure):

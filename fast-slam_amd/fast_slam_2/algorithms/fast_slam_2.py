@@ -27,7 +27,7 @@ from ..models.measurement import Measurement
 from ..models.particle import Particle
 
 _REDUCE = {"auto": nat.FS2_REDUCE_AUTO, "sequential": nat.FS2_REDUCE_SEQUENTIAL,
-           "parallel": nat.FS2_REDUCE_PARALLEL}
+           "parallel": nat.FS2_REDUCE_PARALLEL, "exact": nat.FS2_REDUCE_EXACT}
 
 
 class FastSLAM2:

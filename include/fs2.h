@@ -40,11 +40,18 @@ enum {
     FS2_ERR_CAPACITY = -7   /* a map needs more landmark slots than allowed */
 };
 
-/* Reduction order for normalise / N_eff / resample prefix. */
+/* Reduction order for normalise / N_eff / resample prefix.  The reference sums
+ * the weights with Python's sum (fast_slam_2.py:166), the resample's running
+ * sum one particle at a time (:184-193) and sum(w^2) with numpy (:219-223). */
 enum {
-    FS2_REDUCE_AUTO = 0,       /* sequential up to 4096 particles, parallel above */
-    FS2_REDUCE_SEQUENTIAL = 1, /* the reference's exact summation orders (single lane) */
-    FS2_REDUCE_PARALLEL = 2    /* fixed-order tree reductions (deterministic) */
+    FS2_REDUCE_AUTO = 0,       /* one GPU: SEQUENTIAL up to 4096 particles, EXACT above;
+                                  sharded: PARALLEL (the sum spans ranks) */
+    FS2_REDUCE_SEQUENTIAL = 1, /* the reference's summation orders, one lane */
+    FS2_REDUCE_PARALLEL = 2,   /* fixed-order trees (deterministic, not the reference's
+                                  rounding); fs2_iter_stats.reduce_ambiguous counts the
+                                  decisions that rounding could flip */
+    FS2_REDUCE_EXACT = 3       /* the reference's summation orders, bit-exact, evaluated by
+                                  parallel kernels (one GPU; sharded handles use PARALLEL) */
 };
 
 enum { FS2_HOST = 0, FS2_DEVICE = 1 };   /* where caller buffers live */
@@ -94,7 +101,10 @@ typedef struct fs2_iter_stats {
     uint64_t ambiguous;         /* gate decisions within 1e-9 relative of the threshold */
     uint64_t resample_slots;    /* landmark slots the resampled maps refer to (shared, not copied) */
     int32_t error_flags;        /* bit 0: singular covariance met; bit 1: non-finite weight */
-    int32_t reserved;
+    int32_t reduce_ambiguous;   /* FS2_REDUCE_PARALLEL: resample boundaries (and the N_eff
+                                   rule) within the rounding bound of the reference's
+                                   summation order, i.e. decisions that may differ from it;
+                                   always 0 in the SEQUENTIAL / EXACT modes */
     uint64_t cow_pages;         /* shared 8-slot pages copied before their first write */
     uint64_t new_pages;         /* fresh pages (appends, maps received from other ranks) */
     uint64_t collections;       /* page-pool collections so far (handle lifetime) */
