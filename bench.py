@@ -194,11 +194,10 @@ def main():
             R, t, _ = icp_tickets.pop(s).result()
             if s + 1 != args.warmup and not args.serial_icp:
                 icp_submit(s + 1)
-            # Robot.get_transformation_icp (robot.py:108-120)
-            if tr != 0:
-                rot, tr = 0.0, float(np.linalg.norm(t))
-            else:
-                rot, tr = float(-np.arctan2(R[1, 0], R[0, 0])), 0.0
+            # Robot.get_transformation_icp (robot.py:108-120): the commanded linear
+            # velocity is nonzero on the driving scans of the odometry pattern
+            v = 0.3 if tr != 0 else 0.0
+            rot, tr = (float(q) for q in fast_slam_2.Robot.icp_odometry(R, t, v))
         return f.step(rot, tr, meas[s])
 
     def barrier():

@@ -266,8 +266,9 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
 // Record pool of `n` records (existing records keep their ids), free list, marks.
 static int grow_recs(fs2_handle *h, int64_t n) {
     if (n <= h->nrecs) return FS2_OK;
-    if (n > (int64_t)0xfffffffell * 16)
-        return set_err(&h->err, FS2_ERR_OOM, "record pool of %lld records exceeds the id space", (long long)n);
+    if (n > (int64_t)kRecIdLimit)
+        return set_err(&h->err, FS2_ERR_OOM, "record pool of %lld records exceeds the 32-bit id space",
+                       (long long)n);
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     char *rp = nullptr;
     HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
@@ -315,7 +316,10 @@ static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
         if (rc) return rc;
         if (need > h->rnfree) {
             const int64_t live = h->nrecs - h->rnfree;
-            rc = grow_recs(h, std::max(h->nrecs + h->nrecs / 2, live + 2 * need));
+            // grow by half, clamped to the id space (grow_recs fails beyond it)
+            int64_t want = std::max(h->nrecs + h->nrecs / 2, live + 2 * need);
+            if (want > (int64_t)kRecIdLimit) want = std::max<int64_t>(kRecIdLimit, live + need);
+            rc = grow_recs(h, want);
             if (rc) return rc;
         }
     }
@@ -586,9 +590,9 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     if (rc) return fail(rc);
     // pool: twice the initial maps plus room for a few scans of new pages;
     // records: the initial maps plus room for many scans of writes
-    rc = grow_pool(h, n * h->rows * 2 + 8 * n + 1024);
+    rc = grow_pool(h, cfg->page_pool > 0 ? cfg->page_pool : n * h->rows * 2 + 8 * n + 1024);
     if (rc) return fail(rc);
-    rc = grow_recs(h, n * h->cap + n * h->cap / 4 + 64 * n + 1024);
+    rc = grow_recs(h, cfg->record_pool > 0 ? cfg->record_pool : n * h->cap + n * h->cap / 4 + 64 * n + 1024);
     if (rc) return fail(rc);
     h->sendbuf.assign(G, nullptr);
     h->recvbuf.assign(G, nullptr);
@@ -922,6 +926,11 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         if (sh) {
             rc = exchange_particles(h, rs);
             if (rc) return rc;
+            // received maps can be longer than every local one: rows for the
+            // largest map on any rank (k_global_finalize) before unpacking them
+            rc = grow_rows(h, h->stats_host->max_count);
+            if (rc) return rc;
+            rs.opt = h->pt[nxt];
             // fresh records and pages for the received maps: record r, row k ->
             // page base + r * rows + k; slot q -> record rbase + peer sbase + soff + q
             rc = reserve_recs(h, h->s_recv, &rs.alloc);

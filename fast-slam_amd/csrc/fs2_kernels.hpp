@@ -35,6 +35,7 @@ constexpr int kPageBytes = 128;
 constexpr int kRecBytes = 48;
 constexpr uint32_t kOwned = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7fffffffu;
+constexpr uint32_t kRecIdLimit = 0xffffffffu;   // record ids are uint32 (mirror .w, free lists)
 typedef uint2 Desc;
 
 // Summary grid: box bound codes c in [0, 255]; lo(c) = org + (c - 1) cell (c = 0:

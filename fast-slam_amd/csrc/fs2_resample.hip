@@ -147,7 +147,11 @@ __device__ void global_finalize_body(const ReduceParams &P) {
     // tree sums: a decision this close to the threshold may differ from the
     // reference's summation order
     if (P.flip_margin > 0.0 && fabs(ne - ng / 2.0) <= P.flip_margin * ng) st->reduce_amb += 1;
-    st->max_count = max(st->max_count, P.recs[P.rank].max_count);
+    // the largest map on any rank: a resample may bring it here (the receiver
+    // sizes its page-table rows for it before unpacking)
+    int mc = P.recs[0].max_count;
+    for (int g = 1; g < P.world; ++g) mc = max(mc, P.recs[g].max_count);
+    st->max_count = max(st->max_count, mc);
     st->best_index = bi;
     st->best_w = bv;
     st->pose[0] = P.recs[gb].pose[0];

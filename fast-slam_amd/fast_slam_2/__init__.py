@@ -6,8 +6,9 @@ association / Mahalanobis helpers and the known-landmark clustering
 (update_known_landmarks / cluster_points) run in libfs2.so (HIP, gfx950);
 Serializer writes the viewer's JSON from one device download; the landmark
 front-end (LandmarkUtils.get_measurements_to_landmarks, HoughTransformation)
-runs batched on the device too.  Robot and EvaluationUtils are simulator-bound
-(HAL) and outside this build's scope.
+runs batched on the device too.  Robot keeps its ICP odometry
+(get_transformation_icp); its laser / motor calls and EvaluationUtils are
+simulator-bound (HAL) and outside this build's scope.
 """
 from .algorithms.fast_slam_2 import FastSLAM2
 from .algorithms.hough_transformation import HoughTransformation
@@ -19,11 +20,12 @@ from .models.landmark import Landmark
 from .models.measurement import Measurement
 from .models.particle import Particle
 from .models.point import Point
+from .models.robot import Robot
 from .utils.geometry_utils import GeometryUtils
 from .utils.landmark_utils import LandmarkUtils
 from .utils.serializer import Serializer
 
-_OUT_OF_SCOPE = {"Robot", "EvaluationUtils"}
+_OUT_OF_SCOPE = {"EvaluationUtils"}
 
 
 def __getattr__(name):
@@ -34,4 +36,4 @@ def __getattr__(name):
 
 
 __all__ = ["FastSLAM2", "HoughTransformation", "ICP", "LineFilter", "DirectedPoint", "EvaluationResults", "Landmark",
-           "Measurement", "Particle", "Point", "GeometryUtils", "LandmarkUtils", "Serializer"]
+           "Measurement", "Particle", "Point", "Robot", "GeometryUtils", "LandmarkUtils", "Serializer"]

@@ -53,6 +53,8 @@ class fs2_config(C.Structure):
         ("comm_id", C.c_uint8 * 128),
         ("comm_mode", C.c_int32),
         ("sharded_path", C.c_int32),
+        ("page_pool", C.c_int64),
+        ("record_pool", C.c_int64),
     ]
 
 

@@ -37,7 +37,8 @@ class FastSLAM2:
                  seed: int | None = None, reduce: str = "auto", record_assoc: bool = False,
                  landmark_capacity: int = 64, rank: int = 0, world_size: int = 1,
                  comm_id: bytes | None = None, verbose: bool = True, gate_filter: bool = True,
-                 comm_mode: str = "rccl", sharded_path: bool = False):
+                 comm_mode: str = "rccl", sharded_path: bool = False, page_pool: int = 0,
+                 record_pool: int = 0):
         lib = nat.load()
         cfg = nat.default_config()
         cfg.num_particles = int(config.NUM_PARTICLES if num_particles is None else num_particles)
@@ -60,6 +61,8 @@ class FastSLAM2:
             C.memmove(cfg.comm_id, comm_id, 128)
         cfg.comm_mode = {"rccl": nat.FS2_COMM_RCCL, "local": nat.FS2_COMM_LOCAL}[comm_mode]
         cfg.sharded_path = 1 if sharded_path else 0
+        cfg.page_pool = int(page_pool)          # initial pool sizes (0: defaults; fs2.h)
+        cfg.record_pool = int(record_pool)
         if rng not in ("numpy", "device"):
             raise ValueError("rng must be 'numpy' or 'device'")
         self._rng = rng

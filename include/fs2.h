@@ -85,6 +85,12 @@ typedef struct fs2_config {
     int32_t comm_mode;              /* FS2_COMM_* */
     int32_t sharded_path;           /* 1: run the sharded path (transport, collectives) even
                                        with world_size 1 -- tests the transport on one GPU */
+    int64_t page_pool;              /* initial page pool (128-byte pages); 0 = twice the initial
+                                       maps plus 8 per particle.  Pools are collected when a
+                                       reservation does not fit and grow when a collection
+                                       frees too little */
+    int64_t record_pool;            /* initial slot-record pool (48 B each); 0 = 1.25x the
+                                       initial capacity plus 64 per particle */
 } fs2_config;
 
 typedef struct fs2_iter_stats {

@@ -183,3 +183,50 @@ def test_sharded_long_run_with_collections():
     assert max(h.last_stats.collections for h in shards) >= 2
     for h in shards + [single]:
         h.close()
+
+
+def test_received_maps_longer_than_local_rows():
+    """Rank 0's particles carry 40 landmarks (5 page rows), rank 1's only 4 (one
+    row); peaked weights at the end of rank 0 make every output of rank 1 a copy
+    of a rank-0 particle.  Rank 1 must size its page table for the received maps
+    (the largest map over all ranks), and the result equals a single handle."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    configure()
+    G, N, L = 2, 4000, 40
+    wl = syn.Workload(N, L, seed=13)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    cnt = np.full(N, L, np.int32)
+    cnt[N // 2:] = 4
+    lm[N // 2:, 4:] = 0.0
+    w = np.full(N, 1e-9)
+    w[N // 2 - 100:N // 2] = 1.0
+    single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=2, landmark_capacity=8,
+                                   verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    key = os.urandom(128)
+    shards = [fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=2, landmark_capacity=8,
+                                    rank=g, world_size=G, comm_id=key, comm_mode="local", verbose=False)
+              for g in range(G)]
+    for h in shards:
+        a, b = h.first_global, h.first_global + h.n_local
+        h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+    for s in range(3):
+        ms = np.zeros((0, 2)) if s == 0 else wl.measurements(s)
+        pose1, st1 = single.step(0.0, 0.03, ms)
+        outs = _step_all(shards, 0.0, 0.03, ms)
+        if s == 0:
+            assert st1.resampled == 1
+        for pose, st in outs:
+            assert st.resampled == st1.resampled and st.best_index == st1.best_index, s
+            assert np.allclose(pose, pose1, rtol=1e-9, atol=1e-12), s
+    cap = L + 16
+    s1 = single.get_state(lm_cap=cap)
+    sg = _gather(shards, cap)
+    assert np.array_equal(s1[4], sg[4])
+    assert int(sg[4][N // 2:].min()) >= L          # rank 1 now holds rank 0's long maps
+    assert np.allclose(s1[5], sg[5], rtol=1e-9, atol=1e-12)
+    for h in shards + [single]:
+        h.close()
