@@ -48,21 +48,25 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-gate-filter", action="store_true",
                     help="A/B: read every visited slot's fp64 data (no fp32 gate mirror)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the workload-robustness runs (60-scan continuation, dense map, no gate filter)")
     ap.add_argument("--serial-icp", action="store_true",
                     help="A/B (config 4): align each scan just before its update instead of "
                          "beside the previous scan's update")
     return ap.parse_args()
 
 
-def populate(f, n_local, L, seed, rank):
-    """Synthetic initial state generated on the GPU in chunks."""
+def populate(f, n_local, L, seed, rank, base_map=None):
+    """Synthetic initial state generated on the GPU in chunks; base_map
+    [L][2] replaces the 6 m landmark grid (dense-map variant)."""
     import torch
     import fs2_synthetic as syn
     from fast_slam_2 import _native as nat
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=dev)
     g.manual_seed(1_000_003 * (seed + 1) + rank)
-    base = torch.tensor(syn.common_landmarks(L, seed), dtype=torch.float64, device=dev)
+    base = torch.tensor(syn.common_landmarks(L, seed) if base_map is None else base_map, dtype=torch.float64,
+                        device=dev)
     x = torch.randn(n_local, generator=g, dtype=torch.float64, device=dev) * 0.05
     y = torch.randn(n_local, generator=g, dtype=torch.float64, device=dev) * 0.05
     yaw = torch.randn(n_local, generator=g, dtype=torch.float64, device=dev) * 0.01
@@ -116,27 +120,110 @@ def cpu_baseline(L, P, budget_s, seed):
         return n * scans / t_work, scans, t_work
 
     threads = orc.threads()
+    model = "unknown"
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        pass
     one, s1, t1 = run(6000, 1, budget_s / 2)
     n = 6000 * max(1, min(threads, 32))
     many, sm, tm = run(n, threads, budget_s / 2)
     orc.set_threads(threads)
     return dict(value=many, unit="particle-updates/s", cores=threads, kind="port",
+                cpu_model=model, host_cpus=os.cpu_count(),
                 single_thread_value=one,
                 sample=f"{n} particles x {L} landmarks, M=4, {sm} scans on {threads} OpenMP threads "
                        f"({tm:.1f} s); 1 thread: 6000 particles, {s1} scans ({t1:.1f} s); "
-                       f"C oracle, reference semantics")
+                       f"C oracle, reference semantics and reference algorithm (first-match linear "
+                       f"scan of every map, deep-copied maps on resample): the ratio to the GPU "
+                       f"value mixes algorithm (pruning, page sharing) with hardware")
 
 
-def pmc_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (scripts/pmc_round.sh -> profiles/pmc_{workload}.json), or None."""
+def pmc_record(workload):
+    """The committed PMC summary of `workload` (scripts/pmc_round.sh ->
+    scripts/pmc_summary.py -> profiles/pmc_{workload}.json) if it was measured on a
+    library built from these sources (its source_id equals the build's), else None."""
+    import build
     p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
-    if os.path.exists(p):
-        try:
-            return json.load(open(p)).get(kernel, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+    if not os.path.exists(p):
+        return None
+    try:
+        rec = json.load(open(p))
+    except Exception:
+        return None
+    return rec if rec.get("source_id") == build.source_id() else None
+
+
+def pmc_traffic(rec, kernel):
+    return None if rec is None else rec.get(kernel, {}).get("hbm_bytes_per_launch")
+
+
+def timed_scans(f, scans, meas_of, odo_of, warmup):
+    """Warm-up then timed scans of handle f; (particle-updates/s, ms/scan, stats sums)."""
+    import torch
+    for s in scans[:warmup]:
+        f.step(*odo_of(s), meas_of(s))
+    torch.cuda.synchronize()
+    sums = dict(visited=0, opened=0, appends=0, resamples=0, cow=0)
+    t0 = time.perf_counter()
+    for s in scans[warmup:]:
+        _, st = f.step(*odo_of(s), meas_of(s))
+        sums["visited"] += st.slots_visited
+        sums["opened"] += st.pages_opened
+        sums["appends"] += st.appends
+        sums["resamples"] += st.resampled
+        sums["cow"] += st.cow_pages
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    k = len(scans) - warmup
+    n = f.n_local
+    return {"value": n * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k,
+            "slots_visited_per_particle_scan": sums["visited"] / (n * k),
+            "pages_opened_per_particle_scan": sums["opened"] / (n * k),
+            "appends_per_particle_scan": sums["appends"] / (n * k),
+            "cow_pages_per_particle_scan": sums["cow"] / (n * k), "resamples": sums["resamples"]}
+
+
+def robustness(args, f, L, first_scan):
+    """How much of the headline depends on the synthetic map's sparsity and on the
+    run length: the same handle 40 scans further (60 in all), a dense
+    map (L landmarks uniform over the 20 x 15 m room, several inside every gate),
+    and the grid map without the fp32 gate filter.  Not part of `value`."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    out = {}
+    steps = 40
+    meas = {s: np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64)
+            for s in range(first_scan, first_scan + steps)}
+    out["long_run_60"] = timed_scans(f, list(range(first_scan, first_scan + steps)), meas.__getitem__,
+                                     syn.odometry, 0)
+    out["long_run_60"]["note"] = f"scans {first_scan}..{first_scan + steps - 1} of the headline handle"
+    n = f.n_local
+    # dense map: uniform landmarks, hits near random ones, a miss 30 m outside
+    rng = np.random.default_rng(args.seed + 17)
+    hw, hh = syn.ROOM[0] / 2, syn.ROOM[1] / 2
+    dense = np.column_stack([rng.uniform(-hw, hw, L), rng.uniform(-hh, hh, L)])
+
+    def dense_meas(s):
+        r = np.random.default_rng([args.seed, 900 + s])
+        ks = r.integers(0, L, 3)
+        pts = [dense[k] + r.uniform(-0.3, 0.3, 2) for k in ks] + [np.array([30.0 + s, -30.0])]
+        return np.array([syn.encode(*p) for p in pts])
+
+    scans = list(range(13))
+    g = fast_slam_2.FastSLAM2(n, rng="device", seed=args.seed, landmark_capacity=L + 24, verbose=False)
+    populate(g, n, L, args.seed, 0, base_map=dense)
+    out["dense_map"] = timed_scans(g, scans, dense_meas, syn.odometry, 3)
+    out["dense_map"]["note"] = f"{L} landmarks uniform in the room (grid: 6 m spacing)"
+    g.close()
+    g = fast_slam_2.FastSLAM2(n, rng="device", seed=args.seed, landmark_capacity=L + 24, verbose=False,
+                              gate_filter=False)
+    populate(g, n, L, args.seed, 0)
+    gm = {s: np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64) for s in scans}
+    out["no_gate_filter"] = timed_scans(g, scans, gm.__getitem__, syn.odometry, 3)
+    out["no_gate_filter"]["note"] = "grid map, every slot's fp64 record read (no mirrors, no page boxes)"
+    g.close()
+    return out
 
 
 def main():
@@ -214,6 +301,9 @@ def main():
     copied_slots = 0
     cow_pages = 0
     exact_slots = 0
+    opened = 0
+    ref_visits = 0
+    hits_appends = 0
     barrier()
     t0 = time.perf_counter()
     for s in range(args.warmup, total_scans):
@@ -223,6 +313,9 @@ def main():
         copied_slots += st.resample_slots
         cow_pages += st.cow_pages
         exact_slots += st.candidates
+        opened += st.pages_opened
+        ref_visits += st.reference_visits
+        hits_appends += st.hits + st.appends
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -253,13 +346,27 @@ def main():
                                 (prof["update_bytes"] - prof["filter_bytes"]) / fl)
         else:
             kern["k_update"] = (upd_ms, prof["update_bytes"] / launches)
-        # the roofline line is for the dominant (longest) kernel
+        # the roofline line is for the dominant (longest) kernel: HBM bytes per launch
+        # from the PMC passes on this build (profiles/pmc_<workload>.json), over the
+        # launch's live duration (HIP events on the library's stream, this run)
         kernel = max(kern, key=lambda k: kern[k][0])
-        ms_launch, bytes_launch = kern[kernel]
-        achieved = bytes_launch / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
+        ms_launch, alg_bytes = kern[kernel]
+        pmc = pmc_record(cfg["name"]) if n_per_gpu == cfg["N"] and L == cfg["L"] else None
+        traffic = pmc_traffic(pmc, kernel)
+        alg_GBs = alg_bytes / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
+        if traffic is not None and ms_launch > 0:
+            achieved, basis = traffic / (ms_launch * 1e-3) / 1e9, "pmc_hbm_bytes"
+        else:
+            achieved, basis = alg_GBs, "algorithmic_bytes (no PMC record for this build)"
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(L, cfg["P"], args.cpu_seconds, args.seed)
+        scan_ms = dt / args.steps * 1e3
+        units = f.n_local * args.steps
+        # SURVEY §8(d)'s accounting: the reference layout's bytes (48 B per landmark
+        # its first-match scan reads, 48 B per updated / appended landmark, 104 B of
+        # particle scalars) at this run's scan rate -- a work rate, not a bandwidth
+        ref_bytes = 48.0 * ref_visits + 48.0 * hits_appends + 104.0 * units
         out = {
             "metric": "particle-updates/s",
             "value": N * args.steps / dt,
@@ -267,7 +374,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
+            "ms_per_step": scan_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -278,33 +385,45 @@ def main():
                        "particles_total": N, "landmarks": L, "beams": cfg["P"],
                        "measurements_per_scan": 4, "icp": cfg["icp"],
                        "icp_pipelined": bool(cfg["icp"] and not args.serial_icp),
-                       "gate_filter": not args.no_gate_filter,
+                       "gate_filter": not args.no_gate_filter, "reduce": "exact" if N > 4096 and world == 1
+                       else ("parallel" if world > 1 else "sequential"),
                        "parallelism": f"particle-shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(cfg["name"], kernel),
-                         "kernel": kernel, "bytes_per_launch": bytes_launch,
-                         "ms_per_launch": ms_launch},
+                         "traffic": traffic, "basis": basis,
+                         "kernel": kernel, "ms_per_launch": ms_launch,
+                         "pmc_source": None if pmc is None else pmc.get("source"),
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "algorithmic_GBs": alg_GBs},
             "cpu_baseline": cpu,
             "extra": {"scan_device_ms": prof["scan_ms"] / max(prof["scans"], 1),
                       "update_pass_ms": upd_ms,
-                      "kernels": {k: {"ms_per_launch": v[0], "bytes_per_launch": v[1],
-                                      "achieved_GBs": v[1] / (v[0] * 1e-3) / 1e9 if v[0] > 0 else 0.0,
-                                      "hbm_traffic_per_launch": pmc_traffic(cfg["name"], k)}
+                      "kernels": {k: {"ms_per_launch": v[0], "algorithmic_bytes_per_launch": v[1],
+                                      "algorithmic_GBs": v[1] / (v[0] * 1e-3) / 1e9 if v[0] > 0 else 0.0,
+                                      "hbm_bytes_per_launch": pmc_traffic(pmc, k),
+                                      "hbm_GBs": (pmc_traffic(pmc, k) / (v[0] * 1e-3) / 1e9
+                                                  if pmc_traffic(pmc, k) and v[0] > 0 else None)}
                                   for k, v in kern.items()},
+                      "reference_equivalent": {
+                          "bytes_per_scan": ref_bytes / args.steps,
+                          "work_rate_GBs": ref_bytes / dt / 1e9,
+                          "landmark_reads_per_particle_scan": ref_visits / units,
+                          "note": "SURVEY §8d bytes of the reference's layout and linear scan at this "
+                                  "run's scan rate; not a bandwidth (pruning and page sharing skip them)"},
                       "update_pass_bytes": prof["update_bytes"] / launches,
-                      # normalise / N_eff / estimate, the resample when it fires, the
-                      # stats publication: one event span per scan
                       "reduce_and_resample_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resamples": resamples,
                       "resample_shared_slots": copied_slots,
-                      "cow_pages_per_particle_scan": cow_pages / (f.n_local * args.steps),
+                      "cow_pages_per_particle_scan": cow_pages / units,
                       "pool_collections": st.collections,
                       "pool_pages": st.pool_pages,
-                      "slots_visited_per_particle_scan": visited / (f.n_local * args.steps),
-                      "exact_slots_per_particle_scan": exact_slots / (f.n_local * args.steps),
+                      "pages_opened_per_particle_scan": opened / units,
+                      "slots_visited_per_particle_scan": visited / units,
+                      "exact_slots_per_particle_scan": exact_slots / units,
                       "icp_us": icp_us},
         }
+        if not args.no_extras and world == 1 and not cfg["icp"]:
+            out["extra"]["robustness"] = robustness(args, f, L, total_scans)
         print(json.dumps(out), flush=True)
     f.close()
     if world > 1:

@@ -6,6 +6,7 @@ every FMA explicitly to follow the reference's numpy/OpenBLAS operation order.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -21,14 +22,31 @@ SOURCES = ["fs2_api.hip", "fs2_update.hip", "fs2_resample.hip", "fs2_exact.hip",
 HEADERS = ["fs2_device.hpp", "fs2_kernels.hpp", "fs2_comm.hpp", "fs2_reduce.hpp", "fs2_frontend.hpp"]
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+         "-Wno-unused-value"]
+
+
+def source_id(defines=()) -> str:
+    """Hash of every source and header libfs2.so is built from, the build flags and
+    the target: compiled into the library (fs2_build_id) and checked by the tests,
+    so a library built from other sources is rebuilt here and refused on the GPU box."""
+    h = hashlib.sha256()
+    for f in sorted(SOURCES + HEADERS):
+        h.update(f.encode() + b"\0" + open(os.path.join(CSRC, f), "rb").read())
+    h.update(open(os.path.join(os.path.dirname(HERE), "include", "fs2.h"), "rb").read())
+    h.update(" ".join([ARCH, *FLAGS, *defines]).encode())
+    return h.hexdigest()[:20]
+
+
+def built_id(lib: str = LIB) -> str | None:
+    """The fs2_build_id the library at `lib` was compiled with (read from its
+    sidecar file, written with the library)."""
+    p = lib + ".id"
+    return open(p).read().strip() if os.path.exists(p) and os.path.exists(lib) else None
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "fs2.h"))
-    deps.append(os.path.abspath(__file__))
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return built_id() != source_id()
 
 
 def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
@@ -38,8 +56,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value",
+    sid = source_id(defines)
+    cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, f'-DFS2_BUILD_ID="{sid}"',
            "-I", os.path.join(ROCM, "include"), *defines,
            *[os.path.join(CSRC, s) for s in SOURCES],
            "-o", lib + ".tmp", "-L", os.path.join(ROCM, "lib"), "-lrccl",
@@ -48,6 +66,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(lib + ".tmp", lib)
+    with open(lib + ".id", "w") as fh:
+        fh.write(sid + "\n")
     return lib
 
 
@@ -58,8 +78,9 @@ def build_hooks(verbose: bool = False) -> str:
     """libfs2_hooks.so: fs2_pages.hip alone with -DFS2_TEST_HOOKS (test entry points
     of single kernels; the GPU tests load it beside libfs2.so)."""
     src = os.path.join(CSRC, "fs2_pages.hip")
-    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".hpp")]
-    if os.path.exists(HOOKS) and os.path.getmtime(HOOKS) >= max(os.path.getmtime(d) for d in deps):
+    hid = hashlib.sha256(b"".join(open(os.path.join(CSRC, f), "rb").read()
+                                  for f in ["fs2_pages.hip"] + sorted(HEADERS))).hexdigest()[:20]
+    if os.path.exists(HOOKS) and built_id(HOOKS) == hid:
         return HOOKS
     cmd = [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
            "-shared", "-ffp-contract=off", "-DFS2_TEST_HOOKS", "-I", os.path.join(ROCM, "include"),
@@ -68,6 +89,8 @@ def build_hooks(verbose: bool = False) -> str:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(HOOKS + ".tmp", HOOKS)
+    with open(HOOKS + ".id", "w") as fh:
+        fh.write(hid + "\n")
     return HOOKS
 
 

@@ -147,10 +147,12 @@ struct fs2_handle {
     int32_t n_recv = 0;                             // particles received by the last resample
 
     // exact-order reductions (fs2_exact.hip)
-    int32_t *uinfo = nullptr, *uord = nullptr, *seql = nullptr;
+    int32_t *uinfo = nullptr, *uol = nullptr, *seql = nullptr, *bC = nullptr, *bpc = nullptr;
+    uint32_t *bM = nullptr;
     long long *udelta = nullptr;
-    unsigned long long *ug = nullptr;
-    double *sout = nullptr, *bpre = nullptr, *part_w = nullptr, *np_part = nullptr;
+    unsigned long long *ugl = nullptr, *bD = nullptr, *bpd = nullptr;
+    double *sout = nullptr, *bpre = nullptr, *part_w = nullptr, *np_part = nullptr, *sentry = nullptr;
+    UnitRec *urec = nullptr;
 
     MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb}; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
@@ -171,16 +173,24 @@ struct fs2_handle {
         p.lazy = lazy ? 1 : 0;
         p.uinfo = uinfo;
         p.udelta = udelta;
-        p.ug = ug;
-        p.uord = uord;
+        p.ugl = ugl;
+        p.uol = uol;
+        p.bD = bD;
+        p.bC = bC;
+        p.bM = bM;
+        p.bpd = bpd;
+        p.bpc = bpc;
         p.seql = seql;
         p.sout = sout;
+        p.urec = urec;
+        p.sentry = sentry;
         p.c = c;
         p.total = total;
         p.stats = stats_dev;
         // recursive summation of n terms >= 0: |chain - exact| <= gamma_n exact; the
         // block estimates add gamma_{n/256 + 30}; doubled, plus slack for the scaling
         p.margin = std::ldexp(2.0 * (double)n + 8192.0, -53);
+        p.bpre_ready = 1;        // k_wsum / k_finalize scan the block sums (ReduceParams bpre_*)
         return p;
     }
 };
@@ -411,6 +421,11 @@ extern "C" {
 
 int32_t fs2_abi_version(void) { return FS2_ABI_VERSION; }
 
+#ifndef FS2_BUILD_ID
+#define FS2_BUILD_ID "unknown"
+#endif
+const char *fs2_build_id(void) { return FS2_BUILD_ID; }
+
 void fs2_config_default(fs2_config *c) {
     if (!c) return;
     std::memset(c, 0, sizeof *c);
@@ -456,8 +471,10 @@ static void free_handle(fs2_handle *h) {
     for (char *b : h->sendbuf) hipFree(b);
     for (char *b : h->recvbuf) hipFree(b);
     hipFree(h->cand); hipFree(h->ncand);
-    hipFree(h->uinfo); hipFree(h->uord); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ug);
+    hipFree(h->uinfo); hipFree(h->uol); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ugl);
+    hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
     hipFree(h->sout); hipFree(h->bpre); hipFree(h->part_w); hipFree(h->np_part);
+    hipFree(h->urec); hipFree(h->sentry);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -548,11 +565,19 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     {
         const int64_t nu = (n + 63) / 64;
         ok &= alloc((void **)&h->uinfo, nu * 4) == hipSuccess;
-        ok &= alloc((void **)&h->uord, nu * 4) == hipSuccess;
+        ok &= alloc((void **)&h->uol, nu * 4) == hipSuccess;
+        const int64_t ng = (nu + kChainGroup - 1) / kChainGroup;
+        ok &= alloc((void **)&h->bD, ng * 8) == hipSuccess;
+        ok &= alloc((void **)&h->bC, ng * 4) == hipSuccess;
+        ok &= alloc((void **)&h->bM, ng * 4) == hipSuccess;
+        ok &= alloc((void **)&h->bpd, ng * 8) == hipSuccess;
+        ok &= alloc((void **)&h->bpc, ng * 4) == hipSuccess;
         ok &= alloc((void **)&h->seql, nu * 4) == hipSuccess;
         ok &= alloc((void **)&h->udelta, nu * 8) == hipSuccess;
-        ok &= alloc((void **)&h->ug, nu * 8) == hipSuccess;
+        ok &= alloc((void **)&h->ugl, nu * 8) == hipSuccess;
         ok &= alloc((void **)&h->sout, nu * 8) == hipSuccess;
+        ok &= alloc((void **)&h->sentry, nu * 8) == hipSuccess;
+        ok &= alloc((void **)&h->urec, nu * sizeof(UnitRec)) == hipSuccess;
         ok &= alloc((void **)&h->bpre, nb * 8) == hipSuccess;
         ok &= alloc((void **)&h->part_w, nb * 8) == hipSuccess;
         ok &= alloc((void **)&h->np_part, np_sumsq_chunks(n) * 8) == hipSuccess;
@@ -845,6 +870,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.n_np = (int32_t)np_sumsq_chunks(h->n);
     rp.flip_margin = flip_margin;
     rp.part_w = exact ? h->part_w : nullptr;
+    rp.bpre_w = exact ? h->bpre : nullptr;
+    rp.bpre_n = exact ? h->bpre : nullptr;   // the total's chain is done with bpre by then
     rp.u0_host = u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
@@ -879,6 +906,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.stats = h->stats_dev;
     rs.rec = h->rec;
     rs.flip_margin = flip_margin;
+    rs.use_chain = exact ? 1 : 0;
+    rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout};
 
     // weight total over all ranks (fast_slam_2.py:166)
     HIP_TRY(h, launch_wsum(rp, s));
@@ -1011,6 +1040,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         stats->new_pages = st.new_pages;
         stats->collections = h->collections;
         stats->pool_pages = (uint64_t)h->npool;
+        stats->pages_opened = st.opened;
+        stats->reference_visits = st.ref_visits;
     }
     if (st.error_flags & 1)
         return set_err(&h->err, FS2_ERR_LINALG, "Singular matrix (landmark or observation covariance)");
@@ -1512,6 +1543,10 @@ int fs2_debug_phase_times(uint64_t out[8], int32_t reset) {
     return fs2::debug_phase_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess
                ? FS2_OK
                : FS2_ERR_HIP;
+}
+extern "C" int fs2_debug_chain_times(uint64_t out[8], int32_t reset) {
+    return fs2::debug_chain_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess ? FS2_OK
+                                                                                                    : FS2_ERR_HIP;
 }
 extern "C" int fs2_debug_icp_phase_times(uint64_t out[4], int32_t reset) {
     return fs2::debug_icp_phase_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess

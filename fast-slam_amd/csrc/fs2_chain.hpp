@@ -1,0 +1,147 @@
+// fs2_chain.hpp -- device helpers of the exact-order chain (fs2_exact.hip), shared
+// with the resample's range kernel, which evaluates the running sum's values from
+// the chain's unit table instead of reading a materialised prefix.
+#pragma once
+
+#include "fs2_reduce.hpp"
+
+namespace fs2 {
+
+constexpr int kUnit = 64;                  // chain unit: one wave
+
+__device__ __forceinline__ double bcast(double v, int j) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ long long wave_incl_scan_i64(long long v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// ulp of the binade E (values in [2^E, 2^(E+1))) and a / ulp
+__device__ __forceinline__ double unit_ulp(int E) { return ldexp(1.0, E - 52); }
+__device__ __forceinline__ double scaled(double a, int E) { return ldexp(a, 52 - E); }
+__device__ __forceinline__ int unit_binade(int32_t info) { return (info >> 2) - 4096; }
+
+__device__ __forceinline__ long long bcast_i64(long long v, int j) {
+    return __double_as_longlong(bcast(__longlong_as_double(v), j));
+}
+
+__device__ __forceinline__ double wave_incl_scan_f64(double v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// Exclusive prefix of in[0..n) into out (1024 threads; a tree estimate).
+__device__ inline void block_excl_scan_1024(const double *in, double *out, int n, double *lds16) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int per = (n + 1023) / 1024;
+    const int b0 = min(n, t * per), b1 = min(n, b0 + per);
+    double run = 0.0;
+    for (int b = b0; b < b1; ++b) run += in[b];
+    double incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    __syncthreads();
+    if (lane == 63) lds16[wid] = incl;
+    __syncthreads();
+    double off = incl - run;
+    for (int k = 0; k < wid; ++k) off += lds16[k];
+    for (int b = b0; b < b1; ++b) {
+        out[b] = off;
+        off += in[b];
+    }
+}
+
+// The chain's values inside one unit from its exact entry value s (the value
+// before the unit's first term; `first`: the unit's first term starts the chain).
+// One term per lane, lanes >= cnt ignored.  While s stays in its binade and no
+// term is a rounding tie, the values are s + (prefix of rint(a / u)) u, computed
+// for all lanes at once; the first lane where that fails (the sum reaches the
+// next binade, a tie, a term < 0 or not finite) takes one plain fp64 add --
+// exactly the reference's step -- and the rest restart from there.  Returns the
+// lane's value; s becomes the unit's last value.
+__device__ inline double chain_unit(double a, int cnt, double &s, bool first) {
+    const int lane = threadIdx.x & 63;
+    double mine = 0.0;
+    int j0 = 0;
+    if (first && cnt > 0) {
+        s = bcast(a, 0);
+        if (lane == 0) mine = s;
+        j0 = 1;
+    }
+    while (j0 < cnt) {
+        const bool active = lane >= j0 && lane < cnt;
+        if (s == 0.0) {
+            // a run of zero terms keeps the chain at 0
+            const unsigned long long nz = __ballot(active && a != 0.0);
+            const int jn = nz ? (int)__builtin_ctzll(nz) : cnt;
+            if (active && lane < jn) mine = s;
+            if (jn >= cnt) break;
+            s = s + bcast(a, jn);
+            if (lane == jn) mine = s;
+            j0 = jn + 1;
+            continue;
+        }
+        if (!(s >= 0x1p-1020 && s < 0x1p1020)) {           // outside the regular grid: one step
+            s = s + bcast(a, j0);
+            if (lane == j0) mine = s;
+            ++j0;
+            continue;
+        }
+        const int E = ilogb(s);
+        const double u = unit_ulp(E), top = ldexp(1.0, E + 1);
+        const double q = active ? scaled(a, E) : 0.0;
+        const bool ok = active && a >= 0.0 && q < 0x1p53;    // false for NaN, inf, negative
+        const double fq = ok ? floor(q) : 0.0;
+        const long long r = ok ? (long long)rint(q) : 0;
+        const long long P = wave_incl_scan_i64(r);
+        const double v = s + (double)P * u;
+        const bool bad = active && (!ok || q - fq == 0.5 || v >= top);
+        const unsigned long long bm = __ballot(bad);
+        const int js = bm ? (int)__builtin_ctzll(bm) : cnt;
+        if (active && lane < js) mine = v;
+        if (js >= cnt) {
+            s = bcast(v, cnt - 1);
+            break;
+        }
+        const double sp = (js == j0) ? s : bcast(v, js - 1);
+        s = sp + bcast(a, js);
+        if (lane == js) mine = s;
+        j0 = js + 1;
+    }
+    return mine;
+}
+
+// Chain value before unit k's first term, for a translation unit.
+__device__ __forceinline__ double chain_unit_entry(const ChainView &V, int64_t k, int E) {
+    const int64_t g = k / kChainGroup;
+    const int o = V.bpc[g] + V.uol[k] - 1;            // the last listed unit before k (unit 0 is listed)
+    const int64_t q = V.seql[o];
+    const unsigned long long ugk = V.bpd[g] + V.ugl[k], ugq = V.bpd[q / kChainGroup] + V.ugl[q];
+    return V.sout[o] + (double)(long long)(ugk - ugq) * unit_ulp(E);
+}
+
+}  // namespace fs2

@@ -22,16 +22,19 @@
 // |s_k - R_k| <= k 2^-53 R_k of recursive summation (R: the exact prefix)
 // doubled.  Units that may cross a binade, hold a tie (a / u an odd multiple
 // of 1/2: fl rounds to even, which depends on s), a non-finite or negative
-// term, or the chain's first element are evaluated one add at a time.  Only
-// those (~20-40 per chain: one per binade crossed) are walked serially; the
-// translations between them are an integer scan.
+// term, or the chain's first element are evaluated in order from their exact
+// entry value (chain_unit, fs2_chain.hpp).  Only those (~20-40 per chain: one
+// per binade crossed) are walked serially; the translations between them are an
+// integer scan.
 //
 //   k_chain_bpre   exclusive prefix of the 256-element block sums (tree estimate)
 //   k_chain_units  per unit: translation (binade E, D) or serial
 //   k_chain_walk   one workgroup: integer scan of D, then the serial units in
-//                  order (wave 0, the 64 terms of a unit broadcast lane by lane)
-//   k_chain_fill   prefix mode: each translation unit's values s_in + (scan of
-//                  rint(a/u)) u
+//                  order (wave 0; chain_unit evaluates a unit in a few wave-wide
+//                  steps: one per binade crossed or tie, not one per term)
+// In prefix mode the resample's range kernel evaluates the translation units'
+// values itself (s_in + (scan of rint(a / u)) u, fs2_chain.hpp), so the running
+// sum is never materialised beyond the serial units.
 //
 // numpy sum of squares.  Each full 8192-element chunk is numpy's pairwise tree:
 // 64 leaves of 128 elements (8 accumulators of 16 sequential adds, combined
@@ -39,43 +42,15 @@
 // binary tree in order -- one wave per chunk, xor butterflies.  A partial last
 // chunk is summed by lane 0 with the recursive form.  The chunk sums are added
 // in order by k_finalize.
-#include "fs2_reduce.hpp"
+#include "fs2_chain.hpp"
 
 namespace fs2 {
 
-constexpr int kUnit = 64;                  // chain unit: one wave
 constexpr int kNpChunk = 8192;             // numpy's reduction buffer
 
 __device__ __forceinline__ bool lazy_skip(const ChainParams &P) {
     return P.stats != nullptr && !P.stats->resampled;
 }
-
-__device__ __forceinline__ double bcast(double v, int j) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ long long wave_sum_i64(long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ long long wave_incl_scan_i64(long long v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
-
-// ulp of the binade E (values in [2^E, 2^(E+1))) and a / ulp rounded to nearest
-__device__ __forceinline__ double unit_ulp(int E) { return ldexp(1.0, E - 52); }
-__device__ __forceinline__ double scaled(double a, int E) { return ldexp(a, 52 - E); }
 
 // --------------------------------------------------------------- chain ----
 
@@ -84,182 +59,420 @@ __device__ __forceinline__ double scaled(double a, int E) { return ldexp(a, 52 -
 __global__ __launch_bounds__(1024) void k_chain_bpre(const ChainParams P) {
     __shared__ double lds[16];
     if (P.lazy && lazy_skip(P)) return;
-    const int t = threadIdx.x;
-    const int per = (P.nb + 1023) / 1024;
-    const int b0 = t * per, b1 = min(P.nb, b0 + per);
-    double run = 0.0;
-    for (int b = b0; b < b1; ++b) run += P.bsum[b];
-    // wave inclusive scan, then the waves before
-    double incl = run;
-    const int lane = t & 63, wid = t >> 6;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
-    }
-    if (lane == 63) lds[wid] = incl;
-    __syncthreads();
-    double off = incl - run;
-    for (int k = 0; k < wid; ++k) off += lds[k];
-    for (int b = b0; b < b1; ++b) {
-        P.bpre[b] = off;
-        off += P.bsum[b];
-    }
+    block_excl_scan_1024(P.bsum, P.bpre, P.nb, lds);
 }
 
-// Per 64-element unit (one wave; 4 units per 256-element block): translation
-// (info = (E + 4096) << 1, delta = D) or serial (info bit 0).
-__global__ __launch_bounds__(kBlock) void k_chain_units(const ChainParams P) {
-    __shared__ double s_ws[kBlock / 64];
+// Per 64-term unit (one wave; kChainGroup units per 1024-thread workgroup).
+// Each term's chain value before and after it is estimated (block prefix + wave
+// scan) with the margin; a term is "translation" in binade E when both bounds
+// lie in E, it is finite, >= 0, not a tie and not the chain's first term.  A
+// unit whose terms all translate in one binade is one translation D (uinfo,
+// udelta); otherwise ("listed") its runs of translating terms with equal E and
+// its other terms (one each) become up to kChainSegs segments (urec; a unit
+// with more is evaluated term by term by chain_unit in the walk).  The
+// workgroup also scans its units: ugl / uol (exclusive D, inclusive listed
+// count inside the group) and the group's totals bD / bC / bM (listed mask).
+__global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
+    __shared__ double s_ws[16];
+    __shared__ unsigned long long s_D[16];
+    __shared__ int s_f[16];
     if (P.lazy && lazy_skip(P)) return;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + t;
-    const int64_t k = (int64_t)blockIdx.x * (kBlock / kUnit) + wid;
+    const int64_t i = (int64_t)blockIdx.x * 1024 + t;
+    const int64_t k = (int64_t)blockIdx.x * kChainGroup + wid;
     const int64_t nu = (P.n + kUnit - 1) / kUnit;
-    const double a = (i < P.n) ? P.a[i] : 0.0;
-    const bool bad = (i < P.n) && !(a >= 0.0 && a < INFINITY);
-    const double us = wave_sum(a);
-    if (lane == 0) s_ws[wid] = us;
+    const bool valid = i < P.n;
+    const double a = valid ? P.a[i] : 0.0;
+    const double incl = wave_incl_scan_f64(a);
+    if (lane == 63) s_ws[wid] = incl;
     __syncthreads();
-    if (k >= nu) return;
-    double e_in = P.bpre[blockIdx.x];
-    for (int q = 0; q < wid; ++q) e_in += s_ws[q];
-    const double e_out = e_in + us;
-    const double lo = e_in * (1.0 - P.margin), hi = e_out * (1.0 + P.margin);
-    bool serial = (k == 0) || __any(bad) || !(lo >= 0x1p-1020) || !(hi < 0x1p1020);
-    int E = 0;
-    if (!serial) {
-        E = ilogb(lo);
-        serial = ilogb(hi) != E;
+    unsigned long long D = 0;
+    int listed = 0;
+    if (k < nu) {
+        // estimate of the chain before this unit: the 256-term block prefix, then
+        // the units of that block ahead of this one
+        const int c4 = wid >> 2;
+        double e_in = P.bpre[(int64_t)blockIdx.x * 4 + c4];
+        for (int q = 4 * c4; q < wid; ++q) e_in += s_ws[q];
+        const double lo = (e_in + (incl - a)) * (1.0 - P.margin), hi = (e_in + incl) * (1.0 + P.margin);
+        bool ok = valid && i != 0 && a >= 0.0 && a < INFINITY && lo >= 0x1p-1020 && hi < 0x1p1020;
+        const int E = ok ? ilogb(lo) : -4096;
+        ok = ok && ilogb(hi) == E;
+        long long r = 0;
+        if (ok) {
+            const double q = scaled(a, E);          // < 2^53: exact
+            ok = q - floor(q) != 0.5;               // a tie: the rounding depends on s
+            r = ok ? (long long)rint(q) : 0;
+        }
+        const unsigned long long vmask = __ballot(valid);
+        const int E0 = __builtin_amdgcn_readfirstlane(E);
+        if (k == 0) {
+            // the chain's first unit: its entry is known, so its values are evaluated
+            // here; the walk only sets the value after it
+            listed = 1;
+            double s0 = 0.0;
+            const double mine = chain_unit(a, __popcll(vmask), s0, true);
+            if (P.c && valid) P.c[i] = mine;
+            if (lane == 0) {
+                UnitRec rec;
+#pragma unroll
+                for (int g = 0; g < kChainSegs; ++g) {
+                    rec.meta[g] = 0;
+                    rec.val[g] = 0.0;
+                }
+                rec.meta[0] = __popcll(vmask) | 0x80;
+                rec.val[0] = s0;                     // the value after the unit (set, not added)
+                P.uinfo[k] = 1 | (1 << 3);
+                P.udelta[k] = 0;
+                P.urec[k] = rec;
+            }
+        } else if (__ballot(ok && E == E0) == vmask) {     // one translation
+            D = (unsigned long long)wave_sum_i64(r);
+            if (lane == 0) {
+                P.uinfo[k] = (E0 + 4096) << 2;
+                P.udelta[k] = (long long)D;
+            }
+        } else {
+            listed = 1;
+            const int okp = __shfl_up(ok ? 1 : 0, 1, 64), Ep = __shfl_up(E, 1, 64);
+            const bool start = valid && (lane == 0 || !ok || !okp || E != Ep);
+            unsigned long long sm = __ballot(start);
+            const unsigned long long okm = __ballot(ok);
+            const int nseg = __popcll(sm);
+            if (nseg > kChainSegs) {
+                if (lane == 0) {
+                    P.uinfo[k] = 3;
+                    P.udelta[k] = 0;
+                }
+            } else {
+                const long long ir = wave_incl_scan_i64(r);
+                const int cnt = __popcll(vmask);
+                UnitRec rec;
+#pragma unroll
+                for (int g = 0; g < kChainSegs; ++g) {
+                    rec.meta[g] = 0;
+                    rec.val[g] = 0.0;
+                    if (sm) {
+                        const int st = (int)__builtin_ctzll(sm);
+                        sm &= sm - 1;
+                        const int en = sm ? (int)__builtin_ctzll(sm) : cnt;
+                        if ((okm >> st) & 1ull) {
+                            const int Es = __builtin_amdgcn_readlane(E, st);
+                            rec.meta[g] = (en - st) | ((Es + 4096) << 8);
+                            const long long Dg = bcast_i64(ir, en - 1) - (st > 0 ? bcast_i64(ir, st - 1) : 0ll);
+                            rec.val[g] = (double)Dg * unit_ulp(Es);   // exact: D < 2^53
+                        } else {
+                            rec.meta[g] = 1 | 0x80;
+                            rec.val[g] = bcast(a, st);
+                        }
+                    }
+                }
+                if (lane == 0) {
+                    P.uinfo[k] = 1 | (nseg << 3);
+                    P.udelta[k] = 0;
+                    P.urec[k] = rec;
+                }
+            }
+        }
     }
-    long long r = 0;
-    if (!serial) {
-        const double q = scaled(a, E);         // < 2^53: exact
-        const double fq = floor(q);
-        serial = __any(q - fq == 0.5);         // a tie: rounding depends on s
-        r = (long long)rint(q);
-    }
-    const long long D = serial ? 0 : wave_sum_i64(r);
     if (lane == 0) {
-        P.uinfo[k] = serial ? 1 : ((E + 4096) << 1);
-        P.udelta[k] = D;
+        s_D[wid] = D;
+        s_f[wid] = listed;
+    }
+    __syncthreads();
+    if (t < kChainGroup) {
+        // the group's scan (16 values, lanes 0..15 of wave 0)
+        unsigned long long dx = 0;
+        int cx = 0;
+        unsigned mask = 0;
+        for (int q = 0; q < kChainGroup; ++q) {
+            if (q < t) dx += s_D[q];
+            if (q <= t) cx += s_f[q];
+            mask |= (unsigned)s_f[q] << q;
+        }
+        const int64_t kk = (int64_t)blockIdx.x * kChainGroup + t;
+        if (kk < nu) {
+            P.ugl[kk] = dx;
+            P.uol[kk] = cx;
+        }
+        if (t == kChainGroup - 1) {
+            P.bD[blockIdx.x] = dx + s_D[t];
+            P.bC[blockIdx.x] = cx;
+            P.bM[blockIdx.x] = mask;
+        }
     }
 }
 
-// One workgroup: the integer scan over units, then wave 0 walks the serial
-// units in order.  Writes the value after each serial unit (sout, by ordinal),
-// the chain's values inside serial units (prefix mode) and the total.
+__device__ __forceinline__ int seg_len(int32_t m) { return m & 0x7f; }
+__device__ __forceinline__ bool seg_serial(int32_t m) { return (m & 0x80) != 0; }
+__device__ __forceinline__ int seg_binade(int32_t m) { return (m >> 8) - 4096; }
+
+__device__ __forceinline__ int unit_nseg(int32_t info) { return (info >> 3) & 15; }
+
+// One workgroup.  (1) The scan over the groups' totals (k_chain_units), one
+// group per thread: bpd / bpc (exclusive translation sum and listed count
+// before each group) and the list of listed units in order.  (2) Wave 0 walks those in order,
+// 64 at a time (their table entries and segments loaded at once, one unit per
+// lane, then read lane by lane): the translation run before each is one exact
+// add, a segmented unit one add per segment, a unit of many segments
+// chain_unit.  Writes sentry / sout (the value before / after each), the
+// total, and in prefix mode (3) every value inside the non-translation units
+// (all waves, one unit each).
+constexpr int kWalkStage = 32;          // term-by-term units staged in LDS per batch
+
+// Optional phase timing of k_chain_walk (build with -DFS2_PHASE_TIMING; read back
+// with fs2_debug_chain_times): summed s_memtime cycles of wave 0 per phase, calls,
+// units walked, units evaluated term by term.
+#ifdef FS2_PHASE_TIMING
+__device__ unsigned long long g_chain[8];
+#define FS2_CHAIN_STAMP(k)                                                              \
+    do {                                                                                \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                     \
+        if (t == 0 && (k) > 0) atomicAdd(&g_chain[(k) - 1], t_ - ch_last);              \
+        ch_last = t_;                                                                   \
+    } while (0)
+#else
+#define FS2_CHAIN_STAMP(k) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
-    __shared__ unsigned long long s_d[16];
-    __shared__ int s_c[16];
+    __shared__ unsigned long long s_d[2][16];
+    __shared__ int s_c[2][16];
     __shared__ int s_nseq;
+    __shared__ unsigned long long s_dtot;
+    __shared__ double s_terms[kWalkStage][kUnit];     // term-by-term units of a batch: terms, then values
+    __shared__ double s_val[64][kChainSegs];           // the batch's segment values (wave 0)
+    __shared__ double s_run[64];                       // the translation run ahead of each
+    __shared__ int32_t s_inf[64], s_q[64];
     if (P.lazy && lazy_skip(P)) return;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+#ifdef FS2_PHASE_TIMING
+    unsigned long long ch_last = 0;
+#endif
+    FS2_CHAIN_STAMP(0);
     const int64_t nu = (P.n + kUnit - 1) / kUnit;
     if (nu == 0) {
         if (t == 0 && P.total) *P.total = 0.0;
         return;
     }
-    const int64_t per = (nu + 1023) / 1024;
-    const int64_t k0 = t * per, k1 = min(nu, k0 + per);
-    unsigned long long ds = 0;
-    int sc = 0;
-    for (int64_t k = k0; k < k1; ++k) {
-        ds += (unsigned long long)P.udelta[k];
-        sc += P.uinfo[k] & 1;
-    }
-    // exclusive scans over threads (wrapping uint64: differences inside a run are exact)
-    unsigned long long di = ds;
-    int ci = sc;
+    // (1) the scan over groups of kChainGroup units (one group per thread and step)
+    const int64_t ng = (nu + kChainGroup - 1) / kChainGroup;
+    unsigned long long carry = 0;
+    int ccount = 0;
+    for (int64_t j0 = 0; j0 < ng; j0 += 1024) {
+        const int64_t gi = j0 + t;
+        const bool in = gi < ng;
+        const unsigned long long d = in ? P.bD[gi] : 0ull;
+        const int f = in ? P.bC[gi] : 0;
+        const unsigned m = in ? P.bM[gi] : 0u;
+        const int b = (int)((j0 >> 10) & 1);
+        unsigned long long di = d;
+        int ci = f;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long v = __shfl_up(di, o, 64);
-        const int c = __shfl_up(ci, o, 64);
-        if (lane >= o) {
-            di += v;
-            ci += c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long v = __shfl_up(di, o, 64);
+            const int c = __shfl_up(ci, o, 64);
+            if (lane >= o) {
+                di += v;
+                ci += c;
+            }
         }
+        if (lane == 63) {
+            s_d[b][wid] = di;
+            s_c[b][wid] = ci;
+        }
+        __syncthreads();                          // s_d[b] is rewritten two steps later
+        unsigned long long dx = carry + di - d, tot = 0;
+        int cx = ccount + ci - f, ctot = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if (q < wid) {
+                dx += s_d[b][q];
+                cx += s_c[b][q];
+            }
+            tot += s_d[b][q];
+            ctot += s_c[b][q];
+        }
+        if (in) {
+            P.bpd[gi] = dx;
+            P.bpc[gi] = cx;
+            for (unsigned mm = m; mm; mm &= mm - 1) P.seql[cx++] = (int32_t)(gi * kChainGroup + __builtin_ctz(mm));
+        }
+        carry += tot;
+        ccount += ctot;
     }
-    if (lane == 63) {
-        s_d[wid] = di;
-        s_c[wid] = ci;
+    if (t == 0) {
+        s_nseq = ccount;
+        s_dtot = carry;
     }
     __syncthreads();
-    unsigned long long dx = di - ds;
-    int cx = ci - sc;
-    for (int q = 0; q < wid; ++q) {
-        dx += s_d[q];
-        cx += s_c[q];
-    }
-    if (t == 1023) s_nseq = cx + sc;
-    for (int64_t k = k0; k < k1; ++k) {
-        P.ug[k] = dx;
-        dx += (unsigned long long)P.udelta[k];
-        if (P.uinfo[k] & 1) P.seql[cx++] = (int32_t)k;
-        P.uord[k] = cx - 1;
-    }
-    __syncthreads();
-    if (wid != 0) return;
-    __threadfence_block();
     const int nseq = s_nseq;
-    double s = 0.0;
-    int64_t prev = -1;
-    // the next serial unit's terms are loaded one unit ahead
-    auto load_unit = [&](int o) -> double {
-        if (o >= nseq) return 0.0;
-        const int64_t i = (int64_t)P.seql[o] * kUnit + lane;
-        return i < P.n ? P.a[i] : 0.0;
-    };
-    double a = load_unit(0);
-    for (int o = 0; o < nseq; ++o) {
+    FS2_CHAIN_STAMP(1);
+#ifdef FS2_PHASE_TIMING
+    if (t == 0) {
+        atomicAdd(&g_chain[4], 1ull);
+        atomicAdd(&g_chain[5], (unsigned long long)nseq);
+    }
+#endif
+    // (2) 64 listed units at a time: every wave loads their table entries (one
+    // per lane); the term-by-term ones have their terms staged in LDS by all
+    // waves; wave 0 walks; then the staged values are written out
+    double s = 0.0;                                // the running value (wave 0)
+    unsigned long long gprev = 0;
+    int Eprev = 0;
+    for (int o0 = 0; o0 < nseq; o0 += 64) {
+        const int ol = o0 + lane;
+        int64_t q = 0;
+        unsigned long long g = 0;
+        int32_t info = 0, En = 0;
+        if (ol < nseq) {
+            q = P.seql[ol];
+            info = P.uinfo[q];
+            if (wid == 0) {
+                g = P.bpd[q / kChainGroup] + P.ugl[q];
+                En = (q + 1 < nu) ? unit_binade(P.uinfo[q + 1]) : 0;
+            }
+        }
+        const unsigned long long wsm = __ballot(ol < nseq && (info & 2));   // term by term
+        const int nb = min(64, nseq - o0);
+        // stage the term-by-term units' terms (the j-th of them into slot j % kWalkStage)
+        {
+            unsigned long long m = wsm;
+            for (int r = 0; m; ++r) {
+                const int j = (int)__builtin_ctzll(m);
+                m &= m - 1;
+                if (r % 16 != wid || r >= kWalkStage) continue;
+                const int64_t qj = (int64_t)__builtin_amdgcn_readlane((int)q, j);
+                const int64_t i = qj * kUnit + lane;
+                s_terms[r][lane] = (i < P.n) ? P.a[i] : 0.0;
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {
+            // the batch's table in LDS: each unit's segment values and the exact
+            // translation run ahead of it (from the previous listed unit's table
+            // entries, one lane back; the batch before for lane 0)
+            if (ol < nseq && !(info & 2)) {
+                const UnitRec rr = P.urec[q];
+#pragma unroll
+                for (int u = 0; u < kChainSegs; ++u) s_val[lane][u] = rr.val[u];
+            }
+            const unsigned long long gp = __shfl_up(g, 1, 64);
+            const int Ep = __shfl_up(En, 1, 64);
+            const unsigned long long gb = (lane == 0) ? gprev : gp;
+            const int Eb = (lane == 0) ? Eprev : Ep;
+            s_run[lane] = (ol > 0 && ol < nseq) ? (double)(long long)(g - gb) * unit_ulp(Eb) : 0.0;
+            s_inf[lane] = info;
+            s_q[lane] = (int32_t)q;
+            gprev = bcast_i64((long long)g, nb - 1);
+            Eprev = __builtin_amdgcn_readlane(En, nb - 1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            FS2_CHAIN_STAMP(2);
+            double my_entry = 0.0, my_out = 0.0;      // lane j keeps unit o0 + j's values
+            int r = 0;                                // term-by-term units seen
+            for (int j = 0; j < nb; ++j) {
+                const int32_t infoj = s_inf[j];
+                s = s + s_run[j];                     // the translation run between (exact)
+                if (lane == j) my_entry = s;
+                if (infoj & 2) {
+                    const int64_t qj = s_q[j];
+#ifdef FS2_PHASE_TIMING
+                    if (t == 0) atomicAdd(&g_chain[6], 1ull);
+#endif
+                    const int cnt = (int)min<int64_t>(kUnit, P.n - qj * kUnit);
+                    if (r < kWalkStage) {
+                        const double mine = chain_unit(s_terms[r][lane], cnt, s, qj == 0);
+                        s_terms[r][lane] = mine;
+                    } else {                          // beyond the stage: from memory
+                        const int64_t i = qj * kUnit + lane;
+                        const double a = (i < P.n) ? P.a[i] : 0.0;
+                        const double e = s;
+                        const double mine = chain_unit(a, cnt, s, qj == 0);
+                        if (P.c && lane < cnt) P.c[i] = mine;
+                        if (P.c && qj > 0 && lane == 0) P.c[qj * kUnit - 1] = e;
+                    }
+                    ++r;
+                } else {
+                    // one add per segment (unit 0: the value after it, set)
+                    const int ns = unit_nseg(infoj);
+                    double v[kChainSegs];
+#pragma unroll
+                    for (int u = 0; u < kChainSegs; ++u) v[u] = s_val[j][u];
+                    if (s_q[j] == 0) s = v[0];
+                    else {
+#pragma unroll
+                        for (int u = 0; u < kChainSegs; ++u)
+                            if (u < ns) s = s + v[u];
+                    }
+                }
+                if (lane == j) my_out = s;
+            }
+            if (lane < nb) {
+                P.sentry[o0 + lane] = my_entry;
+                P.sout[o0 + lane] = my_out;
+            }
+        }
+        if (!wsm && o0 + 64 >= nseq) break;      // nothing staged, no further batch
+        __syncthreads();
+        if (P.c) {
+            // the staged term-by-term units' values, and the value before each
+            unsigned long long m = wsm;
+            for (int r = 0; m; ++r) {
+                const int j = (int)__builtin_ctzll(m);
+                m &= m - 1;
+                if (r % 16 != wid || r >= kWalkStage) continue;
+                const int64_t qj = (int64_t)__builtin_amdgcn_readlane((int)q, j);
+                const int64_t i = qj * kUnit + lane;
+                if (i < P.n) P.c[i] = s_terms[r][lane];
+                if (qj > 0 && lane == 0) P.c[qj * kUnit - 1] = P.sentry[o0 + j];
+            }
+        }
+        __syncthreads();
+    }
+    FS2_CHAIN_STAMP(3);
+    if (wid == 0 && lane == 0 && P.total) {
+        // the chain ends in the translation run after the last listed unit (if any)
+        *P.total = s + (double)(long long)(s_dtot - gprev) * unit_ulp(Eprev);
+    }
+    if (!P.c) return;
+    __syncthreads();                             // sentry of the last batch
+    // (3) prefix mode: the values inside the segmented units, one unit per wave
+    for (int o = wid; o < nseq; o += 16) {
         const int64_t q = P.seql[o];
-        const double an = load_unit(o + 1);
-        if (prev >= 0 && q > prev + 1) {       // translation run prev+1 .. q-1
-            const int E = (P.uinfo[prev + 1] >> 1) - 4096;
-            const long long d = (long long)(P.ug[q] - P.ug[prev + 1]);
-            s = s + (double)d * unit_ulp(E);
-        }
+        const int32_t info = P.uinfo[q];
+        if ((info & 2) || q == 0) continue;              // written above / by k_chain_units
+        const UnitRec r = P.urec[q];
+        double sg = P.sentry[o];
         const int cnt = (int)min<int64_t>(kUnit, P.n - q * kUnit);
+        const int64_t i = q * kUnit + lane;
+        const double a = (i < P.n) ? P.a[i] : 0.0;
+        if (q > 0 && lane == 0) P.c[q * kUnit - 1] = sg;
         double mine = 0.0;
-        for (int j = 0; j < cnt; ++j) {
-            const double v = bcast(a, j);
-            s = (q == 0 && j == 0) ? v : s + v;
-            if (lane == j) mine = s;
+        int st = 0;
+#pragma unroll
+        for (int g = 0; g < kChainSegs; ++g) {
+            const int32_t m = r.meta[g];
+            const int len = seg_len(m);
+            if (len == 0) break;
+            const bool in = lane >= st && lane < st + len;
+            if (seg_serial(m)) {
+                if (in) mine = sg + a;
+                sg = sg + r.val[g];
+            } else {
+                const int E = seg_binade(m);
+                const double u = unit_ulp(E);
+                const long long pre = wave_incl_scan_i64(in ? (long long)rint(scaled(a, E)) : 0ll);
+                if (in) mine = sg + (double)pre * u;
+                sg = sg + r.val[g];
+            }
+            st += len;
         }
-        if (P.c && lane < cnt) P.c[q * kUnit + lane] = mine;
-        if (lane == 0) P.sout[o] = s;
-        prev = q;
-        a = an;
+        if (lane < cnt) P.c[i] = mine;
     }
-    if (lane == 0 && P.total) {
-        double tot = s;
-        if (prev < nu - 1) {                    // the chain ends in a translation run
-            const int E = (P.uinfo[prev + 1] >> 1) - 4096;
-            const long long d = (long long)(P.ug[nu - 1] + (unsigned long long)P.udelta[nu - 1] - P.ug[prev + 1]);
-            tot = s + (double)d * unit_ulp(E);
-        }
-        *P.total = tot;
-    }
-}
-
-// Prefix mode: the chain's values inside translation units.
-__global__ __launch_bounds__(kBlock) void k_chain_fill(const ChainParams P) {
-    if (P.lazy && lazy_skip(P)) return;
-    const int t = threadIdx.x, wid = t >> 6;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + t;
-    const int64_t k = (int64_t)blockIdx.x * (kBlock / kUnit) + wid;
-    const int64_t nu = (P.n + kUnit - 1) / kUnit;
-    if (k >= nu) return;
-    const int32_t info = P.uinfo[k];
-    if (info & 1) return;                       // serial units were written by the walk
-    const int E = (info >> 1) - 4096;
-    const int o = P.uord[k];
-    const int64_t q = P.seql[o];
-    const double u = unit_ulp(E);
-    const double s_in = P.sout[o] + (double)(long long)(P.ug[k] - P.ug[q + 1]) * u;
-    const double a = (i < P.n) ? P.a[i] : 0.0;
-    const long long pre = wave_incl_scan_i64((long long)rint(scaled(a, E)));
-    if (i < P.n) P.c[i] = s_in + (double)pre * u;
+    __syncthreads();
+    FS2_CHAIN_STAMP(4);
 }
 
 hipError_t launch_chain(const ChainParams &p, hipStream_t s) {
@@ -267,82 +480,175 @@ hipError_t launch_chain(const ChainParams &p, hipStream_t s) {
         if (p.total) hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
         return hipGetLastError();
     }
-    const unsigned nb = (unsigned)((p.n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_chain_bpre, dim3(1), dim3(1024), 0, s, p);
-    hipLaunchKernelGGL(k_chain_units, dim3(nb), dim3(kBlock), 0, s, p);
+    const unsigned ng = (unsigned)((p.n + 1023) / 1024);
+    if (!p.bpre_ready) hipLaunchKernelGGL(k_chain_bpre, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(k_chain_units, dim3(ng), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
-    if (p.c) hipLaunchKernelGGL(k_chain_fill, dim3(nb), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------- numpy sum of w^2 --
 
-// numpy pairwise summation of a[i]^2 (loops_utils.h.src: PW_BLOCKSIZE 128, 8
-// accumulators), recursive form; used for a partial last chunk.
-__device__ double np_pairwise_sq(const double *a, int64_t n) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int64_t i = 0; i < n; ++i) res += a[i] * a[i];
-        return res;
-    } else if (n <= 128) {
-        double r[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = a[k] * a[k];
-        int64_t i;
-        for (i = 8; i < n - (n % 8); i += 8) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) r[k] += a[i + k] * a[i + k];
+// numpy's recursion over n < 8192 elements (n > 128: halves at n/2 rounded down
+// to a multiple of 8) without recursion: thread 0 lists the leaves in order, the
+// workgroup sums them in parallel, thread 0 adds them back up the same tree.
+constexpr int kNpMaxLeaves = 256;
+
+struct NpFrame {
+    int off, n, stage;
+    double left;
+};
+
+__device__ void np_pairwise_partial(const double *a, int64_t n, double *out) {
+    __shared__ int s_off[kNpMaxLeaves], s_len[kNpMaxLeaves];
+    __shared__ double s_sum[kNpMaxLeaves];
+    __shared__ int s_nl;
+    __shared__ NpFrame st[16];             // thread 0's explicit stack (LDS, not scratch)
+    typedef NpFrame Frame;
+    if (threadIdx.x == 0) {
+        int top = 0, nl = 0;
+        st[0] = Frame{0, (int)n, 0, 0.0};
+        while (top >= 0) {
+            Frame &f = st[top];
+            if (f.n <= 128) {
+                s_off[nl] = f.off;
+                s_len[nl] = f.n;
+                ++nl;
+                --top;
+            } else {
+                int n2 = f.n / 2;
+                n2 -= n2 % 8;
+                const int off = f.off, nn = f.n;
+                --top;
+                st[++top] = Frame{off + n2, nn - n2, 0, 0.0};   // right after left
+                st[++top] = Frame{off, n2, 0, 0.0};
+            }
         }
-        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < n; ++i) res += a[i] * a[i];
-        return res;
+        s_nl = nl;
     }
-    int64_t n2 = n / 2;
-    n2 -= n2 % 8;
-    return np_pairwise_sq(a, n2) + np_pairwise_sq(a + n2, n - n2);
+    __syncthreads();
+    {
+        // 8 lanes per leaf (accumulator k of numpy's 8), all 16 loads issued at once;
+        // the leaf's remainder (n % 8) and leaves under 8 elements by lane k = 0
+        const int grp = threadIdx.x >> 3, k = threadIdx.x & 7, ngrp = blockDim.x >> 3;
+        for (int l0 = 0; l0 < s_nl; l0 += ngrp) {
+            const int l = l0 + grp;
+            const bool in = l < s_nl;
+            const int off = in ? s_off[l] : 0, len = in ? s_len[l] : 0;
+            const int full = len - len % 8;
+            double r = 0.0;
+            if (in && len >= 8) {
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = (8 * q + k < full) ? a[off + 8 * q + k] : 0.0;
+                r = v[0] * v[0];
+#pragma unroll
+                for (int q = 1; q < 16; ++q)
+                    if (8 * q + k < full) r += v[q] * v[q];
+            }
+            r += __shfl_xor(r, 1, 64);             // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+            r += __shfl_xor(r, 2, 64);
+            r += __shfl_xor(r, 4, 64);
+            if (in && k == 0) {
+                double res = (len < 8) ? 0.0 : r;
+                for (int e = (len < 8) ? 0 : full; e < len; ++e) res += a[off + e] * a[off + e];
+                s_sum[l] = res;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int top = 0, leaf = 0;
+        st[0] = Frame{0, (int)n, 0, 0.0};
+        double v = 0.0;
+        bool have = false;                 // v is a finished child value to hand up
+        while (top >= 0) {
+            Frame &f = st[top];
+            if (have) {
+                if (f.stage == 1) {
+                    f.left = v;
+                    f.stage = 2;
+                    have = false;
+                    int n2 = f.n / 2;
+                    n2 -= n2 % 8;
+                    st[top + 1] = Frame{f.off + n2, f.n - n2, 0, 0.0};
+                    ++top;
+                } else {                   // stage 2: both halves done
+                    v = f.left + v;
+                    --top;
+                }
+                continue;
+            }
+            if (f.n <= 128) {
+                v = s_sum[leaf++];
+                have = true;
+                --top;
+            } else {
+                int n2 = f.n / 2;
+                n2 -= n2 % 8;
+                f.stage = 1;
+                st[top + 1] = Frame{f.off, n2, 0, 0.0};
+                ++top;
+            }
+        }
+        *out = v;
+    }
 }
 
-// One wave per 8192-element chunk -> part[chunk].
-__global__ __launch_bounds__(64) void k_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy) {
+// One 512-thread workgroup per 8192-element chunk -> part[chunk]: wave b sums
+// leaves 8b .. 8b+7 (8 lanes per leaf, one accumulator each), the 64 leaf sums
+// meet in LDS and wave 0 adds them as the balanced tree.
+__global__ __launch_bounds__(512) void k_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy) {
+    __shared__ double s_leaf[64];
     if (lazy && !lazy->resampled) return;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, bt = t >> 6;
     const int64_t c0 = (int64_t)blockIdx.x * kNpChunk;
-    const int64_t m = min<int64_t>(kNpChunk, n - c0);
-    if (m < kNpChunk) {
-        if (lane == 0) part[blockIdx.x] = np_pairwise_sq(w + c0, m);
-        return;
-    }
-    // lane = 8 * g + k: accumulator k of leaf 8 * batch + g
+    // lane = 8 g + k: accumulator k of leaf 8 bt + g (elements k, k+8, ..., k+120)
     const int g = lane >> 3, k = lane & 7;
-    double leaf = 0.0;                         // lane l ends up holding leaf l's sum
-#pragma unroll 1
-    for (int bt = 0; bt < 8; ++bt) {
-        const double *p = w + c0 + (int64_t)(8 * bt + g) * 128 + k;
-        double v[16];
+    const double *p = w + c0 + (int64_t)(8 * bt + g) * 128 + k;
+    double v[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = p[8 * q];
-        double r = v[0] * v[0];
+    for (int q = 0; q < 16; ++q) v[q] = p[8 * q];
+    double r = v[0] * v[0];
 #pragma unroll
-        for (int q = 1; q < 16; ++q) r += v[q] * v[q];
-        r += __shfl_xor(r, 1, 64);             // (r0 + r1), (r2 + r3), ...
-        r += __shfl_xor(r, 2, 64);             // ((r0 + r1) + (r2 + r3)), ...
-        r += __shfl_xor(r, 4, 64);
-        // leaf 8 * bt + g's sum sits in lanes 8g .. 8g+7; lane 8 bt + g takes it
-        const double got = __shfl(r, 8 * ((lane - 8 * bt) & 7), 64);
-        if ((lane >> 3) == bt) leaf = got;
+    for (int q = 1; q < 16; ++q) r += v[q] * v[q];
+    r += __shfl_xor(r, 1, 64);                 // (r0 + r1), (r2 + r3), ...
+    r += __shfl_xor(r, 2, 64);                 // ((r0 + r1) + (r2 + r3)), ...
+    r += __shfl_xor(r, 4, 64);
+    if (k == 0) s_leaf[8 * bt + g] = r;
+    __syncthreads();
+    if (bt == 0) {
+        double leaf = s_leaf[lane];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) leaf += __shfl_xor(leaf, o, 64);   // leaves in order, balanced
+        if (lane == 0) part[blockIdx.x] = leaf;
     }
-    // balanced tree over the 64 leaves in order
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) leaf += __shfl_xor(leaf, o, 64);
-    if (lane == 0) part[blockIdx.x] = leaf;
+}
+
+// The partial last chunk (its own launch: the explicit stacks live in scratch).
+__global__ __launch_bounds__(256) void k_np_sumsq_tail(const double *w, int64_t n, double *part, const DevStats *lazy) {
+    if (lazy && !lazy->resampled) return;
+    const int64_t full = n / kNpChunk;
+    np_pairwise_partial(w + full * kNpChunk, n - full * kNpChunk, part + full);
 }
 
 hipError_t launch_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy, hipStream_t s) {
-    const int64_t nc = (n + kNpChunk - 1) / kNpChunk;
-    if (nc == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_np_sumsq, dim3((unsigned)nc), dim3(64), 0, s, w, n, part, lazy);
+    const int64_t full = n / kNpChunk;
+    if (full > 0) hipLaunchKernelGGL(k_np_sumsq, dim3((unsigned)full), dim3(512), 0, s, w, n, part, lazy);
+    if (n % kNpChunk) hipLaunchKernelGGL(k_np_sumsq_tail, dim3(1), dim3(256), 0, s, w, n, part, lazy);
     return hipGetLastError();
 }
+
+#ifdef FS2_PHASE_TIMING
+hipError_t debug_chain_times(unsigned long long out[8], int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_chain), z, sizeof z);
+    }
+    return e;
+}
+#endif
 
 int64_t np_sumsq_chunks(int64_t n) { return (n + kNpChunk - 1) / kNpChunk; }
 

@@ -50,10 +50,10 @@ constexpr uint32_t kSumOpen = 0xff00ff00u;   // unbounded box: never rejected
 // Counters of the update pass, kept per workgroup (cpart[counter][block]: the
 // first pass of a scan stores them, later passes add) and folded into DevStats
 // by k_wsum: no same-address atomics on the hot kernels.
-// k_candidates adds [kCWords, kCVisited], k_update [kCVisited, kCSingular].
+// k_candidates adds [kCWords, kCOpened], k_update [kCVisited, kCSingular].
 enum : int {
-    kCWords, kCGroups, kCVisited, kCCandidates, kCWritten, kCAmbiguous, kCAppends, kCHits, kCCow, kCNew,
-    kCSingular, kNumCounters
+    kCWords, kCGroups, kCVisited, kCOpened, kCCandidates, kCWritten, kCAmbiguous, kCAppends, kCHits, kCCow, kCNew,
+    kCRefVisits, kCSingular, kNumCounters
 };
 
 // Device statistics of one scan (zeroed before every scan).
@@ -81,6 +81,9 @@ struct DevStats {
     int32_t pad2;
     unsigned long long reduce_amb;   // tree reductions: resample boundaries / the N_eff rule within
                                      // the rounding bound of the reference's summation order
+    unsigned long long opened;       // pages whose mirrors k_candidates loaded
+    unsigned long long ref_visits;   // landmarks the reference's first-match scan reads (j + 1 on a
+                                     // match, the map size on an append)
 };
 
 // Per-rank record all-gathered once per scan (and once more after a resample).
@@ -195,6 +198,8 @@ struct ReduceParams {
     int32_t n_np;            // their count
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
+    double *bpre_w;          // exact: k_wsum writes the exclusive scan of wpart here
+    double *bpre_n;          // exact: k_finalize writes the exclusive scan of part_w here
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
     uint64_t seed, scan;
     DevStats *stats;
@@ -202,6 +207,18 @@ struct ReduceParams {
     const RankRecord *recs;  // all ranks' records (== rec when world == 1)
     const double *totals;    // all ranks' weight totals (world > 1)
     int32_t world, rank;
+};
+
+// The unit table of an evaluated chain (fs2_exact.hip k_chain_walk), as the
+// resample's range kernel reads it to evaluate the running sum in place.
+struct ChainView {
+    const int32_t *uinfo;             // [nu] bit 0: listed (values in c), else binade
+    const unsigned long long *ugl;    // [nu] exclusive translation sum inside the unit's group
+    const int32_t *uol;               // [nu] listed units of the group up to and including k
+    const unsigned long long *bpd;    // [ng] exclusive translation sum before each group
+    const int32_t *bpc;               // [ng] listed units before each group
+    const int32_t *seql;              // listed units in order
+    const double *sout;               // chain value after each listed unit
 };
 
 // Resample of a shard of n particles / n outputs starting at global index a.
@@ -215,6 +232,8 @@ struct ResampleParams {
     int32_t nblk;            // 1024-element blocks
     int32_t lazy;            // prefix kernels run only when the resample rule fired
     double flip_margin;      // tree prefix: relative rounding bound counted in reduce_amb (0: off)
+    int32_t use_chain;       // running sum from the exact chain's units (c: serial units only)
+    ChainView chain;
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
     const double *x, *y, *yaw;
@@ -242,6 +261,18 @@ struct ResampleParams {
     RecvPeer peers[kMaxRanks];
 };
 
+// A 64-term chain unit that is not one translation, as up to kChainSegs
+// segments in order (fs2_exact.hip): meta = length (bits 0-6) | serial (bit 7) |
+// (binade + 4096) << 8, 0 past the last segment; val = what the segment adds to
+// the chain (a translation D * ulp, exact; a serial term), or for the chain's
+// first unit the value after it.
+constexpr int kChainSegs = 8;
+constexpr int kChainGroup = 16;    // units per k_chain_units workgroup (1024 terms)
+struct UnitRec {
+    int32_t meta[kChainSegs];
+    double val[kChainSegs];
+};
+
 // The reference's sequential sum / running sum of a[0..n) (a >= 0), in parallel
 // and bit-exactly (fs2_exact.hip): s_0 = a_0, s_k = fl(s_{k-1} + a_k).
 struct ChainParams {
@@ -251,10 +282,20 @@ struct ChainParams {
     double *bpre;            // [nb] their exclusive prefix (written)
     int32_t nb;
     int32_t lazy;            // run only when stats->resampled
-    int32_t *uinfo;          // [nu] per 64-element unit: bit 0 serial, else (binade + 4096) << 1
+    int32_t bpre_ready;      // bpre was written by an earlier kernel (k_wsum / k_finalize)
+    int32_t *uinfo;          // [nu] per 64-term unit: (binade + 4096) << 2 for a translation; bit 0:
+                             // listed: segments (UnitRec, count in bits 3-6), or bit 1: evaluated
+                             // term by term (chain_unit)
+    UnitRec *urec;           // [nu] segments of the units with uinfo bit 0
+    double *sentry;          // [nu] chain value before each non-translation unit (by ordinal)
     long long *udelta;       // [nu] translation in ulps of the unit's binade
-    unsigned long long *ug;  // [nu] exclusive scan of udelta
-    int32_t *uord;           // [nu] ordinal of the last serial unit <= k
+    unsigned long long *ugl; // [nu] exclusive scan of udelta inside each group of kChainGroup units
+    int32_t *uol;            // [nu] listed units of the group up to and including k
+    unsigned long long *bD;  // [ng] per group: translation sum
+    int32_t *bC;             // [ng]            listed units
+    uint32_t *bM;            // [ng]            listed-unit mask
+    unsigned long long *bpd; // [ng] exclusive scans of bD / bC (k_chain_walk)
+    int32_t *bpc;
     int32_t *seql;           // [nu] serial units in order
     double *sout;            // [nu] chain value after each serial unit (by ordinal)
     double *c;               // nullable: the chain's values (prefix mode)
@@ -296,6 +337,7 @@ hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, De
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset);
 hipError_t debug_icp_phase_times(unsigned long long out[4], int reset);
+hipError_t debug_chain_times(unsigned long long out[8], int reset);
 #endif
 // particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
 // alloc.rbase + p * lm_cap + j

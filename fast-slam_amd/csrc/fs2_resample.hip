@@ -17,7 +17,7 @@
 // keeps the source's map; every other output (extra copies, particles received
 // from another rank) takes over the map of a local particle that feeds no
 // local output, whose landmarks were already packed if another rank needs them.
-#include "fs2_reduce.hpp"
+#include "fs2_chain.hpp"
 
 namespace fs2 {
 
@@ -66,22 +66,43 @@ __device__ void global_finalize_body(const ReduceParams &P);
 
 // This rank's record: sum w'^2, first maximum, its pose, normalised total (on
 // one GPU also the global decision, k_global_finalize's work).
+constexpr int kNpStage = 1024;
+
 __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
     __shared__ int lds_i[16];
+    __shared__ double s_np[kNpStage];
+    if (P.exact && threadIdx.x < P.n_np && threadIdx.x < kNpStage) s_np[threadIdx.x] = P.np_part[threadIdx.x];
     double sq = 0.0;
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
     int mc = 0;
-    for (int k = threadIdx.x; k < P.nparts; k += 1024) {
-        sq += P.part_sq[k];
-        argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
-        mc = max(mc, P.part_maxcnt[k]);
+    for (int k0 = threadIdx.x; k0 < P.nparts; k0 += 4 * 1024) {
+        double s4[4], w4[4];                       // 4 parts' loads in flight per thread
+        int64_t i4[4];
+        int m4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + 1024 * u;
+            const bool in = k < P.nparts;
+            s4[u] = in ? P.part_sq[k] : 0.0;
+            w4[u] = in ? P.part_best_w[k] : -INFINITY;
+            i4[u] = in ? P.part_best_i[k] : INT64_MAX;
+            m4[u] = in ? P.part_maxcnt[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            sq += s4[u];
+            argmax_combine(bv, bi, w4[u], i4[u]);
+            mc = max(mc, m4[u]);
+        }
     }
     sq = block_sum<1024>(sq, lds_d);
     block_argmax<1024>(bv, bi, lds_d, lds_l);
     mc = block_max_i<1024>(mc, lds_i);
+    // exact mode: estimates of the running sum at every block start (fs2_exact.hip)
+    if (P.bpre_n) block_excl_scan_1024(P.part_w, P.bpre_n, P.nparts, lds_d);
     if (threadIdx.x == 0) {
         if (P.sequential) {
             // np.sum(weights ** 2): pairwise inside 8192-element chunks
@@ -93,9 +114,20 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
             }
             sq = s;
         } else if (P.exact) {
-            // the same sums, each chunk's tree evaluated by k_np_sumsq
+            // the same sums, each chunk's tree evaluated by k_np_sumsq (staged in
+            // LDS above), added in order
             double s = 0.0;
-            for (int k = 0; k < P.n_np; ++k) s = (k == 0) ? P.np_part[0] : s + P.np_part[k];
+            for (int k0 = 0; k0 < P.n_np; k0 += 8) {
+                double v[8];                       // 8 loads in flight, then 8 adds in order
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = k0 + u;
+                    v[u] = (k >= P.n_np) ? 0.0 : (k < kNpStage ? s_np[k] : P.np_part[k]);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (k0 + u < P.n_np) s = (k0 + u == 0) ? v[u] : s + v[u];
+            }
             sq = s;
         }
         RankRecord r{};
@@ -367,14 +399,35 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     __shared__ unsigned long long lds_u[kBlock / 64];
     int omin = INT32_MAX, omax = -1;
     unsigned amb = 0;
+    // exact chain (one GPU): the running sum of this wave's unit from the unit
+    // table -- a translation unit's values are s_in + (prefix of rint(w / u)) u,
+    // a serial unit's were written by k_chain_walk (with the value before it)
+    double cv = 0.0, cprev = 0.0;
+    if (P.use_chain) {
+        const int64_t k = i / kUnit;
+        const int32_t info = (k * kUnit < P.n) ? P.chain.uinfo[k] : 1;
+        if (info & 1) {
+            cv = (i < P.n) ? P.c[i] : 0.0;
+            cprev = (i > 0 && i - 1 < P.n) ? P.c[i - 1] : 0.0;
+        } else {
+            const int E = unit_binade(info);
+            const double u = unit_ulp(E);
+            const double s_in = chain_unit_entry(P.chain, k, E);
+            const long long r = (i < P.n) ? (long long)rint(scaled(P.w[i], E)) : 0;
+            const long long pre = wave_incl_scan_i64(r);
+            cv = s_in + (double)pre * u;
+            cprev = s_in + (double)(pre - r) * u;
+        }
+    }
     if (i < P.n) {
         const double u0 = P.stats->u0, off = P.stats->offset;
         const int64_t g = P.a + i;
-        const double cur = (P.a == 0) ? P.c[i] : off + P.c[i];
+        const double cur = P.use_chain ? cv : ((P.a == 0) ? P.c[i] : off + P.c[i]);
         int64_t lo;
         if (g == 0) lo = 0;
         else {
-            const double prev = (i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1]);
+            const double prev = P.use_chain ? cprev
+                                            : ((i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1]));
             lo = first_above(prev, u0, P.N);
         }
         const int64_t hi = (g == P.N - 1) ? P.N - 1 : first_above(cur, u0, P.N) - 1;

@@ -20,7 +20,7 @@
 //   k_scan_*, k_resample_src, k_plan_*, k_copy_maps, k_gather_particles,
 //   k_estimate      low-variance resample (:177-199);
 //   k_import/k_export, k_fill, k_iota.
-#include "fs2_reduce.hpp"
+#include "fs2_chain.hpp"
 
 namespace fs2 {
 
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     // entry (a global store inside the walk would serialise the prefetch, since
     // vmcnt counts loads and stores in issue order)
     int nc = 0;
-    unsigned visited = 0, groups = 0;
+    unsigned visited = 0, groups = 0, opened = 0;
 
     // Page g: its descriptor's box codes are tested against every measurement's
     // band first (integer compares; the next descriptors already in flight);
@@ -183,7 +183,10 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         float4 mir[kScanGroup];
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
-        if (om) test_page(mir, g, om);
+        if (om) {
+            ++opened;
+            test_page(mir, g, om);
+        }
     }
     if (live) {
         P.ncand[i] = nc;
@@ -191,9 +194,10 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         for (int q = 0; q < kMaxCand; ++q)
             if (q < nc) P.cand[(int64_t)q * n + i] = s_list[q][tid];
     }
-    const unsigned cv[3] = {(unsigned)min(nc, kMaxCand), groups, visited};   // kCWords, kCGroups, kCVisited
+    // kCWords, kCGroups, kCVisited, kCOpened
+    const unsigned cv[4] = {(unsigned)min(nc, kMaxCand), groups, visited, opened};
     // the first pass of a scan stores its counters, later passes add
-    block_counters<kBlock, kCWords, 3>(cv, P.cpart, P.nblk, blk, P.k0 == 0 ? 0xffffffffu : 0u, 0.0, nullptr);
+    block_counters<kBlock, kCWords, 4>(cv, P.cpart, P.nblk, blk, P.k0 == 0 ? 0xffffffffu : 0u, 0.0, nullptr);
 }
 
 template <int K>
@@ -559,14 +563,20 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     c += nap;
 
     FS2_PHASE(5);
-    // likelihoods in measurement order (fast_slam_2.py:159)
-    unsigned hits = 0;
+    // likelihoods in measurement order (fast_slam_2.py:159); the reference's
+    // first-match scan reads j + 1 landmarks for a match at j, the whole map
+    // (as it stood) for an append
+    unsigned hits = 0, refv = 0, napp = 0;
 #pragma unroll
     for (int k = 0; k < MAXM; ++k) {
         const int ix = s_idx[k][tid];
         if (ix >= 0) {
             w *= s_lik[k][tid];
             ++hits;
+            refv += (unsigned)ix + 1u;
+        } else if (ix == -1) {
+            refv += (unsigned)(c - nap + napp);
+            ++napp;
         }
         if (live && P.assoc && k < P.m) P.assoc[(int64_t)(P.k0 + k) * n + i] = ix;
     }
@@ -584,11 +594,12 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     FS2_PHASE(6);
     // ---- block statistics (every counter) and the weight partial.  The first
     // pass stores, except the counters k_candidates already stored for it ----
-    const unsigned cv[kNumCounters] = {0u, 0u, visited, candidates, written, amb, appends, hits, cow, fresh,
-                                       singular ? 1u : 0u};
-    const unsigned assign = P.k0 != 0 ? 0u
-                                       : (P.filter ? ~((1u << kCWords) | (1u << kCGroups) | (1u << kCVisited))
-                                                   : 0xffffffffu);
+    const unsigned cv[kNumCounters] = {0u, 0u, visited, 0u, candidates, written, amb, appends, hits, cow, fresh,
+                                       refv, singular ? 1u : 0u};
+    const unsigned assign =
+        P.k0 != 0 ? 0u
+                  : (P.filter ? ~((1u << kCWords) | (1u << kCGroups) | (1u << kCVisited) | (1u << kCOpened))
+                              : 0xffffffffu);
     block_counters<kBlock, 0, kNumCounters>(cv, P.cpart, P.nblk, blk, assign, live ? w : 0.0,
                                             P.last_pass ? P.wpart + blk : nullptr);
     lower_slb(map.slb, smin_w);
@@ -622,6 +633,8 @@ __device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k
         case kCAppends: return &st->appends;
         case kCHits: return &st->hits;
         case kCCow: return &st->cow_pages;
+        case kCOpened: return &st->opened;
+        case kCRefVisits: return &st->ref_visits;
         default: return &st->new_pages;
     }
 }
@@ -673,6 +686,8 @@ __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
         }
         return;
     }
+    // exact mode: the block sums' exclusive scan, the chain's estimates (fs2_exact.hip)
+    if (P.bpre_w) block_excl_scan_1024(P.wpart, P.bpre_w, P.nwpart, lds);
     double v = 0.0;
     for (int k = threadIdx.x; k < P.nwpart; k += 1024) v += P.wpart[k];
     const double t = block_sum<1024>(v, lds);

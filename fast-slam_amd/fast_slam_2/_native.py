@@ -78,6 +78,8 @@ class fs2_iter_stats(C.Structure):
         ("new_pages", C.c_uint64),
         ("collections", C.c_uint64),
         ("pool_pages", C.c_uint64),
+        ("pages_opened", C.c_uint64),
+        ("reference_visits", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -123,6 +125,7 @@ _H = C.c_void_p
 # (name, restype, argtypes) for every entry point declared in include/fs2.h
 SIGNATURES = [
     ("fs2_abi_version", C.c_int32, []),
+    ("fs2_build_id", C.c_char_p, []),
     ("fs2_config_default", None, [C.POINTER(fs2_config)]),
     ("fs2_create", C.c_int, [C.POINTER(fs2_config), C.POINTER(_H)]),
     ("fs2_destroy", None, [_H]),

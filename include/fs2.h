@@ -114,7 +114,12 @@ typedef struct fs2_iter_stats {
     uint64_t cow_pages;         /* shared 8-slot pages copied before their first write */
     uint64_t new_pages;         /* fresh pages (appends, maps received from other ranks) */
     uint64_t collections;       /* page-pool collections so far (handle lifetime) */
-    uint64_t pool_pages;        /* pages in the pool (512 B each) */
+    uint64_t pool_pages;        /* pages in the pool (128 B each) */
+    uint64_t pages_opened;      /* pages whose 8 gate mirrors the candidate stream loaded
+                                   (the rest were rejected from their descriptor) */
+    uint64_t reference_visits;  /* landmarks the reference's first-match scan would read:
+                                   j + 1 for a match at j, the map size for an append
+                                   (landmark_utils.py:103-117; SURVEY §8d's V) */
 } fs2_iter_stats;
 
 typedef struct fs2_profile {
@@ -135,6 +140,10 @@ typedef struct fs2_profile {
 /* ---------------------------------------------------------------- core ---- */
 
 int32_t fs2_abi_version(void);
+
+/* Hash of the sources and flags this library was built from (fast-slam_amd/build.py
+ * source_id): the tests refuse a library whose id is not that of the tree they run in. */
+const char *fs2_build_id(void);
 
 /* Fills cfg with the reference's config.py defaults (NUM_PARTICLES=20, ...). */
 void fs2_config_default(fs2_config *cfg);

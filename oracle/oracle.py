@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# ORACLE_LIB selects another build of the same sources (the sanitizer build)
+LIB_PATH = os.environ.get("ORACLE_LIB", os.path.join(HERE, "_build", "liboracle.so"))
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -33,7 +34,8 @@ def build(force: bool = False) -> str:
     srcs = [os.path.join(HERE, f) for f in ("fs2_oracle.c", "fs2_frontend_oracle.c", "Makefile")]
     if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(s)
                                                     for s in srcs):
-        subprocess.run(["make", "-s", "-C", HERE], check=True)
+        target = os.path.relpath(LIB_PATH, HERE) if os.path.dirname(LIB_PATH).startswith(HERE) else ""
+        subprocess.run(["make", "-s", "-C", HERE] + ([target] if target else []), check=True)
     return LIB_PATH
 
 

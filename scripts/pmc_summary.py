@@ -41,16 +41,25 @@ def read(pattern, counter):
 def main():
     out_dir, workload, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     cal, _ = read(f"{out_dir}/pmc_cal/**/*counter_collection.csv", "FETCH_SIZE")
-    soa = cal.get("k_soa", [])
-    # k_soa streams 2^20 particles x 512 slots x 16 B = 2^33 B per launch
-    cal_bytes = float(os.environ.get("PMC_CAL_BYTES", 8589934592))
-    fetch_factor = cal_bytes / (sum(soa) / len(soa) * 1024) if soa else 2.0
+    # known bytes per launch (scripts/ubench_layout.hip): k_soa streams 2^20 x 512 x 16 B
+    # (16 B/lane), k_desc8 2^20 x 512 x 8 B (8 B/lane: the descriptor stream), k_lines128
+    # 2^23 distinct random 128-B lines read 16 B/lane (page opens)
+    known = {"k_soa": 2.0 ** 33, "k_desc8": 2.0 ** 32, "k_lines128": 2.0 ** 30}
+    factors = {k: known[k] / (sum(v) / len(v) * 1024) for k, v in cal.items() if k in known and v}
+    fetch_factor = factors.get("k_soa", 2.0)
     fetch, fdur = read(f"{out_dir}/pmc_fetch/**/*counter_collection.csv", "FETCH_SIZE")
     write, _ = read(f"{out_dir}/pmc_write/**/*counter_collection.csv", "WRITE_SIZE")
-    res = {"workload": workload, "fetch_factor_measured": fetch_factor, "fetch_factor_used": 2.0}
-    lines = [f"PMC summary {tag} workload={workload}",
-             f"FETCH_SIZE calibration on k_soa (known {cal_bytes:.3e} B): factor {fetch_factor:.4f} "
-             f"(guide: 2.0 for 16 B/lane streaming reads)",
+    sys.path.insert(0, os.path.join(REPO, "fast-slam_amd"))
+    import build
+    import subprocess
+    head = subprocess.run(["git", "-C", REPO, "rev-parse", "--short", "HEAD"], capture_output=True,
+                          text=True).stdout.strip()
+    res = {"workload": workload, "source_id": build.source_id(), "source": f"{tag} (HEAD {head})",
+           "fetch_factor_measured": fetch_factor, "fetch_factors": factors, "fetch_factor_used": 2.0}
+    lines = [f"PMC summary {tag} workload={workload} (HEAD {head}, libfs2 {build.source_id()})",
+             "FETCH_SIZE calibration (known bytes / FETCH_SIZE bytes): " +
+             ", ".join(f"{k} {v:.4f}" for k, v in sorted(factors.items())) +
+             " (guide: 2.0 for 16 B/lane streaming reads)",
              f"{'kernel':<22}{'launches':>9}{'fetch GB':>11}{'write GB':>11}{'hbm GB':>10}{'avg ms':>9}"]
     for k in sorted(set(fetch) | set(write)):
         f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1) * 1024 * 2.0

@@ -70,6 +70,41 @@ __global__ __launch_bounds__(256) void k_aosdma(const float4 *d, int64_t n, int 
     if (i < n) out[i] = acc;
 }
 
+// FETCH_SIZE calibration for the access shapes of k_candidates: the descriptor
+// stream ([row][particle] 8-byte entries, 512 B per wave-instruction) and page
+// opens (one random 128-byte line per lane, read as 8 x 16 B), each byte
+// fetched exactly once (a bijective line permutation over a table far beyond L2
+// and the Infinity Cache).
+__global__ __launch_bounds__(256) void k_desc8(const uint2 *d, int64_t n, int rows, unsigned *out) {
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    unsigned acc = 0;
+    for (int r = 0; r < rows; r += 4) {
+        uint2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = d[(int64_t)(r + u) * n + i];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u].x ^ v[u].y;
+    }
+    out[i] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_lines128(const float4 *d, int64_t n, int per, int64_t nlines, float *out) {
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float acc = 0.f;
+    for (int r = 0; r < per; ++r) {
+        const uint64_t line = ((uint64_t)(i * per + r) * 2654435761ull) & (uint64_t)(nlines - 1);
+        const float4 *p = d + line * 8;
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u].x * v[u].y + v[u].z;
+    }
+    out[i] = acc;
+}
+
 int main() {
     const int64_t n = 1 << 20;
     const int S = 512;
@@ -98,5 +133,30 @@ int main() {
             ms /= 5;
             printf("%-7s rep %d: %.3f ms  %.0f GB/s\n", names[k], rep, ms, bytes / (ms * 1e-3) / 1e9);
         }
+    {   // calibration kernels (run once each after a warm-up)
+        const int rows = 512;
+        hipLaunchKernelGGL(k_desc8, dim3(n / 256), dim3(256), 0, 0, (const uint2 *)d, n, rows, (unsigned *)o);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_desc8, dim3(n / 256), dim3(256), 0, 0, (const uint2 *)d, n, rows, (unsigned *)o);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("desc8   : %.3f ms  %.0f GB/s (%zu B)\n", ms, (double)n * rows * 8 / (ms * 1e-3) / 1e9,
+               (size_t)n * rows * 8);
+        const int per = 8;
+        const int64_t nlines = (int64_t)bytes / 128;        // 2^26 lines = 8 GiB
+        hipLaunchKernelGGL(k_lines128, dim3(n / 256), dim3(256), 0, 0, d, n, per, nlines, o);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_lines128, dim3(n / 256), dim3(256), 0, 0, d, n, per, nlines, o);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("lines128: %.3f ms  %.0f GB/s (%zu B)\n", ms, (double)n * per * 128 / (ms * 1e-3) / 1e9,
+               (size_t)n * per * 128);
+    }
     return 0;
 }

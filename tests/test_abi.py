@@ -82,3 +82,37 @@ def test_no_cpu_fallback():
         fast_slam_2.FastSLAM2(10)
     with pytest.raises(FS2Error):
         fast_slam_2.LineFilter.filter(np.zeros((4, 2)))
+
+
+def test_build_id_is_source_hash():
+    """fs2_build_id names the sources the library was built from (build.source_id)."""
+    import build
+    from fast_slam_2 import _native
+    build.build()
+    assert _native.load().fs2_build_id().decode() == build.source_id()
+
+
+def test_struct_sizes_match_c_compiler():
+    """sizeof / offsetof of the ABI structs as gcc lays out include/fs2.h equal the
+    ctypes mirrors (a field added on one side only would shift everything after it)."""
+    import subprocess
+    import tempfile
+    from fast_slam_2 import _native
+    structs = [("fs2_config", _native.fs2_config), ("fs2_iter_stats", _native.fs2_iter_stats),
+               ("fs2_profile", _native.fs2_profile), ("fs2_frontend_out", _native.fs2_frontend_out)]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fs2.h"', "int main(void) {"]
+    for cname, py in structs:
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        open(src, "w").write("\n".join(lines))
+        subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), src, "-o", exe], check=True)
+        out = dict(l.rsplit(" ", 1) for l in subprocess.run([exe], capture_output=True, text=True,
+                                                             check=True).stdout.splitlines())
+    for cname, py in structs:
+        assert int(out[cname]) == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(out[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)

@@ -10,58 +10,85 @@ UNIT = 64
 
 
 def model_chain(a):
+    """fs2_exact.hip: k_chain_units (per-term binade estimates -> one translation,
+    up to 4 segments, or term by term), k_chain_walk and its prefix post-pass."""
     n = len(a)
     nb = (n + 255) // 256
     bsum = np.array([a[b * 256:(b + 1) * 256].sum() for b in range(nb)])   # any order
     bpre = np.concatenate([[0.0], np.cumsum(bsum)[:-1]])
     margin = math.ldexp(2.0 * n + 8192.0, -53)
     nu = (n + UNIT - 1) // UNIT
-    info, delta = [], []
+    units = []
     for k in range(nu):
         seg = a[k * UNIT:(k + 1) * UNIT]
         b = k // 4
         e_in = bpre[b] + sum(a[b * 256 + q * UNIT:b * 256 + (q + 1) * UNIT].sum() for q in range(k % 4))
-        e_out = e_in + seg.sum()
-        lo, hi = e_in * (1 - margin), e_out * (1 + margin)
-        serial = k == 0 or not np.all((seg >= 0) & np.isfinite(seg)) or not (lo >= 2.0 ** -1020) \
-            or not (hi < 2.0 ** 1020)
-        E = 0
-        if not serial:
-            E = math.frexp(lo)[1] - 1
-            serial = (math.frexp(hi)[1] - 1) != E
-        D = 0
-        if not serial:
-            q = np.ldexp(seg, 52 - E)
-            serial = bool(np.any(q - np.floor(q) == 0.5))
-            D = int(np.rint(q).astype(np.int64).sum())
-        info.append((serial, E))
-        delta.append(0 if serial else D)
+        incl = e_in + np.cumsum(seg)
+        lo, hi = (incl - seg) * (1 - margin), incl * (1 + margin)
+        ok, E, r = [], [], []
+        for j, v in enumerate(seg):
+            o = k * UNIT + j != 0 and 0 <= v < np.inf and lo[j] >= 2.0 ** -1020 and hi[j] < 2.0 ** 1020
+            e = math.frexp(lo[j])[1] - 1 if o else -4096
+            o = o and math.frexp(hi[j])[1] - 1 == e
+            rr = 0
+            if o:
+                q = math.ldexp(v, 52 - e)
+                o = q - math.floor(q) != 0.5
+                rr = int(np.rint(q)) if o else 0
+            ok.append(o)
+            E.append(e)
+            r.append(rr)
+        if all(ok) and len(set(E)) == 1:
+            units.append(("t", E[0], sum(r)))
+            continue
+        segs = []
+        for j in range(len(seg)):
+            if j == 0 or not ok[j] or not ok[j - 1] or E[j] != E[j - 1]:
+                segs.append([j, j + 1])
+            else:
+                segs[-1][1] = j + 1
+        if len(segs) > 8:
+            units.append(("w", None, None))
+            continue
+        desc = []
+        for st, en in segs:
+            if ok[st]:
+                desc.append(("t", E[st], sum(r[st:en]), st, en))
+            else:
+                desc.append(("s", None, seg[st], st, en))
+        units.append(("g", desc, None))
     c = np.empty(n)
     s = 0.0
-    prev = -1
-    for k in range(nu):
-        serial, E = info[k]
-        if not serial:
-            continue
-        if prev >= 0 and k > prev + 1:
-            d = sum(delta[prev + 1:k])
-            s = s + float(d) * math.ldexp(1.0, info[prev + 1][1] - 52)
-        for j in range(k * UNIT, min(n, (k + 1) * UNIT)):
-            s = a[j] if j == 0 else s + a[j]
-            c[j] = s
-        sin = s
-        # translation units after k
-        kk = k + 1
-        while kk < nu and not info[kk][0]:
-            E2 = info[kk][1]
-            u = math.ldexp(1.0, E2 - 52)
-            r = np.rint(np.ldexp(a[kk * UNIT:(kk + 1) * UNIT], 52 - E2)).astype(np.int64)
-            pre = np.cumsum(r)
-            c[kk * UNIT:kk * UNIT + len(r)] = sin + pre.astype(np.float64) * u
-            sin = sin + float(pre[-1]) * u
-            kk += 1
-        prev = k
+    for k, (kind, x, y) in enumerate(units):
+        lo_i = k * UNIT
+        vals = a[lo_i:lo_i + UNIT]
+        if kind == "t":
+            u = math.ldexp(1.0, x - 52)
+            pre = np.cumsum(np.rint(np.ldexp(vals, 52 - x)).astype(np.int64))
+            c[lo_i:lo_i + len(vals)] = s + pre.astype(np.float64) * u
+            s = s + float(y) * u
+        elif kind == "w":
+            out, s = chain_unit_ref(vals, s, k == 0)
+            c[lo_i:lo_i + len(vals)] = out
+        else:
+            for sk, e, d, st, en in x:
+                if sk == "s":
+                    c[lo_i + st] = s + d
+                    s = s + d
+                else:
+                    u = math.ldexp(1.0, e - 52)
+                    pre = np.cumsum(np.rint(np.ldexp(vals[st:en], 52 - e)).astype(np.int64))
+                    c[lo_i + st:lo_i + en] = s + pre.astype(np.float64) * u
+                    s = s + float(d) * u
     return c
+
+
+def chain_unit_ref(vals, s, first):
+    out = np.empty(len(vals))
+    for j, v in enumerate(vals):
+        s = v if (first and j == 0) else s + v
+        out[j] = s
+    return out, s
 
 
 def test_chain_model_matches_running_sum():
@@ -77,3 +104,86 @@ def test_chain_model_matches_running_sum():
     for a in cases:
         c = model_chain(a)
         assert np.array_equal(c, np.cumsum(a))
+
+
+def model_chain_unit(a, s, first):
+    """fs2_chain.hpp chain_unit: wave-wide steps inside one binade, one plain add
+    at the first crossing / tie / bad term."""
+    cnt = len(a)
+    out = np.zeros(cnt)
+    j0 = 0
+    if first:
+        s = a[0]
+        out[0] = s
+        j0 = 1
+    while j0 < cnt:
+        if s == 0.0:
+            nz = [j for j in range(j0, cnt) if a[j] != 0.0]
+            jn = nz[0] if nz else cnt
+            out[j0:jn] = s
+            if jn >= cnt:
+                break
+            s = s + a[jn]
+            out[jn] = s
+            j0 = jn + 1
+            continue
+        if not (2.0 ** -1020 <= s < 2.0 ** 1020):
+            s = s + a[j0]
+            out[j0] = s
+            j0 += 1
+            continue
+        E = math.frexp(s)[1] - 1
+        u, top = math.ldexp(1.0, E - 52), math.ldexp(1.0, E + 1)
+        js, P = cnt, 0
+        vals = {}
+        for j in range(j0, cnt):
+            with np.errstate(over="ignore"):
+                q = float(np.ldexp(a[j], 52 - E))
+            ok = a[j] >= 0 and q < 2.0 ** 53
+            r = int(np.rint(q)) if ok else 0
+            P += r
+            v = s + float(P) * u
+            if (not ok) or (q - math.floor(q) == 0.5 if ok else True) or v >= top:
+                js = j
+                break
+            vals[j] = v
+        for j, v in vals.items():
+            out[j] = v
+        if js >= cnt:
+            s = vals[cnt - 1] if vals else s
+            break
+        sp = s if js == j0 else vals[js - 1]
+        s = sp + a[js]
+        out[js] = s
+        j0 = js + 1
+    return out, s
+
+
+def test_chain_unit_model_matches_sequential():
+    rng = np.random.default_rng(7)
+    for trial in range(400):
+        kind = trial % 5
+        if kind == 0:
+            a = rng.random(64) * 10.0 ** rng.uniform(-8, 0)
+            s = float(rng.random() * 10.0 ** rng.uniform(-8, 1))
+        elif kind == 1:                    # crossings inside the unit: s just below a power of 2
+            s = math.ldexp(1.0, int(rng.integers(-20, 5))) * (1 - 1e-9)
+            a = rng.random(64) * s * 1e-3
+        elif kind == 2:                    # ties at [0.5, 1)
+            s = 0.75
+            a = np.full(64, 2.0 ** -20 + 2.0 ** -54)
+        elif kind == 3:                    # zeros, then growth from 0
+            s = 0.0
+            a = np.where(rng.random(64) < 0.5, 0.0, rng.random(64) * 1e-300)
+        else:                              # fast growth from a tiny start
+            s = 1e-300
+            a = 10.0 ** rng.uniform(-300, 2, 64)
+        first = trial % 7 == 0
+        got, send = model_chain_unit(a, s, first)
+        ref = np.empty(64)
+        t = s
+        for j in range(64):
+            t = a[j] if (first and j == 0) else t + a[j]
+            ref[j] = t
+        assert np.array_equal(got, ref), trial
+        assert send == ref[-1]

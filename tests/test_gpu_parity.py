@@ -313,9 +313,19 @@ def test_oracle_parity_n20000(fs):
         ms = wl.measurements(s)
         nz = rng.normal(0, 0.001 if rot else 0.0055, N)
         u0 = rng.uniform(0, 1.0 / N)
+        cur = o.cnt.astype(np.int64)
         pose, st = f.step(rot, tr, ms, None, nz, u0)
         opose, oassoc, ors, one = o.iterate(rot, tr, ms, nz, u0)
         assert np.array_equal(f.associations(), oassoc), s
+        # the reference's first-match scan: j + 1 landmarks for a match at j, the
+        # whole map as it stood for an append
+        ref = 0
+        for k in range(len(ms)):
+            hit = oassoc[k] >= 0
+            ref += int(np.where(hit, oassoc[k] + 1, cur).sum())
+            cur = cur + (~hit)
+        assert st.reference_visits == ref, s
+        assert 0 < st.pages_opened <= st.slots_visited
         assert bool(st.resampled) == ors, s
         assert np.isclose(st.n_eff, one, rtol=1e-9)
         assert np.allclose(pose, opose, rtol=RTOL, atol=1e-12), s
