@@ -417,6 +417,40 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     return FS2_OK;
 }
 
+// Layout of an imported map: slots in an order whose runs of 8
+// (one page each) are spatially compact, so that page boxes are small and the
+// candidate stream opens few pages.  Recursive bisection: split the set along
+// its longer extent at a multiple of 8 near the middle.  The slot index travels
+// in each mirror, so the layout never changes a result; maps with non-finite
+// coordinates keep slot order.
+static bool spatial_order(const double *lm, int L, std::vector<int32_t> &perm) {
+    perm.resize(L);
+    for (int j = 0; j < L; ++j) {
+        perm[j] = j;
+        if (!std::isfinite(lm[6 * j]) || !std::isfinite(lm[6 * j + 1])) return false;
+    }
+    struct Rec {
+        static void go(const double *lm, int32_t *a, int n) {
+            if (n <= kPageSlots) return;
+            double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+            for (int k = 0; k < n; ++k) {
+                x0 = std::min(x0, lm[6 * a[k]]);
+                x1 = std::max(x1, lm[6 * a[k]]);
+                y0 = std::min(y0, lm[6 * a[k] + 1]);
+                y1 = std::max(y1, lm[6 * a[k] + 1]);
+            }
+            const int ax = (x1 - x0 >= y1 - y0) ? 0 : 1;
+            std::stable_sort(a, a + n, [&](int32_t u, int32_t v) { return lm[6 * u + ax] < lm[6 * v + ax]; });
+            int h = ((n / 2 + kPageSlots - 1) / kPageSlots) * kPageSlots;
+            if (h >= n) h = n - kPageSlots;
+            go(lm, a, h);
+            go(lm, a + h, n - h);
+        }
+    };
+    Rec::go(lm, perm.data(), L);
+    return true;
+}
+
 extern "C" {
 
 int32_t fs2_abi_version(void) { return FS2_ABI_VERSION; }
@@ -1103,28 +1137,44 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         const int64_t per = (int64_t)std::max(1, lm_cap) * 6 * 8;
         const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / per);
         double *stage = nullptr;
-        int32_t *cstage = nullptr;
+        int32_t *cstage = nullptr, *perm_dev = nullptr;
         HIP_TRY(h, hipMemsetAsync(h->ext_dev, 0, sizeof(uint32_t), s));
         HIP_TRY(h, hipMalloc(&stage, (size_t)std::min(chunk, count) * per));
         HIP_TRY(h, hipMalloc(&cstage, sizeof(int32_t) * std::min(chunk, count)));
+        HIP_TRY(h, hipMalloc(&perm_dev, sizeof(int32_t) * std::max(1, lm_cap)));
+        std::vector<double> rep((size_t)std::max(1, lm_cap) * 6);
+        std::vector<int32_t> perm;
         int rc2 = FS2_OK;
         for (int64_t o = 0; o < count && rc2 == FS2_OK; o += chunk) {
             const int64_t k = std::min(chunk, count - o);
             hipError_t e = hipMemcpy(stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
             if (e == hipSuccess) e = hipMemcpy(cstage, hc.data() + o, sizeof(int32_t) * k, hipMemcpyHostToDevice);
+            // the chunk's layout, from its first map (the filter's page boxes are
+            // what it serves; handles without the filter keep slot order)
+            int32_t perm_len = -1;
+            if (e == hipSuccess && h->cfg.gate_filter && hc[o] > kPageSlots) {
+                e = hipMemcpy(rep.data(), lm + o * lm_cap * 6, sizeof(double) * 6 * (size_t)hc[o],
+                              where == FS2_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
+                if (e == hipSuccess && spatial_order(rep.data(), hc[o], perm)) {
+                    perm_len = hc[o];
+                    e = hipMemcpy(perm_dev, perm.data(), sizeof(int32_t) * perm_len, hipMemcpyHostToDevice);
+                }
+            }
             PageAlloc pa{};
             rc2 = reserve_recs(h, k * std::max(1, lm_cap), &pa);
             if (rc2) break;
             rc2 = reserve_pages(h, k * rows_each, &pa);
             if (rc2) break;
             if (e == hipSuccess)
-                e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], h->ext_dev, s);
+                e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], h->ext_dev,
+                                  perm_len > 0 ? perm_dev : nullptr, perm_len, s);
             if (e == hipSuccess) e = launch_describe(h->map(), h->cnt[c], first + o, k, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
         }
         hipFree(stage);
         hipFree(cstage);
+        hipFree(perm_dev);
         if (rc2) return rc2;
         // the summary grid covers every imported landmark with room to spare; when it
         // grows, every descriptor is re-encoded on the new grid

@@ -590,9 +590,10 @@ __global__ __launch_bounds__(kBlock) void k_cl_gather_maps(MapRef map, const int
     if (j0 >= c) return;
     const char *pg = page_of(map, j0, i);
     double2 *o = out + off[i];
-    for (int j = j0; j < min(c, j0 + kPageSlots); ++j) {
-        const Slot sl = load_slot(map, pg, j);
-        o[j] = make_double2(sl.mx, sl.my);
+    for (int j = j0; j < min(c, j0 + kPageSlots); ++j) {      // position j holds slot mirror_slot
+        const float4 mv = load_mirror(pg, j);
+        const Slot sl = load_rec(map.recs, mirror_rec(mv));
+        o[mirror_slot(mv)] = make_double2(sl.mx, sl.my);
     }
 }
 

@@ -126,6 +126,21 @@ __device__ __forceinline__ float4 mirror_of(const Slot &sl) {
     return make_float4(__double2float_rn(sl.mx), __double2float_rn(sl.my), s, 0.0f);
 }
 
+// A mirror's z holds s with its 12 low mantissa bits replaced by the slot's
+// index in the map: pages may hold their 8 slots in any order (a map is laid
+// out spatially at import), and the index keeps the reference's
+// list order.  The bits are cleared before s is used, which only lowers it, so
+// it stays a lower bound.
+constexpr uint32_t kSlotBits = 0xfffu;        // slot indices < kMaxSlots = 4096
+__device__ __forceinline__ float mirror_s(const float4 &m) {
+    return __uint_as_float(__float_as_uint(m.z) & ~kSlotBits);
+}
+__device__ __forceinline__ int mirror_slot(const float4 &m) { return (int)(__float_as_uint(m.z) & kSlotBits); }
+__device__ __forceinline__ float4 with_slot(float4 m, int slot) {
+    m.z = __uint_as_float((__float_as_uint(m.z) & ~kSlotBits) | ((uint32_t)slot & kSlotBits));
+    return m;
+}
+
 // true when the mirror proves sqrt(q) >= gate for the observed point (fx, fy).
 //   |true dx| >= |fp32 dx| - ex,  ex = fe + (|x_lm| + |fp32 dx|) 2^-22
 // (fe bounds the fp32 rounding of the observed point; the rounding of x_lm and
@@ -137,7 +152,7 @@ __device__ __forceinline__ bool gate_reject_fast(const float4 &m, float cx, floa
     const float dx = fx - m.x, dy = fy - m.y;
     const float lx = fmaxf(fmaf(fabsf(dx), 0.99999976f, -(fe + cx)), 0.0f);
     const float ly = fmaxf(fmaf(fabsf(dy), 0.99999976f, -(fe + cy)), 0.0f);
-    return m.z * fmaf(lx, lx, ly * ly) > gate2f;
+    return mirror_s(m) * fmaf(lx, lx, ly * ly) > gate2f;
 }
 
 // EKF landmark update + likelihood (fast_slam_2.py:116-159).  Out of line: it

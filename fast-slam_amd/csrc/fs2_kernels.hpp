@@ -165,7 +165,7 @@ struct UpdateParams {
     float gate2f;            // gate2 rounded up to fp32 (mirror test)
     int32_t filter;          // use the fp32 gate mirror
     PageAlloc alloc;         // up to m new pages per lane (copy-on-write, appends)
-    uint64_t *cand;          // [kMaxCand][n] candidates: record id << 16 | slot
+    uint64_t *cand;          // [kMaxCand][n] candidates, slot order: slot << 44 | position << 32 | record
     int32_t *ncand;          // [n] candidates found (> kMaxCand: list truncated)
     double R[4];
     double init_cov[4];
@@ -343,9 +343,12 @@ hipError_t debug_chain_times(unsigned long long out[8], int reset);
 // alloc.rbase + p * lm_cap + j
 // (ext: atomicMax of the float bits of the largest finite |x|, |y| imported; slb
 // lowered to the smallest nonzero mirror s)
+// perm (nullable): maps of exactly perm_len slots are laid out with slot perm[j]
+// at position j (a spatial order: compact page boxes); others in slot order
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
-                         int32_t rows_each, int32_t *cnt, uint32_t *ext, hipStream_t s);
+                         int32_t rows_each, int32_t *cnt, uint32_t *ext, const int32_t *perm,
+                         int32_t perm_len, hipStream_t s);
 // page summaries of rows [0, ceil(cnt/8)) of particles first .. first+count-1
 hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count,
                            hipStream_t s);

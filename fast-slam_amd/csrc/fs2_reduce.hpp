@@ -226,12 +226,13 @@ __device__ __forceinline__ char *fresh_page(const MapRef &m, int row, int64_t i,
 }
 
 // Every slot write stores the fp64 record r and the slot's mirror (fp32 gate
-// shadow + r) in the page.
-__device__ __forceinline__ float4 store_slot(const MapRef &m, char *page, int j, const Slot &s, uint32_t r) {
+// shadow, slot index, r) at position pos of the page.
+__device__ __forceinline__ float4 store_slot(const MapRef &m, char *page, int pos, const Slot &s, uint32_t r,
+                                             int slot) {
     store_rec(m.recs, r, s);
-    float4 mv = mirror_of(s);
+    float4 mv = with_slot(mirror_of(s), slot);
     mv.w = __uint_as_float(r);
-    reinterpret_cast<float4 *>(page)[j & (kPageSlots - 1)] = mv;
+    reinterpret_cast<float4 *>(page)[pos & (kPageSlots - 1)] = mv;
     return mv;
 }
 
@@ -267,7 +268,7 @@ __device__ __forceinline__ Desc describe_page(uint32_t entry, const float4 *mir,
         xmax = fmaxf(xmax, m.x);
         ymin = fminf(ymin, m.y);
         ymax = fmaxf(ymax, m.y);
-        smin = fminf(smin, m.z);
+        smin = fminf(smin, mirror_s(m));
     }
     if (!finite || !(smin > 0.0f)) return make_uint2(entry, kSumOpen);
     return make_uint2(entry, sum_lo(f, xmin) | (sum_hi(f, xmax) << 8) | (sum_lo(f, ymin) << 16) |
@@ -277,7 +278,7 @@ __device__ __forceinline__ Desc describe_page(uint32_t entry, const float4 *mir,
 // Summary after a slot (mirror mv) was written: the box grows to include mv (it
 // may also cover values since replaced: still conservative).
 __device__ __forceinline__ Desc merge_summary(Desc d, const float4 &mv, const SumFrame &f) {
-    if (!(isfinite(mv.x) && isfinite(mv.y)) || !(mv.z > 0.0f)) {
+    if (!(isfinite(mv.x) && isfinite(mv.y)) || !(mirror_s(mv) > 0.0f)) {
         d.y = kSumOpen;
         return d;
     }
@@ -353,7 +354,7 @@ __device__ inline Band gate_band(float fx, float fy, float fe, float slb, float 
 
 __device__ __forceinline__ bool slot_outside_band(const float4 &m, float fx, float fy, float rx, float ry) {
     const float ax = fabsf(fx - m.x), ay = fabsf(fy - m.y);
-    return m.z > 0.0f && ((ax >= rx && ax < INFINITY) || (ay >= ry && ay < INFINITY));
+    return mirror_s(m) > 0.0f && ((ax >= rx && ax < INFINITY) || (ay >= ry && ay < INFINITY));
 }
 
 __device__ __forceinline__ void note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {

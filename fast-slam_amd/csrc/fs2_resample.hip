@@ -641,7 +641,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, 
         for (int k = threadIdx.x; k * kPageSlots < h.cnt; k += kBlock)
             P.rdesc[(int64_t)r * P.map.rows + k] =
                 describe_page(ids[k], mir + k * kPageSlots, min(kPageSlots, h.cnt - k * kPageSlots), P.map.frame);
-        for (int q = threadIdx.x; q < h.cnt; q += kBlock) smin = fminf(smin, mir[q].z > 0.0f ? mir[q].z : INFINITY);
+        for (int q = threadIdx.x; q < h.cnt; q += kBlock) smin = fminf(smin, mirror_s(mir[q]) > 0.0f ? mirror_s(mir[q]) : INFINITY);
         if (threadIdx.x == 0) pages += (h.cnt + kPageSlots - 1) / kPageSlots;
     }
     const unsigned long long b = block_sum_u64<kBlock>(pages, lds_u);

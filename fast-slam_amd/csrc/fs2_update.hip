@@ -71,6 +71,32 @@ __device__ unsigned long long g_phase[8];
 #endif
 constexpr int kDescAhead = FS2_DESC_AHEAD;   // page descriptors a lane keeps in flight
 
+static_assert(kMaxCand == 8, "sort8 sorts the candidate list");
+
+// Candidate list entry: slot index (the reference's list position) in the high
+// bits, so that entries sort in slot order; page position; record id.
+__device__ __forceinline__ uint64_t cand_entry(int slot, int pos, uint32_t rec) {
+    return ((uint64_t)slot << 44) | ((uint64_t)pos << 32) | (uint64_t)rec;
+}
+__device__ __forceinline__ int cand_slot(uint64_t e) { return (int)(e >> 44); }
+__device__ __forceinline__ int cand_pos(uint64_t e) { return (int)((e >> 32) & 0xfffu); }
+__device__ __forceinline__ uint32_t cand_rec(uint64_t e) { return (uint32_t)e; }
+
+__device__ __forceinline__ void cmpx(uint64_t &a, uint64_t &b) {
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+// Batcher's odd-even merge sort of 8 keys (19 compare-exchanges, branch-free)
+__device__ __forceinline__ void sort8(uint64_t (&e)[8]) {
+    cmpx(e[0], e[1]); cmpx(e[2], e[3]); cmpx(e[4], e[5]); cmpx(e[6], e[7]);
+    cmpx(e[0], e[2]); cmpx(e[1], e[3]); cmpx(e[4], e[6]); cmpx(e[5], e[7]);
+    cmpx(e[1], e[2]); cmpx(e[5], e[6]);
+    cmpx(e[0], e[4]); cmpx(e[1], e[5]); cmpx(e[2], e[6]); cmpx(e[3], e[7]);
+    cmpx(e[2], e[4]); cmpx(e[3], e[5]);
+    cmpx(e[1], e[2]); cmpx(e[3], e[4]); cmpx(e[5], e[6]);
+}
+
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ uint64_t s_list[kMaxCand][kBlock];
@@ -162,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                     }
                 }
                 if (hit) {
-                    if (nc < kMaxCand) s_list[nc][tid] = ((uint64_t)mirror_rec(mv) << 16) | (uint64_t)(j0 + u);
+                    if (nc < kMaxCand) s_list[nc][tid] = cand_entry(mirror_slot(mv), j0 + u, mirror_rec(mv));
                     ++nc;
                 }
             }
@@ -190,9 +216,18 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
     if (live) {
         P.ncand[i] = nc;
+        if (nc <= kMaxCand) {
+            // pages may hold their slots in any order: the list goes out in slot
+            // (reference list) order; an overflowing list is not used (k_update
+            // runs the reference's own loop for that particle)
+            uint64_t e[kMaxCand];
 #pragma unroll
-        for (int q = 0; q < kMaxCand; ++q)
-            if (q < nc) P.cand[(int64_t)q * n + i] = s_list[q][tid];
+            for (int q = 0; q < kMaxCand; ++q) e[q] = (q < nc) ? s_list[q][tid] : ~0ull;
+            sort8(e);
+#pragma unroll
+            for (int q = 0; q < kMaxCand; ++q)
+                if (q < nc) P.cand[(int64_t)q * n + i] = e[q];
+        }
     }
     // kCWords, kCGroups, kCVisited, kCOpened
     const unsigned cv[4] = {(unsigned)min(nc, kMaxCand), groups, visited, opened};
@@ -229,6 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ int s_idx[MAXM][kBlock];         // per (measurement, lane) association
     __shared__ uint2 s_cow[kBlock / 64][64 * (MAXM + 1)];   // per wave: (shared page, copy)
     __shared__ float4 s_mv[MAXM][kBlock];       // new mirrors of the slots phase A modified
+    __shared__ int s_best[MAXM][kBlock], s_bpos[MAXM][kBlock];   // overflow path: per-measurement answer
 
 #ifdef FS2_PHASE_TIMING
     unsigned long long ph_last = 0;
@@ -292,15 +328,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     FS2_PHASE(1);
     // ---- exact pass over the candidate slots (association + EKF) ----
-    int ncl = 0, jf = 0;
+    int ncl = 0;
+    bool overflow = false;
     if (live && P.filter) {
         const int nc = P.ncand[i];
         ncl = min(nc, kMaxCand);
-        jf = nc > kMaxCand ? (int)(P.cand[(int64_t)(kMaxCand - 1) * n + i] & 0xffffu) + 1 : c;
+        overflow = nc > kMaxCand;
     }
 
-    // slot j (record rec, value s): test the pending measurements in order, EKF on a match
-    auto visit = [&](int j, Slot s) {
+    // slot `slot` at page position pos (state s): test the pending measurements
+    // in order, EKF on a match
+    auto visit = [&](int slot, int pos, Slot s) {
         ++candidates;
         bool mod = false;
         M2 I;
@@ -323,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             // one EKF site: the matched measurement sees the slot as left by
             // the earlier measurements (fast_slam_2.py:116-153)
             s_lik[km][tid] = ekf_update(s, px, py, pyaw, s_ms[km], R, singular);
-            s_idx[km][tid] = j;
+            s_idx[km][tid] = slot;
             pend &= ~(1u << km);
             mod = true;
             ok = inv2(s.P, I);
@@ -331,45 +369,185 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (!ok) todo = 0u;
         }
         if (mod) {
-            // final: every measurement matching slot j was applied above.  Its new
+            // final: every measurement matching the slot was applied above.  Its new
             // record is private, so it is stored now; the mirror naming it goes
             // into the page in phase B (after the page is owned).
             const uint32_t r = sel_u32(nmod, frec);
             store_rec(map.recs, r, s);
-            float4 m = mirror_of(s);
+            float4 m = with_slot(mirror_of(s), slot);
             m.w = __uint_as_float(r);
-            smin_w = fminf(smin_w, m.z > 0.0f ? m.z : INFINITY);
+            smin_w = fminf(smin_w, mirror_s(m) > 0.0f ? mirror_s(m) : INFINITY);
             s_mv[nmod][tid] = m;
-            mods |= (uint64_t)j << (16 * nmod);
+            mods |= (uint64_t)pos << (16 * nmod);
             ++nmod;
             ++written;
         }
     };
 
-    // Listed candidates in slot order; the list names their records, so while
-    // one is tested the next one's record and the entry after it are in flight
-    // (every load is branch-free: a missing entry reads entry 0 and record 0,
-    // which are never used).
-    {
+    if (!overflow) {
+        // Listed candidates in slot order; the list names their records, so while
+        // one is tested the next one's record and the entry after it are in flight
+        // (every load is branch-free: a missing entry reads entry 0 and record 0,
+        // which are never used).
         const int nl = (pend != 0u) ? ncl : 0;
         auto entry = [&](int p) -> uint64_t { return P.cand[(int64_t)(p < nl ? p : 0) * n + il]; };
-        auto rec_of = [&](int p, uint64_t e) -> uint32_t { return p < nl ? (uint32_t)(e >> 16) : 0u; };
+        auto rec_of = [&](int p, uint64_t e) -> uint32_t { return p < nl ? cand_rec(e) : 0u; };
         uint64_t e0 = entry(0), e1 = entry(1);
         Slot s0 = load_rec(map.recs, rec_of(0, e0));
         for (int p = 0; p < nl && pend != 0u; ++p) {
             const uint64_t e2 = entry(p + 2);
             const Slot s1 = load_rec(map.recs, rec_of(p + 1, e1));
-            visit((int)(e0 & 0xffffu), s0);
+            visit(cand_slot(e0), cand_pos(e0), s0);
             e0 = e1;
             s0 = s1;
             e1 = e2;
         }
-    }
-    // Past an overflowing list (or without the filter): every slot from jf on.
-    for (int j = jf; j < c && pend != 0u; ++j) {
-        const uint32_t r = mirror_rec(load_mirror(page_of(map, j, il), j));
-        if (!P.filter) ++visited;
-        visit(j, load_rec(map.recs, r));
+        // Without the filter: every slot, in order (such maps are imported in
+        // slot order: position j holds slot j).
+        if (!P.filter) {
+            for (int j = 0; j < c && pend != 0u; ++j) {
+                const float4 mv = load_mirror(page_of(map, j, il), j);
+                ++visited;
+                visit(mirror_slot(mv), j, load_rec(map.recs, mirror_rec(mv)));
+            }
+        }
+    } else {
+        // An overflowing list: the reference's loop (landmark_utils.py:103-117),
+        // each pending measurement in order taking the smallest slot index that
+        // passes the exact gate with the states the earlier measurements left.
+        // One pass over the map (page boxes and pre-scan fp32 mirrors skip what
+        // cannot pass) finds, on the pre-scan states, each measurement's smallest
+        // matching slot.  Processed in order, that answer stands unless its slot
+        // was modified meanwhile (then that measurement alone is rescanned); the
+        // slots modified so far are tested with their new states.  A singular
+        // covariance counts only below the match, where the reference would meet it.
+        const int rows = (c + kPageSlots - 1) / kPageSlots;
+        const float slb = *map.slb;
+        // each measurement's smallest matching slot and its position live in LDS
+        // (registers are k_update's occupancy limit)
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k) {
+            s_best[k][tid] = INT_MAX;
+            s_bpos[k][tid] = -1;
+        }
+        int sing = INT_MAX;
+        // pre-scan pass over every page (measurements `want`; `skip_mods`: ignore
+        // slots modified in this pass)
+        auto scan = [&](unsigned want, bool skip_mods) {
+            for (int g = 0; g < rows; ++g) {
+                const Desc d = *pt_entry(map, g, il);
+                unsigned open = 0u;
+#pragma unroll
+                for (int k = 0; k < MAXM; ++k)
+                    if (((want >> k) & 1u) &&
+                        !page_reject(d.y, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
+                        open |= 1u << k;
+                if (!open) continue;
+                const char *pg = page_ptr(map.pool, d.x);
+                for (int u = 0; u < kPageSlots && g * kPageSlots + u < c; ++u) {
+                    const int pos = g * kPageSlots + u;
+                    if (skip_mods) {
+                        bool modded = false;
+#pragma unroll
+                        for (int q = 0; q < MAXM; ++q)
+                            modded |= q < nmod && (int)((mods >> (16 * q)) & 0xffffu) == pos;
+                        if (modded) continue;
+                    }
+                    const float4 mv = load_mirror(pg, u);
+                    const int slot = mirror_slot(mv);
+                    const float cx = fabsf(mv.x) * 2.3841858e-7f, cy = fabsf(mv.y) * 2.3841858e-7f;
+                    unsigned test = 0u;
+#pragma unroll
+                    for (int k = 0; k < MAXM; ++k)
+                        if (((open >> k) & 1u) && slot < s_best[k][tid] &&
+                            !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
+                            test |= 1u << k;
+                    if (!test && !(mirror_s(mv) == 0.0f && slot < sing)) continue;
+                    const Slot s = load_rec(map.recs, mirror_rec(mv));
+                    ++candidates;
+                    M2 I;
+                    if (!inv2(s.P, I)) {
+                        sing = min(sing, slot);
+                        continue;
+                    }
+#pragma unroll
+                    for (int k = 0; k < MAXM; ++k) {
+                        if ((test >> k) & 1u) {
+                            const double qd = quad(I, s_ms[k].ox - s.mx, s_ms[k].oy - s.my);
+                            amb += ambiguous(qd, gate2);
+                            if (qd >= 0.0 && qd < gate2) {
+                                s_best[k][tid] = slot;
+                                s_bpos[k][tid] = pos;
+                            }
+                        }
+                    }
+                }
+            }
+        };
+        scan(pend, false);
+        for (int k = 0; k < MAXM; ++k) {
+            if (!((pend >> k) & 1u)) continue;
+            int t = -1;                            // the pre-scan answer's slot, if modified since
+            const int pb = s_bpos[k][tid];
+#pragma unroll
+            for (int q = 0; q < MAXM; ++q)
+                if (q < nmod && pb >= 0 && (int)((mods >> (16 * q)) & 0xffffu) == pb) t = q;
+            if (t >= 0) {
+                // rescan this measurement over the unmodified slots
+                s_best[k][tid] = INT_MAX;
+                s_bpos[k][tid] = -1;
+                scan(1u << k, true);
+            }
+            int bk = s_best[k][tid], pk = s_bpos[k][tid];
+            // the slots modified so far, with their new states
+            int tk = -1;
+            for (int q = 0; q < nmod; ++q) {
+                const int pos = (int)((mods >> (16 * q)) & 0xffffu);
+                const float4 mq = s_mv[q][tid];
+                const int slot = mirror_slot(mq);
+                if (slot >= bk) continue;
+                const Slot s = load_rec(map.recs, sel_u32(q, frec));
+                ++candidates;
+                M2 I;
+                if (!inv2(s.P, I)) {
+                    sing = min(sing, slot);
+                    continue;
+                }
+                const double qd = quad(I, s_ms[k].ox - s.mx, s_ms[k].oy - s.my);
+                amb += ambiguous(qd, gate2);
+                if (qd >= 0.0 && qd < gate2) {
+                    bk = slot;
+                    pk = pos;
+                    tk = q;
+                }
+            }
+            if (sing < bk) singular = true;
+            if (pk < 0) continue;
+            int t2 = tk;
+            if (t2 < 0) {
+#pragma unroll
+                for (int q = 0; q < MAXM; ++q)
+                    if (q < nmod && (int)((mods >> (16 * q)) & 0xffffu) == pk) t2 = q;
+            }
+            Slot s = load_rec(map.recs, t2 >= 0 ? sel_u32(t2, frec)
+                                                : mirror_rec(load_mirror(page_of(map, pk, il), pk)));
+            s_lik[k][tid] = ekf_update(s, px, py, pyaw, s_ms[k], R, singular);
+            s_idx[k][tid] = bk;
+            pend &= ~(1u << k);
+            if (t2 < 0) {
+                t2 = nmod++;
+                mods |= (uint64_t)pk << (16 * t2);
+                ++written;
+            }
+            const uint32_t r = sel_u32(t2, frec);
+            store_rec(map.recs, r, s);
+            float4 m = with_slot(mirror_of(s), bk);
+            m.w = __uint_as_float(r);
+            smin_w = fminf(smin_w, mirror_s(m) > 0.0f ? mirror_s(m) : INFINITY);
+#pragma unroll
+            for (int q = 0; q < MAXM; ++q)
+                if (q == t2) s_mv[q][tid] = m;
+        }
     }
 
     FS2_PHASE(2);
@@ -528,8 +706,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             const uint32_t r = mirror_rec(load_mirror(pg, jh));
             Slot s = load_rec(map.recs, r);
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
-            const float4 mv = store_slot(map, pg, jh, s, r);
-            smin_w = fminf(smin_w, mv.z > 0.0f ? mv.z : INFINITY);
+            const float4 mv = store_slot(map, pg, jh, s, r, jh);
+            smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
             if (jh / kPageSlots == arow) ad = merge_summary(ad, mv, map.frame);
             else note_write(map, jh, il, mv, false);
             s_idx[k][tid] = c + hit;
@@ -544,13 +722,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 if (arow >= 0) *pt_entry(map, arow, il) = ad;     // leaving that row
                 const uint32_t id = take_page(P.alloc, map.n, il, nalloc);
                 arow = ja / kPageSlots;
-                const float4 mv = store_slot(map, page_ptr(map.pool, id), ja, s, r);
-                smin_w = fminf(smin_w, mv.z > 0.0f ? mv.z : INFINITY);
+                const float4 mv = store_slot(map, page_ptr(map.pool, id), ja, s, r, ja);
+                smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
                 ad = describe_page(id | kOwned, &mv, 1, map.frame);
                 ++fresh;
             } else {
-                const float4 mv = store_slot(map, page_ptr(map.pool, ad.x), ja, s, r);
-                smin_w = fminf(smin_w, mv.z > 0.0f ? mv.z : INFINITY);
+                const float4 mv = store_slot(map, page_ptr(map.pool, ad.x), ja, s, r, ja);
+                smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
                 ad = merge_summary(ad, mv, map.frame);
             }
             s_idx[k][tid] = -1;
@@ -767,7 +945,8 @@ hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
 __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const int32_t *cnt_stage,
                                                    int64_t first, int64_t count, int32_t lm_cap,
                                                    MapRef map, PageAlloc alloc, int32_t rows_each,
-                                                   int32_t *cnt, uint32_t *ext) {
+                                                   int32_t *cnt, uint32_t *ext, const int32_t *perm,
+                                                   int32_t perm_len) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t total = count * lm_cap;
     float smin = INFINITY, amax = 0.0f;
@@ -777,13 +956,15 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         const int c = cnt_stage[p];
         if (j == 0) cnt[first + p] = c;
         if (j >= c) continue;
+        // position j holds slot perm[j] (a spatial layout, fs2_set_state), or slot j
+        const int slot = (perm && c == perm_len) ? perm[j] : j;
         const int row = j / kPageSlots;
         const uint32_t id = alloc.freel[alloc.base + p * rows_each + row];
         if (j % kPageSlots == 0) pt_entry(map, row, first + p)->x = id | kOwned;
-        const double *s = stage + e * 6;
+        const double *s = stage + (p * lm_cap + slot) * 6;
         const float4 mv = store_slot(map, page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}},
-                                     alloc.rfreel[alloc.rbase + e]);
-        smin = fminf(smin, mv.z > 0.0f ? mv.z : INFINITY);
+                                     alloc.rfreel[alloc.rbase + e], slot);
+        smin = fminf(smin, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
         if (isfinite(mv.x)) amax = fmaxf(amax, fabsf(mv.x));
         if (isfinite(mv.y)) amax = fmaxf(amax, fabsf(mv.y));
     }
@@ -801,8 +982,9 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
         const int64_t p = e / lm_cap;
         const int j = (int)(e % lm_cap);
         if (j >= cnt[first + p]) continue;
-        const Slot s = load_slot(map, page_of(map, j, first + p), j);
-        double *d = stage + e * 6;
+        const float4 mv = load_mirror(page_of(map, j, first + p), j);    // position j holds slot mirror_slot
+        const Slot s = load_rec(map.recs, mirror_rec(mv));
+        double *d = stage + (p * lm_cap + mirror_slot(mv)) * 6;
         d[0] = s.mx; d[1] = s.my;
         d[2] = s.P.a00; d[3] = s.P.a01; d[4] = s.P.a10; d[5] = s.P.a11;
     }
@@ -828,9 +1010,10 @@ static unsigned grid_for(int64_t total) {
 
 hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t first,
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
-                         int32_t rows_each, int32_t *cnt, uint32_t *ext, hipStream_t s) {
+                         int32_t rows_each, int32_t *cnt, uint32_t *ext, const int32_t *perm,
+                         int32_t perm_len, hipStream_t s) {
     hipLaunchKernelGGL(k_import, dim3(grid_for(count * lm_cap)), dim3(kBlock), 0, s, stage,
-                       cnt_stage, first, count, lm_cap, map, alloc, rows_each, cnt, ext);
+                       cnt_stage, first, count, lm_cap, map, alloc, rows_each, cnt, ext, perm, perm_len);
     return hipGetLastError();
 }
 
