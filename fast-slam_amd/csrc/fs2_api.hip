@@ -86,6 +86,7 @@ struct fs2_handle {
     char *pool = nullptr;
     int64_t npool = 0;                     // pages in the pool
     Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
+    uint32_t *bbox[2] = {};                // [nblocks][kBBoxRows] workgroup row boxes of pt[0] / pt[1]
     Desc *rdesc = nullptr;                 // descriptors of received pages [n_recv][rows]
     SumFrame frame{-127.0f, 1.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
     float ext_seen = 0.0f;                 // largest |x|, |y| imported so far
@@ -154,7 +155,11 @@ struct fs2_handle {
     double *sout = nullptr, *bpre = nullptr, *part_w = nullptr, *np_part = nullptr, *sentry = nullptr;
     UnitRec *urec = nullptr;
 
-    MapRef map() const { return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb}; }
+    MapRef map() const {
+        return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb, row_boxes(cur)};
+    }
+    // row boxes of buffer b, while the maps fit them (fs2_kernels.hpp)
+    uint32_t *row_boxes(int b) const { return rows <= kBBoxRows ? bbox[b] : nullptr; }
     int64_t nblocks() const { return (n + kBlock - 1) / kBlock; }
     // the reduction order in force (FS2_REDUCE_*, AUTO resolved)
     int reduce() const {
@@ -494,6 +499,7 @@ static void free_handle(fs2_handle *h) {
     for (int s = 0; s < 2; ++s) {
         hipFree(h->x[s]); hipFree(h->y[s]); hipFree(h->yaw[s]); hipFree(h->w[s]); hipFree(h->cnt[s]);
         hipFree(h->pt[s]);
+        hipFree(h->bbox[s]);
     }
     hipFree(h->rdesc);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
@@ -569,6 +575,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= alloc((void **)&h->yaw[s], n * 8) == hipSuccess;
         ok &= alloc((void **)&h->w[s], n * 8) == hipSuccess;
         ok &= alloc((void **)&h->cnt[s], n * 4) == hipSuccess;
+        ok &= alloc((void **)&h->bbox[s], nb * kBBoxRows * 4) == hipSuccess;
     }
     ok &= alloc((void **)&h->nfree_dev, sizeof(int64_t)) == hipSuccess;
     ok &= alloc((void **)&h->rnfree_dev, sizeof(int64_t)) == hipSuccess;
@@ -642,6 +649,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
             hipMemsetAsync(h->y[s], 0, n * 8, h->stream) != hipSuccess ||
             hipMemsetAsync(h->yaw[s], 0, n * 8, h->stream) != hipSuccess ||
             hipMemsetAsync(h->cnt[s], 0, n * 4, h->stream) != hipSuccess ||
+            hipMemsetD32Async((hipDeviceptr_t)h->bbox[s], (int)kBoxEmpty, nb * kBBoxRows, h->stream) != hipSuccess ||
             launch_fill(h->w[s], 1.0 / (double)h->n_global, n, h->stream) != hipSuccess)
             return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     }
@@ -932,6 +940,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
     rs.map = h->map();
     rs.opt = h->pt[nxt];
+    rs.obbox = h->row_boxes(nxt);
     rs.rank_d = h->rank_d;
     rs.rank_e = h->rank_e;
     rs.iblk = h->iblk;
@@ -994,6 +1003,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             rc = grow_rows(h, h->stats_host->max_count);
             if (rc) return rc;
             rs.opt = h->pt[nxt];
+            rs.obbox = h->row_boxes(nxt);
             // fresh records and pages for the received maps: record r, row k ->
             // page base + r * rows + k; slot q -> record rbase + peer sbase + soff + q
             rc = reserve_recs(h, h->s_recv, &rs.alloc);
@@ -1189,6 +1199,8 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             h->frame = SumFrame{-127.0f * cell, cell, 1.0f / cell};
             HIP_TRY(h, launch_describe(h->map(), h->cnt[c], 0, h->n, s));
         }
+        // the workgroup row boxes, rebuilt from the descriptors
+        HIP_TRY(h, launch_bbox_build(h->map(), h->cnt[c], s));
     }
     HIP_TRY(h, hipStreamSynchronize(s));
     return FS2_OK;

@@ -47,6 +47,15 @@ struct SumFrame {
 };
 constexpr uint32_t kSumOpen = 0xff00ff00u;   // unbounded box: never rejected
 
+// Workgroup row boxes: bbox[b * kBBoxRows + r] is a box (same codes) holding the
+// box of row r of every particle of workgroup b (particles [256 b, 256 b + 256)).
+// k_candidates tests it against the measurement bands once per workgroup and
+// streams only the rows it cannot reject, so most descriptors are never read.
+// Boxes only grow between rebuilds (k_update merges what it writes; resampling
+// and imports recompute them); maps of more than kBBoxRows rows run without.
+constexpr int kBBoxRows = 256;
+constexpr uint32_t kBoxEmpty = 0x00ff00ffu;  // x lo = y lo = 255, x hi = y hi = 0: holds nothing
+
 // Counters of the update pass, kept per workgroup (cpart[counter][block]: the
 // first pass of a scan stores them, later passes add) and folded into DevStats
 // by k_wsum: no same-address atomics on the hot kernels.
@@ -133,6 +142,7 @@ struct MapRef {
     char *recs;              // record r at recs + r * kRecBytes
     SumFrame frame;          // summary grid of the descriptors
     float *slb;              // lower bound on every nonzero mirror s (lowered by every write)
+    uint32_t *bbox;          // [nblocks][kBBoxRows] workgroup row boxes (null: rows > kBBoxRows)
 };
 
 // Free pages and records reserved for one launch: lane i's t-th new page is
@@ -242,6 +252,7 @@ struct ResampleParams {
     int32_t *ocnt;
     MapRef map;              // current page table
     Desc *opt;               // next page table [rows][n]
+    uint32_t *obbox;         // its workgroup row boxes (null: none)
     Desc *rdesc;             // [nrecv][rows] descriptors of received pages
     PageAlloc alloc;         // received particle r: row k -> page base + r*rows + k,
                              // slot q -> record rbase + peer sbase + soff + q
@@ -352,6 +363,8 @@ hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t 
 // page summaries of rows [0, ceil(cnt/8)) of particles first .. first+count-1
 hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count,
                            hipStream_t s);
+// workgroup row boxes of every particle's map, from the descriptors (no-op without bbox)
+hipError_t launch_bbox_build(MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm_cap,
                          MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s);

@@ -288,6 +288,84 @@ __device__ __forceinline__ Desc merge_summary(Desc d, const float4 &mv, const Su
     return d;
 }
 
+// ---- workgroup row boxes (fs2_kernels.hpp, MapRef::bbox) ----
+// A box's bytes (x lo, x hi, y lo, y hi) as two packed 16-bit pairs: lows
+// (x lo | y lo << 16, union = min) and highs (x hi | y hi << 16, union = max),
+// so a union is one v_pk_min_u16 and one v_pk_max_u16.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kBoxHalf = 0x00ff00ffu;
+
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t box_union(uint32_t a, uint32_t b) {
+    return pk_min_u16(a & kBoxHalf, b & kBoxHalf) | (pk_max_u16((a >> 8) & kBoxHalf, (b >> 8) & kBoxHalf) << 8);
+}
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void box_dpp_step(uint32_t &lo, uint32_t &hi) {
+    lo = pk_min_u16(lo, (uint32_t)__builtin_amdgcn_update_dpp((int)kBoxHalf, (int)lo, CTRL, ROWS, 0xf, false));
+    hi = pk_max_u16(hi, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROWS, 0xf, false));
+}
+
+// Union of the 64 lanes' boxes (every lane of the wave active), in every lane:
+// row_shr 1/2/4/8 leave each 16-lane row's union in its lane 15, row_bcast 15/31
+// carry them up, lane 63 holds the wave's (the ICP's DPP pattern, fs2_geometry.hip).
+__device__ __forceinline__ uint32_t wave_box_union(uint32_t b) {
+    uint32_t lo = b & kBoxHalf, hi = (b >> 8) & kBoxHalf;
+    box_dpp_step<0x111, 0xf>(lo, hi);
+    box_dpp_step<0x112, 0xf>(lo, hi);
+    box_dpp_step<0x114, 0xf>(lo, hi);
+    box_dpp_step<0x118, 0xf>(lo, hi);
+    box_dpp_step<0x142, 0xa>(lo, hi);
+    box_dpp_step<0x143, 0xc>(lo, hi);
+    lo = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+    hi = (uint32_t)__builtin_amdgcn_readlane((int)hi, 63);
+    return lo | (hi << 8);
+}
+
+// A workgroup's row boxes in LDS, one array per code (LDS atomics per field).
+struct BoxLds {
+    uint32_t xl[kBBoxRows], xh[kBBoxRows], yl[kBBoxRows], yh[kBBoxRows];
+};
+__device__ __forceinline__ void lds_box_set(BoxLds &s, int r, uint32_t b) {
+    s.xl[r] = b & 0xffu;
+    s.xh[r] = (b >> 8) & 0xffu;
+    s.yl[r] = (b >> 16) & 0xffu;
+    s.yh[r] = b >> 24;
+}
+__device__ __forceinline__ uint32_t lds_box_get(const BoxLds &s, int r) {
+    return s.xl[r] | (s.xh[r] << 8) | (s.yl[r] << 16) | (s.yh[r] << 24);
+}
+// grow row r's box to hold b (atomics only when it grows: the row boxes change rarely)
+__device__ __forceinline__ void lds_box_merge(BoxLds &s, int r, uint32_t b) {
+    const uint32_t cur = lds_box_get(s, r);
+    if (box_union(cur, b) == cur) return;
+    atomicMin(&s.xl[r], b & 0xffu);
+    atomicMax(&s.xh[r], (b >> 8) & 0xffu);
+    atomicMin(&s.yl[r], (b >> 16) & 0xffu);
+    atomicMax(&s.yh[r], b >> 24);
+}
+
+// Measurements whose band box `s` (page summary or row box) does not lie outside
+// (bc: band_codes thresholds of each measurement, gate_band).
+template <int MAXM>
+__device__ __forceinline__ unsigned box_open_mask(uint32_t s, const uint32_t (&bc)[MAXM], int m) {
+    const uint32_t xl = s & 0xffu, xh = (s >> 8) & 0xffu, yl = (s >> 16) & 0xffu, yh = s >> 24;
+    unsigned om = 0u;
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k)
+        if (k < m && xl <= (bc[k] & 0xffu) && xh >= ((bc[k] >> 8) & 0xffu) && yl <= ((bc[k] >> 16) & 0xffu) &&
+            yh >= (bc[k] >> 24))
+            om |= 1u << k;
+    return om;
+}
+
 // True when no slot of the page can pass the gate for the observed point: the
 // distance to the box is <= |fx - x_lm| for every slot, the margins use the
 // box's largest |x|, and slb <= s of every slot (a slot with s = 0 opened the
@@ -357,10 +435,13 @@ __device__ __forceinline__ bool slot_outside_band(const float4 &m, float fx, flo
     return mirror_s(m) > 0.0f && ((ax >= rx && ax < INFINITY) || (ay >= ry && ay < INFINITY));
 }
 
-__device__ __forceinline__ void note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
+// the page's summary after slot j (mirror mv) was written; returns the new descriptor
+__device__ __forceinline__ Desc note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
     Desc *pe = pt_entry(m, j / kPageSlots, i);
     const Desc d = *pe;
-    *pe = fresh ? describe_page(d.x, &mv, 1, m.frame) : merge_summary(d, mv, m.frame);
+    const Desc nd = fresh ? describe_page(d.x, &mv, 1, m.frame) : merge_summary(d, mv, m.frame);
+    *pe = nd;
+    return nd;
 }
 
 // Recompute the summary of page `row` of particle i from its mirrors (map size c).

@@ -653,18 +653,35 @@ __global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, 
 // deepcopy, without copying the map: the pages are shared).  A page stays owned
 // only when its source fills exactly one local output; otherwise every output
 // copies it before its first write.
+// The output workgroup's row boxes (obbox): an output's page boxes lie inside
+// its source workgroup's row boxes, so the union of the row boxes of the
+// workgroups its local outputs come from holds them (few: systematic resampling
+// maps consecutive outputs to non-decreasing sources).  Outputs received from
+// another rank have no such box: a workgroup holding some adds the unions of
+// their page boxes, row by row (a wave union per row, LDS across the waves).
 __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParams P) {
     __shared__ double lds_d[kBlock / 64];
     __shared__ int64_t lds_l[kBlock / 64];
+    __shared__ BoxLds s_bb;
+    __shared__ int s_src[kBlock];    // source workgroup of each local output (-1: none)
+    __shared__ int s_sb[kBlock];     // the distinct ones, in order
+    __shared__ int s_wc[kBlock / 64];
     if (!P.stats->resampled) return;
     const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     __shared__ unsigned long long lds_u[kBlock / 64];
+    const bool bb = P.obbox != nullptr && P.map.bbox != nullptr;
+    if (bb) lds_box_set(s_bb, threadIdx.x, kBoxEmpty);      // kBBoxRows == kBlock
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
     unsigned slots = 0;
-    if (m < P.n) {
-        const int32_t s = P.out_src[m];
-        const int64_t n = P.n;
+    const int64_t n = P.n;
+    int32_t s = 0;
+    int rows = 0;                    // rows of this output's map
+    uint32_t keep = 0xffffffffu, own = 0u;
+    const Desc *src = P.map.pt;      // the source's row 0; row k at src + k * stride
+    int64_t stride = 0;
+    if (m < n) {
+        s = P.out_src[m];
         double w;
         int c;
         if (s >= 0) {
@@ -674,21 +691,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             w = P.w[s];
             c = P.cnt[s];
             const int64_t lo = max((int64_t)P.mlo[s], P.a), hi = min((int64_t)P.mhi[s], P.a + n - 1);
-            const uint32_t keep = (hi == lo) ? 0xffffffffu : kIdMask;
-            const int rows = (c + kPageSlots - 1) / kPageSlots;
-            // 8 independent loads in flight per lane (one per iteration would pay a
-            // full memory latency per row)
-            for (int k0 = 0; k0 < rows; k0 += 8) {
-                Desc e[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) e[u] = *pt_entry(P.map, min(k0 + u, rows - 1), s);
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (k0 + u < rows) {
-                        e[u].x &= keep;
-                        P.opt[(int64_t)(k0 + u) * n + m] = e[u];
-                    }
-            }
+            keep = (hi == lo) ? 0xffffffffu : kIdMask;
+            src = pt_entry(P.map, 0, s);
+            stride = n;
         } else {
             const int r = -s - 1;
             const int p = peer_of(P, r);
@@ -698,19 +703,62 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             P.oyaw[m] = h.yaw;
             w = h.w;
             c = h.cnt;
-            const uint32_t own = (h.out_hi == h.out_lo) ? kOwned : 0u;
-            const Desc *rd = P.rdesc + (int64_t)r * P.map.rows;
-            for (int k = 0; k * kPageSlots < c; ++k) {
-                Desc e = rd[k];
-                e.x |= own;
-                P.opt[(int64_t)k * n + m] = e;
-            }
+            own = (h.out_hi == h.out_lo) ? kOwned : 0u;
+            src = P.rdesc + (int64_t)r * P.map.rows;
+            stride = 1;
         }
+        rows = (c + kPageSlots - 1) / kPageSlots;
         P.ocnt[m] = c;
         P.ow[m] = w;
         bv = w;
         bi = m;
         slots = (unsigned)c;
+    }
+    // received outputs in this workgroup: their boxes take the row-union path below
+    const bool recv = bb && __syncthreads_or(m < n && s < 0);
+    if (bb) s_src[threadIdx.x] = (m < n && s >= 0) ? s / kBlock : -1;
+    if (bb) __syncthreads();         // s_bb, s_src written
+    // the page-table row of every output, 8 independent loads in flight per lane
+    // (one per iteration would pay a full memory latency per row); the loop runs
+    // over the wave's longest map so that every lane takes part in the row unions
+    const int wrows = wave_max_i(rows);
+    for (int k0 = 0; k0 < wrows; k0 += 8) {
+        Desc e[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) e[u] = src[(int64_t)max(min(k0 + u, rows - 1), 0) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (k0 + u < rows) {
+                e[u].x = (e[u].x & keep) | own;
+                P.opt[(int64_t)(k0 + u) * n + m] = e[u];
+            }
+        }
+        if (recv) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (k0 + u < wrows) {
+                    const uint32_t b = wave_box_union((k0 + u < rows && s < 0) ? e[u].y : kBoxEmpty);
+                    if ((threadIdx.x & 63) == 0) lds_box_merge(s_bb, k0 + u, b);
+                }
+            }
+        }
+    }
+    // distinct source workgroups, compacted in output order
+    int nsb = 0;
+    if (bb) {
+        const int t = threadIdx.x;
+        const bool first = s_src[t] >= 0 && (t == 0 || s_src[t - 1] != s_src[t]);
+        const uint64_t fm = __ballot(first);
+        const int wid = t >> 6, lane = t & 63;
+        if (lane == 0) s_wc[wid] = __popcll(fm);
+        __syncthreads();
+        int off = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            off += (w < wid) ? s_wc[w] : 0;
+            nsb += s_wc[w];
+        }
+        if (first) s_sb[off + __popcll(fm & ((1ull << lane) - 1ull))] = s_src[t];
     }
     const unsigned long long bs = block_sum_u64<kBlock>(slots, lds_u);
     if (threadIdx.x == 0 && bs) atomicAdd(&P.stats->resample_slots, bs);
@@ -719,6 +767,44 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         P.part_best_w[blockIdx.x] = bv;
         P.part_best_i[blockIdx.x] = bi;
     }
+    // (the barriers above order every LDS write before these reads)
+    if (bb && (int)threadIdx.x < P.map.rows) {
+        uint32_t b = lds_box_get(s_bb, threadIdx.x);
+        for (int q = 0; q < nsb; ++q) b = box_union(b, P.map.bbox[(int64_t)s_sb[q] * kBBoxRows + threadIdx.x]);
+        P.obbox[(int64_t)blockIdx.x * kBBoxRows + threadIdx.x] = b;
+    }
+}
+
+// Workgroup row boxes of every map from its descriptors (after imports, or when
+// the summary grid changes): the same row unions as k_gather_particles.
+__global__ __launch_bounds__(kBlock) void k_bbox_build(const MapRef map, const int32_t *cnt, int64_t n) {
+    __shared__ BoxLds s_bb;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    lds_box_set(s_bb, threadIdx.x, kBoxEmpty);
+    const int rows = (i < n) ? (cnt[i] + kPageSlots - 1) / kPageSlots : 0;
+    __syncthreads();
+    const int wrows = wave_max_i(rows);
+    for (int k0 = 0; k0 < wrows; k0 += 8) {
+        uint32_t e[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) e[u] = pt_entry(map, max(min(k0 + u, rows - 1), 0), i < n ? i : 0)->y;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (k0 + u < wrows) {
+                const uint32_t b = wave_box_union(k0 + u < rows ? e[u] : kBoxEmpty);
+                if ((threadIdx.x & 63) == 0) lds_box_merge(s_bb, k0 + u, b);
+            }
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < map.rows) map.bbox[(int64_t)blockIdx.x * kBBoxRows + threadIdx.x] = lds_box_get(s_bb, threadIdx.x);
+}
+
+hipError_t launch_bbox_build(MapRef map, const int32_t *cnt, hipStream_t s) {
+    if (!map.bbox) return hipSuccess;
+    const unsigned g = (unsigned)((map.n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_bbox_build, dim3(g), dim3(kBlock), 0, s, map, cnt, map.n);
+    return hipGetLastError();
 }
 
 // this rank's first maximum over its outputs -> record (post-resample estimate)

@@ -101,6 +101,8 @@ template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ uint64_t s_list[kMaxCand][kBlock];
     __shared__ Band s_band[MAXM];
+    __shared__ uint16_t s_rows[kBBoxRows];      // rows the row boxes leave open, ascending
+    __shared__ int s_wc[kBlock / 64];
     const int tid = threadIdx.x;
     const int64_t n = P.n;
     const int64_t blk = P.blk0 + blockIdx.x;   // this launch may cover a chunk of the blocks
@@ -147,12 +149,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         unsigned om = 0u;
         if (g * kPageSlots < c) {
             const uint32_t s = d.y;
-            const uint32_t xl = s & 0xffu, xh = (s >> 8) & 0xffu, yl = (s >> 16) & 0xffu, yh = s >> 24;
-#pragma unroll
-            for (int k = 0; k < MAXM; ++k)
-                if (k < P.m && xl <= (bc[k] & 0xffu) && xh >= ((bc[k] >> 8) & 0xffu) &&
-                    yl <= ((bc[k] >> 16) & 0xffu) && yh >= (bc[k] >> 24))
-                    om |= 1u << k;
+            om = box_open_mask<MAXM>(s, bc, P.m);
 #if FS2_PAGE_REFINE
             // the box survived the bands: the full (Euclidean) box test
             if (om) {
@@ -194,14 +191,41 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             }
         }
     };
-    Desc dq[kDescAhead];             // descriptors of pages g .. g + kDescAhead - 1 in flight
+    // The rows to stream: those whose workgroup row box some band leaves open
+    // (every lane's page box of the row lies inside it, and the band test is
+    // monotone in the box, so a rejected row would reject each lane's page);
+    // without row boxes, every row.  One thread per row, compacted in row order.
+    const bool use_bb = map.bbox != nullptr;
+    int nrows = map.rows;
+    if (use_bb) {
+        bool pass = false;
+        if (tid < map.rows) pass = box_open_mask<MAXM>(map.bbox[blk * kBBoxRows + tid], bc, P.m) != 0u;
+        const uint64_t bm = __ballot(pass);
+        const int wid = tid >> 6, lane = tid & 63;
+        if (lane == 0) s_wc[wid] = __popcll(bm);
+        __syncthreads();
+        int off = 0;
+        nrows = 0;
 #pragma unroll
-    for (int q = 0; q < kDescAhead; ++q) dq[q] = ptrow[(int64_t)min(q, rlast) * n];
-    for (int g = 0; __any(g * kPageSlots < c); ++g) {
+        for (int w = 0; w < kBlock / 64; ++w) {
+            off += (w < wid) ? s_wc[w] : 0;
+            nrows += s_wc[w];
+        }
+        if (pass) s_rows[off + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)tid;
+        __syncthreads();
+    }
+    // row of list entry q (past the end: row 0, a valid address whose load is discarded)
+    auto row_at = [&](int q) -> int { return use_bb ? (q < nrows ? (int)s_rows[q] : 0) : min(q, rlast); };
+    Desc dq[kDescAhead];             // descriptors of list entries q .. q + kDescAhead - 1 in flight
+#pragma unroll
+    for (int q = 0; q < kDescAhead; ++q) dq[q] = ptrow[(int64_t)row_at(q) * n];
+    for (int q = 0; q < nrows; ++q) {
+        const int g = row_at(q);
+        if (!__any(g * kPageSlots < c)) break;      // rows ascend: no lane has more
         const Desc d = dq[0];
 #pragma unroll
-        for (int q = 0; q + 1 < kDescAhead; ++q) dq[q] = dq[q + 1];
-        dq[kDescAhead - 1] = ptrow[(int64_t)min(g + kDescAhead, rlast) * n];
+        for (int u = 0; u + 1 < kDescAhead; ++u) dq[u] = dq[u + 1];
+        dq[kDescAhead - 1] = ptrow[(int64_t)row_at(q + kDescAhead) * n];
         if (g * kPageSlots < c) ++groups;
         const unsigned om = open_mask(d, g);
         if (!__any(om)) continue;
@@ -265,6 +289,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ uint2 s_cow[kBlock / 64][64 * (MAXM + 1)];   // per wave: (shared page, copy)
     __shared__ float4 s_mv[MAXM][kBlock];       // new mirrors of the slots phase A modified
     __shared__ int s_best[MAXM][kBlock], s_bpos[MAXM][kBlock];   // overflow path: per-measurement answer
+    __shared__ BoxLds s_bb;                     // this workgroup's row boxes (grown by the writes)
 
 #ifdef FS2_PHASE_TIMING
     unsigned long long ph_last = 0;
@@ -277,6 +302,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     if (tid < MAXM) s_ms[tid] = Meas{P.meas.d[tid], P.meas.b[tid], P.meas.ox[tid], P.meas.oy[tid]};
 #pragma unroll
     for (int k = 0; k < MAXM; ++k) s_idx[k][tid] = -2;
+    if (P.map.bbox && tid < P.map.rows) lds_box_set(s_bb, tid, P.map.bbox[blk * kBBoxRows + tid]);
     __syncthreads();
 
     double px = 0.0, py = 0.0, pyaw = 0.0, w = 0.0;
@@ -321,6 +347,11 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
 
     const M2 R{P.R[0], P.R[1], P.R[2], P.R[3]};
+    // every descriptor box this lane stores grows the workgroup's row box (an LDS
+    // read; atomics only when the row box grows)
+    auto box_note = [&](int row, uint32_t b) {
+        if (map.bbox) lds_box_merge(s_bb, row, b);
+    };
     unsigned pend = live ? ((1u << P.m) - 1u) : 0u;
     unsigned visited = 0, candidates = 0, written = 0, amb = 0, appends = 0;
     bool singular = false;
@@ -657,6 +688,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 for (int u = t; u < MAXM; ++u)
                     if (u < nmod && canon[u] == t) d = merge_summary(d, s_mv[u][tid], map.frame);
                 *pt_entry(map, rrow[t], il) = d;
+                box_note(rrow[t], d.y);
                 rdesc[t] = d;
             }
         }
@@ -709,7 +741,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             const float4 mv = store_slot(map, pg, jh, s, r, jh);
             smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
             if (jh / kPageSlots == arow) ad = merge_summary(ad, mv, map.frame);
-            else note_write(map, jh, il, mv, false);
+            else box_note(jh / kPageSlots, note_write(map, jh, il, mv, false).y);
             s_idx[k][tid] = c + hit;
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
@@ -719,7 +751,10 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             const uint32_t r = sel_u32(nrec, frec);
             ++nrec;
             if (ja % kPageSlots == 0) {
-                if (arow >= 0) *pt_entry(map, arow, il) = ad;     // leaving that row
+                if (arow >= 0) {                                  // leaving that row
+                    *pt_entry(map, arow, il) = ad;
+                    box_note(arow, ad.y);
+                }
                 const uint32_t id = take_page(P.alloc, map.n, il, nalloc);
                 arow = ja / kPageSlots;
                 const float4 mv = store_slot(map, page_ptr(map.pool, id), ja, s, r, ja);
@@ -737,7 +772,10 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         }
         ++written;
     }
-    if (arow >= 0) *pt_entry(map, arow, il) = ad;
+    if (arow >= 0) {
+        *pt_entry(map, arow, il) = ad;
+        box_note(arow, ad.y);
+    }
     c += nap;
 
     FS2_PHASE(5);
@@ -780,6 +818,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                               : 0xffffffffu);
     block_counters<kBlock, 0, kNumCounters>(cv, P.cpart, P.nblk, blk, assign, live ? w : 0.0,
                                             P.last_pass ? P.wpart + blk : nullptr);
+    // (block_counters' barrier orders every box_note before these reads)
+    if (map.bbox && tid < map.rows) map.bbox[blk * kBBoxRows + tid] = lds_box_get(s_bb, tid);
     lower_slb(map.slb, smin_w);
 }
 

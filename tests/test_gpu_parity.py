@@ -657,3 +657,97 @@ def test_sweep_scan_tiles(fs):
         assert lib.fs2_debug_sweep_scan(0, out.ctypes.data, nb, C.byref(tot)) == 0
         assert tot.value == int(cnt.sum()), nb
         assert np.array_equal(out, np.concatenate([[0], np.cumsum(cnt)[:-1]])), nb
+
+
+def _meas_at(pts):
+    """Robot-frame (distance, angle) whose observed point is each (x, y): the
+    association compares that point with world-frame landmarks."""
+    pts = np.asarray(pts, float)
+    return np.stack([np.hypot(pts[:, 0], pts[:, 1]), np.arctan2(pts[:, 1], pts[:, 0])], 1)
+
+
+def test_row_boxes_follow_resampled_and_appended_maps(fs):
+    """Workgroup row boxes (k_candidates skips rows whose workgroup box every band
+    rejects): each of 8 workgroups' maps sits in its own region, so the boxes are
+    tight and disjoint; peaked likelihoods then resample every output from the
+    last workgroup's particles (the other workgroups' boxes must take its rows),
+    and the misses append landmarks in new rows that later scans match.  Filter
+    on / off bit-identical and equal to the oracle at every scan."""
+    from oracle import oracle as orc
+    N, L, cap = 2048, 24, 64
+    rng = np.random.default_rng(41)
+    centres = np.array([[30.0 * np.cos(a), 30.0 * np.sin(a)] for a in np.linspace(0, 2 * np.pi, 9)[:8]])
+    lm = np.zeros((N, L, 6))
+    for b in range(8):
+        sl = slice(256 * b, 256 * b + 256)
+        lm[sl, :, 0:2] = centres[b] + rng.uniform(-4, 4, (L, 2)) + rng.normal(0, 0.05, (256, L, 2))
+    lm[:, :, 2] = lm[:, :, 5] = 0.02
+    x = rng.normal(0, 0.05, N)
+    y = rng.normal(0, 0.05, N)
+    yaw = rng.normal(0, 0.01, N)
+    fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False,
+                       landmark_capacity=cap) for g in (True, False)]
+    for f in fl:
+        f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, cap)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    target = lm[N - 1, 5, 0:2]               # a landmark of the last workgroup's maps
+    scans = [
+        _meas_at([target, centres[0] + [60.0, 0.0]]),         # resample onto workgroup 7; one append
+        _meas_at([target + [0.1, 0.1], centres[0]]),            # every particle now a copy of 7
+        _meas_at([centres[0] + [60.0, 0.0], centres[3] + [9.0, 9.0]]),   # the appended landmark; a new one
+        _meas_at([centres[3] + [9.0, 9.0], target]),
+    ]
+    resampled = hit = app = 0
+    for sc, ms in enumerate(scans):
+        rot, tr = (0.0, 0.02)
+        nz = rng.normal(0, 0.0055, N)
+        u0 = 0.37 / N
+        out = [f.step(rot, tr, ms, None, nz, u0) for f in fl]
+        opose, oassoc, ors, one = o.iterate(rot, tr, ms, nz, u0)
+        assert np.array_equal(fl[0].associations(), fl[1].associations()), sc
+        assert np.array_equal(fl[0].associations(), oassoc), sc
+        assert bool(out[0][1].resampled) == ors, sc
+        assert np.allclose(out[0][0], opose, rtol=RTOL, atol=1e-12), sc
+        resampled += out[0][1].resampled
+        hit += int((oassoc >= 0).sum())
+        app += int((oassoc == -1).sum())
+    assert resampled >= 1 and hit > 0 and app > 0
+    s0, s1 = fl[0].get_state(lm_cap=cap), fl[1].get_state(lm_cap=cap)
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(s0[4], o.cnt)
+    assert np.allclose(s0[5], o.lm, rtol=RTOL, atol=1e-12)
+    for f in fl:
+        f.close()
+
+
+def test_maps_beyond_row_boxes(fs):
+    """Maps of more than 256 page rows (2048 slots) run without workgroup row
+    boxes: filter on / off identical and equal to the oracle."""
+    from oracle import oracle as orc
+    N, L, cap = 300, 2100, 2112
+    rng = np.random.default_rng(43)
+    lm = np.zeros((N, L, 6))
+    lm[:, :, 0:2] = rng.uniform(-50, 50, (L, 2)) + rng.normal(0, 0.05, (N, L, 2))
+    lm[:, :, 2] = lm[:, :, 5] = 0.05
+    x, y, yaw = (rng.normal(0, 0.05, N) for _ in range(3))
+    fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False,
+                       landmark_capacity=cap) for g in (True, False)]
+    for f in fl:
+        f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, cap)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    for sc in range(3):
+        ms = _meas_at([lm[0, 2000 - 7 * sc, 0:2], lm[0, 17 + sc, 0:2], [80.0, 80.0]])
+        nz = rng.normal(0, 0.0055, N)
+        out = [f.step(0.0, 0.02, ms, None, nz, 0.5 / N) for f in fl]
+        opose, oassoc, ors, one = o.iterate(0.0, 0.02, ms, nz, 0.5 / N)
+        assert np.array_equal(fl[0].associations(), fl[1].associations()), sc
+        assert np.array_equal(fl[0].associations(), oassoc), sc
+        assert np.allclose(out[0][0], opose, rtol=RTOL, atol=1e-12), sc
+    s0 = fl[0].get_state(lm_cap=cap)
+    assert np.array_equal(s0[4], o.cnt)
+    assert np.allclose(s0[5], o.lm, rtol=RTOL, atol=1e-12)
+    for f in fl:
+        f.close()
