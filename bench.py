@@ -336,13 +336,13 @@ def main():
     if rank == 0:
         launches = max(prof["update_launches"], 1)
         upd_ms = prof["update_ms"] / launches
-        # per-kernel split of the update pass (HIP events around k_candidates on the
-        # library's stream; k_update is the rest of the pass)
+        # per-kernel split of the update pass: start / end events of each dispatch
+        # (hipExtLaunchKernel on the library's stream, libfs2 fold_profile)
         kern = {}
         if prof["filter_launches"] > 0:
             fl = prof["filter_launches"]
             kern["k_candidates"] = (prof["filter_ms"] / fl, prof["filter_bytes"] / fl)
-            kern["k_update"] = ((prof["update_ms"] - prof["filter_ms"]) / fl,
+            kern["k_update"] = (prof["exact_ms"] / max(prof["exact_launches"], 1),
                                 (prof["update_bytes"] - prof["filter_bytes"]) / fl)
         else:
             kern["k_update"] = (upd_ms, prof["update_bytes"] / launches)

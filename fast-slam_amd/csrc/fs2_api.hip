@@ -55,22 +55,25 @@ double gate_to_q(double gate) {
     return q;
 }
 
-// Profiling: four events per scan (start, after k_candidates, after the update
-// pass, after publication), double-buffered and read at the next scan, so the
-// host never waits for them and only two markers sit between kernels.
+// Profiling: six events per scan, taken by the dispatches themselves
+// (hipExtLaunchKernel, FS2_LAUNCH_EV): 0 start of the update pass, 1 end of
+// k_candidates, 4 start of k_update, 2 end of the update pass, 5 start of the
+// reduction (k_wsum), 3 end of the publication.  Each profiled scan takes the
+// next set of a pool and its times are read only by fs2_get_profile (or when the
+// pool is used up), so no event query sits in the scan loop and no marker packet
+// between kernels.
 struct ProfScan {
-    bool pending = false;
-    int set = 0;
     DevStats st{};
     int passes = 0;
     int m = 0;
     uint64_t fixed_bytes = 0;
 };
+constexpr int kProfSets = 128;
 struct ProfEvents {
-    hipEvent_t e[2][4] = {};
+    hipEvent_t e[kProfSets][6] = {};
+    ProfScan scan[kProfSets];
     bool ok = false;
-    int cur = 0;
-    ProfScan pend;
+    int used = 0;            // sets holding a scan not yet folded
 };
 
 }  // namespace
@@ -116,6 +119,7 @@ struct fs2_handle {
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
     unsigned long long *cpart = nullptr;   // update-pass block counters [kNumCounters][nblocks]
     int64_t *part_best_i = nullptr;
+    unsigned long long *part_slots = nullptr;   // gather: slots per output workgroup
     int32_t *part_maxcnt = nullptr;
     double *cbuf = nullptr, *bsum = nullptr;
     DevStats *stats_dev = nullptr, *stats_host = nullptr;
@@ -515,7 +519,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
     hipFree(h->sout); hipFree(h->bpre); hipFree(h->part_w); hipFree(h->np_part);
     hipFree(h->urec); hipFree(h->sentry);
-    hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i);
+    hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
     if (h->stats_host) hipHostFree(h->stats_host);
@@ -599,6 +603,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_i, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->part_slots, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_maxcnt, nb * 4) == hipSuccess;
     ok &= alloc((void **)&h->cbuf, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->bsum, nsb * 8) == hipSuccess;
@@ -700,7 +705,7 @@ int fs2_set_profiling(fs2_handle *h, int32_t enable) {
             for (auto &e : set) HIP_TRY(h, hipEventCreate(&e));
         h->ev.ok = true;
     }
-    h->ev.pend.pending = false;
+    h->ev.used = 0;
     h->profiling = enable != 0;
     h->prof = fs2_profile{};
     return FS2_OK;
@@ -717,21 +722,34 @@ int fs2_get_profile(const fs2_handle *hc, fs2_profile *out) {
     return FS2_OK;
 }
 
-// Adds the pending profiled scan (ProfEvents) to h->prof.
+static int fold_one(fs2_handle *h, int set);
+
+// Adds every profiled scan not yet folded (ProfEvents) to h->prof.
 static int fold_profile(fs2_handle *h) {
-    ProfScan &p = h->ev.pend;
-    if (!p.pending) return FS2_OK;
-    p.pending = false;
-    hipEvent_t *E = h->ev.e[p.set];
+    const int used = h->ev.used;
+    h->ev.used = 0;
+    for (int k = 0; k < used; ++k) {
+        const int rc = fold_one(h, k);
+        if (rc) return rc;
+    }
+    return FS2_OK;
+}
+
+static int fold_one(fs2_handle *h, int set) {
+    const ProfScan &p = h->ev.scan[set];
+    hipEvent_t *E = h->ev.e[set];
     HIP_TRY(h, hipEventSynchronize(E[3]));
     const DevStats &st = p.st;
-    float a = 0, f = 0, r = 0;
+    float a = 0, f = 0, r = 0, x = 0, t = 0;
     HIP_TRY(h, hipEventElapsedTime(&a, E[0], E[2]));     // update pass(es)
-    HIP_TRY(h, hipEventElapsedTime(&r, E[2], E[3]));     // reduce, resample, publication
+    HIP_TRY(h, hipEventElapsedTime(&r, E[5], E[3]));     // reduce, resample, publication
+    HIP_TRY(h, hipEventElapsedTime(&t, E[0], E[3]));     // the scan on the device
     if (h->cfg.gate_filter && p.m <= kMaxM) {
-        // k_candidates (E[0] directly precedes it: the stats were zeroed by the
-        // previous scan's k_publish, or by a memset ahead of E[0])
+        // k_candidates and, one pass, k_update alone
         HIP_TRY(h, hipEventElapsedTime(&f, E[0], E[1]));
+        HIP_TRY(h, hipEventElapsedTime(&x, E[4], E[2]));
+        h->prof.exact_launches += 1;
+        h->prof.exact_ms += x;
         h->prof.filter_launches += 1;
         h->prof.filter_ms += f;
         // one 8 B descriptor per page, the mirrors of the pages it could not
@@ -743,7 +761,7 @@ static int fold_profile(fs2_handle *h) {
     h->prof.update_launches += p.passes;
     h->prof.update_ms += a;
     h->prof.reduce_ms += r;
-    h->prof.scan_ms += a + r;
+    h->prof.scan_ms += t;
     // mirror reads (16 B) per visited slot when filtering, record reads (48 B) per
     // candidate, slot writes (48 B record + 16 B mirror) and the descriptor of the
     // written row (read + write), candidate list entries written and read back
@@ -816,8 +834,11 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // error return) leaves them to be cleared here
     if (!h->stats_clean) HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
     h->stats_clean = false;
-    hipEvent_t *E = h->ev.e[h->ev.cur];
-    if (prof) HIP_TRY(h, hipEventRecord(E[0], s));
+    if (prof && h->ev.used == kProfSets) {   // pool used up: fold (the scans are long complete)
+        const int rc0 = fold_profile(h);
+        if (rc0) return rc0;
+    }
+    hipEvent_t *E = h->ev.e[h->ev.used];
 
     // ---- fused update passes (move in the first) ----
     UpdateParams up{};
@@ -878,16 +899,17 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         rc = reserve_pages(h, (int64_t)up.m * h->n, &up.alloc);
         if (rc) return rc;
         up.map = h->map();
-        HIP_TRY(h, launch_candidates(up, s));
-        if (prof && k0 == 0) HIP_TRY(h, hipEventRecord(E[1], s));
-        HIP_TRY(h, launch_update(up, s));
+        const bool first = k0 == 0, last = up.last_pass != 0;
+        const bool cand = up.filter && up.blk1 > up.blk0;
+        HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
+        HIP_TRY(h, launch_update(up, s, (prof && first) ? (cand ? E[4] : E[0]) : nullptr,
+                                 (prof && last) ? E[2] : nullptr));
         ++passes;
         // pose/weight/count read + weight/count write; pose write on the move pass
         fixed_bytes += (uint64_t)h->n * (32 + 4 + 8 + 4 + (up.do_move ? 24 : 0));
         if (up.do_move && noise) fixed_bytes += (uint64_t)h->n * 8;
         if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
     }
-    if (prof) HIP_TRY(h, hipEventRecord(E[2], s));
 
     // ---- normalise, N_eff, estimate ----
     ReduceParams rp{};
@@ -946,6 +968,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.iblk = h->iblk;
     rs.part_best_w = h->part_best_w;
     rs.part_best_i = h->part_best_i;
+    rs.part_slots = h->part_slots;
+    rs.out_range = sh ? 1 : 0;
     rs.stats = h->stats_dev;
     rs.rec = h->rec;
     rs.flip_margin = flip_margin;
@@ -953,7 +977,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout};
 
     // weight total over all ranks (fast_slam_2.py:166)
-    HIP_TRY(h, launch_wsum(rp, s));
+    HIP_TRY(h, launch_wsum(rp, s, prof ? E[5] : nullptr));
     // exact: Python's sum (in particle order) from the update pass's block sums
     if (exact) HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false), s));
     if (sh) {
@@ -1035,10 +1059,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // GPU: together with the post-resample estimate, in one launch)
     const unsigned long long pseq = ++h->pub_seq;
     if (sh)
-        HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
+        HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s, prof ? E[3] : nullptr));
     else
-        HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
-    if (prof) HIP_TRY(h, hipEventRecord(E[3], s));
+        HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s, prof ? E[3] : nullptr));
     h->stats_clean = true;
     rc = wait_flag(h, pseq);
     if (rc) return rc;
@@ -1048,17 +1071,11 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     h->last_m = M;
     h->scan += 1;
     if (prof) {
-        // the previous profiled scan's events are complete (this scan ran after them)
-        rc = fold_profile(h);
-        if (rc) return rc;
-        ProfScan &p = h->ev.pend;
-        p.pending = true;
-        p.set = h->ev.cur;
+        ProfScan &p = h->ev.scan[h->ev.used++];
         p.st = st;
         p.passes = passes;
         p.m = M;
         p.fixed_bytes = fixed_bytes;
-        h->ev.cur ^= 1;
     }
     if (out_pose) {
         out_pose[0] = st.pose[0];

@@ -2,6 +2,7 @@
 // fs2_kernels.hip (device code) and fs2_api.hip (host C-ABI).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -261,6 +262,8 @@ struct ResampleParams {
     int32_t *iblk;           // [2 * nblk] per-block counts -> offsets
     double *part_best_w;
     int64_t *part_best_i;
+    unsigned long long *part_slots;   // [blocks] slots of each gather workgroup's outputs
+    int32_t out_range;       // sharded: k_ranges records the rank's output range (out_min/max)
     DevStats *stats;
     RankRecord *rec;         // this rank's post-resample estimate record
     // packing for one destination rank [pa, pb)
@@ -319,10 +322,20 @@ hipError_t launch_chain(const ChainParams &p, hipStream_t s);
 hipError_t launch_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy, hipStream_t s);
 int64_t np_sumsq_chunks(int64_t n);
 
-// ---- launch wrappers (defined in fs2_kernels.hip) ----
-hipError_t launch_candidates(const UpdateParams &p, hipStream_t s);
-hipError_t launch_update(const UpdateParams &p, hipStream_t s);
-hipError_t launch_wsum(const ReduceParams &p, hipStream_t s);
+// Launch of kernel k; with profiling events (e0: its start, e1: its end, either
+// may be null) through hipExtLaunchKernel, which takes both from the dispatch
+// itself: no marker packets between the kernels of a scan.
+#define FS2_LAUNCH_EV(k, g, b, s, e0, e1, ...)                                   \
+    do {                                                                         \
+        if ((e0) || (e1)) hipExtLaunchKernelGGL(k, g, b, 0, s, e0, e1, 0, __VA_ARGS__); \
+        else hipLaunchKernelGGL(k, g, b, 0, s, __VA_ARGS__);                     \
+    } while (0)
+
+// ---- launch wrappers (defined in fs2_*.hip; events: FS2_LAUNCH_EV) ----
+hipError_t launch_candidates(const UpdateParams &p, hipStream_t s, hipEvent_t e0 = nullptr,
+                             hipEvent_t e1 = nullptr);
+hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_wsum(const ReduceParams &p, hipStream_t s, hipEvent_t e0 = nullptr);
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s);
 hipError_t launch_global_total(const ReduceParams &p, hipStream_t s);
 hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s);
@@ -340,10 +353,11 @@ hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 // *flag = seq (system scope, after the stats), and the device copy zeroed for
 // the next scan.  The host spins on the flag instead of a stream sync.
 hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
-                          unsigned long long seq, hipStream_t s);
+                          unsigned long long seq, hipStream_t s, hipEvent_t e1 = nullptr);
 // One GPU: k_estimate + k_global_best (when the resample fired) + k_publish.
 hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
-                              unsigned long long *host_flag, unsigned long long seq, hipStream_t s);
+                              unsigned long long *host_flag, unsigned long long seq, hipStream_t s,
+                              hipEvent_t e1 = nullptr);
 
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset);

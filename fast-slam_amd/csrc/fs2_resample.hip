@@ -256,8 +256,8 @@ __global__ __launch_bounds__(64) void k_publish(DevStats *stats, DevStats *host_
 }
 
 hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
-                          unsigned long long seq, hipStream_t s) {
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, stats, host_stats, host_flag, seq);
+                          unsigned long long seq, hipStream_t s, hipEvent_t e1) {
+    FS2_LAUNCH_EV(k_publish, dim3(1), dim3(64), s, nullptr, e1, stats, host_stats, host_flag, seq);
     return hipGetLastError();
 }
 
@@ -397,7 +397,9 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     if (!P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     __shared__ unsigned long long lds_u[kBlock / 64];
+    __shared__ int64_t s_key[kBlock];
     int omin = INT32_MAX, omax = -1;
+    int64_t llo = INT64_MAX, lhi = -1;       // this particle's local outputs
     unsigned amb = 0;
     // exact chain (one GPU): the running sum of this wave's unit from the unit
     // table -- a translation unit's values are s_in + (prefix of rint(w / u)) u,
@@ -441,19 +443,59 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
             if ((m1 < P.N && u_of(u0, m1, P.N) - cur <= tol) || (m1 > 0 && cur - u_of(u0, m1 - 1, P.N) <= tol))
                 amb = 1;
         }
-        const int64_t llo = max(lo, P.a), lhi = min(hi, P.a + P.n - 1);
-        for (int64_t m = llo; m <= lhi; ++m) P.out_src[m - P.a] = (int32_t)i;
+        llo = max(lo, P.a);
+        lhi = min(hi, P.a + P.n - 1);
         if (lo <= hi) {
             omin = (int)lo;
             omax = (int)hi;
         }
     }
-    // smallest / largest output served by this rank (one atomic per block)
-    const int bmax = block_max_i<kBlock>(omax, lds_i);
-    const int bmin = -block_max_i<kBlock>(omin == INT32_MAX ? INT32_MIN + 1 : -omin, lds_i);
-    if (threadIdx.x == 0 && bmax >= 0) {
-        atomicMin(&P.stats->out_min, bmin);
-        atomicMax(&P.stats->out_max, bmax);
+    // out_src of the local outputs.  The wave's sources are consecutive and their
+    // local output ranges partition one contiguous range in order, so the wave
+    // fills that range together, 64 outputs per step (one lane per source would
+    // store a heavy source's outputs one by one): output o comes from the last
+    // lane whose key <= o, key = the first local output of the lane or, for a lane
+    // with none, of the next lane that has some (a suffix minimum, non-decreasing).
+    {
+        const int lane = threadIdx.x & 63;
+        const bool has = llo <= lhi;
+        int64_t key = has ? llo : INT64_MAX;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t t = __shfl_down(key, o, 64);
+            if (lane + o < 64) key = min(key, t);
+        }
+        s_key[threadIdx.x] = key;
+        int64_t wlo = has ? llo : INT64_MAX, whi = has ? lhi : -1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            wlo = min(wlo, (int64_t)__shfl_xor(wlo, o, 64));
+            whi = max(whi, (int64_t)__shfl_xor(whi, o, 64));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int64_t *wk = s_key + (threadIdx.x - lane);
+        // (a wave without local outputs has wlo = INT64_MAX: no step)
+        for (int64_t o = (wlo <= whi) ? wlo + lane : INT64_MAX; o <= whi; o += 64) {
+            int l = 0, h = 63;
+            while (l < h) {
+                const int mid = (l + h + 1) >> 1;
+                if (wk[mid] <= o) l = mid;
+                else h = mid - 1;
+            }
+            P.out_src[o - P.a] = (int32_t)(i - lane + l);
+        }
+    }
+    // sharded: smallest / largest output served by this rank (one atomic per
+    // block; one GPU serves every output and skips these same-address atomics)
+    if (P.out_range) {
+        const int bmax = block_max_i<kBlock>(omax, lds_i);
+        const int bmin = -block_max_i<kBlock>(omin == INT32_MAX ? INT32_MIN + 1 : -omin, lds_i);
+        if (threadIdx.x == 0 && bmax >= 0) {
+            atomicMin(&P.stats->out_min, bmin);
+            atomicMax(&P.stats->out_max, bmax);
+        }
     }
     if (P.flip_margin > 0.0) {
         const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
@@ -760,12 +802,13 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         }
         if (first) s_sb[off + __popcll(fm & ((1ull << lane) - 1ull))] = s_src[t];
     }
+    // per-block partials (no same-address atomics), folded by estimate_body
     const unsigned long long bs = block_sum_u64<kBlock>(slots, lds_u);
-    if (threadIdx.x == 0 && bs) atomicAdd(&P.stats->resample_slots, bs);
     block_argmax<kBlock>(bv, bi, lds_d, lds_l);
     if (threadIdx.x == 0) {
         P.part_best_w[blockIdx.x] = bv;
         P.part_best_i[blockIdx.x] = bi;
+        P.part_slots[blockIdx.x] = bs;
     }
     // (the barriers above order every LDS write before these reads)
     if (bb && (int)threadIdx.x < P.map.rows) {
@@ -807,15 +850,23 @@ hipError_t launch_bbox_build(MapRef map, const int32_t *cnt, hipStream_t s) {
     return hipGetLastError();
 }
 
-// this rank's first maximum over its outputs -> record (post-resample estimate)
+// this rank's first maximum over its outputs -> record (post-resample estimate);
+// the gather's slot partials -> resample_slots
 __device__ void estimate_body(const ResampleParams &P, int32_t nparts) {
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
+    __shared__ unsigned long long lds_u[16];
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
-    for (int k = threadIdx.x; k < nparts; k += 1024) argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
+    unsigned long long sl = 0;
+    for (int k = threadIdx.x; k < nparts; k += 1024) {
+        argmax_combine(bv, bi, P.part_best_w[k], P.part_best_i[k]);
+        sl += P.part_slots[k];
+    }
     block_argmax<1024>(bv, bi, lds_d, lds_l);
+    sl = block_sum_u64<1024>(sl, lds_u);
     if (threadIdx.x == 0) {
+        P.stats->resample_slots = sl;
         RankRecord r = *P.rec;
         r.best_w = bv;
         r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.a + bi;
@@ -847,9 +898,10 @@ __global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, co
 }
 
 hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
-                              unsigned long long *host_flag, unsigned long long seq, hipStream_t s) {
+                              unsigned long long *host_flag, unsigned long long seq, hipStream_t s,
+                              hipEvent_t e1) {
     const int32_t nparts = (int32_t)((r.n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_tail_single, dim3(1), dim3(1024), 0, s, r, p, nparts, host_stats, host_flag, seq);
+    FS2_LAUNCH_EV(k_tail_single, dim3(1), dim3(1024), s, nullptr, e1, r, p, nparts, host_stats, host_flag, seq);
     return hipGetLastError();
 }
 

@@ -823,17 +823,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     lower_slb(map.slb, smin_w);
 }
 
-hipError_t launch_candidates(const UpdateParams &p, hipStream_t s) {
+hipError_t launch_candidates(const UpdateParams &p, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const unsigned grid = (unsigned)(p.blk1 - p.blk0);
     if (grid == 0 || !p.filter) return hipSuccess;
-    hipLaunchKernelGGL(k_candidates<kMaxM>, dim3(grid), dim3(kBlock), 0, s, p);
+    FS2_LAUNCH_EV(k_candidates<kMaxM>, dim3(grid), dim3(kBlock), s, e0, e1, p);
     return hipGetLastError();
 }
 
-hipError_t launch_update(const UpdateParams &p, hipStream_t s) {
+hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const unsigned grid = (unsigned)(p.blk1 - p.blk0);
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_update<kMaxM>, dim3(grid), dim3(kBlock), 0, s, p);
+    FS2_LAUNCH_EV(k_update<kMaxM>, dim3(grid), dim3(kBlock), s, e0, e1, p);
     return hipGetLastError();
 }
 
@@ -912,8 +912,8 @@ __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
     if (threadIdx.x == 0) P.stats->total = t;
 }
 
-hipError_t launch_wsum(const ReduceParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_wsum, dim3(1 + kWsumCounterBlocks), dim3(1024), 0, s, p);
+hipError_t launch_wsum(const ReduceParams &p, hipStream_t s, hipEvent_t e0) {
+    FS2_LAUNCH_EV(k_wsum, dim3(1 + kWsumCounterBlocks), dim3(1024), s, e0, nullptr, p);
     return hipGetLastError();
 }
 

@@ -99,6 +99,8 @@ class fs2_profile(C.Structure):
         ("filter_launches", C.c_int64),
         ("filter_ms", C.c_double),
         ("filter_bytes", C.c_uint64),
+        ("exact_launches", C.c_int64),
+        ("exact_ms", C.c_double),
     ]
 
     def as_dict(self):
@@ -179,8 +181,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fs2_abi_version() != 1:
-        raise ImportError(f"libfs2 ABI {lib.fs2_abi_version()} != 1")
+    if lib.fs2_abi_version() != 2:
+        raise ImportError(f"libfs2 ABI {lib.fs2_abi_version()} != 2")
     _lib = lib
     return lib
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define FS2_ABI_VERSION 1
+#define FS2_ABI_VERSION 2
 
 enum {
     FS2_OK = 0,
@@ -135,6 +135,8 @@ typedef struct fs2_profile {
     int64_t filter_launches;    /* timed candidate-stream launches (k_candidates) */
     double filter_ms;           /* their summed device time (HIP events) */
     uint64_t filter_bytes;      /* their algorithmic bytes (mirrors, lists, counts) */
+    int64_t exact_launches;     /* timed exact-association launches (k_update; scans of one pass) */
+    double exact_ms;            /* their summed device time (HIP events) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */

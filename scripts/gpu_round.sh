@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 STAGE=${1:-all}
 python -c "import torch; print('torch', torch.__version__, torch.cuda.is_available(), torch.cuda.get_device_name(0))" > gpurun_out/env.log 2>&1
 if [[ $STAGE == all || $STAGE == tests ]]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
   rc=$?
   echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests.log
   if [[ $rc -ne 0 && $rc -ne 1 ]]; then exit $rc; fi

@@ -35,7 +35,7 @@ def load(name):
 def test_native_loaded(fs):
     from fast_slam_2 import _native
     lib = _native.load()
-    assert lib.fs2_abi_version() == 1
+    assert lib.fs2_abi_version() == 2
 
 
 def test_mahalanobis_bit_exact(fs):
