@@ -223,7 +223,62 @@ def robustness(args, f, L, first_scan):
     out["no_gate_filter"] = timed_scans(g, scans, gm.__getitem__, syn.odometry, 3)
     out["no_gate_filter"]["note"] = "grid map, every slot's fp64 record read (no mirrors, no page boxes)"
     g.close()
+    out["sharded_local_g2"] = sharded_local(args, L, n)
     return out
+
+
+def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
+    """The sharded path (fs2_comm.hpp) with G ranks as threads of this process on
+    this GPU (in-process transport: device copies + host barriers), n_total
+    particles in all: the per-scan time and the host time inside the transport
+    calls and mid-scan waits (libfs2 profile comm_ms).  Not an RCCL figure."""
+    import threading
+    import fast_slam_2
+    import fs2_synthetic as syn
+    key = os.urandom(128)
+    hs = [fast_slam_2.FastSLAM2(n_total, rng="device", seed=args.seed, landmark_capacity=L + scans + 8, rank=g,
+                                world_size=G, comm_id=key, comm_mode="local", verbose=False) for g in range(G)]
+    for g, h in enumerate(hs):
+        populate(h, h.n_local, L, args.seed, g)
+    meas = {s: np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64) for s in range(scans)}
+    res = [0] * G
+
+    def step_all(s):
+        err = []
+
+        def run(g):
+            try:
+                _, st = hs[g].step(*syn.odometry(s), meas[s])
+                res[g] += st.resampled
+            except Exception as e:  # surfaced below
+                err.append(e)
+        th = [threading.Thread(target=run, args=(g,)) for g in range(G)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise err[0]
+    for s in range(warm):
+        step_all(s)
+    for h in hs:
+        h.set_profiling(True)
+    res = [0] * G
+    t0 = time.perf_counter()
+    for s in range(warm, scans):
+        step_all(s)
+    dt = time.perf_counter() - t0
+    k = scans - warm
+    profs = [h.profile() for h in hs]
+    for h in hs:
+        h.close()
+    return {"value": n_total * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k, "ranks": G, "resamples": res[0],
+            "comm_ms_per_scan": max(p["comm_ms"] for p in profs) / k,
+            "comm_calls_per_scan": profs[0]["comm_calls"] / k,
+            "scan_device_ms": max(p["scan_ms"] / max(p["scans"], 1) for p in profs),
+            "note": f"{G} ranks as threads on one GPU, in-process transport, {n_total} particles in all; "
+                    "comm: host time in transport calls and mid-scan waits (a wait includes the collectives "
+                    "queued before it)"}
 
 
 def main():

@@ -17,6 +17,7 @@
 #include "fs2_comm.hpp"
 #include "fs2_frontend.hpp"
 #include "fs2_kernels.hpp"
+#include "fs2_plan.hpp"
 
 using namespace fs2;
 
@@ -114,7 +115,8 @@ struct fs2_handle {
     int64_t *rbcnt = nullptr;
     int64_t *rnfree_dev = nullptr;
     int64_t s_recv = 0;                    // slots received by the last resample
-    int32_t *rank_d = nullptr, *rank_e = nullptr, *iblk = nullptr;
+    int32_t *rank_d = nullptr, *rank_e = nullptr;
+    int64_t *iblk = nullptr;
     int cap = 0, max_cap = kMaxSlots;
     double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
     unsigned long long *cpart = nullptr;   // update-pass block counters [kNumCounters][nblocks]
@@ -122,7 +124,12 @@ struct fs2_handle {
     unsigned long long *part_slots = nullptr;   // gather: slots per output workgroup
     int32_t *part_maxcnt = nullptr;
     double *cbuf = nullptr, *bsum = nullptr;
-    DevStats *stats_dev = nullptr, *stats_host = nullptr;
+    DevStats *stats_dev = nullptr;
+    // mid-scan posts of sharded ranks (k_post): DevStats + transfer sizes, then the flag
+    char *post_host = nullptr, *post = nullptr;       // host / device view of one coherent block
+    unsigned long long *post_flag = nullptr, *post_flag_dev = nullptr;
+    unsigned long long post_seq = 0;
+    PackPlan *plan = nullptr;                       // [kMaxRanks] what goes to each rank
     // end-of-scan publication (k_publish): stats + sequence flag in coherent host memory
     DevStats *pub_stats = nullptr, *pub_stats_dev = nullptr;
     unsigned long long *pub_flag = nullptr, *pub_flag_dev = nullptr;
@@ -203,6 +210,20 @@ struct fs2_handle {
         return p;
     }
 };
+
+// Host wall time of one transport call or mid-scan wait, into the profile.
+struct CommTimer {
+    fs2_handle *h;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit CommTimer(fs2_handle *hh) : h(hh) {}
+    ~CommTimer();
+};
+
+CommTimer::~CommTimer() {
+    if (!h->profiling) return;
+    h->prof.comm_calls += 1;
+    h->prof.comm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 
 // Page-table rows for maps of up to need_slots slots (current buffer kept).
 static int grow_rows(fs2_handle *h, int need_slots) {
@@ -361,50 +382,76 @@ static int ensure_buf(fs2_handle *h, std::vector<char *> &bufs, std::vector<size
     return FS2_OK;
 }
 
-// Sharded resample: pack the local particles whose output range reaches another
-// rank, agree on transfer sizes, move them with one grouped exchange and
-// describe what arrived to the apply kernels.
+// Wait for a post (k_post / k_publish) whose flag reaches seq: spin for up to
+// 50 ms, then fall back to a stream sync, which also reports a fault.
+static int wait_seq(fs2_handle *h, const unsigned long long *flag, unsigned long long seq, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return FS2_OK;
+        if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+        __builtin_ia32_pause();
+    }
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) return set_err(&h->err, FS2_ERR_HIP, "%s were not posted", what);
+    return FS2_OK;
+}
+
+// Sharded ranks, mid-scan: the statistics so far (the resample decision, the
+// largest map on any rank) and, with xmat, the all-gathered transfer sizes, read
+// through the post block.
+static int post_and_wait(fs2_handle *h, bool sizes) {
+    CommTimer ct(h);
+    const int G = h->cfg.world_size;
+    const unsigned long long seq = ++h->post_seq;
+    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? 2 * G * G : 0, h->post, h->post_flag_dev,
+                           seq, h->stream));
+    return wait_seq(h, h->post_flag, seq, "mid-scan statistics");
+}
+static const DevStats &posted_stats(const fs2_handle *h) { return *reinterpret_cast<const DevStats *>(h->post_host); }
+static const int64_t *posted_xmat(const fs2_handle *h) {
+    return reinterpret_cast<const int64_t *>(h->post_host + sizeof(DevStats));
+}
+
+// Sharded resample: plan what goes to every other rank on the device (one run of
+// local particles per destination, fs2_plan.hpp), all-gather the sizes, learn
+// them with one post, pack all destinations in one launch and move them with one
+// grouped exchange; then describe what arrived to the apply kernels.
 static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     const int G = h->cfg.world_size, R = h->cfg.rank;
-    const int64_t N = h->n_global;
     hipStream_t s = h->stream;
-    HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
-    HIP_TRY(h, hipStreamSynchronize(s));
-    const int64_t omin = h->stats_host->out_min, omax = h->stats_host->out_max;
-    std::vector<int64_t> row(2 * G, 0);
-    int32_t tot[2];
-    for (int p = 0; p < G; ++p) {
-        const int64_t pa = N * p / G, pb = N * (p + 1) / G;
-        if (p == R || omax < pa || omin >= pb) continue;
-        rs.pa = pa;
-        rs.pb = pb;
-        HIP_TRY(h, launch_pack_count(rs, s));
-        HIP_TRY(h, hipMemcpyAsync(tot, h->iblk + 2 * rs.nblk, sizeof tot, hipMemcpyDeviceToHost, s));
-        HIP_TRY(h, hipStreamSynchronize(s));
-        const int64_t K = tot[0], S = tot[1];
-        if (K == 0) continue;
-        int rc = ensure_buf(h, h->sendbuf, h->sendcap, p, (size_t)(K + S) * 64);
-        if (rc) return rc;
-        rs.shdr = reinterpret_cast<PackHeader *>(h->sendbuf[p]);
-        rs.spay = h->sendbuf[p] + K * 64;
-        HIP_TRY(h, launch_pack_write(rs, (int32_t)K, s));
-        row[2 * p] = K;
-        row[2 * p + 1] = S;
+    rs.world = G;
+    rs.rank = R;
+    rs.plan = h->plan;
+    rs.xrow = h->xrow;
+    HIP_TRY(h, launch_pack_count(rs, s));
+    int rc;
+    {
+        CommTimer ct(h);
+        rc = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 2 * G, s, &h->err);
     }
-    HIP_TRY(h, hipMemcpyAsync(h->xrow, row.data(), sizeof(int64_t) * 2 * G, hipMemcpyHostToDevice, s));
-    int rc = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 2 * G, s, &h->err);
     if (rc) return rc;
-    std::vector<int64_t> mat(2 * G * G);
-    HIP_TRY(h, hipMemcpyAsync(mat.data(), h->xmat, sizeof(int64_t) * 2 * G * G, hipMemcpyDeviceToHost, s));
-    HIP_TRY(h, hipStreamSynchronize(s));
+    rc = post_and_wait(h, true);
+    if (rc) return rc;
+    const std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + 2 * G * G);
+    int64_t nsend = 0;
     std::vector<fs2comm::Xfer> sends, recvs;
+    for (int p = 0; p < G; ++p) {
+        rs.sbuf[p] = nullptr;
+        const int64_t K = mat[(size_t)R * 2 * G + 2 * p], S = mat[(size_t)R * 2 * G + 2 * p + 1];
+        if (p == R || K == 0) continue;
+        rc = ensure_buf(h, h->sendbuf, h->sendcap, p, (size_t)(K + S) * 64);
+        if (rc) return rc;
+        rs.sbuf[p] = h->sendbuf[p];
+        sends.push_back({p, h->sendbuf[p], (size_t)(K + S) * 64});
+        nsend += K;
+    }
+    if (nsend > INT32_MAX) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld particles to send", (long long)nsend);
+    HIP_TRY(h, launch_pack_write(rs, (int32_t)nsend, s));
     rs.npeers = 0;
     int32_t kbase = 0;
     int64_t sbase = 0;
     for (int q = 0; q < G; ++q) {
         if (q == R) continue;
-        if (row[2 * q])
-            sends.push_back({q, h->sendbuf[q], (size_t)(row[2 * q] + row[2 * q + 1]) * 64});
         const int64_t K = mat[(size_t)q * 2 * G + 2 * R], S = mat[(size_t)q * 2 * G + 2 * R + 1];
         if (!K) continue;
         rc = ensure_buf(h, h->recvbuf, h->recvcap, q, (size_t)(K + S) * 64);
@@ -419,7 +466,10 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         kbase += (int32_t)K;
         sbase += S;
     }
-    rc = h->tp->exchange(sends, recvs, s, &h->err);
+    {
+        CommTimer ct(h);
+        rc = h->tp->exchange(sends, recvs, s, &h->err);
+    }
     if (rc) return rc;
     h->n_recv = kbase;
     h->s_recv = sbase;
@@ -522,7 +572,8 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
-    if (h->stats_host) hipHostFree(h->stats_host);
+    if (h->post_host) hipHostFree(h->post_host);
+    hipFree(h->plan);
     if (h->pub_stats) hipHostFree(h->pub_stats);
     if (h->noise_pin) hipHostFree(h->noise_pin);
     if (h->u0_pin) hipHostFree(h->u0_pin);
@@ -597,7 +648,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 2 * G * G) == hipSuccess;
     ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 4) == hipSuccess;
+    ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->cpart, nb * 8 * kNumCounters) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
@@ -630,7 +681,20 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     }
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
-    ok &= hipHostMalloc((void **)&h->stats_host, sizeof(DevStats), 0) == hipSuccess;
+    {
+        // post block: DevStats, xmat (2 G x G words), then the flag on its own line
+        const size_t body = sizeof(DevStats) + sizeof(int64_t) * 2 * kMaxRanks * kMaxRanks;
+        const size_t off = ((body + 63) / 64) * 64;
+        ok &= hipHostMalloc((void **)&h->post_host, off + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
+              hipSuccess;
+        if (ok) {
+            h->post_flag = reinterpret_cast<unsigned long long *>(h->post_host + off);
+            *h->post_flag = 0;
+            ok &= hipHostGetDevicePointer((void **)&h->post, h->post_host, 0) == hipSuccess;
+            if (ok) h->post_flag_dev = reinterpret_cast<unsigned long long *>(h->post + off);
+        }
+    }
+    ok &= alloc((void **)&h->plan, sizeof(PackPlan) * kMaxRanks) == hipSuccess;
     // one coherent block: the published stats, then the flag on its own 64-byte line
     ok &= hipHostMalloc((void **)&h->pub_stats, sizeof(DevStats) + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
           hipSuccess;
@@ -969,7 +1033,6 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.part_best_w = h->part_best_w;
     rs.part_best_i = h->part_best_i;
     rs.part_slots = h->part_slots;
-    rs.out_range = sh ? 1 : 0;
     rs.stats = h->stats_dev;
     rs.rec = h->rec;
     rs.flip_margin = flip_margin;
@@ -981,7 +1044,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // exact: Python's sum (in particle order) from the update pass's block sums
     if (exact) HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false), s));
     if (sh) {
-        rc = h->tp->allgather(&h->stats_dev->total, h->totals, sizeof(double), s, &h->err);
+        {
+            CommTimer ct(h);
+            rc = h->tp->allgather(&h->stats_dev->total, h->totals, sizeof(double), s, &h->err);
+        }
         if (rc) return rc;
         HIP_TRY(h, launch_global_total(rp, s));
     }
@@ -993,7 +1059,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
     HIP_TRY(h, launch_finalize(rp, s));
     if (sh) {
-        rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+        {
+            CommTimer ct(h);
+            rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+        }
         if (rc) return rc;
     }
     // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183); on
@@ -1011,9 +1080,9 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // rule fired, sharded ranks learn the decision first (sizes of the transfers) ----
     bool run_resample = true;
     if (sh) {
-        HIP_TRY(h, hipMemcpyAsync(h->stats_host, h->stats_dev, sizeof(DevStats), hipMemcpyDeviceToHost, s));
-        HIP_TRY(h, hipStreamSynchronize(s));
-        run_resample = h->stats_host->resampled != 0;
+        rc = post_and_wait(h, false);
+        if (rc) return rc;
+        run_resample = posted_stats(h).resampled != 0;
     }
     if (run_resample) {
         // every local output is written below: the output ranges of the local
@@ -1024,7 +1093,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             if (rc) return rc;
             // received maps can be longer than every local one: rows for the
             // largest map on any rank (k_global_finalize) before unpacking them
-            rc = grow_rows(h, h->stats_host->max_count);
+            rc = grow_rows(h, posted_stats(h).max_count);
             if (rc) return rc;
             rs.opt = h->pt[nxt];
             rs.obbox = h->row_boxes(nxt);
@@ -1048,7 +1117,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         }
         HIP_TRY(h, launch_resample_apply(rs, sh, s));
         if (sh) {
-            rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+            {
+                CommTimer ct(h);
+                rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+            }
             if (rc) return rc;
             HIP_TRY(h, launch_global_best(rp, s));
         }
@@ -1763,6 +1835,49 @@ int fs2_comm_unique_id(uint8_t out[128]) {
     std::string err;
     int rc = fs2comm::unique_id(out, &err);
     if (rc) return set_err(nullptr, rc, "%s", err.c_str());
+    return FS2_OK;
+}
+
+int fs2_plan_ranges(const double *c, int64_t n, int64_t first_global, int64_t N, double offset, double u0,
+                    int32_t *mlo, int32_t *mhi) {
+    if ((n > 0 && (!c || !mlo || !mhi)) || n < 0 || first_global < 0 || first_global + n > N || N > INT32_MAX)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_plan_ranges: bad arguments");
+    // k_ranges without the exact chain: the running value through particle i
+    const bool r0 = first_global == 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t g = first_global + i;
+        const double cur = r0 ? c[i] : offset + c[i];
+        const double prev = (g == 0) ? 0.0 : ((i == 0) ? offset : (r0 ? c[i - 1] : offset + c[i - 1]));
+        int64_t lo, hi;
+        plan_range(g, N, prev, cur, u0, lo, hi);
+        mlo[i] = (int32_t)lo;
+        mhi[i] = (int32_t)hi;
+    }
+    return FS2_OK;
+}
+
+int fs2_plan_sends(const int32_t *mlo, const int32_t *mhi, const int32_t *cnt, int64_t n, int64_t N,
+                   int32_t world, int32_t rank, int64_t *run, int64_t *K, int64_t *S) {
+    if ((n > 0 && (!mlo || !mhi || !cnt)) || !run || !K || !S || world < 1 || world > kMaxRanks || rank < 0 ||
+        rank >= world || n < 0)
+        return set_err(nullptr, FS2_ERR_ARG, "fs2_plan_sends: bad arguments");
+    // k_pack_plan / k_pack_bounds: exclusive counts of non-empty ranges and their slots
+    std::vector<int64_t> E(n + 1, 0), C(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        const bool ne = mlo[i] <= mhi[i];
+        E[i + 1] = E[i] + (ne ? 1 : 0);
+        C[i + 1] = C[i] + (ne ? cnt[i] : 0);
+    }
+    for (int p = 0; p < world; ++p) {
+        int64_t i0 = 0, i1 = 0;
+        if (p != rank)
+            plan_run(n, shard_begin(N, world, p), shard_begin(N, world, p + 1), [&](int64_t i) { return (int64_t)mlo[i]; },
+                     [&](int64_t i) { return (int64_t)mhi[i]; }, i0, i1);
+        run[2 * p] = i0;
+        run[2 * p + 1] = i1;
+        K[p] = E[i1] - E[i0];
+        S[p] = C[i1] - C[i0];
+    }
     return FS2_OK;
 }
 

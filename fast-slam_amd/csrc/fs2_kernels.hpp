@@ -120,6 +120,16 @@ struct PackHeader {
 
 constexpr int kMaxRanks = 16;
 
+// What this rank sends to one destination (k_pack_bounds): the run [i0, i1) of
+// local particles whose outputs may reach its shard [pa, pb), the exclusive
+// counts of non-empty ranges / slots before i0, and the transfer's records / slots.
+struct PackPlan {
+    int64_t i0, i1;
+    int64_t e0, c0;
+    int64_t K, S;
+    int64_t pa, pb;
+};
+
 struct RecvPeer {
     const PackHeader *hdr;   // K headers
     const char *pay;         // payload base
@@ -257,19 +267,19 @@ struct ResampleParams {
     Desc *rdesc;             // [nrecv][rows] descriptors of received pages
     PageAlloc alloc;         // received particle r: row k -> page base + r*rows + k,
                              // slot q -> record rbase + peer sbase + soff + q
-    int32_t *rank_d;         // [n] rank among packed records
-    int32_t *rank_e;         // [n] packed slot offset
-    int32_t *iblk;           // [2 * nblk] per-block counts -> offsets
+    int32_t *rank_d;         // [n] non-empty ranges before i in its 1024-block
+    int32_t *rank_e;         // [n] their slots
+    int64_t *iblk;           // [2 * nblk + 2] per-block totals -> exclusive offsets, grand totals
     double *part_best_w;
     int64_t *part_best_i;
     unsigned long long *part_slots;   // [blocks] slots of each gather workgroup's outputs
-    int32_t out_range;       // sharded: k_ranges records the rank's output range (out_min/max)
     DevStats *stats;
     RankRecord *rec;         // this rank's post-resample estimate record
-    // packing for one destination rank [pa, pb)
-    int64_t pa, pb;
-    PackHeader *shdr;        // send headers
-    char *spay;              // send payload
+    // packing for the other ranks (k_pack_plan / k_pack_bounds / k_pack_*)
+    int32_t world, rank;
+    PackPlan *plan;          // [world] per destination
+    int64_t *xrow;           // [2 world] records, slots sent to each rank (all-gathered)
+    char *sbuf[kMaxRanks];   // per destination: K x 64 B headers, then S x 64 B payload
     // received particles
     int32_t npeers;
     RecvPeer peers[kMaxRanks];
@@ -354,6 +364,10 @@ hipError_t launch_global_best(const ReduceParams &p, hipStream_t s);
 // the next scan.  The host spins on the flag instead of a stream sync.
 hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
                           unsigned long long seq, hipStream_t s, hipEvent_t e1 = nullptr);
+// Sharded ranks, mid-scan: DevStats (decision, max count) and nx words of xmat
+// into host (coherent, mapped), then *flag = seq.
+hipError_t launch_post(const DevStats *stats, const int64_t *xmat, int32_t nx, char *host,
+                       unsigned long long *host_flag, unsigned long long seq, hipStream_t s);
 // One GPU: k_estimate + k_global_best (when the resample fired) + k_publish.
 hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
                               unsigned long long *host_flag, unsigned long long seq, hipStream_t s,

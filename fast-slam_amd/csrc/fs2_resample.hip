@@ -18,6 +18,7 @@
 // from another rank) takes over the map of a local particle that feeds no
 // local output, whose landmarks were already packed if another rank needs them.
 #include "fs2_chain.hpp"
+#include "fs2_plan.hpp"
 
 namespace fs2 {
 
@@ -255,6 +256,26 @@ __global__ __launch_bounds__(64) void k_publish(DevStats *stats, DevStats *host_
     publish_body(stats, host_stats, host_flag, seq);
 }
 
+// Mid-scan post (sharded ranks): the scan's statistics so far and the
+// all-gathered transfer sizes into coherent host memory, then the flag; the host
+// spins on it instead of a copy and a stream sync.
+__global__ __launch_bounds__(256) void k_post(const DevStats *stats, const int64_t *xmat, int32_t nx, char *host,
+                                              unsigned long long *host_flag, unsigned long long seq) {
+    constexpr int W = sizeof(DevStats) / 8;
+    const int t = threadIdx.x;
+    if (t < W) reinterpret_cast<uint64_t *>(host)[t] = reinterpret_cast<const uint64_t *>(stats)[t];
+    for (int k = t; k < nx; k += blockDim.x) reinterpret_cast<int64_t *>(host + sizeof(DevStats))[k] = xmat[k];
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_post(const DevStats *stats, const int64_t *xmat, int32_t nx, char *host,
+                       unsigned long long *host_flag, unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, s, stats, xmat, nx, host, host_flag, seq);
+    return hipGetLastError();
+}
+
 hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
                           unsigned long long seq, hipStream_t s, hipEvent_t e1) {
     FS2_LAUNCH_EV(k_publish, dim3(1), dim3(64), s, nullptr, e1, stats, host_stats, host_flag, seq);
@@ -366,39 +387,13 @@ hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s)
 }
 
 // ----------------------------------------------------------------- ranges --
-
-__device__ __forceinline__ double u_of(double u0, int64_t m, int64_t N) {
-    return u0 + (double)m * (1.0 / (double)N);      // fast_slam_2.py:189, as written
-}
-
-// first output m in [0, N] with u_m > v.  u_m is non-decreasing in m (the
-// rounded product and sum are monotone), so the answer is unique: start from
-// the real-arithmetic estimate and step to it (a step or two at most, bounded
-// by a binary search fallback).
-__device__ __forceinline__ int64_t first_above(double v, double u0, int64_t N) {
-    const double est = (v - u0) * (double)N;
-    int64_t m = (est < 0.0) ? 0 : (est >= (double)N ? N : (int64_t)est + 1);
-    for (int it = 0; it < 8; ++it) {
-        if (m > 0 && u_of(u0, m - 1, N) > v) --m;
-        else if (m < N && !(u_of(u0, m, N) > v)) ++m;
-        else return m;
-    }
-    int64_t lo = 0, hi = N;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (u_of(u0, mid, N) > v) hi = mid;
-        else lo = mid + 1;
-    }
-    return lo;
-}
+// (plan arithmetic: fs2_plan.hpp, shared with the host entry points fs2_plan_*)
 
 __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
-    __shared__ int lds_i[kBlock / 64];
     if (!P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     __shared__ unsigned long long lds_u[kBlock / 64];
     __shared__ int64_t s_key[kBlock];
-    int omin = INT32_MAX, omax = -1;
     int64_t llo = INT64_MAX, lhi = -1;       // this particle's local outputs
     unsigned amb = 0;
     // exact chain (one GPU): the running sum of this wave's unit from the unit
@@ -425,14 +420,11 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         const double u0 = P.stats->u0, off = P.stats->offset;
         const int64_t g = P.a + i;
         const double cur = P.use_chain ? cv : ((P.a == 0) ? P.c[i] : off + P.c[i]);
-        int64_t lo;
-        if (g == 0) lo = 0;
-        else {
-            const double prev = P.use_chain ? cprev
-                                            : ((i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1]));
-            lo = first_above(prev, u0, P.N);
-        }
-        const int64_t hi = (g == P.N - 1) ? P.N - 1 : first_above(cur, u0, P.N) - 1;
+        const double prev = (g == 0) ? 0.0
+                                     : (P.use_chain ? cprev
+                                                    : ((i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1])));
+        int64_t lo, hi;
+        plan_range(g, P.N, prev, cur, u0, lo, hi);
         P.mlo[i] = (int32_t)lo;
         P.mhi[i] = (int32_t)hi;
         // tree prefix: a u_m within the rounding bound of this boundary might fall
@@ -440,15 +432,11 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         if (P.flip_margin > 0.0 && g != P.N - 1) {
             const int64_t m1 = hi + 1;                  // first output with u > cur
             const double tol = P.flip_margin * cur;
-            if ((m1 < P.N && u_of(u0, m1, P.N) - cur <= tol) || (m1 > 0 && cur - u_of(u0, m1 - 1, P.N) <= tol))
+            if ((m1 < P.N && plan_u(u0, m1, P.N) - cur <= tol) || (m1 > 0 && cur - plan_u(u0, m1 - 1, P.N) <= tol))
                 amb = 1;
         }
         llo = max(lo, P.a);
         lhi = min(hi, P.a + P.n - 1);
-        if (lo <= hi) {
-            omin = (int)lo;
-            omax = (int)hi;
-        }
     }
     // out_src of the local outputs.  The wave's sources are consecutive and their
     // local output ranges partition one contiguous range in order, so the wave
@@ -487,16 +475,6 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
             P.out_src[o - P.a] = (int32_t)(i - lane + l);
         }
     }
-    // sharded: smallest / largest output served by this rank (one atomic per
-    // block; one GPU serves every output and skips these same-address atomics)
-    if (P.out_range) {
-        const int bmax = block_max_i<kBlock>(omax, lds_i);
-        const int bmin = -block_max_i<kBlock>(omin == INT32_MAX ? INT32_MIN + 1 : -omin, lds_i);
-        if (threadIdx.x == 0 && bmax >= 0) {
-            atomicMin(&P.stats->out_min, bmin);
-            atomicMax(&P.stats->out_max, bmax);
-        }
-    }
     if (P.flip_margin > 0.0) {
         const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
         if (threadIdx.x == 0 && ba) atomicAdd(&P.stats->reduce_amb, ba);
@@ -510,31 +488,44 @@ hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-// ------------------------------------------------- packing for another rank --
+// ------------------------------------------------- packing for other ranks --
+//
+// The local particles whose outputs reach rank p form one run [i0_p, i1_p) of
+// the local index (fs2_plan.hpp plan_run), so one exclusive count E of the
+// non-empty ranges and one of their map sizes C serve every destination: the
+// particle at i is record E[i] - E[i0_p] of rank p's transfer and its slots start
+// at C[i] - C[i0_p].  No host round trip per destination: the counts go to every
+// rank in one all-gather of xrow.
 
-// Block-local exclusive ranks of two 0/1-or-count streams and per-block totals.
-template <typename F>
-__device__ void rank2(const ResampleParams &P, F flags) {
-    __shared__ int lds[2][kBlock / 64];
+// E, C inside each 1024-particle block (rank_d, rank_e) and per-block totals
+// (iblk[b], iblk[nblk + b]); lanes past n count nothing.
+__global__ __launch_bounds__(kBlock) void k_pack_plan(const ResampleParams P) {
+    __shared__ long long lds[2][kBlock / 64];
+    if (!P.stats->resampled) return;
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
-    int fa[kScanPer], fb[kScanPer];
-    int sa = 0, sb = 0;
+    int fa[kScanPer];
+    long long fb[kScanPer];
+    long long sa = 0, sb = 0;
 #pragma unroll
     for (int e = 0; e < kScanPer; ++e) {
         const int64_t t = base + e;
-        fa[e] = fb[e] = 0;
-        if (t < P.n) flags(t, fa[e], fb[e]);
+        fa[e] = 0;
+        fb[e] = 0;
+        if (t < P.n && P.mlo[t] <= P.mhi[t]) {
+            fa[e] = 1;
+            fb[e] = P.cnt[t];
+        }
         sa += fa[e];
         sb += fb[e];
     }
-    const int ia = wave_incl_scan_i(sa), ib = wave_incl_scan_i(sb);
+    const long long ia = wave_incl_scan_i64(sa), ib = wave_incl_scan_i64(sb);
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 63) {
         lds[0][wid] = ia;
         lds[1][wid] = ib;
     }
     __syncthreads();
-    int oa = ia - sa, ob = ib - sb;
+    long long oa = ia - sa, ob = ib - sb;
     for (int k = 0; k < wid; ++k) {
         oa += lds[0][k];
         ob += lds[1][k];
@@ -543,8 +534,8 @@ __device__ void rank2(const ResampleParams &P, F flags) {
     for (int e = 0; e < kScanPer; ++e) {
         const int64_t t = base + e;
         if (t < P.n) {
-            P.rank_d[t] = oa;
-            P.rank_e[t] = ob;
+            P.rank_d[t] = (int32_t)oa;          // < 1024
+            P.rank_e[t] = (int32_t)ob;          // < 1024 * kMaxSlots
         }
         oa += fa[e];
         ob += fb[e];
@@ -555,74 +546,109 @@ __device__ void rank2(const ResampleParams &P, F flags) {
     }
 }
 
-// exclusive scan of the block totals; grand totals at iblk[2*nblk], iblk[2*nblk+1]
-__global__ __launch_bounds__(1) void k_rank_blocks(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    int a = 0, b = 0;
-    for (int k = 0; k < P.nblk; ++k) {
-        const int ta = P.iblk[k], tb = P.iblk[P.nblk + k];
-        P.iblk[k] = a;
-        P.iblk[P.nblk + k] = b;
-        a += ta;
-        b += tb;
-    }
-    P.iblk[2 * P.nblk] = a;
-    P.iblk[2 * P.nblk + 1] = b;
-}
-
-// particles whose output range meets [pa, pb): record rank and payload slot offset
-__global__ __launch_bounds__(kBlock) void k_pack_local(const ResampleParams P) {
-    if (!P.stats->resampled) return;
-    rank2(P, [&](int64_t i, int &fa, int &fb) {
-        const int64_t lo = P.mlo[i], hi = P.mhi[i];
-        if (lo <= hi && lo < P.pb && hi >= P.pa) {
-            fa = 1;
-            fb = P.cnt[i];
+// Exclusive scans of the block totals (totals at iblk[2 nblk], iblk[2 nblk + 1]),
+// then per destination its run, bases and transfer size (xrow: records, slots;
+// zero for this rank and when the rule did not fire).
+__global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
+    __shared__ long long lds[16];
+    const bool fired = P.stats->resampled != 0;
+    if (fired) {
+        for (int half = 0; half < 2; ++half) {
+            int64_t *v = P.iblk + (int64_t)half * P.nblk;
+            const int per = (P.nblk + 1023) / 1024;
+            const int b0 = min(P.nblk, (int)threadIdx.x * per), b1 = min(P.nblk, b0 + per);
+            long long run = 0;
+            for (int b = b0; b < b1; ++b) run += v[b];
+            const long long incl = wave_incl_scan_i64(run);
+            const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            __syncthreads();
+            if (lane == 63) lds[wid] = incl;
+            __syncthreads();
+            long long off = incl - run;
+            for (int k = 0; k < wid; ++k) off += lds[k];
+            for (int b = b0; b < b1; ++b) {
+                const long long t = v[b];
+                v[b] = off;
+                off += t;
+            }
+            if (threadIdx.x == 1023) P.iblk[2 * P.nblk + half] = off;
         }
-    });
+        __syncthreads();
+    }
+    const int p = threadIdx.x;
+    if (p >= P.world) return;
+    PackPlan pl{};
+    if (fired && p != P.rank) {
+        const int64_t pa = shard_begin(P.N, P.world, p), pb = shard_begin(P.N, P.world, p + 1);
+        plan_run(P.n, pa, pb, [&](int64_t i) { return (int64_t)P.mlo[i]; }, [&](int64_t i) { return (int64_t)P.mhi[i]; },
+                 pl.i0, pl.i1);
+        auto E = [&](int64_t i, int half) -> int64_t {
+            return (i >= P.n) ? P.iblk[2 * P.nblk + half]
+                              : P.iblk[(int64_t)half * P.nblk + i / kScanBlock] + (half ? P.rank_e[i] : P.rank_d[i]);
+        };
+        pl.e0 = E(pl.i0, 0);
+        pl.c0 = E(pl.i0, 1);
+        pl.K = E(pl.i1, 0) - pl.e0;
+        pl.S = E(pl.i1, 1) - pl.c0;
+        pl.pa = pa;
+        pl.pb = pb;
+    }
+    P.plan[p] = pl;
+    P.xrow[2 * p] = pl.K;
+    P.xrow[2 * p + 1] = pl.S;
 }
 
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_pack_local, dim3(p.nblk), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_rank_blocks, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL(k_pack_plan, dim3(p.nblk), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_pack_bounds, dim3(1), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
+// Headers of every local particle sent to another rank, into each destination's
+// send buffer (records K x 64 B, then the payload).
 __global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P) {
     if (!P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= P.n) return;
     const int64_t lo = P.mlo[i], hi = P.mhi[i];
-    if (!(lo <= hi && lo < P.pb && hi >= P.pa)) return;
-    const int b = (int)(i / kScanBlock);
-    const int k = P.iblk[b] + P.rank_d[i];
-    PackHeader h{};
-    h.gsrc = P.a + i;
-    h.out_lo = (int32_t)max(lo, P.pa);
-    h.out_hi = (int32_t)min(hi, P.pb - 1);
-    h.cnt = P.cnt[i];
-    h.soff = P.iblk[P.nblk + b] + P.rank_e[i];
-    h.x = P.x[i];
-    h.y = P.y[i];
-    h.yaw = P.yaw[i];
-    h.w = P.w[i];
-    P.shdr[k] = h;
+    if (lo > hi) return;
+    const int64_t b = i / kScanBlock;
+    const int64_t e = P.iblk[b] + P.rank_d[i], c = P.iblk[P.nblk + b] + P.rank_e[i];
+    for (int p = 0; p < P.world; ++p) {
+        const PackPlan &pl = P.plan[p];
+        if (p == P.rank || i < pl.i0 || i >= pl.i1) continue;
+        PackHeader h{};
+        h.gsrc = P.a + i;
+        h.out_lo = (int32_t)max(lo, pl.pa);
+        h.out_hi = (int32_t)min(hi, pl.pb - 1);
+        h.cnt = P.cnt[i];
+        h.soff = (int32_t)(c - pl.c0);
+        h.x = P.x[i];
+        h.y = P.y[i];
+        h.yaw = P.yaw[i];
+        h.w = P.w[i];
+        reinterpret_cast<PackHeader *>(P.sbuf[p])[e - pl.e0] = h;
+    }
 }
 
-// one workgroup per record: pages + records -> packed (cnt x 16 B mirrors, cnt x 48 B slots)
+// One workgroup per sent record: pages + records -> packed (cnt x 16 B mirrors,
+// cnt x 48 B slots); records of all destinations in one grid.
 __global__ __launch_bounds__(kBlock) void k_pack_payload(const ResampleParams P, int32_t nrec) {
     if (!P.stats->resampled) return;
-    for (int k = blockIdx.x; k < nrec; k += gridDim.x) {
-        const PackHeader h = P.shdr[k];
+    for (int r = blockIdx.x; r < nrec; r += gridDim.x) {
+        int p = 0, k = r;
+        while (p < P.world && k >= P.plan[p].K) k -= (int)P.plan[p++].K;
+        const PackPlan &pl = P.plan[p];
+        const PackHeader h = reinterpret_cast<const PackHeader *>(P.sbuf[p])[k];
         const int64_t i = h.gsrc - P.a;
-        int4 *dm = reinterpret_cast<int4 *>(P.spay + (int64_t)h.soff * 64);
+        int4 *dm = reinterpret_cast<int4 *>(P.sbuf[p] + pl.K * 64 + (int64_t)h.soff * 64);
         int4 *df = dm + h.cnt;
         for (int q = threadIdx.x; q < h.cnt; q += kBlock)
             dm[q] = reinterpret_cast<const int4 *>(page_of(P.map, q, i))[q % kPageSlots];
         for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
             const int j = q / 3;
-            const uint32_t r = mirror_rec(load_mirror(page_of(P.map, j, i), j));
-            df[q] = reinterpret_cast<const int4 *>(P.map.recs + (int64_t)r * kRecBytes)[q - 3 * j];
+            const uint32_t rr = mirror_rec(load_mirror(page_of(P.map, j, i), j));
+            df[q] = reinterpret_cast<const int4 *>(P.map.recs + (int64_t)rr * kRecBytes)[q - 3 * j];
         }
     }
 }

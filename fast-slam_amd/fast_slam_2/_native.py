@@ -101,6 +101,8 @@ class fs2_profile(C.Structure):
         ("filter_bytes", C.c_uint64),
         ("exact_launches", C.c_int64),
         ("exact_ms", C.c_double),
+        ("comm_calls", C.c_int64),
+        ("comm_ms", C.c_double),
     ]
 
     def as_dict(self):
@@ -163,6 +165,8 @@ SIGNATURES = [
     ("fs2_frontend", C.c_int, [C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _dp, C.c_int32, C.c_int32,
                                C.POINTER(fs2_frontend_out)]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("fs2_plan_ranges", C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double, _vp, _vp]),
+    ("fs2_plan_sends", C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),
 ]
 
 _lib = None

@@ -137,6 +137,9 @@ typedef struct fs2_profile {
     uint64_t filter_bytes;      /* their algorithmic bytes (mirrors, lists, counts) */
     int64_t exact_launches;     /* timed exact-association launches (k_update; scans of one pass) */
     double exact_ms;            /* their summed device time (HIP events) */
+    int64_t comm_calls;         /* sharded: transport calls and mid-scan waits timed */
+    double comm_ms;             /* their summed host wall time (a mid-scan wait includes the
+                                   collectives queued before it on the stream) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */
@@ -317,6 +320,24 @@ int fs2_frontend(int32_t device, int32_t B, const int64_t *offsets, const double
 
 /* ncclUniqueId for fs2_config.comm_id (call on rank 0, broadcast to all ranks). */
 int fs2_comm_unique_id(uint8_t out[128]);
+
+/* The sharded low-variance resample plan of one rank (replaces the loop of
+ * FastSLAM2.__low_variance_resample, algorithms/fast_slam_2.py:177-199, for the
+ * rank's particles; csrc/fs2_plan.hpp), on the host with the arithmetic the
+ * device kernels k_ranges / k_pack_bounds run, for callers that plan transfers
+ * themselves and for the CPU tests.  Host pointers.
+ * fs2_plan_ranges: the output range [mlo[i], mhi[i]] (empty when mlo > mhi) of
+ *   local particle i (global first_global + i) from the local inclusive prefix
+ *   c[0..n) of the normalised weights, the sum `offset` of the earlier ranks'
+ *   totals (0 on rank 0) and the start u0; outputs follow u_m = u0 + m (1/N).
+ * fs2_plan_sends: for every rank p of `world` (shard [N p / world, N (p+1) / world)),
+ *   the run [run[2p], run[2p+1]) of local particles whose ranges reach that shard
+ *   and the K[p] particles (non-empty ranges) and S[p] map slots (cnt) this rank
+ *   sends it (0 for p == rank). */
+int fs2_plan_ranges(const double *c, int64_t n, int64_t first_global, int64_t N, double offset, double u0,
+                    int32_t *mlo, int32_t *mhi);
+int fs2_plan_sends(const int32_t *mlo, const int32_t *mhi, const int32_t *cnt, int64_t n, int64_t N,
+                   int32_t world, int32_t rank, int64_t *run, int64_t *K, int64_t *S);
 
 #ifdef __cplusplus
 }
