@@ -264,9 +264,12 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
     for h in hs:
         h.set_profiling(True)
     res = [0] * G
+    per = []
     t0 = time.perf_counter()
     for s in range(warm, scans):
+        t1 = time.perf_counter()
         step_all(s)
+        per.append((time.perf_counter() - t1) * 1e3)
     dt = time.perf_counter() - t0
     k = scans - warm
     profs = [h.profile() for h in hs]
@@ -276,6 +279,7 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
             "comm_ms_per_scan": max(p["comm_ms"] for p in profs) / k,
             "comm_calls_per_scan": profs[0]["comm_calls"] / k,
             "scan_device_ms": max(p["scan_ms"] / max(p["scans"], 1) for p in profs),
+            "scan_ms_each": [round(v, 3) for v in per],
             "note": f"{G} ranks as threads on one GPU, in-process transport, {n_total} particles in all; "
                     "comm: host time in transport calls and mid-scan waits (a wait includes the collectives "
                     "queued before it)"}
