@@ -33,6 +33,7 @@ CONFIGS = {
     "4": dict(N=1_000_000, L=500, P=720, icp=True, name="cfg4_N1e6_L500_720beam_icp"),
 }
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PROFILE_EVERY = 4            # timed scans per profiled scan (libfs2 fs2_set_profiling)
 
 
 def parse():
@@ -354,7 +355,9 @@ def main():
 
     for s in range(args.warmup):
         one_scan(s)
-    f.set_profiling(True)
+    # kernel events on every 4th timed scan: a dispatch's start / end events delay
+    # the next dispatch by ~4.5 us, which the other scans do not pay
+    f.set_profiling(True, every=PROFILE_EVERY)
     resamples = 0
     visited = 0
     copied_slots = 0

@@ -144,6 +144,8 @@ struct fs2_handle {
     double gate2 = 64.0;
     std::string err;
     bool profiling = false;
+    int32_t prof_period = 1;               // profile every prof_period-th scan
+    uint64_t prof_tick = 0;
     ProfEvents ev;
     fs2_profile prof{};
     // sharding (world_size > 1)
@@ -163,7 +165,7 @@ struct fs2_handle {
     uint32_t *bM = nullptr;
     long long *udelta = nullptr;
     unsigned long long *ugl = nullptr, *bD = nullptr, *bpd = nullptr;
-    double *sout = nullptr, *bpre = nullptr, *part_w = nullptr, *np_part = nullptr, *sentry = nullptr;
+    double *sout = nullptr, *part_w = nullptr, *np_part = nullptr, *np_leaf = nullptr, *sentry = nullptr;
     UnitRec *urec = nullptr;
 
     MapRef map() const {
@@ -184,7 +186,6 @@ struct fs2_handle {
         p.a = a;
         p.n = n;
         p.bsum = bsum;
-        p.bpre = bpre;
         p.nb = (int32_t)nblocks();
         p.lazy = lazy ? 1 : 0;
         p.uinfo = uinfo;
@@ -206,7 +207,6 @@ struct fs2_handle {
         // recursive summation of n terms >= 0: |chain - exact| <= gamma_n exact; the
         // block estimates add gamma_{n/256 + 30}; doubled, plus slack for the scaling
         p.margin = std::ldexp(2.0 * (double)n + 8192.0, -53);
-        p.bpre_ready = 1;        // k_wsum / k_finalize scan the block sums (ReduceParams bpre_*)
         return p;
     }
 };
@@ -567,7 +567,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->cand); hipFree(h->ncand);
     hipFree(h->uinfo); hipFree(h->uol); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ugl);
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
-    hipFree(h->sout); hipFree(h->bpre); hipFree(h->part_w); hipFree(h->np_part);
+    hipFree(h->sout); hipFree(h->np_leaf); hipFree(h->part_w); hipFree(h->np_part);
     hipFree(h->urec); hipFree(h->sentry);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
@@ -675,7 +675,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= alloc((void **)&h->sout, nu * 8) == hipSuccess;
         ok &= alloc((void **)&h->sentry, nu * 8) == hipSuccess;
         ok &= alloc((void **)&h->urec, nu * sizeof(UnitRec)) == hipSuccess;
-        ok &= alloc((void **)&h->bpre, nb * 8) == hipSuccess;
+        ok &= alloc((void **)&h->np_leaf, (np_sumsq_chunks(n) * 64 + 64) * 8) == hipSuccess;
         ok &= alloc((void **)&h->part_w, nb * 8) == hipSuccess;
         ok &= alloc((void **)&h->np_part, np_sumsq_chunks(n) * 8) == hipSuccess;
     }
@@ -770,7 +770,9 @@ int fs2_set_profiling(fs2_handle *h, int32_t enable) {
         h->ev.ok = true;
     }
     h->ev.used = 0;
-    h->profiling = enable != 0;
+    h->profiling = enable > 0;
+    h->prof_period = enable > 0 ? enable : 1;
+    h->prof_tick = 0;
     h->prof = fs2_profile{};
     return FS2_OK;
 }
@@ -876,7 +878,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // tree sums: |tree - reference| <= (2n + 64) 2^-53 of the value, for the
     // total and hence for every normalised weight and prefix
     const double flip_margin = (red == FS2_REDUCE_PARALLEL) ? std::ldexp(2.0 * (double)h->n_global + 64.0, -53) : 0.0;
-    const bool prof = h->profiling;
+    const bool prof = h->profiling && (h->prof_tick++ % (uint64_t)h->prof_period) == 0;
 
     if (noise) {
         std::memcpy(h->noise_pin, noise, sizeof(double) * h->n);
@@ -998,8 +1000,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.n_np = (int32_t)np_sumsq_chunks(h->n);
     rp.flip_margin = flip_margin;
     rp.part_w = exact ? h->part_w : nullptr;
-    rp.bpre_w = exact ? h->bpre : nullptr;
-    rp.bpre_n = exact ? h->bpre : nullptr;   // the total's chain is done with bpre by then
+    rp.np_leaf = exact ? h->np_leaf : nullptr;
     rp.u0_host = u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
@@ -1039,10 +1040,18 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rs.use_chain = exact ? 1 : 0;
     rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout};
 
-    // weight total over all ranks (fast_slam_2.py:166)
-    HIP_TRY(h, launch_wsum(rp, s, prof ? E[5] : nullptr));
-    // exact: Python's sum (in particle order) from the update pass's block sums
-    if (exact) HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false), s));
+    // weight total over all ranks (fast_slam_2.py:166).  Exact: Python's sum (in
+    // particle order) from the update pass's block sums, the chain's units also
+    // folding the update counters (k_wsum's other job)
+    if (exact) {
+        ChainParams cp = h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false);
+        cp.cpart = h->cpart;
+        cp.ncpart = (int32_t)h->nblocks();
+        cp.cstats = h->stats_dev;
+        HIP_TRY(h, launch_chain(cp, s, prof ? E[5] : nullptr));
+    } else {
+        HIP_TRY(h, launch_wsum(rp, s, prof ? E[5] : nullptr));
+    }
     if (sh) {
         {
             CommTimer ct(h);
@@ -1053,7 +1062,6 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     }
     // normalise (:161-175), local prefix of the normalised weights, this rank's record
     HIP_TRY(h, launch_normalize(rp, s));
-    if (exact) HIP_TRY(h, launch_np_sumsq(h->w[cur], h->n, h->np_part, nullptr, s));
     // sharded ranks need their prefix end in the record; one GPU needs the
     // prefix only when the rule fires (computed below, kernels exit otherwise)
     if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));

@@ -17,19 +17,11 @@ __device__ __forceinline__ double bcast(double v, int j) {
 }
 
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return lane63(dpp_scan(v, 0ll, [](long long a, long long b) { return a + b; }));
 }
 
 __device__ __forceinline__ long long wave_incl_scan_i64(long long v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+    return dpp_scan(v, 0ll, [](long long a, long long b) { return a + b; });
 }
 
 // ulp of the binade E (values in [2^E, 2^(E+1))) and a / ulp
@@ -42,13 +34,7 @@ __device__ __forceinline__ long long bcast_i64(long long v, int j) {
 }
 
 __device__ __forceinline__ double wave_incl_scan_f64(double v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+    return dpp_scan(v, 0.0, [](double a, double b) { return a + b; });
 }
 
 // Exclusive prefix of in[0..n) into out (1024 threads; a tree estimate).
@@ -142,6 +128,116 @@ __device__ __forceinline__ double chain_unit_entry(const ChainView &V, int64_t k
     const int64_t q = V.seql[o];
     const unsigned long long ugk = V.bpd[g] + V.ugl[k], ugq = V.bpd[q / kChainGroup] + V.ugl[q];
     return V.sout[o] + (double)(long long)(ugk - ugq) * unit_ulp(E);
+}
+
+// ------------------------------------------------------- numpy sum of w^2 --
+
+constexpr int kNpChunk = 8192;             // numpy's reduction buffer
+
+// numpy's recursion over n < 8192 elements (n > 128: halves at n/2 rounded down
+// to a multiple of 8) without recursion: thread 0 lists the leaves in order, the
+// workgroup sums them in parallel, thread 0 adds them back up the same tree.
+constexpr int kNpMaxLeaves = 256;
+
+struct NpFrame {
+    int off, n, stage;
+    double left;
+};
+
+__device__ inline void np_pairwise_partial(const double *a, int64_t n, double *out) {
+    __shared__ int s_off[kNpMaxLeaves], s_len[kNpMaxLeaves];
+    __shared__ double s_sum[kNpMaxLeaves];
+    __shared__ int s_nl;
+    __shared__ NpFrame st[16];             // thread 0's explicit stack (LDS, not scratch)
+    typedef NpFrame Frame;
+    if (threadIdx.x == 0) {
+        int top = 0, nl = 0;
+        st[0] = Frame{0, (int)n, 0, 0.0};
+        while (top >= 0) {
+            Frame &f = st[top];
+            if (f.n <= 128) {
+                s_off[nl] = f.off;
+                s_len[nl] = f.n;
+                ++nl;
+                --top;
+            } else {
+                int n2 = f.n / 2;
+                n2 -= n2 % 8;
+                const int off = f.off, nn = f.n;
+                --top;
+                st[++top] = Frame{off + n2, nn - n2, 0, 0.0};   // right after left
+                st[++top] = Frame{off, n2, 0, 0.0};
+            }
+        }
+        s_nl = nl;
+    }
+    __syncthreads();
+    {
+        // 8 lanes per leaf (accumulator k of numpy's 8), all 16 loads issued at once;
+        // the leaf's remainder (n % 8) and leaves under 8 elements by lane k = 0
+        const int grp = threadIdx.x >> 3, k = threadIdx.x & 7, ngrp = blockDim.x >> 3;
+        for (int l0 = 0; l0 < s_nl; l0 += ngrp) {
+            const int l = l0 + grp;
+            const bool in = l < s_nl;
+            const int off = in ? s_off[l] : 0, len = in ? s_len[l] : 0;
+            const int full = len - len % 8;
+            double r = 0.0;
+            if (in && len >= 8) {
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = (8 * q + k < full) ? a[off + 8 * q + k] : 0.0;
+                r = v[0] * v[0];
+#pragma unroll
+                for (int q = 1; q < 16; ++q)
+                    if (8 * q + k < full) r += v[q] * v[q];
+            }
+            r += __shfl_xor(r, 1, 64);             // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+            r += __shfl_xor(r, 2, 64);
+            r += __shfl_xor(r, 4, 64);
+            if (in && k == 0) {
+                double res = (len < 8) ? 0.0 : r;
+                for (int e = (len < 8) ? 0 : full; e < len; ++e) res += a[off + e] * a[off + e];
+                s_sum[l] = res;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int top = 0, leaf = 0;
+        st[0] = Frame{0, (int)n, 0, 0.0};
+        double v = 0.0;
+        bool have = false;                 // v is a finished child value to hand up
+        while (top >= 0) {
+            Frame &f = st[top];
+            if (have) {
+                if (f.stage == 1) {
+                    f.left = v;
+                    f.stage = 2;
+                    have = false;
+                    int n2 = f.n / 2;
+                    n2 -= n2 % 8;
+                    st[top + 1] = Frame{f.off + n2, f.n - n2, 0, 0.0};
+                    ++top;
+                } else {                   // stage 2: both halves done
+                    v = f.left + v;
+                    --top;
+                }
+                continue;
+            }
+            if (f.n <= 128) {
+                v = s_sum[leaf++];
+                have = true;
+                --top;
+            } else {
+                int n2 = f.n / 2;
+                n2 -= n2 % 8;
+                f.stage = 1;
+                st[top + 1] = Frame{f.off, n2, 0, 0.0};
+                ++top;
+            }
+        }
+        *out = v;
+    }
 }
 
 }  // namespace fs2

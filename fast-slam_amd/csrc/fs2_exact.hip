@@ -27,8 +27,10 @@
 // per binade crossed) are walked serially; the translations between them are an
 // integer scan.
 //
-//   k_chain_bpre   exclusive prefix of the 256-element block sums (tree estimate)
-//   k_chain_units  per unit: translation (binade E, D) or serial
+//   k_chain_units  per unit: translation (binade E, D) or serial (each workgroup
+//                  estimates the chain at its block starts from the block sums
+//                  before it; in total mode 8 more workgroups fold the update
+//                  pass's counters, k_wsum's other job)
 //   k_chain_walk   one workgroup: integer scan of D, then the serial units in
 //                  order (wave 0; chain_unit evaluates a unit in a few wave-wide
 //                  steps: one per binade crossed or tie, not one per term)
@@ -39,28 +41,19 @@
 // numpy sum of squares.  Each full 8192-element chunk is numpy's pairwise tree:
 // 64 leaves of 128 elements (8 accumulators of 16 sequential adds, combined
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))), the leaves combined as a balanced
-// binary tree in order -- one wave per chunk, xor butterflies.  A partial last
-// chunk is summed by lane 0 with the recursive form.  The chunk sums are added
-// in order by k_finalize.
+// binary tree in order.  k_normalize sums the leaves of its 256 weights as it
+// writes them; k_finalize adds each chunk's leaves up the tree (one wave per
+// chunk, xor butterflies), sums a partial last chunk with numpy's recursion
+// (np_pairwise_partial, fs2_chain.hpp) and adds the chunk sums in order.
 #include "fs2_chain.hpp"
 
 namespace fs2 {
-
-constexpr int kNpChunk = 8192;             // numpy's reduction buffer
 
 __device__ __forceinline__ bool lazy_skip(const ChainParams &P) {
     return P.stats != nullptr && !P.stats->resampled;
 }
 
 // --------------------------------------------------------------- chain ----
-
-// Exclusive prefix of the block sums (one workgroup): estimates of the chain's
-// value at every block start.
-__global__ __launch_bounds__(1024) void k_chain_bpre(const ChainParams P) {
-    __shared__ double lds[16];
-    if (P.lazy && lazy_skip(P)) return;
-    block_excl_scan_1024(P.bsum, P.bpre, P.nb, lds);
-}
 
 // Per 64-term unit (one wave; kChainGroup units per 1024-thread workgroup).
 // Each term's chain value before and after it is estimated (block prefix + wave
@@ -76,7 +69,30 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     __shared__ double s_ws[16];
     __shared__ unsigned long long s_D[16];
     __shared__ int s_f[16];
+    __shared__ double s_red[16], s_bp[4];
+    __shared__ unsigned long long s_c[16][kNumCounters];
     if (P.lazy && lazy_skip(P)) return;
+    const int64_t ngroups = (P.n + 1023) / 1024;
+    if (blockIdx.x >= ngroups) {     // the update pass's counters (total mode)
+        fold_counters(P.cpart, P.ncpart, P.cstats, (int)(blockIdx.x - ngroups), s_c);
+        return;
+    }
+    {
+        // estimates of the chain at this workgroup's four 256-term block starts:
+        // the block sums before them in any order (the margin bounds every order)
+        const int64_t nb0 = (int64_t)blockIdx.x * 4;
+        double v = 0.0;
+        for (int64_t j = threadIdx.x; j < nb0; j += 1024) v += P.bsum[j];
+        const double base = block_sum<1024>(v, s_red);
+        if (threadIdx.x == 0) {
+            double e = base;
+            for (int c = 0; c < 4; ++c) {
+                s_bp[c] = e;
+                if (nb0 + c < P.nb) e += P.bsum[nb0 + c];
+            }
+        }
+        __syncthreads();
+    }
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int64_t i = (int64_t)blockIdx.x * 1024 + t;
     const int64_t k = (int64_t)blockIdx.x * kChainGroup + wid;
@@ -92,7 +108,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         // estimate of the chain before this unit: the 256-term block prefix, then
         // the units of that block ahead of this one
         const int c4 = wid >> 2;
-        double e_in = P.bpre[(int64_t)blockIdx.x * 4 + c4];
+        double e_in = s_bp[c4];
         for (int q = 4 * c4; q < wid; ++q) e_in += s_ws[q];
         const double lo = (e_in + (incl - a)) * (1.0 - P.margin), hi = (e_in + incl) * (1.0 + P.margin);
         bool ok = valid && i != 0 && a >= 0.0 && a < INFINITY && lo >= 0x1p-1020 && hi < 0x1p1020;
@@ -475,169 +491,18 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     FS2_CHAIN_STAMP(4);
 }
 
-hipError_t launch_chain(const ChainParams &p, hipStream_t s) {
+hipError_t launch_chain(const ChainParams &p, hipStream_t s, hipEvent_t e0) {
     if (p.n <= 0) {
         if (p.total) hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
         return hipGetLastError();
     }
-    const unsigned ng = (unsigned)((p.n + 1023) / 1024);
-    if (!p.bpre_ready) hipLaunchKernelGGL(k_chain_bpre, dim3(1), dim3(1024), 0, s, p);
-    hipLaunchKernelGGL(k_chain_units, dim3(ng), dim3(1024), 0, s, p);
+    const unsigned ng = (unsigned)((p.n + 1023) / 1024) + (p.cpart ? kFoldBlocks : 0);
+    FS2_LAUNCH_EV(k_chain_units, dim3(ng), dim3(1024), s, e0, nullptr, p);
     hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------- numpy sum of w^2 --
-
-// numpy's recursion over n < 8192 elements (n > 128: halves at n/2 rounded down
-// to a multiple of 8) without recursion: thread 0 lists the leaves in order, the
-// workgroup sums them in parallel, thread 0 adds them back up the same tree.
-constexpr int kNpMaxLeaves = 256;
-
-struct NpFrame {
-    int off, n, stage;
-    double left;
-};
-
-__device__ void np_pairwise_partial(const double *a, int64_t n, double *out) {
-    __shared__ int s_off[kNpMaxLeaves], s_len[kNpMaxLeaves];
-    __shared__ double s_sum[kNpMaxLeaves];
-    __shared__ int s_nl;
-    __shared__ NpFrame st[16];             // thread 0's explicit stack (LDS, not scratch)
-    typedef NpFrame Frame;
-    if (threadIdx.x == 0) {
-        int top = 0, nl = 0;
-        st[0] = Frame{0, (int)n, 0, 0.0};
-        while (top >= 0) {
-            Frame &f = st[top];
-            if (f.n <= 128) {
-                s_off[nl] = f.off;
-                s_len[nl] = f.n;
-                ++nl;
-                --top;
-            } else {
-                int n2 = f.n / 2;
-                n2 -= n2 % 8;
-                const int off = f.off, nn = f.n;
-                --top;
-                st[++top] = Frame{off + n2, nn - n2, 0, 0.0};   // right after left
-                st[++top] = Frame{off, n2, 0, 0.0};
-            }
-        }
-        s_nl = nl;
-    }
-    __syncthreads();
-    {
-        // 8 lanes per leaf (accumulator k of numpy's 8), all 16 loads issued at once;
-        // the leaf's remainder (n % 8) and leaves under 8 elements by lane k = 0
-        const int grp = threadIdx.x >> 3, k = threadIdx.x & 7, ngrp = blockDim.x >> 3;
-        for (int l0 = 0; l0 < s_nl; l0 += ngrp) {
-            const int l = l0 + grp;
-            const bool in = l < s_nl;
-            const int off = in ? s_off[l] : 0, len = in ? s_len[l] : 0;
-            const int full = len - len % 8;
-            double r = 0.0;
-            if (in && len >= 8) {
-                double v[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = (8 * q + k < full) ? a[off + 8 * q + k] : 0.0;
-                r = v[0] * v[0];
-#pragma unroll
-                for (int q = 1; q < 16; ++q)
-                    if (8 * q + k < full) r += v[q] * v[q];
-            }
-            r += __shfl_xor(r, 1, 64);             // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
-            r += __shfl_xor(r, 2, 64);
-            r += __shfl_xor(r, 4, 64);
-            if (in && k == 0) {
-                double res = (len < 8) ? 0.0 : r;
-                for (int e = (len < 8) ? 0 : full; e < len; ++e) res += a[off + e] * a[off + e];
-                s_sum[l] = res;
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int top = 0, leaf = 0;
-        st[0] = Frame{0, (int)n, 0, 0.0};
-        double v = 0.0;
-        bool have = false;                 // v is a finished child value to hand up
-        while (top >= 0) {
-            Frame &f = st[top];
-            if (have) {
-                if (f.stage == 1) {
-                    f.left = v;
-                    f.stage = 2;
-                    have = false;
-                    int n2 = f.n / 2;
-                    n2 -= n2 % 8;
-                    st[top + 1] = Frame{f.off + n2, f.n - n2, 0, 0.0};
-                    ++top;
-                } else {                   // stage 2: both halves done
-                    v = f.left + v;
-                    --top;
-                }
-                continue;
-            }
-            if (f.n <= 128) {
-                v = s_sum[leaf++];
-                have = true;
-                --top;
-            } else {
-                int n2 = f.n / 2;
-                n2 -= n2 % 8;
-                f.stage = 1;
-                st[top + 1] = Frame{f.off, n2, 0, 0.0};
-                ++top;
-            }
-        }
-        *out = v;
-    }
-}
-
-// One 512-thread workgroup per 8192-element chunk -> part[chunk]: wave b sums
-// leaves 8b .. 8b+7 (8 lanes per leaf, one accumulator each), the 64 leaf sums
-// meet in LDS and wave 0 adds them as the balanced tree.
-__global__ __launch_bounds__(512) void k_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy) {
-    __shared__ double s_leaf[64];
-    if (lazy && !lazy->resampled) return;
-    const int t = threadIdx.x, lane = t & 63, bt = t >> 6;
-    const int64_t c0 = (int64_t)blockIdx.x * kNpChunk;
-    // lane = 8 g + k: accumulator k of leaf 8 bt + g (elements k, k+8, ..., k+120)
-    const int g = lane >> 3, k = lane & 7;
-    const double *p = w + c0 + (int64_t)(8 * bt + g) * 128 + k;
-    double v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = p[8 * q];
-    double r = v[0] * v[0];
-#pragma unroll
-    for (int q = 1; q < 16; ++q) r += v[q] * v[q];
-    r += __shfl_xor(r, 1, 64);                 // (r0 + r1), (r2 + r3), ...
-    r += __shfl_xor(r, 2, 64);                 // ((r0 + r1) + (r2 + r3)), ...
-    r += __shfl_xor(r, 4, 64);
-    if (k == 0) s_leaf[8 * bt + g] = r;
-    __syncthreads();
-    if (bt == 0) {
-        double leaf = s_leaf[lane];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) leaf += __shfl_xor(leaf, o, 64);   // leaves in order, balanced
-        if (lane == 0) part[blockIdx.x] = leaf;
-    }
-}
-
-// The partial last chunk (its own launch: the explicit stacks live in scratch).
-__global__ __launch_bounds__(256) void k_np_sumsq_tail(const double *w, int64_t n, double *part, const DevStats *lazy) {
-    if (lazy && !lazy->resampled) return;
-    const int64_t full = n / kNpChunk;
-    np_pairwise_partial(w + full * kNpChunk, n - full * kNpChunk, part + full);
-}
-
-hipError_t launch_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy, hipStream_t s) {
-    const int64_t full = n / kNpChunk;
-    if (full > 0) hipLaunchKernelGGL(k_np_sumsq, dim3((unsigned)full), dim3(512), 0, s, w, n, part, lazy);
-    if (n % kNpChunk) hipLaunchKernelGGL(k_np_sumsq_tail, dim3(1), dim3(256), 0, s, w, n, part, lazy);
-    return hipGetLastError();
-}
 
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_chain_times(unsigned long long out[8], int reset) {

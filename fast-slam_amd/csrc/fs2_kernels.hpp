@@ -215,12 +215,11 @@ struct ReduceParams {
     double floor;
     int32_t sequential;      // one lane, the reference's orders
     int32_t exact;           // the reference's orders in parallel (fs2_exact.hip)
-    const double *np_part;   // exact: numpy chunk sums of w'^2 (k_np_sumsq)
+    double *np_part;         // exact: numpy chunk sums of w'^2 (k_finalize, beyond its LDS stage)
     int32_t n_np;            // their count
+    double *np_leaf;         // exact: numpy's 128-element leaves of the full chunks (k_normalize)
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
-    double *bpre_w;          // exact: k_wsum writes the exclusive scan of wpart here
-    double *bpre_n;          // exact: k_finalize writes the exclusive scan of part_w here
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
     uint64_t seed, scan;
     DevStats *stats;
@@ -303,10 +302,11 @@ struct ChainParams {
     const double *a;
     int64_t n;
     const double *bsum;      // [nb] sums of 256-element blocks (any order: an estimate)
-    double *bpre;            // [nb] their exclusive prefix (written)
     int32_t nb;
     int32_t lazy;            // run only when stats->resampled
-    int32_t bpre_ready;      // bpre was written by an earlier kernel (k_wsum / k_finalize)
+    const unsigned long long *cpart;   // non-null: fold these update counters [kNumCounters][ncpart]
+    int32_t ncpart;
+    DevStats *cstats;        // into these statistics (k_wsum's other job; total mode)
     int32_t *uinfo;          // [nu] per 64-term unit: (binade + 4096) << 2 for a translation; bit 0:
                              // listed: segments (UnitRec, count in bits 3-6), or bit 1: evaluated
                              // term by term (chain_unit)
@@ -327,9 +327,8 @@ struct ChainParams {
     const DevStats *stats;
     double margin;           // relative bound on |estimate - chain| (doubled)
 };
-hipError_t launch_chain(const ChainParams &p, hipStream_t s);
-// numpy np.sum(w ** 2) chunk sums (8192-element buffers), added in order by the caller
-hipError_t launch_np_sumsq(const double *w, int64_t n, double *part, const DevStats *lazy, hipStream_t s);
+hipError_t launch_chain(const ChainParams &p, hipStream_t s, hipEvent_t e0 = nullptr);
+// numpy np.sum(w ** 2): 8192-element chunks (k_normalize leaves, k_finalize trees)
 int64_t np_sumsq_chunks(int64_t n);
 
 // Launch of kernel k; with profiling events (e0: its start, e1: its end, either

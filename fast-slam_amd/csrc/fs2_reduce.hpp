@@ -8,23 +8,74 @@
 namespace fs2 {
 
 // ------------------------------------------------------------ reductions ---
+//
+// Wave scans and reductions on DPP (gfx9 row_shr 1/2/4/8, then row_bcast 15/31):
+// six VALU steps with the neighbour's value as an operand modifier, no LDS
+// traffic (a __shfl_* is a ds_bpermute through the LDS crossbar; the reductions
+// at the end of every update kernel cost ~100 of them per wave).  After the six
+// steps lane l holds the inclusive scan of lanes 0..l (Hillis-Steele inside each
+// 16-lane row, then the rows' totals carried up) and lane 63 the wave's
+// reduction, which readlane broadcasts (the same bits in every lane).  Every
+// lane of the wave must be active.  A lane whose source is out of its row
+// reads `id` (the operation's identity).
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t id) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v, uint64_t id) {
+    return (uint64_t)dpp32<CTRL, ROWS>((uint32_t)v, (uint32_t)id) |
+           ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(v >> 32), (uint32_t)(id >> 32)) << 32);
+}
+template <typename T>
+__device__ __forceinline__ uint64_t to_bits(T v) {
+    if constexpr (sizeof(T) == 8) return __builtin_bit_cast(uint64_t, v);
+    else return (uint64_t)__builtin_bit_cast(uint32_t, v);
+}
+template <typename T>
+__device__ __forceinline__ T from_bits(uint64_t b) {
+    if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, b);
+    else return __builtin_bit_cast(T, (uint32_t)b);
+}
+template <int CTRL, int ROWS, typename T>
+__device__ __forceinline__ T dpp_move(T v, T id) {
+    if constexpr (sizeof(T) == 8) return from_bits<T>(dpp64<CTRL, ROWS>(to_bits(v), to_bits(id)));
+    else return from_bits<T>(dpp32<CTRL, ROWS>((uint32_t)to_bits(v), (uint32_t)to_bits(id)));
+}
+template <typename T>
+__device__ __forceinline__ T lane63(T v) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t b = to_bits(v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+        return from_bits<T>((uint64_t)lo | ((uint64_t)hi << 32));
+    } else {
+        return from_bits<T>((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)to_bits(v), 63));
+    }
+}
+// inclusive scan of op over the wave (op associative and commutative)
+template <typename T, typename Op>
+__device__ __forceinline__ T dpp_scan(T v, T id, Op op) {
+    v = op(v, dpp_move<0x111, 0xf>(v, id));     // row_shr:1
+    v = op(v, dpp_move<0x112, 0xf>(v, id));     // row_shr:2
+    v = op(v, dpp_move<0x114, 0xf>(v, id));     // row_shr:4
+    v = op(v, dpp_move<0x118, 0xf>(v, id));     // row_shr:8
+    v = op(v, dpp_move<0x142, 0xa>(v, id));     // row_bcast:15 into rows 1, 3
+    v = op(v, dpp_move<0x143, 0xc>(v, id));     // row_bcast:31 into rows 2, 3
+    return v;
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return lane63(dpp_scan(v, 0.0, [](double a, double b) { return a + b; }));
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return lane63(dpp_scan(v, 0ull, [](unsigned long long a, unsigned long long b) { return a + b; }));
 }
 
 __device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
+    return lane63(dpp_scan(v, INT_MIN, [](int a, int b) { return max(a, b); }));
 }
 
 // (value, index) argmax, lowest index among equal maxima (Python max).
@@ -35,13 +86,22 @@ __device__ __forceinline__ void argmax_combine(double &v, int64_t &i, double v2,
     }
 }
 
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void argmax_step(double &v, int64_t &i) {
+    const double v2 = dpp_move<CTRL, ROWS, double>(v, -(double)INFINITY);
+    const int64_t i2 = dpp_move<CTRL, ROWS, int64_t>(i, (int64_t)INT64_MAX);
+    argmax_combine(v, i, v2, i2);
+}
+
 __device__ __forceinline__ void wave_argmax(double &v, int64_t &i) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double v2 = __shfl_xor(v, o, 64);
-        const int64_t i2 = __shfl_xor(i, o, 64);
-        argmax_combine(v, i, v2, i2);
-    }
+    argmax_step<0x111, 0xf>(v, i);
+    argmax_step<0x112, 0xf>(v, i);
+    argmax_step<0x114, 0xf>(v, i);
+    argmax_step<0x118, 0xf>(v, i);
+    argmax_step<0x142, 0xa>(v, i);
+    argmax_step<0x143, 0xc>(v, i);
+    v = lane63(v);
+    i = lane63(i);
 }
 
 // Deterministic block sum (fixed tree), result valid in every thread.
@@ -88,9 +148,7 @@ __device__ void block_argmax(double &v, int64_t &i, double *ldv, int64_t *ldi) {
 }
 
 __device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return lane63(dpp_scan(v, 0u, [](unsigned a, unsigned b) { return a + b; }));
 }
 
 // The counters of this workgroup (NV per lane: counters FIRST .. FIRST+NV-1)
@@ -126,6 +184,58 @@ __device__ void block_counters(const unsigned (&v)[NV], unsigned long long *cpar
 #pragma unroll
         for (int q = 0; q < NT / 64; ++q) t += s_w[q];
         *wsum = t;
+    }
+}
+
+// DevStats field of update counter k (fs2_kernels.hpp kC*).
+__device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k) {
+    switch (k) {
+        case kCWords: return &st->words;
+        case kCGroups: return &st->groups;
+        case kCVisited: return &st->visited;
+        case kCCandidates: return &st->candidates;
+        case kCWritten: return &st->written;
+        case kCAmbiguous: return &st->ambiguous;
+        case kCAppends: return &st->appends;
+        case kCHits: return &st->hits;
+        case kCCow: return &st->cow_pages;
+        case kCOpened: return &st->opened;
+        case kCRefVisits: return &st->ref_visits;
+        default: return &st->new_pages;
+    }
+}
+
+// The update pass's block counters (cpart[counter][nb]) folded into the scan
+// statistics by kFoldBlocks 1024-thread workgroups, workgroup cb over a slice of
+// the columns (atomics into DevStats: integer sums, order-free).
+constexpr int kFoldBlocks = 8;
+__device__ inline void fold_counters(const unsigned long long *cpart, int32_t nb, DevStats *stats, int cb,
+                                     unsigned long long (*s_c)[kNumCounters]) {
+    const int per = (nb + kFoldBlocks - 1) / kFoldBlocks;
+    const int b0 = cb * per, b1 = min(nb, b0 + per);
+    // every counter column of the slice at once: independent loads, one LDS exchange
+    unsigned long long v[kNumCounters] = {};
+    for (int b = b0 + threadIdx.x; b < b1; b += 1024) {
+#pragma unroll
+        for (int k = 0; k < kNumCounters; ++k) v[k] += cpart[(int64_t)k * nb + b];
+    }
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kNumCounters; ++k) {
+        v[k] = wave_sum_u64(v[k]);
+        if (lane == 0) s_c[wid][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < kNumCounters) {
+        const int k = threadIdx.x;
+        unsigned long long t = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += s_c[q][k];
+        if (k == kCSingular) {
+            if (t) atomicOr(&stats->error_flags, 1);
+        } else if (t) {
+            atomicAdd(counter_field(stats, k), t);
+        }
     }
 }
 
@@ -457,8 +567,7 @@ __device__ __forceinline__ void refresh_summary(const MapRef &m, int row, int64_
 // whole wave converged.
 __device__ __forceinline__ void lower_slb(float *slb, float s) {
     float v = (s > 0.0f) ? s : INFINITY;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    v = lane63(dpp_scan(v, INFINITY, [](float a, float b) { return fminf(a, b); }));
     if ((threadIdx.x & 63) == 0 && v < *slb) atomicMin(reinterpret_cast<unsigned *>(slb), __float_as_uint(v));
 }
 

@@ -74,7 +74,34 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     __shared__ int64_t lds_l[16];
     __shared__ int lds_i[16];
     __shared__ double s_np[kNpStage];
-    if (P.exact && threadIdx.x < P.n_np && threadIdx.x < kNpStage) s_np[threadIdx.x] = P.np_part[threadIdx.x];
+    if (P.exact) {
+        // numpy's chunk sums: each full chunk's 64 leaves (k_normalize) as a balanced
+        // tree in order (a wave per chunk, xor butterflies; 8 chunks' loads in flight),
+        // the partial last chunk by numpy's recursion; added in order below
+        const int64_t nfull = P.n / kNpChunk;
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (int64_t c0 = wid; c0 < nfull; c0 += 16 * 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t c = c0 + 16 * u;
+                v[u] = (c < nfull) ? P.np_leaf[c * 64 + lane] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) v[u] += __shfl_xor(v[u], o, 64);
+                const int64_t c = c0 + 16 * u;
+                if (lane == 0 && c < nfull) {
+                    if (c < kNpStage) s_np[c] = v[u];
+                    else P.np_part[c] = v[u];
+                }
+            }
+        }
+        if (P.n % kNpChunk)
+            np_pairwise_partial(P.w + nfull * kNpChunk, P.n % kNpChunk, nfull < kNpStage ? s_np + nfull : P.np_part + nfull);
+        __syncthreads();
+    }
     double sq = 0.0;
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
@@ -102,8 +129,6 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     sq = block_sum<1024>(sq, lds_d);
     block_argmax<1024>(bv, bi, lds_d, lds_l);
     mc = block_max_i<1024>(mc, lds_i);
-    // exact mode: estimates of the running sum at every block start (fs2_exact.hip)
-    if (P.bpre_n) block_excl_scan_1024(P.part_w, P.bpre_n, P.nparts, lds_d);
     if (threadIdx.x == 0) {
         if (P.sequential) {
             // np.sum(weights ** 2): pairwise inside 8192-element chunks
@@ -285,23 +310,11 @@ hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long l
 // ------------------------------------------------------------ local prefix --
 
 __device__ __forceinline__ double wave_incl_scan(double v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+    return dpp_scan(v, 0.0, [](double a, double b) { return a + b; });
 }
 
 __device__ __forceinline__ int wave_incl_scan_i(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+    return dpp_scan(v, 0, [](int a, int b) { return a + b; });
 }
 
 // Sequential running sum, the reference's order (fast_slam_2.py:184-193).

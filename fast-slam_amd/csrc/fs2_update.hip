@@ -839,61 +839,15 @@ hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0, hi
 
 // ------------------------------------------------------- normalise & N_eff --
 
-// Weight total. Sequential mode: Python builtin sum in particle order.
-__device__ __forceinline__ unsigned long long *counter_field(DevStats *st, int k) {
-    switch (k) {
-        case kCWords: return &st->words;
-        case kCGroups: return &st->groups;
-        case kCVisited: return &st->visited;
-        case kCCandidates: return &st->candidates;
-        case kCWritten: return &st->written;
-        case kCAmbiguous: return &st->ambiguous;
-        case kCAppends: return &st->appends;
-        case kCHits: return &st->hits;
-        case kCCow: return &st->cow_pages;
-        case kCOpened: return &st->opened;
-        case kCRefVisits: return &st->ref_visits;
-        default: return &st->new_pages;
-    }
-}
-
 // Weight total (Python builtin sum in particle order in sequential mode) in
 // workgroup 0, and the update pass's block counters folded into the scan
-// statistics by workgroups 1 .. kWsumCounterBlocks, each over a slice of the
+// statistics by workgroups 1 .. kFoldBlocks, each over a slice of the
 // columns (atomics into DevStats: integer sums, order-free), in parallel.
-constexpr int kWsumCounterBlocks = 8;
-
 __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
     __shared__ double lds[16];
     __shared__ unsigned long long s_c[16][kNumCounters];
     if (blockIdx.x > 0) {
-        const int cb = blockIdx.x - 1;
-        const int per = (P.nwpart + kWsumCounterBlocks - 1) / kWsumCounterBlocks;
-        const int b0 = cb * per, b1 = min(P.nwpart, b0 + per);
-        // every counter column of the slice at once: independent loads, one LDS exchange
-        unsigned long long v[kNumCounters] = {};
-        for (int b = b0 + threadIdx.x; b < b1; b += 1024) {
-#pragma unroll
-            for (int k = 0; k < kNumCounters; ++k) v[k] += P.cpart[(int64_t)k * P.nwpart + b];
-        }
-        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-        for (int k = 0; k < kNumCounters; ++k) {
-            v[k] = wave_sum_u64(v[k]);
-            if (lane == 0) s_c[wid][k] = v[k];
-        }
-        __syncthreads();
-        if (threadIdx.x < kNumCounters) {
-            const int k = threadIdx.x;
-            unsigned long long t = 0;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) t += s_c[q][k];
-            if (k == kCSingular) {
-                if (t) atomicOr(&P.stats->error_flags, 1);
-            } else if (t) {
-                atomicAdd(counter_field(P.stats, k), t);
-            }
-        }
+        fold_counters(P.cpart, P.nwpart, P.stats, blockIdx.x - 1, s_c);
         return;
     }
     if (P.sequential) {
@@ -904,8 +858,6 @@ __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
         }
         return;
     }
-    // exact mode: the block sums' exclusive scan, the chain's estimates (fs2_exact.hip)
-    if (P.bpre_w) block_excl_scan_1024(P.wpart, P.bpre_w, P.nwpart, lds);
     double v = 0.0;
     for (int k = threadIdx.x; k < P.nwpart; k += 1024) v += P.wpart[k];
     const double t = block_sum<1024>(v, lds);
@@ -913,7 +865,7 @@ __global__ __launch_bounds__(1024) void k_wsum(const ReduceParams P) {
 }
 
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s, hipEvent_t e0) {
-    FS2_LAUNCH_EV(k_wsum, dim3(1 + kWsumCounterBlocks), dim3(1024), s, e0, nullptr, p);
+    FS2_LAUNCH_EV(k_wsum, dim3(1 + kFoldBlocks), dim3(1024), s, e0, nullptr, p);
     return hipGetLastError();
 }
 
@@ -932,6 +884,25 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
         if (total < P.floor) w = 1.0 / (double)P.n_global;
         else w = (w < P.floor) ? w : w / total;
         P.w[i] = w;
+    }
+    // exact: this block's two numpy leaves (fs2_exact.hip: 128 elements, 8
+    // accumulators of 16 squares added in order, combined ((r0 + r1) + (r2 + r3)) +
+    // ((r4 + r5) + (r6 + r7))) when they lie in a full 8192-element chunk;
+    // k_finalize adds them up the chunk trees
+    if (P.np_leaf && ((int64_t)blockIdx.x + 1) * kBlock <= (P.n / kNpChunk) * kNpChunk) {
+        __shared__ double s_sq2[kBlock];
+        s_sq2[threadIdx.x] = w * w;
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            const int g = threadIdx.x >> 3, k = threadIdx.x & 7;
+            double r = s_sq2[g * 128 + k];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) r += s_sq2[g * 128 + 8 * q + k];
+            r += __shfl_xor(r, 1, 64);
+            r += __shfl_xor(r, 2, 64);
+            r += __shfl_xor(r, 4, 64);
+            if (k == 0) P.np_leaf[(int64_t)blockIdx.x * 2 + g] = r;
+        }
     }
     // block_sum / block_argmax / block_max_i (same trees) with one barrier
     const double sq = wave_sum(live ? w * w : 0.0);

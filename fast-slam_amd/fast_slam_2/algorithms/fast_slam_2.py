@@ -224,8 +224,10 @@ class FastSLAM2:
                                           buf.size, C.byref(m)), self._h)
         return buf[:m.value * self.n_local].reshape(m.value, self.n_local).copy()
 
-    def set_profiling(self, enable: bool = True):
-        nat.check(self._lib.fs2_set_profiling(self._h, 1 if enable else 0), self._h)
+    def set_profiling(self, enable: bool = True, every: int = 1):
+        """Device-event timing of the update kernels on every `every`-th scan (libfs2
+        fs2_set_profiling; resets the profile)."""
+        nat.check(self._lib.fs2_set_profiling(self._h, max(1, int(every)) if enable else 0), self._h)
 
     def profile(self) -> dict:
         p = nat.fs2_profile()

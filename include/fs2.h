@@ -204,7 +204,10 @@ int fs2_shard_info(const fs2_handle *h, int64_t *n_local, int64_t *first_global,
 
 int fs2_synchronize(fs2_handle *h);
 
-/* Device-event timing of the hot-path kernels (bench.py roofline). */
+/* Device-event timing of the hot-path kernels (bench.py roofline): enable = 0
+ * off, k >= 1 every k-th scan (the start / end events of a dispatch delay the next
+ * dispatch by a few microseconds, so sampling keeps that out of most scans).
+ * Resets the profile. */
 int fs2_set_profiling(fs2_handle *h, int32_t enable);
 int fs2_get_profile(const fs2_handle *h, fs2_profile *out);
 
