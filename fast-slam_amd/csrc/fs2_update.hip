@@ -69,6 +69,9 @@ __device__ unsigned long long g_phase[8];
 #ifndef FS2_SLOT_BAND
 #define FS2_SLOT_BAND 0
 #endif
+#ifndef FS2_COPY_BATCH
+#define FS2_COPY_BATCH 8
+#endif
 constexpr int kDescAhead = FS2_DESC_AHEAD;   // page descriptors a lane keeps in flight
 
 static_assert(kMaxCand == 8, "sort8 sorts the candidate list");
@@ -641,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int off = (lane & 7) * 16;
-        constexpr int CB = 8;         // pages per lane and batch (8 lanes per page)
+        constexpr int CB = FS2_COPY_BATCH;   // pages per lane and batch (8 lanes per page)
         v4i va[CB];                   // clang vector type: HIP's int4 struct defeats SROA here
         uint32_t da[CB];
         auto load_batch = [&](int base, v4i *v, uint32_t *d) {
