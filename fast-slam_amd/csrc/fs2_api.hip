@@ -166,6 +166,7 @@ struct fs2_handle {
     long long *udelta = nullptr;
     unsigned long long *ugl = nullptr, *bD = nullptr, *bpd = nullptr;
     double *sout = nullptr, *part_w = nullptr, *np_part = nullptr, *np_leaf = nullptr, *sentry = nullptr;
+    NpTailPlan *np_tail = nullptr;         // device: numpy's tree over the partial last chunk (null: none)
     UnitRec *urec = nullptr;
 
     MapRef map() const {
@@ -567,7 +568,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->cand); hipFree(h->ncand);
     hipFree(h->uinfo); hipFree(h->uol); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ugl);
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
-    hipFree(h->sout); hipFree(h->np_leaf); hipFree(h->part_w); hipFree(h->np_part);
+    hipFree(h->sout); hipFree(h->np_leaf); hipFree(h->part_w); hipFree(h->np_part); hipFree(h->np_tail);
     hipFree(h->urec); hipFree(h->sentry);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
@@ -721,6 +722,14 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
             hipMemsetD32Async((hipDeviceptr_t)h->bbox[s], (int)kBoxEmpty, nb * kBBoxRows, h->stream) != hipSuccess ||
             launch_fill(h->w[s], 1.0 / (double)h->n_global, n, h->stream) != hipSuccess)
             return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
+    }
+    {
+        NpTailPlan plan;
+        if (np_tail_plan(h->n, &plan)) {
+            if (hipMalloc(&h->np_tail, sizeof plan) != hipSuccess ||
+                hipMemcpy(h->np_tail, &plan, sizeof plan, hipMemcpyHostToDevice) != hipSuccess)
+                return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
+        }
     }
     int rc = grow_rows(h, std::max(cfg->landmark_capacity, 1));
     if (rc) return fail(rc);
@@ -1001,6 +1010,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.flip_margin = flip_margin;
     rp.part_w = exact ? h->part_w : nullptr;
     rp.np_leaf = exact ? h->np_leaf : nullptr;
+    rp.np_tail = exact ? h->np_tail : nullptr;
     rp.u0_host = u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
@@ -1706,6 +1716,10 @@ int fs2_debug_phase_times(uint64_t out[8], int32_t reset) {
 extern "C" int fs2_debug_chain_times(uint64_t out[8], int32_t reset) {
     return fs2::debug_chain_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess ? FS2_OK
                                                                                                     : FS2_ERR_HIP;
+}
+extern "C" int fs2_debug_finalize_times(uint64_t out[8], int32_t reset) {
+    return fs2::debug_fin_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess ? FS2_OK
+                                                                                                  : FS2_ERR_HIP;
 }
 extern "C" int fs2_debug_icp_phase_times(uint64_t out[4], int32_t reset) {
     return fs2::debug_icp_phase_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess

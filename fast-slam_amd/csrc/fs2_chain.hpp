@@ -132,112 +132,49 @@ __device__ __forceinline__ double chain_unit_entry(const ChainView &V, int64_t k
 
 // ------------------------------------------------------- numpy sum of w^2 --
 
-constexpr int kNpChunk = 8192;             // numpy's reduction buffer
-
 // numpy's recursion over n < 8192 elements (n > 128: halves at n/2 rounded down
-// to a multiple of 8) without recursion: thread 0 lists the leaves in order, the
-// workgroup sums them in parallel, thread 0 adds them back up the same tree.
-constexpr int kNpMaxLeaves = 256;
-
-struct NpFrame {
-    int off, n, stage;
-    double left;
-};
-
-__device__ inline void np_pairwise_partial(const double *a, int64_t n, double *out) {
-    __shared__ int s_off[kNpMaxLeaves], s_len[kNpMaxLeaves];
-    __shared__ double s_sum[kNpMaxLeaves];
-    __shared__ int s_nl;
-    __shared__ NpFrame st[16];             // thread 0's explicit stack (LDS, not scratch)
-    typedef NpFrame Frame;
-    if (threadIdx.x == 0) {
-        int top = 0, nl = 0;
-        st[0] = Frame{0, (int)n, 0, 0.0};
-        while (top >= 0) {
-            Frame &f = st[top];
-            if (f.n <= 128) {
-                s_off[nl] = f.off;
-                s_len[nl] = f.n;
-                ++nl;
-                --top;
-            } else {
-                int n2 = f.n / 2;
-                n2 -= n2 % 8;
-                const int off = f.off, nn = f.n;
-                --top;
-                st[++top] = Frame{off + n2, nn - n2, 0, 0.0};   // right after left
-                st[++top] = Frame{off, n2, 0, 0.0};
-            }
-        }
-        s_nl = nl;
-    }
-    __syncthreads();
-    {
-        // 8 lanes per leaf (accumulator k of numpy's 8), all 16 loads issued at once;
-        // the leaf's remainder (n % 8) and leaves under 8 elements by lane k = 0
-        const int grp = threadIdx.x >> 3, k = threadIdx.x & 7, ngrp = blockDim.x >> 3;
-        for (int l0 = 0; l0 < s_nl; l0 += ngrp) {
-            const int l = l0 + grp;
-            const bool in = l < s_nl;
-            const int off = in ? s_off[l] : 0, len = in ? s_len[l] : 0;
-            const int full = len - len % 8;
-            double r = 0.0;
-            if (in && len >= 8) {
-                double v[16];
+// to a multiple of 8; leaves of <= 128).
+// One wave: numpy's pairwise sum of x[i]^2 over the partial chunk planned by pl.
+// The wave sums the leaves 8 lanes per leaf (accumulator k of numpy's 8, 16
+// loads in flight), lane 0 runs the plan's adds.  Returns lane 0's value.
+__device__ inline double np_pairwise_wave(const double *x, const NpTailPlan *pl) {
+    __shared__ double s_node[2 * kNpMaxLeaves];
+    const int lane = threadIdx.x & 63;
+    const int nl = pl->nl;
+    const int grp = lane >> 3, k = lane & 7;
+    for (int l0 = 0; l0 < nl; l0 += 8) {
+        const int l = l0 + grp;
+        const bool in = l < nl;
+        const int off = in ? pl->off[l] : 0, len = in ? pl->len[l] : 0;
+        const int full = len - len % 8;
+        double r = 0.0;
+        if (in && len >= 8) {
+            double v[16];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = (8 * q + k < full) ? a[off + 8 * q + k] : 0.0;
-                r = v[0] * v[0];
+            for (int q = 0; q < 16; ++q) v[q] = (8 * q + k < full) ? x[off + 8 * q + k] : 0.0;
+            r = v[0] * v[0];
 #pragma unroll
-                for (int q = 1; q < 16; ++q)
-                    if (8 * q + k < full) r += v[q] * v[q];
-            }
-            r += __shfl_xor(r, 1, 64);             // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
-            r += __shfl_xor(r, 2, 64);
-            r += __shfl_xor(r, 4, 64);
-            if (in && k == 0) {
-                double res = (len < 8) ? 0.0 : r;
-                for (int e = (len < 8) ? 0 : full; e < len; ++e) res += a[off + e] * a[off + e];
-                s_sum[l] = res;
-            }
+            for (int q = 1; q < 16; ++q)
+                if (8 * q + k < full) r += v[q] * v[q];
+        }
+        r += __shfl_xor(r, 1, 64);             // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+        r += __shfl_xor(r, 2, 64);
+        r += __shfl_xor(r, 4, 64);
+        if (in && k == 0) {
+            double res = (len < 8) ? 0.0 : r;
+            for (int e = (len < 8) ? 0 : full; e < len; ++e) res += x[off + e] * x[off + e];
+            s_node[l] = res;
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int top = 0, leaf = 0;
-        st[0] = Frame{0, (int)n, 0, 0.0};
-        double v = 0.0;
-        bool have = false;                 // v is a finished child value to hand up
-        while (top >= 0) {
-            Frame &f = st[top];
-            if (have) {
-                if (f.stage == 1) {
-                    f.left = v;
-                    f.stage = 2;
-                    have = false;
-                    int n2 = f.n / 2;
-                    n2 -= n2 % 8;
-                    st[top + 1] = Frame{f.off + n2, f.n - n2, 0, 0.0};
-                    ++top;
-                } else {                   // stage 2: both halves done
-                    v = f.left + v;
-                    --top;
-                }
-                continue;
-            }
-            if (f.n <= 128) {
-                v = s_sum[leaf++];
-                have = true;
-                --top;
-            } else {
-                int n2 = f.n / 2;
-                n2 -= n2 % 8;
-                f.stage = 1;
-                st[top + 1] = Frame{f.off, n2, 0, 0.0};
-                ++top;
-            }
-        }
-        *out = v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double v = 0.0;
+    if (lane == 0) {
+        for (int q = 0; q + 1 < nl; ++q) s_node[nl + q] = s_node[pl->a[q]] + s_node[pl->b[q]];
+        v = s_node[2 * nl - 2];
     }
+    return v;
 }
 
 }  // namespace fs2

@@ -517,4 +517,38 @@ hipError_t debug_chain_times(unsigned long long out[8], int reset) {
 
 int64_t np_sumsq_chunks(int64_t n) { return (n + kNpChunk - 1) / kNpChunk; }
 
+// numpy's pairwise_sum recursion (loops_utils.h.src) over the partial last chunk
+// of n elements: n > 128 splits at n2 = n / 2 rounded down to a multiple of 8;
+// leaves in order, internal nodes in post-order.  False when there is none.
+bool np_tail_plan(int64_t n, NpTailPlan *out) {
+    const int m = (int)(n % kNpChunk);
+    *out = NpTailPlan{};
+    if (m == 0) return false;
+    struct Rec {
+        NpTailPlan *p;
+        int nodes = 0;
+        int go(int off, int len) {            // returns the node index of [off, off + len)
+            if (len <= 128) {
+                p->off[p->nl] = off;
+                p->len[p->nl] = len;
+                return p->nl++;
+            }
+            int n2 = len / 2;
+            n2 -= n2 % 8;
+            const int l = go(off, n2), r = go(off + n2, len - n2);
+            p->a[nodes] = l;
+            p->b[nodes] = r;
+            return -(++nodes);                // internal: resolved below
+        }
+    } rec{out};
+    // two passes: the first counts the leaves (internal node ids are nl + k)
+    rec.go(0, m);
+    const int nl = out->nl;
+    for (int k = 0; k < rec.nodes; ++k) {
+        if (out->a[k] < 0) out->a[k] = nl - out->a[k] - 1;
+        if (out->b[k] < 0) out->b[k] = nl - out->b[k] - 1;
+    }
+    return true;
+}
+
 }  // namespace fs2

@@ -96,6 +96,18 @@ struct DevStats {
                                      // match, the map size on an append)
 };
 
+// numpy's np.sum over 8192-element buffers (fs2_exact.hip).  The recursion over a
+// partial last chunk is fixed by the handle's particle count (np_tail_plan, host):
+// its leaves in order, then its internal nodes in post-order, node nl + k = node
+// a[k] + node b[k] (the last is the root).
+constexpr int kNpChunk = 8192;
+constexpr int kNpMaxLeaves = 256;
+struct NpTailPlan {
+    int32_t nl;                      // leaves (0: no partial chunk)
+    int32_t off[kNpMaxLeaves], len[kNpMaxLeaves];
+    int32_t a[kNpMaxLeaves], b[kNpMaxLeaves];
+};
+
 // Per-rank record all-gathered once per scan (and once more after a resample).
 struct RankRecord {
     double sumsq;            // sum of normalised w^2 (local)
@@ -218,6 +230,7 @@ struct ReduceParams {
     double *np_part;         // exact: numpy chunk sums of w'^2 (k_finalize, beyond its LDS stage)
     int32_t n_np;            // their count
     double *np_leaf;         // exact: numpy's 128-element leaves of the full chunks (k_normalize)
+    const NpTailPlan *np_tail;   // exact: the partial last chunk's tree (null: none)
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
@@ -328,7 +341,9 @@ struct ChainParams {
     double margin;           // relative bound on |estimate - chain| (doubled)
 };
 hipError_t launch_chain(const ChainParams &p, hipStream_t s, hipEvent_t e0 = nullptr);
-// numpy np.sum(w ** 2): 8192-element chunks (k_normalize leaves, k_finalize trees)
+// numpy np.sum(w ** 2): 8192-element chunks (k_normalize leaves, k_finalize trees);
+// the partial last chunk's tree (NpTailPlan, fs2_chain.hpp) planned on the host
+bool np_tail_plan(int64_t n, NpTailPlan *out);
 int64_t np_sumsq_chunks(int64_t n);
 
 // Launch of kernel k; with profiling events (e0: its start, e1: its end, either
@@ -376,6 +391,7 @@ hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, De
 hipError_t debug_phase_times(unsigned long long out[8], int reset);
 hipError_t debug_icp_phase_times(unsigned long long out[4], int reset);
 hipError_t debug_chain_times(unsigned long long out[8], int reset);
+hipError_t debug_fin_times(unsigned long long out[8], int reset);
 #endif
 // particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
 // alloc.rbase + p * lm_cap + j

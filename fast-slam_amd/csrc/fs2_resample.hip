@@ -63,55 +63,53 @@ __device__ double pairwise_sq(const double *a, int64_t n) {
     return pairwise_sq(a, n2) + pairwise_sq(a + n2, n - n2);
 }
 
-__device__ void global_finalize_body(const ReduceParams &P);
+template <typename RecOf>
+__device__ void global_finalize_impl(const ReduceParams &P, RecOf rec);
 
 // This rank's record: sum w'^2, first maximum, its pose, normalised total (on
 // one GPU also the global decision, k_global_finalize's work).
 constexpr int kNpStage = 1024;
+
+// Optional phase stamps of k_finalize (build with -DFS2_PHASE_TIMING; read back
+// with fs2_debug_finalize_times): thread 0's s_memtime deltas, summed.
+#ifdef FS2_PHASE_TIMING
+__device__ unsigned long long g_fin[8];
+#define FS2_FIN(k)                                                                   \
+    do {                                                                             \
+        if (threadIdx.x == 0) {                                                      \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+            if ((k) > 0) atomicAdd(&g_fin[(k) - 1], t_ - fin_last);                 \
+            fin_last = t_;                                                           \
+        }                                                                            \
+    } while (0)
+#else
+#define FS2_FIN(k) do { } while (0)
+#endif
 
 __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
     __shared__ int lds_i[16];
     __shared__ double s_np[kNpStage];
-    if (P.exact) {
-        // numpy's chunk sums: each full chunk's 64 leaves (k_normalize) as a balanced
-        // tree in order (a wave per chunk, xor butterflies; 8 chunks' loads in flight),
-        // the partial last chunk by numpy's recursion; added in order below
-        const int64_t nfull = P.n / kNpChunk;
-        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (int64_t c0 = wid; c0 < nfull; c0 += 16 * 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int64_t c = c0 + 16 * u;
-                v[u] = (c < nfull) ? P.np_leaf[c * 64 + lane] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) v[u] += __shfl_xor(v[u], o, 64);
-                const int64_t c = c0 + 16 * u;
-                if (lane == 0 && c < nfull) {
-                    if (c < kNpStage) s_np[c] = v[u];
-                    else P.np_part[c] = v[u];
-                }
-            }
-        }
-        if (P.n % kNpChunk)
-            np_pairwise_partial(P.w + nfull * kNpChunk, P.n % kNpChunk, nfull < kNpStage ? s_np + nfull : P.np_part + nfull);
-        __syncthreads();
-    }
+    __shared__ double s_bv[16];
+#ifdef FS2_PHASE_TIMING
+    unsigned long long fin_last = 0;
+#endif
+    FS2_FIN(0);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the normalise partials: every thread's loads issued first, so that their
+    // latency overlaps the numpy trees below
+    constexpr int PL = 4;
+    double s4[PL], w4[PL];
+    int64_t i4[PL];
+    int m4[PL];
     double sq = 0.0;
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
     int mc = 0;
-    for (int k0 = threadIdx.x; k0 < P.nparts; k0 += 4 * 1024) {
-        double s4[4], w4[4];                       // 4 parts' loads in flight per thread
-        int64_t i4[4];
-        int m4[4];
+    auto load_parts = [&](int k0) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PL; ++u) {
             const int k = k0 + 1024 * u;
             const bool in = k < P.nparts;
             s4[u] = in ? P.part_sq[k] : 0.0;
@@ -119,16 +117,83 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
             i4[u] = in ? P.part_best_i[k] : INT64_MAX;
             m4[u] = in ? P.part_maxcnt[k] : 0;
         }
+    };
+    auto fold_parts = [&] {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PL; ++u) {
             sq += s4[u];
             argmax_combine(bv, bi, w4[u], i4[u]);
             mc = max(mc, m4[u]);
         }
+    };
+    load_parts(threadIdx.x);
+    if (P.exact) {
+        // numpy's chunk sums: each full chunk's 64 leaves (k_normalize) as a balanced
+        // tree in order (a wave per chunk, xor butterflies; 16 chunks' loads in
+        // flight) on waves 0..14, the partial last chunk by numpy's recursion on
+        // wave 15 meanwhile; added in order by thread 0 below
+        const int64_t nfull = P.n / kNpChunk;
+        if (wid < 15) {
+            for (int64_t c0 = wid; c0 < nfull; c0 += 15 * 16) {
+                double v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int64_t c = c0 + 15 * u;
+                    v[u] = (c < nfull) ? P.np_leaf[c * 64 + lane] : 0.0;
+                }
+                // the DPP reduction's tree is numpy's: row_shr 1/2/4/8 pair the
+                // leaves of each 16-lane row as a balanced tree in order (the adds
+                // commute), the row broadcasts then pair rows 0+1, 2+3 and the halves
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    v[u] = lane63(dpp_scan(v[u], 0.0, [](double a, double b) { return a + b; }));
+                    const int64_t c = c0 + 15 * u;
+                    if (lane == 0 && c < nfull) {
+                        if (c < kNpStage) s_np[c] = v[u];
+                        else P.np_part[c] = v[u];
+                    }
+                }
+            }
+        } else if (P.np_tail) {
+            const double t = np_pairwise_wave(P.w + nfull * kNpChunk, P.np_tail);
+            if (lane == 0) {
+                if (nfull < kNpStage) s_np[nfull] = t;
+                else P.np_part[nfull] = t;
+            }
+        }
     }
-    sq = block_sum<1024>(sq, lds_d);
-    block_argmax<1024>(bv, bi, lds_d, lds_l);
-    mc = block_max_i<1024>(mc, lds_i);
+    FS2_FIN(1);
+    fold_parts();
+    for (int k0 = threadIdx.x + PL * 1024; k0 < P.nparts; k0 += PL * 1024) {
+        load_parts(k0);
+        fold_parts();
+    }
+    FS2_FIN(2);
+    // the three block reductions behind one barrier (wave trees on DPP)
+    sq = wave_sum(sq);
+    wave_argmax(bv, bi);
+    mc = wave_max_i(mc);
+    if (lane == 0) {
+        lds_d[wid] = sq;
+        s_bv[wid] = bv;
+        lds_l[wid] = bi;
+        lds_i[wid] = mc;
+    }
+    __syncthreads();
+    FS2_FIN(3);
+    if (threadIdx.x == 0) {
+        sq = lds_d[0];
+        bv = s_bv[0];
+        bi = lds_l[0];
+        mc = lds_i[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            sq += lds_d[k];
+            argmax_combine(bv, bi, s_bv[k], lds_l[k]);
+            mc = max(mc, lds_i[k]);
+        }
+    }
+    FS2_FIN(4);
     if (threadIdx.x == 0) {
         if (P.sequential) {
             // np.sum(weights ** 2): pairwise inside 8192-element chunks
@@ -140,22 +205,16 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
             }
             sq = s;
         } else if (P.exact) {
-            // the same sums, each chunk's tree evaluated by k_np_sumsq (staged in
-            // LDS above), added in order
-            double s = 0.0;
-            for (int k0 = 0; k0 < P.n_np; k0 += 8) {
-                double v[8];                       // 8 loads in flight, then 8 adds in order
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int k = k0 + u;
-                    v[u] = (k >= P.n_np) ? 0.0 : (k < kNpStage ? s_np[k] : P.np_part[k]);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (k0 + u < P.n_np) s = (k0 + u == 0) ? v[u] : s + v[u];
-            }
+            // the same sums: each chunk's tree (above), added in order
+            // (the LDS-staged ones first: one address space per loop, so the loads
+            // stay ds_read instead of flat)
+            const int nl = min(P.n_np, kNpStage);
+            double s = (nl > 0) ? s_np[0] : 0.0;
+            for (int k = 1; k < nl; ++k) s = s + s_np[k];
+            for (int k = nl; k < P.n_np; ++k) s = s + P.np_part[k];
             sq = s;
         }
+        FS2_FIN(5);
         RankRecord r{};
         r.sumsq = sq;
         r.best_w = bv;
@@ -168,9 +227,28 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
         r.t_local = P.stats->t_local;
         r.max_count = mc;
         *P.rec = r;
-        if (P.world == 1 && P.recs == P.rec) global_finalize_body(P);   // one GPU: no record exchange
+        FS2_FIN(6);
+        // one GPU: no record exchange (the record from registers)
+        if (P.world == 1 && P.recs == P.rec) global_finalize_impl(P, [&](int) -> const RankRecord & { return r; });
+        FS2_FIN(7);
+        if (threadIdx.x == 0) {
+#ifdef FS2_PHASE_TIMING
+            atomicAdd(&g_fin[7], 1ull);
+#endif
+        }
     }
 }
+
+#ifdef FS2_PHASE_TIMING
+hipError_t debug_fin_times(unsigned long long out[8], int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_fin), z, sizeof z);
+    }
+    return e;
+}
+#endif
 
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, p);
@@ -179,24 +257,25 @@ hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
 
 // N_eff (fast_slam_2.py:212-223), the N_eff < N/2 rule (:62), the estimate
 // (:201-210), u0 (:183) and this rank's prefix offset, from all records.
-__device__ void global_finalize_body(const ReduceParams &P) {
+template <typename RecOf>
+__device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
     DevStats *st = P.stats;
-    double sq = P.recs[0].sumsq;
-    double bv = P.recs[0].best_w;
-    int64_t bi = P.recs[0].best_gidx;
+    double sq = rec(0).sumsq;
+    double bv = rec(0).best_w;
+    int64_t bi = rec(0).best_gidx;
     int gb = 0;
     double off = 0.0;
     for (int g = 1; g < P.world; ++g) {
-        sq = sq + P.recs[g].sumsq;
-        const double v = P.recs[g].best_w;
-        const int64_t i = P.recs[g].best_gidx;
+        sq = sq + rec(g).sumsq;
+        const double v = rec(g).best_w;
+        const int64_t i = rec(g).best_gidx;
         if (v > bv || (v == bv && i < bi)) {
             bv = v;
             bi = i;
             gb = g;
         }
     }
-    for (int g = 0; g < P.rank; ++g) off = (g == 0) ? P.recs[0].t_local : off + P.recs[g].t_local;
+    for (int g = 0; g < P.rank; ++g) off = (g == 0) ? rec(0).t_local : off + rec(g).t_local;
     const double ng = (double)P.n_global;
     const double ne = (sq < 1.0 / ng) ? ng : 1.0 / sq;
     st->sumsq = sq;
@@ -207,14 +286,14 @@ __device__ void global_finalize_body(const ReduceParams &P) {
     if (P.flip_margin > 0.0 && fabs(ne - ng / 2.0) <= P.flip_margin * ng) st->reduce_amb += 1;
     // the largest map on any rank: a resample may bring it here (the receiver
     // sizes its page-table rows for it before unpacking)
-    int mc = P.recs[0].max_count;
-    for (int g = 1; g < P.world; ++g) mc = max(mc, P.recs[g].max_count);
+    int mc = rec(0).max_count;
+    for (int g = 1; g < P.world; ++g) mc = max(mc, rec(g).max_count);
     st->max_count = max(st->max_count, mc);
     st->best_index = bi;
     st->best_w = bv;
-    st->pose[0] = P.recs[gb].pose[0];
-    st->pose[1] = P.recs[gb].pose[1];
-    st->pose[2] = P.recs[gb].pose[2];
+    st->pose[0] = rec(gb).pose[0];
+    st->pose[1] = rec(gb).pose[1];
+    st->pose[2] = rec(gb).pose[2];
     st->offset = off;
     st->out_min = INT32_MAX;
     st->out_max = -1;
@@ -222,7 +301,9 @@ __device__ void global_finalize_body(const ReduceParams &P) {
                        : (1.0 / ng) * philox_uniform01(P.seed, P.scan | (1ull << 63), 0);
 }
 
-__global__ void k_global_finalize(const ReduceParams P) { global_finalize_body(P); }
+__global__ void k_global_finalize(const ReduceParams P) {
+    global_finalize_impl(P, [&](int g) -> const RankRecord & { return P.recs[g]; });
+}
 
 hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_global_finalize, dim3(1), dim3(1), 0, s, p);

@@ -33,6 +33,9 @@ def main():
         f.step(*syn.odometry(s), syn.scan_measurements(L, s, 0))
     f.synchronize()
     fn(out, 1)
+    fin0 = nat.load().fs2_debug_finalize_times
+    fin0.argtypes = [C.POINTER(C.c_uint64), C.c_int32]
+    fin0((C.c_uint64 * 8)(), 1)
     for s in range(3, 23):
         f.step(*syn.odometry(s), syn.scan_measurements(L, s, 0))
     f.synchronize()
@@ -43,6 +46,15 @@ def main():
     for k, nme in enumerate(names):
         print(f"{nme:<20} {out[k] / calls:10.0f} cycles per walk (~{out[k] / calls / 2400.0:.2f} us at 2.4 GHz)")
     f.close()
+    # k_finalize: thread 0's stamps (fs2_resample.hip FS2_FIN), same scans
+    fin = nat.load().fs2_debug_finalize_times
+    fin.argtypes = [C.POINTER(C.c_uint64), C.c_int32]
+    fo = (C.c_uint64 * 8)()
+    fin(fo, 0)
+    n = max(fo[7], 1)
+    for k, nme in enumerate(["loads issued + numpy trees", "partials folded", "block_sum", "argmax + max",
+                             "thread 0: chunk sums in order", "pose loads + record", "decision + stats"]):
+        print(f"k_finalize {nme:<32} {fo[k] / n:10.0f} cycles per call")
 
 
 if __name__ == "__main__":

@@ -83,6 +83,11 @@ def cases():
     w[::2] = 2.0 / M
     out.append(("neff_half", w, 0.5 / M))
     out.append(("full_chunks", rng.random(3 * 8192) ** 3, 0.2 / (3 * 8192)))
+    # partial last chunks of 3 (under numpy's 8-element block), 100 (one leaf) and
+    # 8191 (the deepest tree) elements
+    for tail in (3, 100, 8191):
+        n = 2 * 8192 + tail
+        out.append((f"tail_{tail}", rng.random(n) ** 2, 0.3 / n))
     out.append(("cfg3_size", rng.lognormal(0.0, 2.0, 1_000_000), 0.77e-6))
     return out
 
