@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -91,7 +92,13 @@ struct fs2_handle {
     int64_t npool = 0;                     // pages in the pool
     Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
     uint32_t *bbox[2] = {};                // [nblocks][kBBoxRows] workgroup row boxes of pt[0] / pt[1]
-    Desc *rdesc = nullptr;                 // descriptors of received pages [n_recv][rows]
+    Desc *rdesc = nullptr;                 // received particles' rows [n_recv][rows]
+    Desc *udesc = nullptr;                 // received distinct pages [u_recv]
+    size_t udesc_cap = 0;
+    // page dedup of the outgoing transfers (XferTable)
+    unsigned long long *xt_key = nullptr;
+    uint32_t *xt_ref = nullptr, *xt_uidx = nullptr, *xt_eslot = nullptr, *xt_ulist = nullptr;
+    int64_t xt_cap = 0, xt_ecap = 0;
     SumFrame frame{-127.0f, 1.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
     float ext_seen = 0.0f;                 // largest |x|, |y| imported so far
     float *slb = nullptr;                  // device: lower bound on every nonzero mirror s
@@ -114,7 +121,7 @@ struct fs2_handle {
     uint8_t repoch = 0;
     int64_t *rbcnt = nullptr;
     int64_t *rnfree_dev = nullptr;
-    int64_t s_recv = 0;                    // slots received by the last resample
+    int64_t u_recv = 0;                    // distinct pages received by the last resample
     int32_t *rank_d = nullptr, *rank_e = nullptr;
     int64_t *iblk = nullptr;
     int cap = 0, max_cap = kMaxSlots;
@@ -152,7 +159,7 @@ struct fs2_handle {
     fs2comm::Transport *tp = nullptr;
     RankRecord *rec = nullptr, *recs = nullptr;     // this rank's record / all ranks'
     double *totals = nullptr;                       // all ranks' weight totals
-    int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (records, slots) per peer
+    int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (particles, rows, pages) per peer
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr;
     uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
@@ -404,7 +411,7 @@ static int post_and_wait(fs2_handle *h, bool sizes) {
     CommTimer ct(h);
     const int G = h->cfg.world_size;
     const unsigned long long seq = ++h->post_seq;
-    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? 2 * G * G : 0, h->post, h->post_flag_dev,
+    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? 3 * G * G : 0, h->post, h->post_flag_dev,
                            seq, h->stream));
     return wait_seq(h, h->post_flag, seq, "mid-scan statistics");
 }
@@ -414,9 +421,11 @@ static const int64_t *posted_xmat(const fs2_handle *h) {
 }
 
 // Sharded resample: plan what goes to every other rank on the device (one run of
-// local particles per destination, fs2_plan.hpp), all-gather the sizes, learn
-// them with one post, pack all destinations in one launch and move them with one
-// grouped exchange; then describe what arrived to the apply kernels.
+// local particles per destination, fs2_plan.hpp), all-gather the sizes and learn
+// them with a post; find the distinct pages of every destination's rows
+// (k_dedup_*), all-gather and learn their counts; pack all destinations in one
+// pass and move them with one grouped exchange; then describe what arrived to the
+// apply kernels.
 static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     const int G = h->cfg.world_size, R = h->cfg.rank;
     hipStream_t s = h->stream;
@@ -426,46 +435,104 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     rs.xrow = h->xrow;
     HIP_TRY(h, launch_pack_count(rs, s));
     int rc;
-    {
-        CommTimer ct(h);
-        rc = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 2 * G, s, &h->err);
+    auto gather_sizes = [&]() -> int {
+        {
+            CommTimer ct(h);
+            const int r = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 3 * G, s, &h->err);
+            if (r) return r;
+        }
+        return post_and_wait(h, true);
+    };
+    rc = gather_sizes();
+    if (rc) return rc;
+    std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + 3 * G * G);
+    auto at = [&](int from, int to, int f) { return mat[(size_t)from * 3 * G + 3 * to + f]; };
+    // distinct pages of the rows sent (every rank takes part in the all-gather)
+    XferTable &T = rs.xt;
+    T = XferTable{};
+    for (int p = 0; p < G; ++p) T.ebase[p + 1] = T.ebase[p] + (p == R ? 0 : at(R, p, 1));
+    const int64_t nrows = T.ebase[G];
+    if (nrows > 0) {
+        int lg = 10;
+        while ((int64_t(1) << lg) < 2 * nrows) ++lg;
+        if (lg > 31) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld page-table rows to send", (long long)nrows);
+        const int64_t cap = int64_t(1) << lg;
+        if (h->xt_cap < cap) {
+            HIP_TRY(h, hipStreamSynchronize(s));
+            hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx);
+            h->xt_key = nullptr; h->xt_ref = h->xt_uidx = nullptr;
+            h->xt_cap = 0;
+            HIP_TRY(h, hipMalloc((void **)&h->xt_key, (size_t)cap * 8));
+            HIP_TRY(h, hipMalloc((void **)&h->xt_ref, (size_t)cap * 4));
+            HIP_TRY(h, hipMalloc((void **)&h->xt_uidx, (size_t)cap * 4));
+            h->xt_cap = cap;
+        }
+        if (h->xt_ecap < nrows) {
+            HIP_TRY(h, hipStreamSynchronize(s));
+            hipFree(h->xt_eslot); hipFree(h->xt_ulist);
+            h->xt_eslot = h->xt_ulist = nullptr;
+            h->xt_ecap = 0;
+            const int64_t want = nrows + nrows / 4;
+            HIP_TRY(h, hipMalloc((void **)&h->xt_eslot, (size_t)want * 4));
+            HIP_TRY(h, hipMalloc((void **)&h->xt_ulist, (size_t)want * 4));
+            h->xt_ecap = want;
+        }
+        T.key = h->xt_key;
+        T.ref = h->xt_ref;
+        T.uidx = h->xt_uidx;
+        T.eslot = h->xt_eslot;
+        T.ulist = h->xt_ulist;
+        T.cap = cap;
+        T.log2cap = lg;
+        HIP_TRY(h, hipMemsetAsync(T.key, 0, (size_t)cap * 8, s));
+        HIP_TRY(h, hipMemsetAsync(T.ref, 0, (size_t)cap * 4, s));
+        HIP_TRY(h, launch_pack_dedup(rs, s));
     }
+    rc = gather_sizes();
     if (rc) return rc;
-    rc = post_and_wait(h, true);
-    if (rc) return rc;
-    const std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + 2 * G * G);
+    mat.assign(posted_xmat(h), posted_xmat(h) + 3 * G * G);
+    static const bool log_xfer = std::getenv("FS2_XFER_LOG") != nullptr;
     int64_t nsend = 0;
     std::vector<fs2comm::Xfer> sends, recvs;
     for (int p = 0; p < G; ++p) {
         rs.sbuf[p] = nullptr;
-        const int64_t K = mat[(size_t)R * 2 * G + 2 * p], S = mat[(size_t)R * 2 * G + 2 * p + 1];
+        T.ubase[p + 1] = T.ubase[p] + (p == R ? 0 : at(R, p, 2));
+        const int64_t K = at(R, p, 0), S = at(R, p, 1), U = at(R, p, 2);
+        if (log_xfer && p != R)
+            std::fprintf(stderr, "fs2 xfer scan %lld rank %d -> %d: %lld particles, %lld rows, %lld pages, %lld B\n",
+                         (long long)h->scan, R, p, (long long)K, (long long)S, (long long)U,
+                         (long long)xfer_bytes(K, S, U));
         if (p == R || K == 0) continue;
-        rc = ensure_buf(h, h->sendbuf, h->sendcap, p, (size_t)(K + S) * 64);
+        const size_t bytes = (size_t)xfer_bytes(K, S, U);
+        rc = ensure_buf(h, h->sendbuf, h->sendcap, p, bytes);
         if (rc) return rc;
         rs.sbuf[p] = h->sendbuf[p];
-        sends.push_back({p, h->sendbuf[p], (size_t)(K + S) * 64});
+        sends.push_back({p, h->sendbuf[p], bytes});
         nsend += K;
     }
     if (nsend > INT32_MAX) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld particles to send", (long long)nsend);
-    HIP_TRY(h, launch_pack_write(rs, (int32_t)nsend, s));
+    HIP_TRY(h, launch_pack_write(rs, s));
     rs.npeers = 0;
     int32_t kbase = 0;
-    int64_t sbase = 0;
+    int64_t ubase = 0;
     for (int q = 0; q < G; ++q) {
         if (q == R) continue;
-        const int64_t K = mat[(size_t)q * 2 * G + 2 * R], S = mat[(size_t)q * 2 * G + 2 * R + 1];
+        const int64_t K = at(q, R, 0), S = at(q, R, 1), U = at(q, R, 2);
         if (!K) continue;
-        rc = ensure_buf(h, h->recvbuf, h->recvcap, q, (size_t)(K + S) * 64);
+        const size_t bytes = (size_t)xfer_bytes(K, S, U);
+        rc = ensure_buf(h, h->recvbuf, h->recvcap, q, bytes);
         if (rc) return rc;
-        recvs.push_back({q, h->recvbuf[q], (size_t)(K + S) * 64});
+        recvs.push_back({q, h->recvbuf[q], bytes});
         RecvPeer &pp = rs.peers[rs.npeers++];
         pp.hdr = reinterpret_cast<const PackHeader *>(h->recvbuf[q]);
-        pp.pay = h->recvbuf[q] + K * 64;
+        pp.idx = reinterpret_cast<const uint32_t *>(h->recvbuf[q] + xfer_idx_off(K));
+        pp.pages = h->recvbuf[q] + xfer_page_off(K, S);
         pp.K = (int32_t)K;
         pp.kbase = kbase;
-        pp.sbase = sbase;
+        pp.U = U;
+        pp.ubase = ubase;
         kbase += (int32_t)K;
-        sbase += S;
+        ubase += U;
     }
     {
         CommTimer ct(h);
@@ -473,7 +540,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     }
     if (rc) return rc;
     h->n_recv = kbase;
-    h->s_recv = sbase;
+    h->u_recv = ubase;
     return FS2_OK;
 }
 
@@ -556,7 +623,8 @@ static void free_handle(fs2_handle *h) {
         hipFree(h->pt[s]);
         hipFree(h->bbox[s]);
     }
-    hipFree(h->rdesc);
+    hipFree(h->rdesc); hipFree(h->udesc);
+    hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_eslot); hipFree(h->xt_ulist);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->ext_dev);
@@ -645,8 +713,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
     ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
     ok &= alloc((void **)&h->totals, sizeof(double) * G) == hipSuccess;
-    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * 2 * G) == hipSuccess;
-    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 2 * G * G) == hipSuccess;
+    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * 3 * G) == hipSuccess;
+    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 3 * G * G) == hipSuccess;
     ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
@@ -683,8 +751,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
     {
-        // post block: DevStats, xmat (2 G x G words), then the flag on its own line
-        const size_t body = sizeof(DevStats) + sizeof(int64_t) * 2 * kMaxRanks * kMaxRanks;
+        // post block: DevStats, xmat (3 G x G words), then the flag on its own line
+        const size_t body = sizeof(DevStats) + sizeof(int64_t) * 3 * kMaxRanks * kMaxRanks;
         const size_t off = ((body + 63) / 64) * 64;
         ok &= hipHostMalloc((void **)&h->post_host, off + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
               hipSuccess;
@@ -1115,11 +1183,11 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
             if (rc) return rc;
             rs.opt = h->pt[nxt];
             rs.obbox = h->row_boxes(nxt);
-            // fresh records and pages for the received maps: record r, row k ->
-            // page base + r * rows + k; slot q -> record rbase + peer sbase + soff + q
-            rc = reserve_recs(h, h->s_recv, &rs.alloc);
+            // fresh pages and records for the received distinct pages: page u ->
+            // page freel[base + u], its slot j -> record rfreel[rbase + 8 u + j]
+            rc = reserve_recs(h, h->u_recv * kPageSlots, &rs.alloc);
             if (rc) return rc;
-            rc = reserve_pages(h, (int64_t)h->n_recv * h->rows, &rs.alloc);
+            rc = reserve_pages(h, h->u_recv, &rs.alloc);
             if (rc) return rc;
             rs.map = h->map();
             const size_t rbytes = sizeof(Desc) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
@@ -1131,6 +1199,16 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
                 HIP_TRY(h, hipMalloc(&h->rdesc, rbytes + rbytes / 4));
                 h->rdesc_cap = rbytes + rbytes / 4;
             }
+            const size_t ubytes = sizeof(Desc) * (size_t)std::max<int64_t>(h->u_recv, 1);
+            if (ubytes > h->udesc_cap) {
+                HIP_TRY(h, hipStreamSynchronize(s));
+                hipFree(h->udesc);
+                h->udesc = nullptr;
+                h->udesc_cap = 0;
+                HIP_TRY(h, hipMalloc(&h->udesc, ubytes + ubytes / 4));
+                h->udesc_cap = ubytes + ubytes / 4;
+            }
+            rs.udesc = h->udesc;
             rs.rdesc = h->rdesc;
         }
         HIP_TRY(h, launch_resample_apply(rs, sh, s));

@@ -119,13 +119,28 @@ struct RankRecord {
     int32_t pad;
 };
 
-// Header of a particle sent to another rank by the resample (64 B); its map
-// follows in the payload region as cnt x 16 B mirrors then cnt x 48 B slots.
+// A transfer to one rank (fs2_resample.hip, "packing"): K particle headers (64 B
+// each), then one 32-bit entry per page-table row of each particle (S rows,
+// padded to 64 B), then the U distinct pages those rows name, kXferPageBytes
+// each: the 8 gate mirrors (a slot past the page's fill has rec = kNoRec) and
+// the 8 slots' fp64 records.  Particles that descend from one ancestor share
+// most pages, so U is far below S.  Entry = unique page index | kEntryOwned
+// when the receiver may own the page (named once, by a particle that fills
+// one output).
+constexpr int kXferPageBytes = 128 + kPageSlots * kRecBytes;   // 512
+constexpr uint32_t kNoRec = 0xffffffffu;
+constexpr uint32_t kEntryOwned = 0x80000000u;
+__host__ __device__ inline int64_t xfer_idx_off(int64_t K) { return K * 64; }
+__host__ __device__ inline int64_t xfer_page_off(int64_t K, int64_t S) { return K * 64 + ((S * 4 + 63) / 64) * 64; }
+__host__ __device__ inline int64_t xfer_bytes(int64_t K, int64_t S, int64_t U) {
+    return xfer_page_off(K, S) + U * kXferPageBytes;
+}
+
 struct PackHeader {
     int64_t gsrc;            // global index of the source particle
     int32_t out_lo, out_hi;  // outputs it fills on the receiver (global, inclusive)
     int32_t cnt;
-    int32_t soff;            // payload offset in slots within the sender's payload
+    int32_t soff;            // its first row entry within the transfer's entries
     double x, y, yaw, w;
     int64_t pad;
 };
@@ -134,7 +149,8 @@ constexpr int kMaxRanks = 16;
 
 // What this rank sends to one destination (k_pack_bounds): the run [i0, i1) of
 // local particles whose outputs may reach its shard [pa, pb), the exclusive
-// counts of non-empty ranges / slots before i0, and the transfer's records / slots.
+// counts of non-empty ranges / page-table rows before i0, and the transfer's
+// particles / rows.
 struct PackPlan {
     int64_t i0, i1;
     int64_t e0, c0;
@@ -144,10 +160,29 @@ struct PackPlan {
 
 struct RecvPeer {
     const PackHeader *hdr;   // K headers
-    const char *pay;         // payload base
-    int32_t K;               // records from this peer
-    int32_t kbase;           // index of its first record among all received
-    int64_t sbase;           // index of its first slot among all received slots
+    const uint32_t *idx;     // row entries
+    const char *pages;       // U distinct pages
+    int32_t K;               // particles from this peer
+    int32_t kbase;           // index of its first particle among all received
+    int64_t U;               // distinct pages from this peer
+    int64_t ubase;           // index of its first page among all received pages
+};
+
+// Page dedup of the outgoing transfers: an open-addressing table keyed by
+// fill << 40 | (destination + 1) << 32 | page id (0: empty) with the number of
+// row entries naming each key and its index among the destination's distinct
+// pages; every outgoing row entry's table slot (| kEntryOwned when its particle
+// fills one output), destination-major from ebase[p].
+struct XferTable {
+    unsigned long long *key;   // [cap]
+    uint32_t *ref;             // [cap]
+    uint32_t *uidx;            // [cap]
+    uint32_t *eslot;           // [sum S] per row entry
+    uint32_t *ulist;           // [sum S] destination p's distinct pages' slots from ebase[p]
+    int64_t cap;               // power of two
+    int32_t log2cap;
+    int64_t ebase[kMaxRanks + 1];
+    int64_t ubase[kMaxRanks + 1];   // exclusive prefix of U over destinations (k_pack_pages)
 };
 
 struct MeasPack {
@@ -276,11 +311,12 @@ struct ResampleParams {
     MapRef map;              // current page table
     Desc *opt;               // next page table [rows][n]
     uint32_t *obbox;         // its workgroup row boxes (null: none)
-    Desc *rdesc;             // [nrecv][rows] descriptors of received pages
-    PageAlloc alloc;         // received particle r: row k -> page base + r*rows + k,
-                             // slot q -> record rbase + peer sbase + soff + q
+    Desc *rdesc;             // [nrecv][rows] descriptors of received particles' rows
+    Desc *udesc;             // [sum U] descriptors of the received distinct pages
+    PageAlloc alloc;         // received page u -> page freel[base + u], its slot j ->
+                             // record rfreel[rbase + 8 u + j]
     int32_t *rank_d;         // [n] non-empty ranges before i in its 1024-block
-    int32_t *rank_e;         // [n] their slots
+    int32_t *rank_e;         // [n] their page-table rows
     int64_t *iblk;           // [2 * nblk + 2] per-block totals -> exclusive offsets, grand totals
     double *part_best_w;
     int64_t *part_best_i;
@@ -290,8 +326,9 @@ struct ResampleParams {
     // packing for the other ranks (k_pack_plan / k_pack_bounds / k_pack_*)
     int32_t world, rank;
     PackPlan *plan;          // [world] per destination
-    int64_t *xrow;           // [2 world] records, slots sent to each rank (all-gathered)
-    char *sbuf[kMaxRanks];   // per destination: K x 64 B headers, then S x 64 B payload
+    int64_t *xrow;           // [3 world] particles, rows, distinct pages sent to each rank
+    char *sbuf[kMaxRanks];   // per destination: the transfer (xfer_bytes)
+    XferTable xt;
     // received particles
     int32_t npeers;
     RecvPeer peers[kMaxRanks];
@@ -368,7 +405,11 @@ hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s);
 // resample, split where the sharded path needs the host (sizes of transfers)
 hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
-hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t s);
+// the distinct pages of every destination's rows (xt sized for sum S, key and
+// ref zeroed by the caller), counted into xrow[3 p + 2]
+hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s);
+// headers, row entries and pages into sbuf (sizes from the all-gathered xrow)
+hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s);
 // estimate: also this rank's post-resample record (k_estimate); one GPU leaves
 // it to launch_tail_single
 hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStream_t s);

@@ -586,12 +586,14 @@ hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s) {
 //
 // The local particles whose outputs reach rank p form one run [i0_p, i1_p) of
 // the local index (fs2_plan.hpp plan_run), so one exclusive count E of the
-// non-empty ranges and one of their map sizes C serve every destination: the
-// particle at i is record E[i] - E[i0_p] of rank p's transfer and its slots start
-// at C[i] - C[i0_p].  No host round trip per destination: the counts go to every
-// rank in one all-gather of xrow.
+// non-empty ranges and one of their page-table rows C serve every destination:
+// the particle at i is header E[i] - E[i0_p] of rank p's transfer and its row
+// entries start at C[i] - C[i0_p].  The rows name pages, sent once per
+// destination however many particles name them (k_dedup_*: siblings of one
+// resample share every page neither has written since).  No host round trip
+// per destination: the sizes go to every rank in all-gathers of xrow.
 
-// E, C inside each 1024-particle block (rank_d, rank_e) and per-block totals
+// E, C (page-table rows) inside each 1024-particle block (rank_d, rank_e) and per-block totals
 // (iblk[b], iblk[nblk + b]); lanes past n count nothing.
 __global__ __launch_bounds__(kBlock) void k_pack_plan(const ResampleParams P) {
     __shared__ long long lds[2][kBlock / 64];
@@ -607,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const ResampleParams P) {
         fb[e] = 0;
         if (t < P.n && P.mlo[t] <= P.mhi[t]) {
             fa[e] = 1;
-            fb[e] = P.cnt[t];
+            fb[e] = (P.cnt[t] + kPageSlots - 1) / kPageSlots;
         }
         sa += fa[e];
         sb += fb[e];
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const ResampleParams P) {
         const int64_t t = base + e;
         if (t < P.n) {
             P.rank_d[t] = (int32_t)oa;          // < 1024
-            P.rank_e[t] = (int32_t)ob;          // < 1024 * kMaxSlots
+            P.rank_e[t] = (int32_t)ob;          // < 1024 * kMaxRows
         }
         oa += fa[e];
         ob += fb[e];
@@ -641,7 +643,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const ResampleParams P) {
 }
 
 // Exclusive scans of the block totals (totals at iblk[2 nblk], iblk[2 nblk + 1]),
-// then per destination its run, bases and transfer size (xrow: records, slots;
+// then per destination its run, bases and transfer size (xrow: particles, rows;
 // zero for this rank and when the rule did not fire).
 __global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
     __shared__ long long lds[16];
@@ -688,8 +690,9 @@ __global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
         pl.pb = pb;
     }
     P.plan[p] = pl;
-    P.xrow[2 * p] = pl.K;
-    P.xrow[2 * p + 1] = pl.S;
+    P.xrow[3 * p] = pl.K;
+    P.xrow[3 * p + 1] = pl.S;
+    P.xrow[3 * p + 2] = 0;   // distinct pages: k_dedup_assign
 }
 
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s) {
@@ -699,7 +702,7 @@ hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s) {
 }
 
 // Headers of every local particle sent to another rank, into each destination's
-// send buffer (records K x 64 B, then the payload).
+// transfer.
 __global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P) {
     if (!P.stats->resampled) return;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -725,33 +728,127 @@ __global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P)
     }
 }
 
-// One workgroup per sent record: pages + records -> packed (cnt x 16 B mirrors,
-// cnt x 48 B slots); records of all destinations in one grid.
-__global__ __launch_bounds__(kBlock) void k_pack_payload(const ResampleParams P, int32_t nrec) {
-    if (!P.stats->resampled) return;
-    for (int r = blockIdx.x; r < nrec; r += gridDim.x) {
-        int p = 0, k = r;
-        while (p < P.world && k >= P.plan[p].K) k -= (int)P.plan[p++].K;
+// ---- page dedup (XferTable) ----
+__device__ __forceinline__ uint32_t xt_hash(unsigned long long key, int log2cap) {
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
+}
+
+// Every row of every particle sent: its (destination, page) key into the table
+// (one thread per local particle; the rows' descriptors are coalesced loads).
+__global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P.n) return;
+    const int64_t lo = P.mlo[i], hi = P.mhi[i];
+    if (lo > hi) return;
+    const int c = P.cnt[i];
+    const int rows = (c + kPageSlots - 1) / kPageSlots;
+    const int64_t cpos = P.iblk[P.nblk + i / kScanBlock] + P.rank_e[i];
+    const XferTable &T = P.xt;
+    const uint32_t mask = (uint32_t)(T.cap - 1);
+    for (int p = 0; p < P.world; ++p) {
         const PackPlan &pl = P.plan[p];
-        const PackHeader h = reinterpret_cast<const PackHeader *>(P.sbuf[p])[k];
-        const int64_t i = h.gsrc - P.a;
-        int4 *dm = reinterpret_cast<int4 *>(P.sbuf[p] + pl.K * 64 + (int64_t)h.soff * 64);
-        int4 *df = dm + h.cnt;
-        for (int q = threadIdx.x; q < h.cnt; q += kBlock)
-            dm[q] = reinterpret_cast<const int4 *>(page_of(P.map, q, i))[q % kPageSlots];
-        for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
-            const int j = q / 3;
-            const uint32_t rr = mirror_rec(load_mirror(page_of(P.map, j, i), j));
-            df[q] = reinterpret_cast<const int4 *>(P.map.recs + (int64_t)rr * kRecBytes)[q - 3 * j];
+        if (p == P.rank || i < pl.i0 || i >= pl.i1) continue;
+        const bool single = max(lo, pl.pa) == min(hi, pl.pb - 1);
+        uint32_t *es = T.eslot + T.ebase[p] + (cpos - pl.c0);
+        for (int k = 0; k < rows; ++k) {
+            const uint32_t page = pt_entry(P.map, k, i)->x & kIdMask;
+            const unsigned long long fill = (unsigned long long)min(kPageSlots, c - k * kPageSlots);
+            const unsigned long long key = (fill << 40) | ((unsigned long long)(p + 1) << 32) | page;
+            uint32_t h = xt_hash(key, T.log2cap);
+            for (;;) {
+                const unsigned long long old = atomicCAS(T.key + h, 0ull, key);
+                if (old == 0ull || old == key) break;
+                h = (h + 1u) & mask;
+            }
+            atomicAdd(T.ref + h, 1u);
+            es[k] = h | (single ? kEntryOwned : 0u);
         }
     }
 }
 
-hipError_t launch_pack_write(const ResampleParams &p, int32_t nrec, hipStream_t s) {
+// Index of every distinct page among its destination's (any order: the entries
+// name pages by index), the count into xrow[3 p + 2], the slot into ulist.
+__global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P) {
+    __shared__ uint32_t s_cnt[kMaxRanks], s_base[kMaxRanks];
+    const XferTable &T = P.xt;
+    const int64_t h = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (threadIdx.x < kMaxRanks) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned long long key = (h < T.cap) ? T.key[h] : 0ull;
+    const int d = key ? (int)((key >> 32) & 0xffu) - 1 : -1;
+    const uint32_t local = (d >= 0) ? atomicAdd(&s_cnt[d], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < (unsigned)P.world && s_cnt[threadIdx.x])
+        s_base[threadIdx.x] = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long *>(P.xrow + 3 * threadIdx.x + 2),
+                                                  (unsigned long long)s_cnt[threadIdx.x]);
+    __syncthreads();
+    if (d >= 0) {
+        const uint32_t u = s_base[d] + local;
+        T.uidx[h] = u;
+        T.ulist[T.ebase[d] + u] = (uint32_t)h;
+    }
+}
+
+hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s) {
     const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_pack_headers, dim3(g), dim3(kBlock), 0, s, p);
-    if (nrec > 0)
-        hipLaunchKernelGGL(k_pack_payload, dim3(min(nrec, 2048)), dim3(kBlock), 0, s, p, nrec);
+    if (g) hipLaunchKernelGGL(k_dedup_insert, dim3(g), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(k_dedup_assign, dim3((unsigned)((p.xt.cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ int dest_of(const int64_t *base, int world, int64_t e) {
+    int p = 0;
+    while (p + 1 < world && e >= base[p + 1]) ++p;
+    return p;
+}
+
+// Row entries: the page's index among the destination's distinct pages, owned
+// when the particle fills one output and no other entry names the page.
+__global__ __launch_bounds__(kBlock) void k_pack_index(const ResampleParams P, int64_t total) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= total) return;
+    const XferTable &T = P.xt;
+    const int p = dest_of(T.ebase, P.world, e);
+    const uint32_t es = T.eslot[e];
+    const uint32_t h = es & ~kEntryOwned;
+    const bool own = (es & kEntryOwned) && T.ref[h] == 1u;
+    reinterpret_cast<uint32_t *>(P.sbuf[p] + xfer_idx_off(P.plan[p].K))[e - T.ebase[p]] =
+        T.uidx[h] | (own ? kEntryOwned : 0u);
+}
+
+// Distinct pages: mirrors and records, 8 lanes per page (lane j: slot j).
+__global__ __launch_bounds__(kBlock) void k_pack_pages(const ResampleParams P, int64_t total) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t g = t / kPageSlots;
+    const int j = (int)(t % kPageSlots);
+    if (g >= total) return;
+    const XferTable &T = P.xt;
+    const int p = dest_of(T.ubase, P.world, g);
+    const int64_t u = g - T.ubase[p];
+    const unsigned long long key = T.key[T.ulist[T.ebase[p] + u]];
+    const uint32_t page = (uint32_t)(key & 0xffffffffu);
+    const int fill = (int)((key >> 40) & 0xfu);
+    char *blk = P.sbuf[p] + xfer_page_off(P.plan[p].K, P.plan[p].S) + u * kXferPageBytes;
+    int4 m = make_int4(0, 0, 0, (int)kNoRec);
+    if (j < fill) {
+        m = reinterpret_cast<const int4 *>(page_ptr(P.map.pool, page))[j];
+        const int4 *src = reinterpret_cast<const int4 *>(P.map.recs + (int64_t)(uint32_t)m.w * kRecBytes);
+        int4 *dst = reinterpret_cast<int4 *>(blk + 128 + j * kRecBytes);
+        dst[0] = src[0];
+        dst[1] = src[1];
+        dst[2] = src[2];
+    }
+    reinterpret_cast<int4 *>(blk)[j] = m;
+}
+
+hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s) {
+    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
+    if (g) hipLaunchKernelGGL(k_pack_headers, dim3(g), dim3(kBlock), 0, s, p);
+    const int64_t ne = p.xt.ebase[p.world], nu = p.xt.ubase[p.world];
+    if (ne > 0) hipLaunchKernelGGL(k_pack_index, dim3((unsigned)((ne + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, ne);
+    if (nu > 0)
+        hipLaunchKernelGGL(k_pack_pages, dim3((unsigned)((nu * kPageSlots + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                           p, nu);
     return hipGetLastError();
 }
 
@@ -773,48 +870,63 @@ __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P,
     for (int64_t m = h.out_lo; m <= h.out_hi; ++m) P.out_src[m - P.a] = -(k + 1);
 }
 
-// Received particles' maps into fresh pages and records: record r, row k takes
-// reserved page alloc.base + r * rows + k, its slot q reserved record
-// alloc.rbase + (peer's sbase) + soff + q (one workgroup per received particle).
-__global__ __launch_bounds__(kBlock) void k_unpack_recv(const ResampleParams P, int32_t nrecv) {
-    __shared__ unsigned long long lds_u[kBlock / 64];
-    if (!P.stats->resampled) return;
-    unsigned long long pages = 0;
+// Received distinct pages into fresh pages and records: received page u takes
+// page freel[base + u], its slot j record rfreel[rbase + 8 u + j]; 8 lanes per
+// page (lane j: slot j), lane 0 describes the page (udesc).
+__global__ __launch_bounds__(kBlock) void k_unpack_pages(const ResampleParams P, int64_t nu) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t g = t / kPageSlots;
+    const int j = (int)(t % kPageSlots);
     float smin = INFINITY;           // smallest positive s received (slb)
-    for (int r = blockIdx.x; r < nrecv; r += gridDim.x) {
-        const int p = peer_of(P, r);
-        const PackHeader &h = P.peers[p].hdr[r - P.peers[p].kbase];
-        const int4 *sm = reinterpret_cast<const int4 *>(P.peers[p].pay + (int64_t)h.soff * 64);
-        const int4 *sf = sm + h.cnt;
-        const uint32_t *ids = P.alloc.freel + P.alloc.base + (int64_t)r * P.map.rows;
-        const uint32_t *rids = P.alloc.rfreel + P.alloc.rbase + P.peers[p].sbase + h.soff;
-        for (int q = threadIdx.x; q < h.cnt; q += kBlock) {
-            int4 m = sm[q];
-            m.w = (int)rids[q];       // the sender's record id, replaced by the local one
-            reinterpret_cast<int4 *>(page_ptr(P.map.pool, ids[q / kPageSlots]))[q % kPageSlots] = m;
+    if (g < nu) {
+        int q = 0;
+        while (q + 1 < P.npeers && g >= P.peers[q + 1].ubase) ++q;
+        const char *blk = P.peers[q].pages + (g - P.peers[q].ubase) * kXferPageBytes;
+        int4 m = reinterpret_cast<const int4 *>(blk)[j];
+        const uint32_t id = P.alloc.freel[P.alloc.base + g];
+        if ((uint32_t)m.w != kNoRec) {
+            const uint32_t rid = P.alloc.rfreel[P.alloc.rbase + g * kPageSlots + j];
+            const int4 *src = reinterpret_cast<const int4 *>(blk + 128 + j * kRecBytes);
+            int4 *dst = reinterpret_cast<int4 *>(P.map.recs + (int64_t)rid * kRecBytes);
+            dst[0] = src[0];
+            dst[1] = src[1];
+            dst[2] = src[2];
+            m.w = (int)rid;
+            const float s = __int_as_float(m.z);
+            smin = s > 0.0f ? s : INFINITY;
         }
-        for (int q = threadIdx.x; q < 3 * h.cnt; q += kBlock) {
-            const int j = q / 3;
-            reinterpret_cast<int4 *>(P.map.recs + (int64_t)rids[j] * kRecBytes)[q - 3 * j] = sf[q];
+        reinterpret_cast<int4 *>(page_ptr(P.map.pool, id))[j] = m;
+        if (j == 0) {
+            const int4 *mm = reinterpret_cast<const int4 *>(blk);
+            int fill = 0;
+            while (fill < kPageSlots && (uint32_t)mm[fill].w != kNoRec) ++fill;
+            P.udesc[g] = describe_page(id, reinterpret_cast<const float4 *>(blk), fill, P.map.frame);
         }
-        __syncthreads();
-        // summaries of the new pages, from the payload's mirrors
-        const float4 *mir = reinterpret_cast<const float4 *>(sm);
-        for (int k = threadIdx.x; k * kPageSlots < h.cnt; k += kBlock)
-            P.rdesc[(int64_t)r * P.map.rows + k] =
-                describe_page(ids[k], mir + k * kPageSlots, min(kPageSlots, h.cnt - k * kPageSlots), P.map.frame);
-        for (int q = threadIdx.x; q < h.cnt; q += kBlock) smin = fminf(smin, mirror_s(mir[q]) > 0.0f ? mirror_s(mir[q]) : INFINITY);
-        if (threadIdx.x == 0) pages += (h.cnt + kPageSlots - 1) / kPageSlots;
     }
-    const unsigned long long b = block_sum_u64<kBlock>(pages, lds_u);
-    if (threadIdx.x == 0 && b) atomicAdd(&P.stats->new_pages, b);
     lower_slb(P.map.slb, smin);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.stats->new_pages, (unsigned long long)nu);
+}
+
+// Page-table rows of the received particles (rdesc [r][rows]) from their entries.
+__global__ __launch_bounds__(kBlock) void k_unpack_rows(const ResampleParams P, int32_t nrecv) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= nrecv) return;
+    const int q = peer_of(P, r);
+    const RecvPeer &pp = P.peers[q];
+    const PackHeader &h = pp.hdr[r - pp.kbase];
+    const int rows = (h.cnt + kPageSlots - 1) / kPageSlots;
+    for (int k = 0; k < rows; ++k) {
+        const uint32_t ent = pp.idx[h.soff + k];
+        Desc d = P.udesc[pp.ubase + (ent & ~kEntryOwned)];
+        d.x = (d.x & kIdMask) | ((ent & kEntryOwned) ? kOwned : 0u);
+        P.rdesc[(int64_t)r * P.map.rows + k] = d;
+    }
 }
 
 // Outputs take their source's scalars and page-table row (fast_slam_2.py:196
 // deepcopy, without copying the map: the pages are shared).  A page stays owned
-// only when its source fills exactly one local output; otherwise every output
-// copies it before its first write.
+// only when its source fills exactly one local output (a received row: as its
+// entry says); otherwise every output copies it before its first write.
 // The output workgroup's row boxes (obbox): an output's page boxes lie inside
 // its source workgroup's row boxes, so the union of the row boxes of the
 // workgroups its local outputs come from holds them (few: systematic resampling
@@ -839,7 +951,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     const int64_t n = P.n;
     int32_t s = 0;
     int rows = 0;                    // rows of this output's map
-    uint32_t keep = 0xffffffffu, own = 0u;
+    uint32_t keep = 0xffffffffu;
     const Desc *src = P.map.pt;      // the source's row 0; row k at src + k * stride
     int64_t stride = 0;
     if (m < n) {
@@ -865,7 +977,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             P.oyaw[m] = h.yaw;
             w = h.w;
             c = h.cnt;
-            own = (h.out_hi == h.out_lo) ? kOwned : 0u;
             src = P.rdesc + (int64_t)r * P.map.rows;
             stride = 1;
         }
@@ -891,7 +1002,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if (k0 + u < rows) {
-                e[u].x = (e[u].x & keep) | own;
+                e[u].x &= keep;
                 P.opt[(int64_t)(k0 + u) * n + m] = e[u];
             }
         }
@@ -1029,10 +1140,17 @@ hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStre
     const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
     if (g == 0) return hipSuccess;
     int32_t nrecv = 0;
-    for (int q = 0; q < p.npeers; ++q) nrecv += p.peers[q].K;
+    int64_t nu = 0;
+    for (int q = 0; q < p.npeers; ++q) {
+        nrecv += p.peers[q].K;
+        nu += p.peers[q].U;
+    }
     if (nrecv > 0) {
         hipLaunchKernelGGL(k_scatter_recv, dim3((nrecv + kBlock - 1) / kBlock), dim3(kBlock), 0, s, p, nrecv);
-        hipLaunchKernelGGL(k_unpack_recv, dim3(min(nrecv, 4096)), dim3(kBlock), 0, s, p, nrecv);
+        if (nu > 0)
+            hipLaunchKernelGGL(k_unpack_pages, dim3((unsigned)((nu * kPageSlots + kBlock - 1) / kBlock)), dim3(kBlock),
+                               0, s, p, nu);
+        hipLaunchKernelGGL(k_unpack_rows, dim3((nrecv + kBlock - 1) / kBlock), dim3(kBlock), 0, s, p, nrecv);
     }
     hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
     if (estimate) hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);

@@ -69,6 +69,9 @@ __device__ unsigned long long g_phase[8];
 #ifndef FS2_SLOT_BAND
 #define FS2_SLOT_BAND 0
 #endif
+#ifndef FS2_PAGE_PRED
+#define FS2_PAGE_PRED 0
+#endif
 #ifndef FS2_COPY_BATCH
 #define FS2_COPY_BATCH 8
 #endif
@@ -232,6 +235,17 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         if (g * kPageSlots < c) ++groups;
         const unsigned om = open_mask(d, g);
         if (!__any(om)) continue;
+#if FS2_PAGE_PRED
+        // only lanes whose page is open load it
+        if (om) {
+            const char *pg = page_ptr(map.pool, d.x);
+            float4 mir[kScanGroup];
+#pragma unroll
+            for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
+            ++opened;
+            test_page(mir, g, om);
+        }
+#else
         const char *pg = page_ptr(map.pool, om ? d.x : 0u);
         float4 mir[kScanGroup];
 #pragma unroll
@@ -240,6 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             ++opened;
             test_page(mir, g, om);
         }
+#endif
     }
     if (live) {
         P.ncand[i] = nc;
