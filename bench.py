@@ -281,6 +281,10 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
             "comm_calls_per_scan": profs[0]["comm_calls"] / k,
             "scan_device_ms": max(p["scan_ms"] / max(p["scans"], 1) for p in profs),
             "scan_ms_each": [round(v, 3) for v in per],
+            "bytes_sent_per_resample": sum(p["sent_bytes"] for p in profs) / max(res[0], 1),
+            "particles_sent_per_resample": sum(p["sent_particles"] for p in profs) / max(res[0], 1),
+            "page_dedup_ratio": (sum(p["sent_rows"] for p in profs) / sum(p["sent_pages"] for p in profs)
+                                 if sum(p["sent_pages"] for p in profs) else None),
             "note": f"{G} ranks as threads on one GPU, in-process transport, {n_total} particles in all; "
                     "comm: host time in transport calls and mid-scan waits (a wait includes the collectives "
                     "queued before it)"}
@@ -366,10 +370,13 @@ def main():
     opened = 0
     ref_visits = 0
     hits_appends = 0
+    step_ms = []                 # (host ms, resampled) of each timed scan on this rank
     barrier()
     t0 = time.perf_counter()
     for s in range(args.warmup, total_scans):
+        t1 = time.perf_counter()
         _, st = one_scan(s)
+        step_ms.append(((time.perf_counter() - t1) * 1e3, st.resampled))
         resamples += st.resampled
         visited += st.slots_visited
         copied_slots += st.resample_slots
@@ -385,6 +392,30 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     prof = f.profile()
+    migration = None
+    if world > 1:
+        # the sharded resample's transfers, summed over the ranks
+        keys = ("migrations", "sent_particles", "sent_rows", "sent_pages", "sent_bytes", "migrate_ms", "comm_ms")
+        mt = torch.tensor([float(prof[k]) for k in keys], dtype=torch.float64, device="cuda")
+        dist.all_reduce(mt, op=dist.ReduceOp.SUM)
+        tot = dict(zip(keys, mt.tolist()))
+        per = max(resamples, 1)
+        rs_ms = sorted(m for m, r in step_ms if r)
+        ot_ms = sorted(m for m, r in step_ms if not r)
+        migration = {
+            "resamples": resamples,
+            "particles_sent_per_resample": tot["sent_particles"] / per,
+            "rows_sent_per_resample": tot["sent_rows"] / per,
+            "pages_sent_per_resample": tot["sent_pages"] / per,
+            "bytes_sent_per_resample": tot["sent_bytes"] / per,
+            "page_dedup_ratio": tot["sent_rows"] / tot["sent_pages"] if tot["sent_pages"] else None,
+            "host_ms_per_resample_rank_mean": tot["migrate_ms"] / world / per,
+            "comm_ms_per_scan_rank_mean": tot["comm_ms"] / world / args.steps,
+            "scan_ms_resample_median_rank0": rs_ms[len(rs_ms) // 2] if rs_ms else None,
+            "scan_ms_other_median_rank0": ot_ms[len(ot_ms) // 2] if ot_ms else None,
+            "note": "every resample moves the particles whose outputs land on another rank's shard, "
+                    "each destination's distinct pages once; Q6/Q8 (sum of weights > 1) shift "
+                    "outputs toward lower global indices, so the flow is mostly rank p -> p+1.."}
     icp_us = None
     if scans_pts is not None:
         # one alignment through the synchronous call, warm (its stream and scratch
@@ -484,6 +515,8 @@ def main():
                       "exact_slots_per_particle_scan": exact_slots / units,
                       "icp_us": icp_us},
         }
+        if migration is not None:
+            out["extra"]["migration"] = migration
         if not args.no_extras and world == 1 and not cfg["icp"]:
             out["extra"]["robustness"] = robustness(args, f, L, total_scans)
         print(json.dumps(out), flush=True)

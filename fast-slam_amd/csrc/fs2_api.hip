@@ -428,6 +428,7 @@ static const int64_t *posted_xmat(const fs2_handle *h) {
 // apply kernels.
 static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     const int G = h->cfg.world_size, R = h->cfg.rank;
+    const auto t_start = std::chrono::steady_clock::now();
     hipStream_t s = h->stream;
     rs.world = G;
     rs.rank = R;
@@ -541,6 +542,23 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     if (rc) return rc;
     h->n_recv = kbase;
     h->u_recv = ubase;
+    if (h->profiling) {
+        uint64_t np = 0, nr = 0, nu = 0, nb = 0;
+        for (int p = 0; p < G; ++p) {
+            if (p == R) continue;
+            np += at(R, p, 0);
+            nr += at(R, p, 1);
+            nu += at(R, p, 2);
+            nb += at(R, p, 0) ? xfer_bytes(at(R, p, 0), at(R, p, 1), at(R, p, 2)) : 0;
+        }
+        h->prof.migrations += np ? 1 : 0;
+        h->prof.sent_particles += np;
+        h->prof.sent_rows += nr;
+        h->prof.sent_pages += nu;
+        h->prof.sent_bytes += nb;
+        h->prof.migrate_ms +=
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
     return FS2_OK;
 }
 
@@ -802,10 +820,16 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     int rc = grow_rows(h, std::max(cfg->landmark_capacity, 1));
     if (rc) return fail(rc);
     // pool: twice the initial maps plus room for a few scans of new pages;
-    // records: the initial maps plus room for many scans of writes
-    rc = grow_pool(h, cfg->page_pool > 0 ? cfg->page_pool : n * h->rows * 2 + 8 * n + 1024);
+    // records: the initial maps plus room for many scans of writes; a sharded
+    // rank also room to receive half its shard's maps without sharing (the first
+    // resamples, before the particles share ancestors), so that no resample
+    // grows a pool (a large hipMalloc and copy: hundreds of ms)
+    const int64_t recv_pages = G > 1 ? n / 2 * h->rows : 0;
+    const int64_t recv_recs = G > 1 ? n / 2 * h->rows * kPageSlots : 0;
+    rc = grow_pool(h, cfg->page_pool > 0 ? cfg->page_pool : n * h->rows * 2 + 8 * n + recv_pages + 1024);
     if (rc) return fail(rc);
-    rc = grow_recs(h, cfg->record_pool > 0 ? cfg->record_pool : n * h->cap + n * h->cap / 4 + 64 * n + 1024);
+    rc = grow_recs(h, cfg->record_pool > 0 ? cfg->record_pool
+                                            : n * h->cap + n * h->cap / 4 + 64 * n + recv_recs + 1024);
     if (rc) return fail(rc);
     h->sendbuf.assign(G, nullptr);
     h->recvbuf.assign(G, nullptr);

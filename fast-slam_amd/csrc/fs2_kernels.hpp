@@ -169,13 +169,13 @@ struct RecvPeer {
 };
 
 // Page dedup of the outgoing transfers: an open-addressing table keyed by
-// fill << 40 | (destination + 1) << 32 | page id (0: empty) with the number of
-// row entries naming each key and its index among the destination's distinct
+// fill << 40 | (destination + 1) << 32 | page id (0: empty), whether more than
+// one row entry names the key, and its index among the destination's distinct
 // pages; every outgoing row entry's table slot (| kEntryOwned when its particle
 // fills one output), destination-major from ebase[p].
 struct XferTable {
     unsigned long long *key;   // [cap]
-    uint32_t *ref;             // [cap]
+    uint32_t *ref;             // [cap] 1: named by more than one row
     uint32_t *uidx;            // [cap]
     uint32_t *eslot;           // [sum S] per row entry
     uint32_t *ulist;           // [sum S] destination p's distinct pages' slots from ebase[p]

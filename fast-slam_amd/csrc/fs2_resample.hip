@@ -733,66 +733,140 @@ __device__ __forceinline__ uint32_t xt_hash(unsigned long long key, int log2cap)
     return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
 }
 
-// Every row of every particle sent: its (destination, page) key into the table
-// (one thread per local particle; the rows' descriptors are coalesced loads).
+// Row k of local particle i as a table key for destination p (0: the particle
+// sends nothing there or has no such row).
+struct DedupRow {
+    unsigned long long key;
+    bool single;             // the particle fills one output of p's shard
+};
+__device__ __forceinline__ DedupRow dedup_row(const ResampleParams &P, int p, int64_t i, int k) {
+    DedupRow r{0ull, false};
+    if (i < 0 || i >= P.n) return r;
+    const PackPlan &pl = P.plan[p];
+    if (i < pl.i0 || i >= pl.i1) return r;
+    const int c = P.cnt[i];
+    if (k * kPageSlots >= c) return r;
+    const int64_t lo = P.mlo[i], hi = P.mhi[i];
+    if (lo > hi) return r;
+    const uint32_t page = pt_entry(P.map, k, i)->x & kIdMask;
+    const unsigned long long fill = (unsigned long long)min(kPageSlots, c - k * kPageSlots);
+    r.key = (fill << 40) | ((unsigned long long)(p + 1) << 32) | page;
+    r.single = max(lo, pl.pa) == min(hi, pl.pb - 1);
+    return r;
+}
+
+__device__ __forceinline__ int64_t dedup_entry(const ResampleParams &P, int p, int64_t i, int k) {
+    return P.xt.ebase[p] + (P.iblk[P.nblk + i / kScanBlock] + P.rank_e[i] + k - P.plan[p].c0);
+}
+
+// Every row of every particle sent: its (destination, page) key into the table,
+// one thread per (particle, row) (grid y: rows; a row's descriptor loads are
+// coalesced over x).  Only the first of a run of neighbours naming the same
+// page inserts (siblings of one resample share every page neither has written
+// since): few atomics, and the followers find the key in k_dedup_follow.  A key
+// named more than once is marked shared (ref).
 __global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= P.n) return;
-    const int64_t lo = P.mlo[i], hi = P.mhi[i];
-    if (lo > hi) return;
-    const int c = P.cnt[i];
-    const int rows = (c + kPageSlots - 1) / kPageSlots;
-    const int64_t cpos = P.iblk[P.nblk + i / kScanBlock] + P.rank_e[i];
+    const int k = blockIdx.y;
     const XferTable &T = P.xt;
     const uint32_t mask = (uint32_t)(T.cap - 1);
     for (int p = 0; p < P.world; ++p) {
-        const PackPlan &pl = P.plan[p];
-        if (p == P.rank || i < pl.i0 || i >= pl.i1) continue;
-        const bool single = max(lo, pl.pa) == min(hi, pl.pb - 1);
-        uint32_t *es = T.eslot + T.ebase[p] + (cpos - pl.c0);
-        for (int k = 0; k < rows; ++k) {
-            const uint32_t page = pt_entry(P.map, k, i)->x & kIdMask;
-            const unsigned long long fill = (unsigned long long)min(kPageSlots, c - k * kPageSlots);
-            const unsigned long long key = (fill << 40) | ((unsigned long long)(p + 1) << 32) | page;
-            uint32_t h = xt_hash(key, T.log2cap);
-            for (;;) {
-                const unsigned long long old = atomicCAS(T.key + h, 0ull, key);
-                if (old == 0ull || old == key) break;
-                h = (h + 1u) & mask;
+        if (p == P.rank) continue;
+        const DedupRow r = dedup_row(P, p, i, k);
+        if (!r.key || dedup_row(P, p, i - 1, k).key == r.key) continue;
+        bool shared = dedup_row(P, p, i + 1, k).key == r.key;
+        uint32_t h = xt_hash(r.key, T.log2cap);
+        for (;;) {
+            const unsigned long long old = atomicCAS(T.key + h, 0ull, r.key);
+            if (old == 0ull) break;
+            if (old == r.key) {
+                shared = true;
+                break;
             }
-            atomicAdd(T.ref + h, 1u);
-            es[k] = h | (single ? kEntryOwned : 0u);
+            h = (h + 1u) & mask;
         }
+        if (shared) T.ref[h] = 1u;
+        T.eslot[dedup_entry(P, p, i, k)] = h | (r.single ? kEntryOwned : 0u);
+    }
+}
+
+// The rows that did not insert: their key's slot (read-only probes; neighbours
+// hit the same line).
+__global__ __launch_bounds__(kBlock) void k_dedup_follow(const ResampleParams P) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int k = blockIdx.y;
+    const XferTable &T = P.xt;
+    const uint32_t mask = (uint32_t)(T.cap - 1);
+    for (int p = 0; p < P.world; ++p) {
+        if (p == P.rank) continue;
+        const DedupRow r = dedup_row(P, p, i, k);
+        if (!r.key || dedup_row(P, p, i - 1, k).key != r.key) continue;
+        uint32_t h = xt_hash(r.key, T.log2cap);
+        while (T.key[h] != r.key) h = (h + 1u) & mask;
+        T.eslot[dedup_entry(P, p, i, k)] = h | (r.single ? kEntryOwned : 0u);
     }
 }
 
 // Index of every distinct page among its destination's (any order: the entries
-// name pages by index), the count into xrow[3 p + 2], the slot into ulist.
+// name pages by index), the count into xrow[3 p + 2], the slot into ulist.  A
+// workgroup takes a contiguous chunk of the table: it counts per destination
+// (ballot per wave, LDS per workgroup), claims each destination's range with one
+// global atomic, then hands out indices in it.
+constexpr int kAssignChunk = 16 * kBlock;
+__device__ __forceinline__ void wave_dest_add(uint32_t *s_cnt, int d, uint32_t &local) {
+    const int lane = threadIdx.x & 63;
+    uint64_t todo = __ballot(d >= 0);
+    while (todo) {
+        const int lead = __builtin_ctzll(todo);
+        const int dd = __shfl(d, lead, 64);
+        const uint64_t m = __ballot(d == dd);
+        uint32_t wb = 0;
+        if (lane == lead) wb = atomicAdd(&s_cnt[dd], (uint32_t)__popcll(m));
+        wb = __shfl(wb, lead, 64);
+        if (d == dd) local = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        todo &= ~m;
+    }
+}
 __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P) {
-    __shared__ uint32_t s_cnt[kMaxRanks], s_base[kMaxRanks];
+    __shared__ uint32_t s_cnt[kMaxRanks], s_run[kMaxRanks], s_base[kMaxRanks];
     const XferTable &T = P.xt;
-    const int64_t h = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (threadIdx.x < kMaxRanks) s_cnt[threadIdx.x] = 0;
+    const int64_t c0 = (int64_t)blockIdx.x * kAssignChunk;
+    const int64_t c1 = min(c0 + kAssignChunk, T.cap);
+    if (threadIdx.x < kMaxRanks) s_cnt[threadIdx.x] = s_run[threadIdx.x] = 0;
     __syncthreads();
-    const unsigned long long key = (h < T.cap) ? T.key[h] : 0ull;
-    const int d = key ? (int)((key >> 32) & 0xffu) - 1 : -1;
-    const uint32_t local = (d >= 0) ? atomicAdd(&s_cnt[d], 1u) : 0u;
+    auto dest = [&](int64_t h) {
+        const unsigned long long key = (h < c1) ? T.key[h] : 0ull;
+        return key ? (int)((key >> 32) & 0xffu) - 1 : -1;
+    };
+    for (int64_t h = c0 + threadIdx.x; h < c0 + kAssignChunk; h += kBlock) {
+        uint32_t dummy = 0;
+        wave_dest_add(s_cnt, dest(h), dummy);
+    }
     __syncthreads();
     if (threadIdx.x < (unsigned)P.world && s_cnt[threadIdx.x])
         s_base[threadIdx.x] = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long *>(P.xrow + 3 * threadIdx.x + 2),
                                                   (unsigned long long)s_cnt[threadIdx.x]);
     __syncthreads();
-    if (d >= 0) {
-        const uint32_t u = s_base[d] + local;
-        T.uidx[h] = u;
-        T.ulist[T.ebase[d] + u] = (uint32_t)h;
+    for (int64_t h = c0 + threadIdx.x; h < c0 + kAssignChunk; h += kBlock) {
+        const int d = dest(h);
+        uint32_t local = 0;
+        wave_dest_add(s_run, d, local);
+        if (d >= 0) {
+            const uint32_t u = s_base[d] + local;
+            T.uidx[h] = u;
+            T.ulist[T.ebase[d] + u] = (uint32_t)h;
+        }
     }
 }
 
 hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s) {
     const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
-    if (g) hipLaunchKernelGGL(k_dedup_insert, dim3(g), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(k_dedup_assign, dim3((unsigned)((p.xt.cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p);
+    if (g && p.map.rows > 0) {
+        hipLaunchKernelGGL(k_dedup_insert, dim3(g, (unsigned)p.map.rows), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL(k_dedup_follow, dim3(g, (unsigned)p.map.rows), dim3(kBlock), 0, s, p);
+    }
+    hipLaunchKernelGGL(k_dedup_assign, dim3((unsigned)((p.xt.cap + kAssignChunk - 1) / kAssignChunk)), dim3(kBlock), 0,
+                       s, p);
     return hipGetLastError();
 }
 
@@ -811,7 +885,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_index(const ResampleParams P, i
     const int p = dest_of(T.ebase, P.world, e);
     const uint32_t es = T.eslot[e];
     const uint32_t h = es & ~kEntryOwned;
-    const bool own = (es & kEntryOwned) && T.ref[h] == 1u;
+    const bool own = (es & kEntryOwned) && T.ref[h] == 0u;
     reinterpret_cast<uint32_t *>(P.sbuf[p] + xfer_idx_off(P.plan[p].K))[e - T.ebase[p]] =
         T.uidx[h] | (own ? kEntryOwned : 0u);
 }
@@ -907,15 +981,18 @@ __global__ __launch_bounds__(kBlock) void k_unpack_pages(const ResampleParams P,
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.stats->new_pages, (unsigned long long)nu);
 }
 
-// Page-table rows of the received particles (rdesc [r][rows]) from their entries.
+// Page-table rows of the received particles (rdesc [r][rows]) from their
+// entries: one wave per received particle, lanes over its rows (coalesced entry
+// reads and descriptor writes).
 __global__ __launch_bounds__(kBlock) void k_unpack_rows(const ResampleParams P, int32_t nrecv) {
-    const int r = blockIdx.x * kBlock + threadIdx.x;
+    const int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (r >= nrecv) return;
     const int q = peer_of(P, r);
     const RecvPeer &pp = P.peers[q];
     const PackHeader &h = pp.hdr[r - pp.kbase];
     const int rows = (h.cnt + kPageSlots - 1) / kPageSlots;
-    for (int k = 0; k < rows; ++k) {
+    for (int k = lane; k < rows; k += 64) {
         const uint32_t ent = pp.idx[h.soff + k];
         Desc d = P.udesc[pp.ubase + (ent & ~kEntryOwned)];
         d.x = (d.x & kIdMask) | ((ent & kEntryOwned) ? kOwned : 0u);
@@ -1150,7 +1227,7 @@ hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStre
         if (nu > 0)
             hipLaunchKernelGGL(k_unpack_pages, dim3((unsigned)((nu * kPageSlots + kBlock - 1) / kBlock)), dim3(kBlock),
                                0, s, p, nu);
-        hipLaunchKernelGGL(k_unpack_rows, dim3((nrecv + kBlock - 1) / kBlock), dim3(kBlock), 0, s, p, nrecv);
+        hipLaunchKernelGGL(k_unpack_rows, dim3((nrecv + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, s, p, nrecv);
     }
     hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
     if (estimate) hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);

@@ -103,6 +103,12 @@ class fs2_profile(C.Structure):
         ("exact_ms", C.c_double),
         ("comm_calls", C.c_int64),
         ("comm_ms", C.c_double),
+        ("migrations", C.c_int64),
+        ("sent_particles", C.c_uint64),
+        ("sent_rows", C.c_uint64),
+        ("sent_pages", C.c_uint64),
+        ("sent_bytes", C.c_uint64),
+        ("migrate_ms", C.c_double),
     ]
 
     def as_dict(self):

@@ -140,6 +140,12 @@ typedef struct fs2_profile {
     int64_t comm_calls;         /* sharded: transport calls and mid-scan waits timed */
     double comm_ms;             /* their summed host wall time (a mid-scan wait includes the
                                    collectives queued before it on the stream) */
+    int64_t migrations;         /* sharded: resamples whose plan sent particles to other ranks */
+    uint64_t sent_particles;    /* particles sent (one per source and destination) */
+    uint64_t sent_rows;         /* their page-table rows */
+    uint64_t sent_pages;        /* distinct pages those rows name (sent once per destination) */
+    uint64_t sent_bytes;        /* transfer bytes (headers, row entries, pages with their records) */
+    double migrate_ms;          /* host wall time from the plan to the end of the exchange */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */
