@@ -97,7 +97,8 @@ struct fs2_handle {
     size_t udesc_cap = 0;
     // page dedup of the outgoing transfers (XferTable)
     unsigned long long *xt_key = nullptr;
-    uint32_t *xt_ref = nullptr, *xt_uidx = nullptr, *xt_eslot = nullptr, *xt_ulist = nullptr;
+    uint32_t *xt_ref = nullptr, *xt_uidx = nullptr, *xt_cmask = nullptr, *xt_cbase = nullptr;
+    uint32_t *xt_eslot = nullptr, *xt_ulist = nullptr;
     int64_t xt_cap = 0, xt_ecap = 0;
     SumFrame frame{-127.0f, 1.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
     float ext_seen = 0.0f;                 // largest |x|, |y| imported so far
@@ -159,7 +160,7 @@ struct fs2_handle {
     fs2comm::Transport *tp = nullptr;
     RankRecord *rec = nullptr, *recs = nullptr;     // this rank's record / all ranks'
     double *totals = nullptr;                       // all ranks' weight totals
-    int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (particles, rows, pages) per peer
+    int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (particles, rows, pages, covariances) per peer
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr;
     uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
@@ -411,7 +412,7 @@ static int post_and_wait(fs2_handle *h, bool sizes) {
     CommTimer ct(h);
     const int G = h->cfg.world_size;
     const unsigned long long seq = ++h->post_seq;
-    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? 3 * G * G : 0, h->post, h->post_flag_dev,
+    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? 4 * G * G : 0, h->post, h->post_flag_dev,
                            seq, h->stream));
     return wait_seq(h, h->post_flag, seq, "mid-scan statistics");
 }
@@ -432,6 +433,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     hipStream_t s = h->stream;
     rs.world = G;
     rs.rank = R;
+    std::memcpy(rs.init_cov, h->cfg.init_landmark_cov, sizeof rs.init_cov);
     rs.plan = h->plan;
     rs.xrow = h->xrow;
     HIP_TRY(h, launch_pack_count(rs, s));
@@ -439,15 +441,15 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     auto gather_sizes = [&]() -> int {
         {
             CommTimer ct(h);
-            const int r = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 3 * G, s, &h->err);
+            const int r = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 4 * G, s, &h->err);
             if (r) return r;
         }
         return post_and_wait(h, true);
     };
     rc = gather_sizes();
     if (rc) return rc;
-    std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + 3 * G * G);
-    auto at = [&](int from, int to, int f) { return mat[(size_t)from * 3 * G + 3 * to + f]; };
+    std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + 4 * G * G);
+    auto at = [&](int from, int to, int f) { return mat[(size_t)from * 4 * G + 4 * to + f]; };
     // distinct pages of the rows sent (every rank takes part in the all-gather)
     XferTable &T = rs.xt;
     T = XferTable{};
@@ -460,12 +462,15 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         const int64_t cap = int64_t(1) << lg;
         if (h->xt_cap < cap) {
             HIP_TRY(h, hipStreamSynchronize(s));
-            hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx);
-            h->xt_key = nullptr; h->xt_ref = h->xt_uidx = nullptr;
+            hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
+            h->xt_key = nullptr;
+            h->xt_ref = h->xt_uidx = h->xt_cmask = h->xt_cbase = nullptr;
             h->xt_cap = 0;
             HIP_TRY(h, hipMalloc((void **)&h->xt_key, (size_t)cap * 8));
             HIP_TRY(h, hipMalloc((void **)&h->xt_ref, (size_t)cap * 4));
             HIP_TRY(h, hipMalloc((void **)&h->xt_uidx, (size_t)cap * 4));
+            HIP_TRY(h, hipMalloc((void **)&h->xt_cmask, (size_t)cap * 4));
+            HIP_TRY(h, hipMalloc((void **)&h->xt_cbase, (size_t)cap * 4));
             h->xt_cap = cap;
         }
         if (h->xt_ecap < nrows) {
@@ -481,6 +486,8 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         T.key = h->xt_key;
         T.ref = h->xt_ref;
         T.uidx = h->xt_uidx;
+        T.cmask = h->xt_cmask;
+        T.cbase = h->xt_cbase;
         T.eslot = h->xt_eslot;
         T.ulist = h->xt_ulist;
         T.cap = cap;
@@ -491,20 +498,22 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     }
     rc = gather_sizes();
     if (rc) return rc;
-    mat.assign(posted_xmat(h), posted_xmat(h) + 3 * G * G);
+    mat.assign(posted_xmat(h), posted_xmat(h) + 4 * G * G);
     static const bool log_xfer = std::getenv("FS2_XFER_LOG") != nullptr;
     int64_t nsend = 0;
     std::vector<fs2comm::Xfer> sends, recvs;
     for (int p = 0; p < G; ++p) {
         rs.sbuf[p] = nullptr;
         T.ubase[p + 1] = T.ubase[p] + (p == R ? 0 : at(R, p, 2));
-        const int64_t K = at(R, p, 0), S = at(R, p, 1), U = at(R, p, 2);
+        const int64_t K = at(R, p, 0), S = at(R, p, 1), U = at(R, p, 2), C = at(R, p, 3);
         if (log_xfer && p != R)
-            std::fprintf(stderr, "fs2 xfer scan %lld rank %d -> %d: %lld particles, %lld rows, %lld pages, %lld B\n",
-                         (long long)h->scan, R, p, (long long)K, (long long)S, (long long)U,
-                         (long long)xfer_bytes(K, S, U));
+            std::fprintf(stderr,
+                         "fs2 xfer scan %lld rank %d -> %d: %lld particles, %lld rows, %lld pages, %lld covariances, "
+                         "%lld B\n",
+                         (long long)h->scan, R, p, (long long)K, (long long)S, (long long)U, (long long)C,
+                         (long long)xfer_bytes(K, S, U, C));
         if (p == R || K == 0) continue;
-        const size_t bytes = (size_t)xfer_bytes(K, S, U);
+        const size_t bytes = (size_t)xfer_bytes(K, S, U, C);
         rc = ensure_buf(h, h->sendbuf, h->sendcap, p, bytes);
         if (rc) return rc;
         rs.sbuf[p] = h->sendbuf[p];
@@ -518,16 +527,17 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     int64_t ubase = 0;
     for (int q = 0; q < G; ++q) {
         if (q == R) continue;
-        const int64_t K = at(q, R, 0), S = at(q, R, 1), U = at(q, R, 2);
+        const int64_t K = at(q, R, 0), S = at(q, R, 1), U = at(q, R, 2), C = at(q, R, 3);
         if (!K) continue;
-        const size_t bytes = (size_t)xfer_bytes(K, S, U);
+        const size_t bytes = (size_t)xfer_bytes(K, S, U, C);
         rc = ensure_buf(h, h->recvbuf, h->recvcap, q, bytes);
         if (rc) return rc;
         recvs.push_back({q, h->recvbuf[q], bytes});
         RecvPeer &pp = rs.peers[rs.npeers++];
         pp.hdr = reinterpret_cast<const PackHeader *>(h->recvbuf[q]);
         pp.idx = reinterpret_cast<const uint32_t *>(h->recvbuf[q] + xfer_idx_off(K));
-        pp.pages = h->recvbuf[q] + xfer_page_off(K, S);
+        pp.pages = reinterpret_cast<const XferPage *>(h->recvbuf[q] + xfer_page_off(K, S));
+        pp.covs = reinterpret_cast<const double2 *>(h->recvbuf[q] + xfer_cov_off(K, S, U));
         pp.K = (int32_t)K;
         pp.kbase = kbase;
         pp.U = U;
@@ -549,7 +559,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
             np += at(R, p, 0);
             nr += at(R, p, 1);
             nu += at(R, p, 2);
-            nb += at(R, p, 0) ? xfer_bytes(at(R, p, 0), at(R, p, 1), at(R, p, 2)) : 0;
+            nb += at(R, p, 0) ? xfer_bytes(at(R, p, 0), at(R, p, 1), at(R, p, 2), at(R, p, 3)) : 0;
         }
         h->prof.migrations += np ? 1 : 0;
         h->prof.sent_particles += np;
@@ -642,7 +652,8 @@ static void free_handle(fs2_handle *h) {
         hipFree(h->bbox[s]);
     }
     hipFree(h->rdesc); hipFree(h->udesc);
-    hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_eslot); hipFree(h->xt_ulist);
+    hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
+    hipFree(h->xt_eslot); hipFree(h->xt_ulist);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->ext_dev);
@@ -731,8 +742,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
     ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
     ok &= alloc((void **)&h->totals, sizeof(double) * G) == hipSuccess;
-    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * 3 * G) == hipSuccess;
-    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 3 * G * G) == hipSuccess;
+    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * 4 * G) == hipSuccess;
+    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 4 * G * G) == hipSuccess;
     ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
@@ -769,8 +780,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
     {
-        // post block: DevStats, xmat (3 G x G words), then the flag on its own line
-        const size_t body = sizeof(DevStats) + sizeof(int64_t) * 3 * kMaxRanks * kMaxRanks;
+        // post block: DevStats, xmat (4 G x G words), then the flag on its own line
+        const size_t body = sizeof(DevStats) + sizeof(int64_t) * 4 * kMaxRanks * kMaxRanks;
         const size_t off = ((body + 63) / 64) * 64;
         ok &= hipHostMalloc((void **)&h->post_host, off + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
               hipSuccess;

@@ -121,19 +121,34 @@ struct RankRecord {
 
 // A transfer to one rank (fs2_resample.hip, "packing"): K particle headers (64 B
 // each), then one 32-bit entry per page-table row of each particle (S rows,
-// padded to 64 B), then the U distinct pages those rows name, kXferPageBytes
-// each: the 8 gate mirrors (a slot past the page's fill has rec = kNoRec) and
-// the 8 slots' fp64 records.  Particles that descend from one ancestor share
-// most pages, so U is far below S.  Entry = unique page index | kEntryOwned
-// when the receiver may own the page (named once, by a particle that fills
-// one output).
-constexpr int kXferPageBytes = 128 + kPageSlots * kRecBytes;   // 512
-constexpr uint32_t kNoRec = 0xffffffffu;
+// padded to 64 B), then the U distinct pages those rows name, then C
+// covariances.  Particles that descend from one ancestor share most pages, so U
+// is far below S.  Entry = unique page index | kEntryOwned when the receiver may
+// own the page (named once, by a particle filling one output).  A page travels
+// compact (XferPage, 160 B): its slots' fp64 means and map indices; a slot's
+// covariance only when it differs from the configured initial one (most
+// landmarks keep it: appended with it, and only the observed ones change), the
+// receiver rebuilding records and gate mirrors (mirror_of, a pure function of
+// the record) bit for bit.
+struct XferPage {
+    uint32_t cbase;          // index of its first covariance among the transfer's
+    uint8_t fill;            // slots in use
+    uint8_t cmask;           // bit j: slot j's covariance follows in the covariance section
+    uint16_t pad0;
+    uint16_t slot[8];        // map index of each slot (the mirror's slot bits)
+    uint64_t pad1;
+    double2 xy[8];           // means
+};
+static_assert(sizeof(XferPage) == 160, "XferPage layout");
+constexpr int kXferCovBytes = 32;
 constexpr uint32_t kEntryOwned = 0x80000000u;
 __host__ __device__ inline int64_t xfer_idx_off(int64_t K) { return K * 64; }
 __host__ __device__ inline int64_t xfer_page_off(int64_t K, int64_t S) { return K * 64 + ((S * 4 + 63) / 64) * 64; }
-__host__ __device__ inline int64_t xfer_bytes(int64_t K, int64_t S, int64_t U) {
-    return xfer_page_off(K, S) + U * kXferPageBytes;
+__host__ __device__ inline int64_t xfer_cov_off(int64_t K, int64_t S, int64_t U) {
+    return xfer_page_off(K, S) + U * (int64_t)sizeof(XferPage);
+}
+__host__ __device__ inline int64_t xfer_bytes(int64_t K, int64_t S, int64_t U, int64_t C) {
+    return xfer_cov_off(K, S, U) + C * kXferCovBytes;
 }
 
 struct PackHeader {
@@ -161,7 +176,8 @@ struct PackPlan {
 struct RecvPeer {
     const PackHeader *hdr;   // K headers
     const uint32_t *idx;     // row entries
-    const char *pages;       // U distinct pages
+    const XferPage *pages;   // U distinct pages
+    const double2 *covs;     // their covariances that differ from the initial one (2 per)
     int32_t K;               // particles from this peer
     int32_t kbase;           // index of its first particle among all received
     int64_t U;               // distinct pages from this peer
@@ -170,13 +186,16 @@ struct RecvPeer {
 
 // Page dedup of the outgoing transfers: an open-addressing table keyed by
 // fill << 40 | (destination + 1) << 32 | page id (0: empty), whether more than
-// one row entry names the key, and its index among the destination's distinct
-// pages; every outgoing row entry's table slot (| kEntryOwned when its particle
-// fills one output), destination-major from ebase[p].
+// one row entry names the key, its index among the destination's distinct
+// pages, its covariance mask and the index of its first covariance; every
+// outgoing row entry's table slot (| kEntryOwned when its particle fills one
+// output), destination-major from ebase[p].
 struct XferTable {
     unsigned long long *key;   // [cap]
     uint32_t *ref;             // [cap] 1: named by more than one row
     uint32_t *uidx;            // [cap]
+    uint32_t *cmask;           // [cap] slots whose covariance is not the initial one
+    uint32_t *cbase;           // [cap] index of the page's first covariance (destination's)
     uint32_t *eslot;           // [sum S] per row entry
     uint32_t *ulist;           // [sum S] destination p's distinct pages' slots from ebase[p]
     int64_t cap;               // power of two
@@ -326,9 +345,10 @@ struct ResampleParams {
     // packing for the other ranks (k_pack_plan / k_pack_bounds / k_pack_*)
     int32_t world, rank;
     PackPlan *plan;          // [world] per destination
-    int64_t *xrow;           // [3 world] particles, rows, distinct pages sent to each rank
+    int64_t *xrow;           // [4 world] particles, rows, distinct pages, covariances sent to each rank
     char *sbuf[kMaxRanks];   // per destination: the transfer (xfer_bytes)
     XferTable xt;
+    double init_cov[4];      // the configured initial landmark covariance (compact transfers)
     // received particles
     int32_t npeers;
     RecvPeer peers[kMaxRanks];
@@ -406,7 +426,8 @@ hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s);
 hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
 // the distinct pages of every destination's rows (xt sized for sum S, key and
-// ref zeroed by the caller), counted into xrow[3 p + 2]
+// ref zeroed by the caller), counted into xrow[4 p + 2], their covariances
+// into xrow[4 p + 3]
 hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s);
 // headers, row entries and pages into sbuf (sizes from the all-gathered xrow)
 hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s);

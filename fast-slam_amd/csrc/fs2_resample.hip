@@ -690,9 +690,10 @@ __global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
         pl.pb = pb;
     }
     P.plan[p] = pl;
-    P.xrow[3 * p] = pl.K;
-    P.xrow[3 * p + 1] = pl.S;
-    P.xrow[3 * p + 2] = 0;   // distinct pages: k_dedup_assign
+    P.xrow[4 * p] = pl.K;
+    P.xrow[4 * p + 1] = pl.S;
+    P.xrow[4 * p + 2] = 0;   // distinct pages, covariances: k_dedup_assign
+    P.xrow[4 * p + 3] = 0;
 }
 
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s) {
@@ -808,10 +809,11 @@ __global__ __launch_bounds__(kBlock) void k_dedup_follow(const ResampleParams P)
 }
 
 // Index of every distinct page among its destination's (any order: the entries
-// name pages by index), the count into xrow[3 p + 2], the slot into ulist.  A
-// workgroup takes a contiguous chunk of the table: it counts per destination
-// (ballot per wave, LDS per workgroup), claims each destination's range with one
-// global atomic, then hands out indices in it.
+// name pages by index) and of its first covariance, the counts into
+// xrow[4 p + 2] / [4 p + 3], the slot into ulist.  A workgroup takes a
+// contiguous chunk of the table: it counts per destination (ballot per wave,
+// LDS per workgroup), claims each destination's ranges with one global atomic
+// each, then hands out indices in them.
 constexpr int kAssignChunk = 16 * kBlock;
 __device__ __forceinline__ void wave_dest_add(uint32_t *s_cnt, int d, uint32_t &local) {
     const int lane = threadIdx.x & 63;
@@ -827,25 +829,52 @@ __device__ __forceinline__ void wave_dest_add(uint32_t *s_cnt, int d, uint32_t &
         todo &= ~m;
     }
 }
+__device__ __forceinline__ bool same_bits(double a, double b) {
+    return __double_as_longlong(a) == __double_as_longlong(b);
+}
+// slots of a page whose covariance is not the initial one
+__device__ __forceinline__ uint32_t page_cov_mask(const ResampleParams &P, uint32_t page, int fill) {
+    uint32_t mask = 0;
+    for (int j = 0; j < fill; ++j) {
+        const float4 m = load_mirror(page_ptr(P.map.pool, page), j);
+        const double2 *r = reinterpret_cast<const double2 *>(P.map.recs + (int64_t)mirror_rec(m) * kRecBytes);
+        const double2 b = r[1], c = r[2];
+        if (!(same_bits(b.x, P.init_cov[0]) && same_bits(b.y, P.init_cov[1]) && same_bits(c.x, P.init_cov[2]) &&
+              same_bits(c.y, P.init_cov[3])))
+            mask |= 1u << j;
+    }
+    return mask;
+}
 __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P) {
     __shared__ uint32_t s_cnt[kMaxRanks], s_run[kMaxRanks], s_base[kMaxRanks];
+    __shared__ uint32_t s_ccnt[kMaxRanks], s_crun[kMaxRanks], s_cbase[kMaxRanks];
     const XferTable &T = P.xt;
     const int64_t c0 = (int64_t)blockIdx.x * kAssignChunk;
     const int64_t c1 = min(c0 + kAssignChunk, T.cap);
-    if (threadIdx.x < kMaxRanks) s_cnt[threadIdx.x] = s_run[threadIdx.x] = 0;
+    if (threadIdx.x < kMaxRanks) s_cnt[threadIdx.x] = s_run[threadIdx.x] = s_ccnt[threadIdx.x] = s_crun[threadIdx.x] = 0;
     __syncthreads();
     auto dest = [&](int64_t h) {
         const unsigned long long key = (h < c1) ? T.key[h] : 0ull;
         return key ? (int)((key >> 32) & 0xffu) - 1 : -1;
     };
     for (int64_t h = c0 + threadIdx.x; h < c0 + kAssignChunk; h += kBlock) {
+        const int d = dest(h);
         uint32_t dummy = 0;
-        wave_dest_add(s_cnt, dest(h), dummy);
+        wave_dest_add(s_cnt, d, dummy);
+        if (d >= 0) {
+            const unsigned long long key = T.key[h];
+            const uint32_t mask = page_cov_mask(P, (uint32_t)(key & 0xffffffffu), (int)((key >> 40) & 0xfu));
+            T.cmask[h] = mask;
+            if (mask) atomicAdd(&s_ccnt[d], (uint32_t)__popc(mask));
+        }
     }
     __syncthreads();
-    if (threadIdx.x < (unsigned)P.world && s_cnt[threadIdx.x])
-        s_base[threadIdx.x] = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long *>(P.xrow + 3 * threadIdx.x + 2),
-                                                  (unsigned long long)s_cnt[threadIdx.x]);
+    if (threadIdx.x < (unsigned)P.world) {
+        unsigned long long *row = reinterpret_cast<unsigned long long *>(P.xrow + 4 * threadIdx.x);
+        if (s_cnt[threadIdx.x]) s_base[threadIdx.x] = (uint32_t)atomicAdd(row + 2, (unsigned long long)s_cnt[threadIdx.x]);
+        if (s_ccnt[threadIdx.x])
+            s_cbase[threadIdx.x] = (uint32_t)atomicAdd(row + 3, (unsigned long long)s_ccnt[threadIdx.x]);
+    }
     __syncthreads();
     for (int64_t h = c0 + threadIdx.x; h < c0 + kAssignChunk; h += kBlock) {
         const int d = dest(h);
@@ -853,7 +882,9 @@ __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P)
         wave_dest_add(s_run, d, local);
         if (d >= 0) {
             const uint32_t u = s_base[d] + local;
+            const uint32_t mask = T.cmask[h];
             T.uidx[h] = u;
+            T.cbase[h] = mask ? s_cbase[d] + atomicAdd(&s_crun[d], (uint32_t)__popc(mask)) : 0u;
             T.ulist[T.ebase[d] + u] = (uint32_t)h;
         }
     }
@@ -890,7 +921,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_index(const ResampleParams P, i
         T.uidx[h] | (own ? kEntryOwned : 0u);
 }
 
-// Distinct pages: mirrors and records, 8 lanes per page (lane j: slot j).
+// Distinct pages, compact (XferPage): 8 lanes per page, lane j slot j's mean,
+// map index and, when it is not the initial one, covariance.
 __global__ __launch_bounds__(kBlock) void k_pack_pages(const ResampleParams P, int64_t total) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t g = t / kPageSlots;
@@ -899,20 +931,36 @@ __global__ __launch_bounds__(kBlock) void k_pack_pages(const ResampleParams P, i
     const XferTable &T = P.xt;
     const int p = dest_of(T.ubase, P.world, g);
     const int64_t u = g - T.ubase[p];
-    const unsigned long long key = T.key[T.ulist[T.ebase[p] + u]];
+    const uint32_t h = T.ulist[T.ebase[p] + u];
+    const unsigned long long key = T.key[h];
     const uint32_t page = (uint32_t)(key & 0xffffffffu);
     const int fill = (int)((key >> 40) & 0xfu);
-    char *blk = P.sbuf[p] + xfer_page_off(P.plan[p].K, P.plan[p].S) + u * kXferPageBytes;
-    int4 m = make_int4(0, 0, 0, (int)kNoRec);
-    if (j < fill) {
-        m = reinterpret_cast<const int4 *>(page_ptr(P.map.pool, page))[j];
-        const int4 *src = reinterpret_cast<const int4 *>(P.map.recs + (int64_t)(uint32_t)m.w * kRecBytes);
-        int4 *dst = reinterpret_cast<int4 *>(blk + 128 + j * kRecBytes);
-        dst[0] = src[0];
-        dst[1] = src[1];
-        dst[2] = src[2];
+    const uint32_t mask = T.cmask[h], cb = T.cbase[h];
+    const PackPlan &pl = P.plan[p];
+    XferPage *xp = reinterpret_cast<XferPage *>(P.sbuf[p] + xfer_page_off(pl.K, pl.S)) + u;
+    if (j == 0) {
+        xp->cbase = cb;
+        xp->fill = (uint8_t)fill;
+        xp->cmask = (uint8_t)mask;
+        xp->pad0 = 0;
+        xp->pad1 = 0;
     }
-    reinterpret_cast<int4 *>(blk)[j] = m;
+    uint16_t slot = 0;
+    double2 xy = make_double2(0.0, 0.0);
+    if (j < fill) {
+        const float4 m = load_mirror(page_ptr(P.map.pool, page), j);
+        const double2 *r = reinterpret_cast<const double2 *>(P.map.recs + (int64_t)mirror_rec(m) * kRecBytes);
+        slot = (uint16_t)mirror_slot(m);
+        xy = r[0];
+        if ((mask >> j) & 1u) {
+            double2 *cv = reinterpret_cast<double2 *>(P.sbuf[p] + xfer_cov_off(pl.K, pl.S, T.ubase[p + 1] - T.ubase[p])) +
+                          2 * (int64_t)(cb + (uint32_t)__popc(mask & ((1u << j) - 1u)));
+            cv[0] = r[1];
+            cv[1] = r[2];
+        }
+    }
+    xp->slot[j] = slot;
+    xp->xy[j] = xy;
 }
 
 hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s) {
@@ -945,37 +993,65 @@ __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P,
 }
 
 // Received distinct pages into fresh pages and records: received page u takes
-// page freel[base + u], its slot j record rfreel[rbase + 8 u + j]; 8 lanes per
-// page (lane j: slot j), lane 0 describes the page (udesc).
+// page freel[base + u], its slot j record rfreel[rbase + 8 u + j].  8 lanes per
+// page (lane j: slot j) rebuild the records (the initial covariance where the
+// page's mask says so) and the gate mirrors (mirror_of, the sender's own
+// function of the record); the page's descriptor from 8-lane reductions (the
+// same box as describe_page).
 __global__ __launch_bounds__(kBlock) void k_unpack_pages(const ResampleParams P, int64_t nu) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t g = t / kPageSlots;
+    const int64_t g = min(t / kPageSlots, max(nu - 1, (int64_t)0));
     const int j = (int)(t % kPageSlots);
+    const bool live = t / kPageSlots < nu;
     float smin = INFINITY;           // smallest positive s received (slb)
-    if (g < nu) {
-        int q = 0;
-        while (q + 1 < P.npeers && g >= P.peers[q + 1].ubase) ++q;
-        const char *blk = P.peers[q].pages + (g - P.peers[q].ubase) * kXferPageBytes;
-        int4 m = reinterpret_cast<const int4 *>(blk)[j];
-        const uint32_t id = P.alloc.freel[P.alloc.base + g];
-        if ((uint32_t)m.w != kNoRec) {
-            const uint32_t rid = P.alloc.rfreel[P.alloc.rbase + g * kPageSlots + j];
-            const int4 *src = reinterpret_cast<const int4 *>(blk + 128 + j * kRecBytes);
-            int4 *dst = reinterpret_cast<int4 *>(P.map.recs + (int64_t)rid * kRecBytes);
-            dst[0] = src[0];
-            dst[1] = src[1];
-            dst[2] = src[2];
-            m.w = (int)rid;
-            const float s = __int_as_float(m.z);
-            smin = s > 0.0f ? s : INFINITY;
+    int q = 0;
+    while (q + 1 < P.npeers && g >= P.peers[q + 1].ubase) ++q;
+    const XferPage *xp = P.peers[q].pages + (g - P.peers[q].ubase);
+    const int fill = xp->fill;
+    const uint32_t mask = xp->cmask;
+    const uint32_t id = P.alloc.freel[P.alloc.base + g];
+    float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY, bs = INFINITY;
+    bool finite = true;
+    if (live && j < fill) {
+        const double2 xy = xp->xy[j];
+        Slot sl{xy.x, xy.y, M2{P.init_cov[0], P.init_cov[1], P.init_cov[2], P.init_cov[3]}};
+        if ((mask >> j) & 1u) {
+            const double2 *cv = P.peers[q].covs + 2 * (int64_t)(xp->cbase + (uint32_t)__popc(mask & ((1u << j) - 1u)));
+            const double2 b = cv[0], c = cv[1];
+            sl.P = M2{b.x, b.y, c.x, c.y};
         }
-        reinterpret_cast<int4 *>(page_ptr(P.map.pool, id))[j] = m;
-        if (j == 0) {
-            const int4 *mm = reinterpret_cast<const int4 *>(blk);
-            int fill = 0;
-            while (fill < kPageSlots && (uint32_t)mm[fill].w != kNoRec) ++fill;
-            P.udesc[g] = describe_page(id, reinterpret_cast<const float4 *>(blk), fill, P.map.frame);
-        }
+        const uint32_t rid = P.alloc.rfreel[P.alloc.rbase + g * kPageSlots + j];
+        store_rec(P.map.recs, rid, sl);
+        float4 mv = with_slot(mirror_of(sl), xp->slot[j]);
+        mv.w = __uint_as_float(rid);
+        reinterpret_cast<float4 *>(page_ptr(P.map.pool, id))[j] = mv;
+        const float s = mirror_s(mv);
+        smin = s > 0.0f ? s : INFINITY;
+        finite = isfinite(mv.x) && isfinite(mv.y);
+        bx0 = fminf(INFINITY, mv.x);
+        bx1 = fmaxf(-INFINITY, mv.x);
+        by0 = fminf(INFINITY, mv.y);
+        by1 = fmaxf(-INFINITY, mv.y);
+        bs = fminf(INFINITY, s);
+    }
+#pragma unroll
+    for (int o = 1; o < kPageSlots; o <<= 1) {
+        bx0 = fminf(bx0, __shfl_xor(bx0, o, 64));
+        bx1 = fmaxf(bx1, __shfl_xor(bx1, o, 64));
+        by0 = fminf(by0, __shfl_xor(by0, o, 64));
+        by1 = fmaxf(by1, __shfl_xor(by1, o, 64));
+        bs = fminf(bs, __shfl_xor(bs, o, 64));
+        finite = finite && (__shfl_xor((int)finite, o, 64) != 0);
+    }
+    if (live && j == 0) {
+        Desc d;
+        d.x = id;
+        if (!(finite && fill > 0) || !(bs > 0.0f))
+            d.y = kSumOpen;
+        else
+            d.y = sum_lo(P.map.frame, bx0) | (sum_hi(P.map.frame, bx1) << 8) | (sum_lo(P.map.frame, by0) << 16) |
+                  (sum_hi(P.map.frame, by1) << 24);
+        P.udesc[g] = d;
     }
     lower_slb(P.map.slb, smin);
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.stats->new_pages, (unsigned long long)nu);
