@@ -79,6 +79,19 @@ class FastSLAM2:
         self.first_global = int(first.value)
         self._particles = None
         self.last_stats = None
+        # step(): fs2_iterate through a prototype of plain addresses and buffers
+        # made once (ndarray.ctypes conversions cost ~3 us each, a scan ~500 us)
+        proto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_double, C.c_double, C.c_void_p, C.c_void_p, C.c_int32,
+                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
+        self._iterate_raw = proto(C.cast(lib.fs2_iterate, C.c_void_p).value)
+        self._hv = h.value
+        self._mcap = 0
+        self._pose = np.empty(3)
+        self._pose_addr = self._pose.ctypes.data
+        self._st = nat.fs2_iter_stats()
+        self._st_addr = C.addressof(self._st)
+        self._u0 = np.empty(1)
+        self._u0_addr = self._u0.ctypes.data
 
     # ------------------------------------------------------------------ core
     def iterate(self, rotation: float, translation: float,
@@ -120,23 +133,36 @@ class FastSLAM2:
         """iterate() with explicit inputs: meas [M][2] (distance, yaw); observed [M][2]
         robot-frame points (None: computed in libfs2); noise [N_local] motion draws and
         u0 the resample start (None: Philox on the device).  Returns (pose, stats)."""
-        meas = nat.f64(meas, (-1, 2))
-        M = len(meas)
-        obs = None if observed is None else nat.f64(observed, (-1, 2))
-        nz = None if noise is None else nat.f64(noise)
-        if nz is not None and nz.size != self.n_local:
-            raise ValueError(f"noise must have {self.n_local} values")
-        u = None if u0 is None else np.array([float(u0)])
-        pose = np.empty(3)
-        st = nat.fs2_iter_stats()
-        rc = self._lib.fs2_iterate(self._h, float(rotation), float(translation),
-                                   nat.ptr(meas) if M else None,
-                                   nat.ptr(obs) if (M and obs is not None) else None, M,
-                                   nat.ptr(nz), nat.ptr(u), nat.dptr(pose), C.byref(st))
+        meas = np.asarray(meas, dtype=np.float64).reshape(-1, 2)
+        M = meas.shape[0]
+        if M > self._mcap:
+            self._mcap = max(M, 2 * self._mcap, 8)
+            self._mbuf = np.empty((self._mcap, 2))
+            self._obuf = np.empty((self._mcap, 2))
+            self._mbuf_addr = self._mbuf.ctypes.data
+            self._obuf_addr = self._obuf.ctypes.data
+        oa = None
+        if M:
+            self._mbuf[:M] = meas
+            if observed is not None:
+                self._obuf[:M] = np.asarray(observed, dtype=np.float64).reshape(-1, 2)
+                oa = self._obuf_addr
+        nz = None
+        if noise is not None:
+            nz = nat.f64(noise)
+            if nz.size != self.n_local:
+                raise ValueError(f"noise must have {self.n_local} values")
+        ua = None
+        if u0 is not None:
+            self._u0[0] = float(u0)
+            ua = self._u0_addr
+        rc = self._iterate_raw(self._hv, float(rotation), float(translation), self._mbuf_addr if M else None, oa,
+                               M, None if nz is None else nz.ctypes.data, ua, self._pose_addr, self._st_addr)
         self._particles = None
+        st = nat.fs2_iter_stats.from_buffer_copy(self._st)
         self.last_stats = st
         nat.check(rc, self._h)
-        return pose, st
+        return self._pose.copy(), st
 
     # ------------------------------------------------------------ particles
     def get_state(self, first: int = 0, count: int | None = None, lm_cap: int | None = None):

@@ -20,6 +20,6 @@ if [[ $STAGE == all || $STAGE == bench ]]; then
   tail -1 gpurun_out/bench.log
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-extras > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof.log; exit 5; }
-  python scripts/prof_summary.py gpurun_out/prof gpurun_out/prof_summary.txt "${PROF_TITLE:-}" > /dev/null && head -12 gpurun_out/prof_summary.txt
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python bench.py --no-cpu-baseline --no-extras > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof.log; exit 5; }
+  python scripts/prof_summary.py /tmp/prof gpurun_out/prof_summary.txt "${PROF_TITLE:-}" > /dev/null && head -12 gpurun_out/prof_summary.txt
 fi
