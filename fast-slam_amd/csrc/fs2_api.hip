@@ -421,6 +421,35 @@ static const int64_t *posted_xmat(const fs2_handle *h) {
     return reinterpret_cast<const int64_t *>(h->post_host + sizeof(DevStats));
 }
 
+// The page-dedup table (XferTable) for `cap` slots and `nrows` row entries.
+static int reserve_xfer_table(fs2_handle *h, int64_t cap, int64_t nrows) {
+    hipStream_t s = h->stream;
+    if (h->xt_cap < cap) {
+        HIP_TRY(h, hipStreamSynchronize(s));
+        hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
+        h->xt_key = nullptr;
+        h->xt_ref = h->xt_uidx = h->xt_cmask = h->xt_cbase = nullptr;
+        h->xt_cap = 0;
+        HIP_TRY(h, hipMalloc((void **)&h->xt_key, (size_t)cap * 8));
+        HIP_TRY(h, hipMalloc((void **)&h->xt_ref, (size_t)cap * 4));
+        HIP_TRY(h, hipMalloc((void **)&h->xt_uidx, (size_t)cap * 4));
+        HIP_TRY(h, hipMalloc((void **)&h->xt_cmask, (size_t)cap * 4));
+        HIP_TRY(h, hipMalloc((void **)&h->xt_cbase, (size_t)cap * 4));
+        h->xt_cap = cap;
+    }
+    if (h->xt_ecap < nrows) {
+        HIP_TRY(h, hipStreamSynchronize(s));
+        hipFree(h->xt_eslot); hipFree(h->xt_ulist);
+        h->xt_eslot = h->xt_ulist = nullptr;
+        h->xt_ecap = 0;
+        const int64_t want = nrows + nrows / 4;
+        HIP_TRY(h, hipMalloc((void **)&h->xt_eslot, (size_t)want * 4));
+        HIP_TRY(h, hipMalloc((void **)&h->xt_ulist, (size_t)want * 4));
+        h->xt_ecap = want;
+    }
+    return FS2_OK;
+}
+
 // Sharded resample: plan what goes to every other rank on the device (one run of
 // local particles per destination, fs2_plan.hpp), all-gather the sizes and learn
 // them with a post; find the distinct pages of every destination's rows
@@ -460,29 +489,8 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         while ((int64_t(1) << lg) < 2 * nrows) ++lg;
         if (lg > 31) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld page-table rows to send", (long long)nrows);
         const int64_t cap = int64_t(1) << lg;
-        if (h->xt_cap < cap) {
-            HIP_TRY(h, hipStreamSynchronize(s));
-            hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
-            h->xt_key = nullptr;
-            h->xt_ref = h->xt_uidx = h->xt_cmask = h->xt_cbase = nullptr;
-            h->xt_cap = 0;
-            HIP_TRY(h, hipMalloc((void **)&h->xt_key, (size_t)cap * 8));
-            HIP_TRY(h, hipMalloc((void **)&h->xt_ref, (size_t)cap * 4));
-            HIP_TRY(h, hipMalloc((void **)&h->xt_uidx, (size_t)cap * 4));
-            HIP_TRY(h, hipMalloc((void **)&h->xt_cmask, (size_t)cap * 4));
-            HIP_TRY(h, hipMalloc((void **)&h->xt_cbase, (size_t)cap * 4));
-            h->xt_cap = cap;
-        }
-        if (h->xt_ecap < nrows) {
-            HIP_TRY(h, hipStreamSynchronize(s));
-            hipFree(h->xt_eslot); hipFree(h->xt_ulist);
-            h->xt_eslot = h->xt_ulist = nullptr;
-            h->xt_ecap = 0;
-            const int64_t want = nrows + nrows / 4;
-            HIP_TRY(h, hipMalloc((void **)&h->xt_eslot, (size_t)want * 4));
-            HIP_TRY(h, hipMalloc((void **)&h->xt_ulist, (size_t)want * 4));
-            h->xt_ecap = want;
-        }
+        rc = reserve_xfer_table(h, cap, nrows);
+        if (rc) return rc;
         T.key = h->xt_key;
         T.ref = h->xt_ref;
         T.uidx = h->xt_uidx;
@@ -846,6 +854,22 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     h->recvbuf.assign(G, nullptr);
     h->sendcap.assign(G, 0);
     h->recvcap.assign(G, 0);
+    if (G > 1) {
+        // the sharded resample's buffers, made here rather than in a timed scan: the
+        // dedup table and transfers to / from the neighbouring ranks for a quarter
+        // of the shard with nothing shared (the first resamples)
+        const int64_t K = n / 4 + 1, S = K * h->rows;
+        int lg = 10;
+        while ((int64_t(1) << lg) < 2 * S && lg < 31) ++lg;
+        rc = reserve_xfer_table(h, int64_t(1) << lg, S);
+        const size_t bytes = (size_t)xfer_bytes(K, S, S, 0);
+        for (int p = (int)r - 1; !rc && p <= (int)r + 1; p += 2) {
+            if (p < 0 || p >= G) continue;
+            rc = ensure_buf(h, h->sendbuf, h->sendcap, p, bytes);
+            if (!rc) rc = ensure_buf(h, h->recvbuf, h->recvcap, p, bytes);
+        }
+        if (rc) return fail(rc);
+    }
     if (G > 1 || cfg->sharded_path) {
         rc = (cfg->comm_mode == FS2_COMM_LOCAL)
                  ? fs2comm::create_local(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
