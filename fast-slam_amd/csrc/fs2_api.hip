@@ -412,7 +412,7 @@ static int post_and_wait(fs2_handle *h, bool sizes) {
     CommTimer ct(h);
     const int G = h->cfg.world_size;
     const unsigned long long seq = ++h->post_seq;
-    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? 4 * G * G : 0, h->post, h->post_flag_dev,
+    HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? kXrowWords * G * G : 0, h->post, h->post_flag_dev,
                            seq, h->stream));
     return wait_seq(h, h->post_flag, seq, "mid-scan statistics");
 }
@@ -470,19 +470,27 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     auto gather_sizes = [&]() -> int {
         {
             CommTimer ct(h);
-            const int r = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * 4 * G, s, &h->err);
+            const int r = h->tp->allgather(h->xrow, h->xmat, sizeof(int64_t) * kXrowWords * G, s, &h->err);
             if (r) return r;
         }
         return post_and_wait(h, true);
     };
     rc = gather_sizes();
     if (rc) return rc;
-    std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + 4 * G * G);
-    auto at = [&](int from, int to, int f) { return mat[(size_t)from * 4 * G + 4 * to + f]; };
+    std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + kXrowWords * G * G);
+    auto at = [&](int from, int to, int f) { return mat[(size_t)from * kXrowWords * G + kXrowWords * to + f]; };
     // distinct pages of the rows sent (every rank takes part in the all-gather)
     XferTable &T = rs.xt;
     T = XferTable{};
-    for (int p = 0; p < G; ++p) T.ebase[p + 1] = T.ebase[p] + (p == R ? 0 : at(R, p, 1));
+    T.i_lo = h->n;
+    T.i_hi = 0;
+    for (int p = 0; p < G; ++p) {
+        T.ebase[p + 1] = T.ebase[p] + (p == R ? 0 : at(R, p, 1));
+        if (p != R && at(R, p, 0) > 0) {
+            T.i_lo = std::min(T.i_lo, at(R, p, 4));
+            T.i_hi = std::max(T.i_hi, at(R, p, 5));
+        }
+    }
     const int64_t nrows = T.ebase[G];
     if (nrows > 0) {
         int lg = 10;
@@ -506,7 +514,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     }
     rc = gather_sizes();
     if (rc) return rc;
-    mat.assign(posted_xmat(h), posted_xmat(h) + 4 * G * G);
+    mat.assign(posted_xmat(h), posted_xmat(h) + kXrowWords * G * G);
     static const bool log_xfer = std::getenv("FS2_XFER_LOG") != nullptr;
     int64_t nsend = 0;
     std::vector<fs2comm::Xfer> sends, recvs;
@@ -750,8 +758,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
     ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
     ok &= alloc((void **)&h->totals, sizeof(double) * G) == hipSuccess;
-    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * 4 * G) == hipSuccess;
-    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * 4 * G * G) == hipSuccess;
+    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * kXrowWords * G) == hipSuccess;
+    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * kXrowWords * G * G) == hipSuccess;
     ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
@@ -788,8 +796,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
     ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
     {
-        // post block: DevStats, xmat (4 G x G words), then the flag on its own line
-        const size_t body = sizeof(DevStats) + sizeof(int64_t) * 4 * kMaxRanks * kMaxRanks;
+        // post block: DevStats, xmat (kXrowWords G x G words), then the flag on its own line
+        const size_t body = sizeof(DevStats) + sizeof(int64_t) * kXrowWords * kMaxRanks * kMaxRanks;
         const size_t off = ((body + 63) / 64) * 64;
         ok &= hipHostMalloc((void **)&h->post_host, off + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
               hipSuccess;

@@ -141,6 +141,10 @@ struct XferPage {
 };
 static_assert(sizeof(XferPage) == 160, "XferPage layout");
 constexpr int kXferCovBytes = 32;
+// Per destination, the words of xrow / xmat: particles K, rows S, distinct pages
+// U, covariances C (all-gathered to every rank), and the run [i0, i1) of local
+// particles that send there (k_pack_bounds; the dedup kernels' grid).
+constexpr int kXrowWords = 6;
 constexpr uint32_t kEntryOwned = 0x80000000u;
 __host__ __device__ inline int64_t xfer_idx_off(int64_t K) { return K * 64; }
 __host__ __device__ inline int64_t xfer_page_off(int64_t K, int64_t S) { return K * 64 + ((S * 4 + 63) / 64) * 64; }
@@ -202,6 +206,7 @@ struct XferTable {
     int32_t log2cap;
     int64_t ebase[kMaxRanks + 1];
     int64_t ubase[kMaxRanks + 1];   // exclusive prefix of U over destinations (k_pack_pages)
+    int64_t i_lo, i_hi;      // local particles [i_lo, i_hi) hold every outgoing row
 };
 
 struct MeasPack {
@@ -345,7 +350,7 @@ struct ResampleParams {
     // packing for the other ranks (k_pack_plan / k_pack_bounds / k_pack_*)
     int32_t world, rank;
     PackPlan *plan;          // [world] per destination
-    int64_t *xrow;           // [4 world] particles, rows, distinct pages, covariances sent to each rank
+    int64_t *xrow;           // [kXrowWords world] per destination (K, S, U, C, i0, i1)
     char *sbuf[kMaxRanks];   // per destination: the transfer (xfer_bytes)
     XferTable xt;
     double init_cov[4];      // the configured initial landmark covariance (compact transfers)
@@ -426,8 +431,8 @@ hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s);
 hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
 // the distinct pages of every destination's rows (xt sized for sum S, key and
-// ref zeroed by the caller), counted into xrow[4 p + 2], their covariances
-// into xrow[4 p + 3]
+// ref zeroed by the caller), counted into xrow[6 p + 2], their covariances
+// into xrow[6 p + 3]
 hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s);
 // headers, row entries and pages into sbuf (sizes from the all-gathered xrow)
 hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s);

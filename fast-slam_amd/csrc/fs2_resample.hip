@@ -690,10 +690,13 @@ __global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
         pl.pb = pb;
     }
     P.plan[p] = pl;
-    P.xrow[4 * p] = pl.K;
-    P.xrow[4 * p + 1] = pl.S;
-    P.xrow[4 * p + 2] = 0;   // distinct pages, covariances: k_dedup_assign
-    P.xrow[4 * p + 3] = 0;
+    int64_t *xr = P.xrow + kXrowWords * p;
+    xr[0] = pl.K;
+    xr[1] = pl.S;
+    xr[2] = 0;               // distinct pages, covariances: k_dedup_assign
+    xr[3] = 0;
+    xr[4] = pl.i0;
+    xr[5] = pl.i1;
 }
 
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s) {
@@ -760,6 +763,30 @@ __device__ __forceinline__ int64_t dedup_entry(const ResampleParams &P, int p, i
     return P.xt.ebase[p] + (P.iblk[P.nblk + i / kScanBlock] + P.rank_e[i] + k - P.plan[p].c0);
 }
 
+__device__ __forceinline__ bool same_bits(double a, double b) {
+    return __double_as_longlong(a) == __double_as_longlong(b);
+}
+// slots of a page whose covariance is not the initial one (the 8 mirror loads,
+// then the records' covariance loads, issued together)
+__device__ __forceinline__ uint32_t page_cov_mask(const ResampleParams &P, uint32_t page, int fill) {
+    uint32_t rec[kPageSlots];
+#pragma unroll
+    for (int j = 0; j < kPageSlots; ++j) rec[j] = mirror_rec(load_mirror(page_ptr(P.map.pool, page), j));
+    double2 b[kPageSlots], c[kPageSlots];
+#pragma unroll
+    for (int j = 0; j < kPageSlots; ++j) {
+        const double2 *r = reinterpret_cast<const double2 *>(P.map.recs + (int64_t)rec[j < fill ? j : 0] * kRecBytes);
+        b[j] = r[1];
+        c[j] = r[2];
+    }
+    uint32_t mask = 0;
+#pragma unroll
+    for (int j = 0; j < kPageSlots; ++j)
+        if (j < fill && !(same_bits(b[j].x, P.init_cov[0]) && same_bits(b[j].y, P.init_cov[1]) &&
+                          same_bits(c[j].x, P.init_cov[2]) && same_bits(c[j].y, P.init_cov[3])))
+            mask |= 1u << j;
+    return mask;
+}
 // Every row of every particle sent: its (destination, page) key into the table,
 // one thread per (particle, row) (grid y: rows; a row's descriptor loads are
 // coalesced over x).  Only the first of a run of neighbours naming the same
@@ -767,7 +794,7 @@ __device__ __forceinline__ int64_t dedup_entry(const ResampleParams &P, int p, i
 // since): few atomics, and the followers find the key in k_dedup_follow.  A key
 // named more than once is marked shared (ref).
 __global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i = P.xt.i_lo + (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int k = blockIdx.y;
     const XferTable &T = P.xt;
     const uint32_t mask = (uint32_t)(T.cap - 1);
@@ -777,9 +804,13 @@ __global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P)
         if (!r.key || dedup_row(P, p, i - 1, k).key == r.key) continue;
         bool shared = dedup_row(P, p, i + 1, k).key == r.key;
         uint32_t h = xt_hash(r.key, T.log2cap);
+        bool first = false;
         for (;;) {
             const unsigned long long old = atomicCAS(T.key + h, 0ull, r.key);
-            if (old == 0ull) break;
+            if (old == 0ull) {
+                first = true;
+                break;
+            }
             if (old == r.key) {
                 shared = true;
                 break;
@@ -787,6 +818,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P)
             h = (h + 1u) & mask;
         }
         if (shared) T.ref[h] = 1u;
+        if (first) T.cmask[h] = page_cov_mask(P, (uint32_t)(r.key & 0xffffffffu), (int)((r.key >> 40) & 0xfu));
         T.eslot[dedup_entry(P, p, i, k)] = h | (r.single ? kEntryOwned : 0u);
     }
 }
@@ -794,7 +826,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P)
 // The rows that did not insert: their key's slot (read-only probes; neighbours
 // hit the same line).
 __global__ __launch_bounds__(kBlock) void k_dedup_follow(const ResampleParams P) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i = P.xt.i_lo + (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int k = blockIdx.y;
     const XferTable &T = P.xt;
     const uint32_t mask = (uint32_t)(T.cap - 1);
@@ -810,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_follow(const ResampleParams P)
 
 // Index of every distinct page among its destination's (any order: the entries
 // name pages by index) and of its first covariance, the counts into
-// xrow[4 p + 2] / [4 p + 3], the slot into ulist.  A workgroup takes a
+// xrow[6 p + 2] / [6 p + 3], the slot into ulist.  A workgroup takes a
 // contiguous chunk of the table: it counts per destination (ballot per wave,
 // LDS per workgroup), claims each destination's ranges with one global atomic
 // each, then hands out indices in them.
@@ -829,22 +861,6 @@ __device__ __forceinline__ void wave_dest_add(uint32_t *s_cnt, int d, uint32_t &
         todo &= ~m;
     }
 }
-__device__ __forceinline__ bool same_bits(double a, double b) {
-    return __double_as_longlong(a) == __double_as_longlong(b);
-}
-// slots of a page whose covariance is not the initial one
-__device__ __forceinline__ uint32_t page_cov_mask(const ResampleParams &P, uint32_t page, int fill) {
-    uint32_t mask = 0;
-    for (int j = 0; j < fill; ++j) {
-        const float4 m = load_mirror(page_ptr(P.map.pool, page), j);
-        const double2 *r = reinterpret_cast<const double2 *>(P.map.recs + (int64_t)mirror_rec(m) * kRecBytes);
-        const double2 b = r[1], c = r[2];
-        if (!(same_bits(b.x, P.init_cov[0]) && same_bits(b.y, P.init_cov[1]) && same_bits(c.x, P.init_cov[2]) &&
-              same_bits(c.y, P.init_cov[3])))
-            mask |= 1u << j;
-    }
-    return mask;
-}
 __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P) {
     __shared__ uint32_t s_cnt[kMaxRanks], s_run[kMaxRanks], s_base[kMaxRanks];
     __shared__ uint32_t s_ccnt[kMaxRanks], s_crun[kMaxRanks], s_cbase[kMaxRanks];
@@ -862,15 +878,13 @@ __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P)
         uint32_t dummy = 0;
         wave_dest_add(s_cnt, d, dummy);
         if (d >= 0) {
-            const unsigned long long key = T.key[h];
-            const uint32_t mask = page_cov_mask(P, (uint32_t)(key & 0xffffffffu), (int)((key >> 40) & 0xfu));
-            T.cmask[h] = mask;
+            const uint32_t mask = T.cmask[h];
             if (mask) atomicAdd(&s_ccnt[d], (uint32_t)__popc(mask));
         }
     }
     __syncthreads();
     if (threadIdx.x < (unsigned)P.world) {
-        unsigned long long *row = reinterpret_cast<unsigned long long *>(P.xrow + 4 * threadIdx.x);
+        unsigned long long *row = reinterpret_cast<unsigned long long *>(P.xrow + kXrowWords * threadIdx.x);
         if (s_cnt[threadIdx.x]) s_base[threadIdx.x] = (uint32_t)atomicAdd(row + 2, (unsigned long long)s_cnt[threadIdx.x]);
         if (s_ccnt[threadIdx.x])
             s_cbase[threadIdx.x] = (uint32_t)atomicAdd(row + 3, (unsigned long long)s_ccnt[threadIdx.x]);
@@ -891,8 +905,8 @@ __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P)
 }
 
 hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s) {
-    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
-    if (g && p.map.rows > 0) {
+    const unsigned g = (unsigned)((p.xt.i_hi - p.xt.i_lo + kBlock - 1) / kBlock);
+    if (p.xt.i_hi > p.xt.i_lo && p.map.rows > 0) {
         hipLaunchKernelGGL(k_dedup_insert, dim3(g, (unsigned)p.map.rows), dim3(kBlock), 0, s, p);
         hipLaunchKernelGGL(k_dedup_follow, dim3(g, (unsigned)p.map.rows), dim3(kBlock), 0, s, p);
     }
