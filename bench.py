@@ -357,8 +357,10 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    coll0 = 0
     for s in range(args.warmup):
-        one_scan(s)
+        _, st0 = one_scan(s)
+        coll0 = st0.collections
     # kernel events on every 4th timed scan: a dispatch's start / end events delay
     # the next dispatch by ~4.5 us, which the other scans do not pay
     f.set_profiling(True, every=PROFILE_EVERY)
@@ -509,6 +511,7 @@ def main():
                       "resample_shared_slots": copied_slots,
                       "cow_pages_per_particle_scan": cow_pages / units,
                       "pool_collections": st.collections,
+                      "pool_collections_timed": st.collections - coll0,
                       "pool_pages": st.pool_pages,
                       "pages_opened_per_particle_scan": opened / units,
                       "slots_visited_per_particle_scan": visited / units,
