@@ -282,11 +282,22 @@ __device__ __forceinline__ Slot load_rec(const char *recs, uint32_t r) {
     return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
 }
 
+#ifndef FS2_NT_REC
+#define FS2_NT_REC 1           // record stores non-temporal (written once per kernel; A/B: k_update -5%)
+#endif
 __device__ __forceinline__ void store_rec(char *recs, uint32_t r, const Slot &s) {
     double2 *q = reinterpret_cast<double2 *>(recs + (int64_t)r * kRecBytes);
+#if FS2_NT_REC
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    v2d *qv = reinterpret_cast<v2d *>(q);
+    __builtin_nontemporal_store((v2d){s.mx, s.my}, qv);
+    __builtin_nontemporal_store((v2d){s.P.a00, s.P.a01}, qv + 1);
+    __builtin_nontemporal_store((v2d){s.P.a10, s.P.a11}, qv + 2);
+#else
     q[0] = make_double2(s.mx, s.my);
     q[1] = make_double2(s.P.a00, s.P.a01);
     q[2] = make_double2(s.P.a10, s.P.a11);
+#endif
 }
 
 // Slot j of a page: its mirror names the record.

@@ -72,6 +72,9 @@ __device__ unsigned long long g_phase[8];
 #ifndef FS2_PAGE_PRED
 #define FS2_PAGE_PRED 0
 #endif
+#ifndef FS2_NT_COPY
+#define FS2_NT_COPY 0          // A/B knob: copy-on-write page stores non-temporal
+#endif
 #ifndef FS2_COPY_BATCH
 #define FS2_COPY_BATCH 8
 #endif
@@ -672,7 +675,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         };
         auto store_batch = [&](const v4i *v, const uint32_t *d) {
 #pragma unroll
-            for (int u = 0; u < CB; ++u) *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
+            for (int u = 0; u < CB; ++u) {
+#if FS2_NT_COPY
+                __builtin_nontemporal_store(v[u], reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off));
+#else
+                *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
+#endif
+            }
         };
         for (int base = 0; base < T; base += 8 * CB) {
             load_batch(base, va, da);
