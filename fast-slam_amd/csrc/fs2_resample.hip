@@ -990,6 +990,10 @@ hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s) {
 
 // ---------------------------------------------------------------- apply ----
 
+#ifndef FS2_NT_GATHER
+#define FS2_NT_GATHER 1        // the gather's page-table stores non-temporal (A/B: scan -3%)
+#endif
+
 __device__ __forceinline__ int peer_of(const ResampleParams &P, int k) {
     int p = 0;
     while (p + 1 < P.npeers && k >= P.peers[p + 1].kbase) ++p;
@@ -1170,7 +1174,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         for (int u = 0; u < 8; ++u) {
             if (k0 + u < rows) {
                 e[u].x &= keep;
+#if FS2_NT_GATHER
+                __builtin_nontemporal_store(((unsigned long long)e[u].y << 32) | e[u].x,
+                                            reinterpret_cast<unsigned long long *>(P.opt + (int64_t)(k0 + u) * n + m));
+#else
                 P.opt[(int64_t)(k0 + u) * n + m] = e[u];
+#endif
             }
         }
         if (recv) {

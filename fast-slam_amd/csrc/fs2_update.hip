@@ -702,7 +702,16 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
                 for (int u = 0; u < NR; ++u)
                     if (u == canon[t]) id = rdesc[u].x;
+#if FS2_NT_COPY
+                {
+                    const float4 mv = s_mv[t][tid];
+                    __builtin_nontemporal_store((v4i){(int)__float_as_uint(mv.x), (int)__float_as_uint(mv.y),
+                                                      (int)__float_as_uint(mv.z), (int)__float_as_uint(mv.w)},
+                                                reinterpret_cast<v4i *>(page_ptr(map.pool, id)) + (j & (kPageSlots - 1)));
+                }
+#else
                 reinterpret_cast<float4 *>(page_ptr(map.pool, id))[j & (kPageSlots - 1)] = s_mv[t][tid];
+#endif
             }
         }
         nrec = nmod;
