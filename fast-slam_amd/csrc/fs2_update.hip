@@ -72,6 +72,9 @@ __device__ unsigned long long g_phase[8];
 #ifndef FS2_PAGE_PRED
 #define FS2_PAGE_PRED 0
 #endif
+#ifndef FS2_B1_DESC_STORE
+#define FS2_B1_DESC_STORE 0    // A/B knob: store the owned pages' ids in B1 as well
+#endif
 #ifndef FS2_NT_COPY
 #define FS2_NT_COPY 0          // A/B knob: copy-on-write page stores non-temporal
 #endif
@@ -654,9 +657,14 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             if (task) s_cow[wid][T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
             T += __popcll(bm);
         }
+#if FS2_B1_DESC_STORE
 #pragma unroll
         for (int t = 0; t < NR; ++t)
             if (t < nrows && canon[t] == t) pt_entry(map, rrow[t], il)->x = rdesc[t].x;
+#endif
+        // (the owned pages' descriptors reach memory with their summaries: B2 stores
+        // the modified rows, the appends the partly filled row; nothing reads them
+        // from memory before)
         // the task list is per wave: a wave-level barrier orders its LDS writes and reads
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
