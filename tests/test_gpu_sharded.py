@@ -45,7 +45,7 @@ def _gather(handles, cap):
     return [np.concatenate([p[k] for p in parts]) for k in range(6)]
 
 
-@pytest.mark.parametrize("G,N,L", [(2, 6000, 40), (3, 10007, 30), (4, 8192, 24)])
+@pytest.mark.parametrize("G,N,L", [(2, 6000, 40), (3, 10007, 30), (4, 8192, 24), (8, 16384, 20)])
 def test_sharded_matches_single(G, N, L):
     import torch  # noqa: F401
     import fast_slam_2
@@ -70,6 +70,7 @@ def test_sharded_matches_single(G, N, L):
     for h in shards:
         a, b = h.first_global, h.first_global + h.n_local
         h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+        h.set_profiling(True)
     resamples = 0
     moved = 0
     for s in range(8):
@@ -94,6 +95,12 @@ def test_sharded_matches_single(G, N, L):
             assert np.allclose(s1[k], sg[k], rtol=1e-9, atol=1e-15), (s, k)
         assert np.allclose(s1[5], sg[5], rtol=1e-9, atol=1e-12), s
     assert resamples >= 2
+    # transfers: each destination gets each distinct page once, so once particles
+    # share ancestors the pages sent are fewer than the rows they fill
+    prof = [h.profile() for h in shards]
+    if sum(p["migrations"] for p in prof) >= 2:
+        assert sum(p["sent_particles"] for p in prof) > 0
+        assert sum(p["sent_pages"] for p in prof) < sum(p["sent_rows"] for p in prof)
     for h in shards + [single]:
         h.close()
 
