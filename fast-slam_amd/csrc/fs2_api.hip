@@ -1221,7 +1221,10 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183); on
     // one GPU k_finalize did this already
     if (sh) HIP_TRY(h, launch_global_finalize(rp, s));
+    const unsigned long long pseq = ++h->pub_seq;
     if (!sh) {
+        // a scan whose rule did not fire is published here, before the lazy kernels
+        HIP_TRY(h, launch_publish_kept(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
         rs.lazy = 1;
         if (exact)   // the resample's running sum (fast_slam_2.py:184-193), bit-exact
             HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->part_w, h->cbuf, nullptr, true), s));
@@ -1292,7 +1295,6 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // publish the stats to host memory and spin on the flag: a stream sync's
     // wake-up and a copy launch cost more than the whole reduction phase (one
     // GPU: together with the post-resample estimate, in one launch)
-    const unsigned long long pseq = ++h->pub_seq;
     if (sh)
         HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s, prof ? E[3] : nullptr));
     else

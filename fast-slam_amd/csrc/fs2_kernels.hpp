@@ -449,7 +449,12 @@ hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long l
 // into host (coherent, mapped), then *flag = seq.
 hipError_t launch_post(const DevStats *stats, const int64_t *xmat, int32_t nx, char *host,
                        unsigned long long *host_flag, unsigned long long seq, hipStream_t s);
-// One GPU: k_estimate + k_global_best (when the resample fired) + k_publish.
+// One GPU, right after the decision: publish now when the rule did not fire
+// (the lazy resample kernels then run while the host returns and enqueues the
+// next scan); otherwise nothing, and launch_tail_single publishes.
+hipError_t launch_publish_kept(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                               unsigned long long seq, hipStream_t s);
+// One GPU, when the resample fired: k_estimate + k_global_best + k_publish.
 hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
                               unsigned long long *host_flag, unsigned long long seq, hipStream_t s,
                               hipEvent_t e1 = nullptr);

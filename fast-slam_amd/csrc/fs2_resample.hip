@@ -1290,16 +1290,31 @@ __global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32
     if (P.stats->resampled) estimate_body(P, nparts);
 }
 
-// One GPU, end of a scan: the estimate after a resample and the stats
-// publication (k_estimate + k_global_best + k_publish in one launch).
+// One GPU, right after k_finalize: a scan whose rule did not fire is complete
+// (k_finalize wrote the estimate), so its stats are published here and zeroed,
+// which also makes the lazy resample kernels after it exit.
+__global__ __launch_bounds__(64) void k_publish_kept(DevStats *stats, DevStats *host_stats,
+                                                     unsigned long long *host_flag, unsigned long long seq) {
+    if (stats->resampled) return;
+    publish_body(stats, host_stats, host_flag, seq);
+}
+
+hipError_t launch_publish_kept(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                               unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_publish_kept, dim3(1), dim3(64), 0, s, stats, host_stats, host_flag, seq);
+    return hipGetLastError();
+}
+
+// One GPU, end of a scan that resampled: the estimate after the resample and
+// the stats publication (k_estimate + k_global_best + k_publish in one launch);
+// a scan without a resample was published by k_publish_kept (stats zeroed).
 __global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, const ReduceParams P, int32_t nparts,
                                                      DevStats *host_stats, unsigned long long *host_flag,
                                                      unsigned long long seq) {
-    if (R.stats->resampled) {
-        estimate_body(R, nparts);
-        __syncthreads();
-        if (threadIdx.x == 0) global_best_body(P);
-    }
+    if (!R.stats->resampled) return;
+    estimate_body(R, nparts);
+    __syncthreads();
+    if (threadIdx.x == 0) global_best_body(P);
     __syncthreads();
     publish_body(P.stats, host_stats, host_flag, seq);
 }
