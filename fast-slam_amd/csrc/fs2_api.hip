@@ -1210,6 +1210,14 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // sharded ranks need their prefix end in the record; one GPU needs the
     // prefix only when the rule fires (computed below, kernels exit otherwise)
     if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    // one GPU: k_finalize publishes a scan whose rule did not fire, before the
+    // lazy resample kernels (they run while the host returns)
+    const unsigned long long pseq = ++h->pub_seq;
+    if (!sh) {
+        rp.pub_host = h->pub_stats_dev;
+        rp.pub_flag = h->pub_flag_dev;
+        rp.pub_seq = pseq;
+    }
     HIP_TRY(h, launch_finalize(rp, s));
     if (sh) {
         {
@@ -1221,10 +1229,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183); on
     // one GPU k_finalize did this already
     if (sh) HIP_TRY(h, launch_global_finalize(rp, s));
-    const unsigned long long pseq = ++h->pub_seq;
     if (!sh) {
-        // a scan whose rule did not fire is published here, before the lazy kernels
-        HIP_TRY(h, launch_publish_kept(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s));
         rs.lazy = 1;
         if (exact)   // the resample's running sum (fast_slam_2.py:184-193), bit-exact
             HIP_TRY(h, launch_chain(h->chain(h->w[cur], h->part_w, h->cbuf, nullptr, true), s));

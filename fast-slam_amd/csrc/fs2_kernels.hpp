@@ -299,6 +299,10 @@ struct ReduceParams {
     const RankRecord *recs;  // all ranks' records (== rec when world == 1)
     const double *totals;    // all ranks' weight totals (world > 1)
     int32_t world, rank;
+    // one GPU: k_finalize publishes a scan whose rule did not fire (null: never)
+    DevStats *pub_host;
+    unsigned long long *pub_flag;
+    unsigned long long pub_seq;
 };
 
 // The unit table of an evaluated chain (fs2_exact.hip k_chain_walk), as the
@@ -449,12 +453,8 @@ hipError_t launch_publish(DevStats *stats, DevStats *host_stats, unsigned long l
 // into host (coherent, mapped), then *flag = seq.
 hipError_t launch_post(const DevStats *stats, const int64_t *xmat, int32_t nx, char *host,
                        unsigned long long *host_flag, unsigned long long seq, hipStream_t s);
-// One GPU, right after the decision: publish now when the rule did not fire
-// (the lazy resample kernels then run while the host returns and enqueues the
-// next scan); otherwise nothing, and launch_tail_single publishes.
-hipError_t launch_publish_kept(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
-                               unsigned long long seq, hipStream_t s);
-// One GPU, when the resample fired: k_estimate + k_global_best + k_publish.
+// One GPU, when the resample fired: k_estimate + k_global_best + k_publish (a
+// scan whose rule did not fire was published by k_finalize, ReduceParams.pub_*).
 hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, DevStats *host_stats,
                               unsigned long long *host_flag, unsigned long long seq, hipStream_t s,
                               hipEvent_t e1 = nullptr);

@@ -86,7 +86,11 @@ __device__ unsigned long long g_fin[8];
 #define FS2_FIN(k) do { } while (0)
 #endif
 
+__device__ void publish_body(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
+                             unsigned long long seq);
+
 __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
+    __shared__ int s_kept;
     __shared__ double lds_d[16];
     __shared__ int64_t lds_l[16];
     __shared__ int lds_i[16];
@@ -236,7 +240,12 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
             atomicAdd(&g_fin[7], 1ull);
 #endif
         }
+        s_kept = (P.pub_flag != nullptr && !P.stats->resampled) ? 1 : 0;
     }
+    // one GPU, rule not fired: the scan is complete, publish it now (the lazy
+    // resample kernels then run while the host returns and enqueues the next scan)
+    __syncthreads();
+    if (s_kept) publish_body(P.stats, P.pub_host, P.pub_flag, P.pub_seq);
 }
 
 #ifdef FS2_PHASE_TIMING
@@ -1290,24 +1299,9 @@ __global__ __launch_bounds__(1024) void k_estimate(const ResampleParams P, int32
     if (P.stats->resampled) estimate_body(P, nparts);
 }
 
-// One GPU, right after k_finalize: a scan whose rule did not fire is complete
-// (k_finalize wrote the estimate), so its stats are published here and zeroed,
-// which also makes the lazy resample kernels after it exit.
-__global__ __launch_bounds__(64) void k_publish_kept(DevStats *stats, DevStats *host_stats,
-                                                     unsigned long long *host_flag, unsigned long long seq) {
-    if (stats->resampled) return;
-    publish_body(stats, host_stats, host_flag, seq);
-}
-
-hipError_t launch_publish_kept(DevStats *stats, DevStats *host_stats, unsigned long long *host_flag,
-                               unsigned long long seq, hipStream_t s) {
-    hipLaunchKernelGGL(k_publish_kept, dim3(1), dim3(64), 0, s, stats, host_stats, host_flag, seq);
-    return hipGetLastError();
-}
-
 // One GPU, end of a scan that resampled: the estimate after the resample and
 // the stats publication (k_estimate + k_global_best + k_publish in one launch);
-// a scan without a resample was published by k_publish_kept (stats zeroed).
+// a scan without a resample was published by k_finalize (stats zeroed).
 __global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, const ReduceParams P, int32_t nparts,
                                                      DevStats *host_stats, unsigned long long *host_flag,
                                                      unsigned long long seq) {
