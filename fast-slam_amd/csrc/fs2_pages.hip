@@ -167,15 +167,47 @@ __global__ __launch_bounds__(kBlock) void k_sweep_write(const uint8_t *mark, int
     for (int j = threadIdx.x; j < tot; j += kBlock) dst[j] = s_ids[j];
 }
 
-// one lane per (page, slot) of the pool: 8 consecutive lanes read one 128-byte page
+// 8 consecutive lanes per page of the pool, each reading one 16-byte mirror of
+// the page (one 128-byte line per 8 lanes).  A fixed grid strides over the pool,
+// kMarkRecsAhead items per lane with their mark bytes loaded together: most pages
+// are unmarked, and a one-item lane per (page, slot) needed npool/32 workgroups
+// whose dispatch, not the bytes, set the kernel's time.
+#ifndef FS2_MARK_RECS_STRIDE
+#define FS2_MARK_RECS_STRIDE 1
+#endif
+constexpr int kMarkRecsAhead = 4;
+constexpr unsigned kMarkRecsGrid = 4096;
 __global__ __launch_bounds__(kBlock) void k_mark_recs(const char *pool, int64_t npool, const uint8_t *mark,
                                                       uint8_t epoch, int64_t nrecs, uint8_t *rmark,
                                                       uint8_t repoch) {
+#if FS2_MARK_RECS_STRIDE
+    const int64_t lanes = npool * kPageSlots;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; t0 < lanes; t0 += kMarkRecsAhead * stride) {
+        bool live[kMarkRecsAhead];
+#pragma unroll
+        for (int u = 0; u < kMarkRecsAhead; ++u) {
+            const int64_t t = t0 + u * stride;
+            live[u] = t < lanes && mark[t / kPageSlots] == epoch;
+        }
+        uint32_t r[kMarkRecsAhead];
+#pragma unroll
+        for (int u = 0; u < kMarkRecsAhead; ++u) {
+            const int64_t t = t0 + u * stride;
+            r[u] = live[u] ? mirror_rec(load_mirror(pool + (t / kPageSlots) * kPageBytes, (int)(t % kPageSlots)))
+                           : 0xffffffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < kMarkRecsAhead; ++u)
+            if (live[u] && (int64_t)r[u] < nrecs) rmark[r[u]] = repoch;
+    }
+#else
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t id = t / kPageSlots;
     if (id >= npool || mark[id] != epoch) return;
     const uint32_t r = mirror_rec(load_mirror(pool + id * kPageBytes, (int)(t % kPageSlots)));
     if ((int64_t)r < nrecs) rmark[r] = repoch;
+#endif
 }
 
 hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,
@@ -183,9 +215,14 @@ hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t
                                   uint32_t *rfreel, int64_t *rnfree_dev, hipStream_t s) {
     const int64_t nb = collect_blocks(nrecs);
     const int64_t lanes = npool * kPageSlots;
-    if (lanes > 0)
-        hipLaunchKernelGGL(k_mark_recs, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, pool,
-                           npool, mark, epoch, nrecs, rmark, repoch);
+    if (lanes > 0) {
+        int64_t grid = (lanes + kBlock - 1) / kBlock;
+#if FS2_MARK_RECS_STRIDE
+        grid = std::min<int64_t>(grid, kMarkRecsGrid);
+#endif
+        hipLaunchKernelGGL(k_mark_recs, dim3((unsigned)grid), dim3(kBlock), 0, s, pool, npool, mark, epoch, nrecs,
+                           rmark, repoch);
+    }
     hipLaunchKernelGGL(k_sweep_count, dim3((unsigned)nb), dim3(kBlock), 0, s, rmark, nrecs, repoch, rbcnt);
     hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, rbcnt, nb, rnfree_dev);
     hipLaunchKernelGGL(k_sweep_write, dim3((unsigned)nb), dim3(kBlock), 0, s, rmark, nrecs, repoch, rbcnt, rfreel);
