@@ -10,6 +10,12 @@ the timed region starts.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, particles sharded)
 
+`python bench.py --gpus N` (N > 1) without WORLD_SIZE in the environment starts
+the N ranks itself: one child process per GPU with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT, spawned before this process touches the
+GPU (no exec); it fails loudly when fewer than N GPUs are visible.  Rank 0
+prints the JSON line.  `--dry-run` prints the children's environments instead.
+
 Default workload: BASELINE config 3, 1e6 particles per GPU x 500 landmarks.
 """
 from __future__ import annotations
@@ -36,7 +42,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PROFILE_EVERY = 4            # timed scans per profiled scan (libfs2 fs2_set_profiling)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -54,7 +60,85 @@ def parse():
     ap.add_argument("--serial-icp", action="store_true",
                     help="A/B (config 4): align each scan just before its update instead of "
                          "beside the previous scan's update")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="with --gpus N > 1 and no WORLD_SIZE: print the ranks' environments, start nothing")
+    ap.add_argument("--dropin", action="store_true",
+                    help="time the drop-in FastSLAM2.iterate() (numpy RNG) beside the device-RNG step")
+    return ap.parse_args(argv)
+
+
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def rank_envs(n, port, base=None):
+    """The environment of each of the n rank processes bench.py starts itself
+    (the variables torch.distributed.run would set; 127.0.0.1 rendezvous)."""
+    base = dict(os.environ if base is None else base)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")      # RCCL over dmabuf IPC on this pool
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(n)]
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def visible_gpus():
+    """GPUs this process could use, counted without initialising HIP
+    (torch.cuda.device_count() reads the device list only, on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 outside torch.distributed.run: start N rank processes (children,
+    this process never touches the GPU), wait for all, exit with the worst status.
+    A rank that fails ends the others (their collectives would wait forever)."""
+    import signal
+    import subprocess
+    n = args.gpus
+    envs = rank_envs(n, free_port())
+    if args.dry_run:
+        print(json.dumps([{k: e[k] for k in RANK_ENV} for e in envs]), flush=True)
+        return 0
+    have = visible_gpus()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this process sees {have}; "
+              f"refusing to time fewer ranks than asked", file=sys.stderr, flush=True)
+        return 2
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e) for e in envs]
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+            bad = [r for r, rc in enumerate(rcs) if rc not in (None, 0)]
+            if bad:
+                time.sleep(5)                   # a failing rank's peers get a moment to report
+                for r, p in enumerate(procs):
+                    if p.poll() is None:
+                        print(f"bench.py: rank {bad[0]} exited with {rcs[bad[0]]}; stopping rank {r}",
+                              file=sys.stderr, flush=True)
+                        p.send_signal(signal.SIGTERM)
+                for r, p in enumerate(procs):
+                    try:
+                        rcs[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[r] = p.wait()
+                break
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise
+    worst = max((abs(rc) for rc in rcs), default=0)
+    return 0 if worst == 0 else (worst if worst < 256 else 1)
 
 
 def populate(f, n_local, L, seed, rank, base_map=None):
@@ -290,9 +374,15 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
                     "queued before it)"}
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; timing {world} ranks",
+              file=sys.stderr, flush=True)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch

@@ -58,11 +58,28 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     os.makedirs(LIB_DIR, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     sid = source_id(defines)
-    cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, f'-DFS2_BUILD_ID="{sid}"',
-           "-I", os.path.join(ROCM, "include"), *defines,
-           *[os.path.join(CSRC, s) for s in SOURCES],
-           "-o", lib + ".tmp", "-L", os.path.join(ROCM, "lib"), "-lrccl",
-           "-Wl,-rpath," + os.path.join(ROCM, "lib")]
+    # one object per source, compiled in parallel, then linked (no -fgpu-rdc: each
+    # translation unit's device code is self-contained, as in a one-command build)
+    objdir = os.path.join(LIB_DIR, "obj", os.path.basename(lib))
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f"--offload-arch={ARCH}", *[f for f in FLAGS if f != "-shared"], f'-DFS2_BUILD_ID="{sid}"',
+              "-I", os.path.join(ROCM, "include"), *defines]
+    objs = [os.path.join(objdir, os.path.splitext(src)[0] + ".o") for src in SOURCES]
+    cmds = [[hipcc, *cflags, "-c", os.path.join(CSRC, src), "-o", o] for src, o in zip(SOURCES, objs)]
+    if verbose:
+        for c in cmds:
+            print(" ".join(c), flush=True)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        res = list(ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds))
+    for c, r in zip(cmds, res):
+        if r.stdout or r.stderr:
+            print(r.stdout + r.stderr, file=sys.stderr, flush=True)
+        if r.returncode:
+            raise subprocess.CalledProcessError(r.returncode, c)
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib + ".tmp",
+           "-L", os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib")]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -21,6 +21,7 @@
 #include "fs2_plan.hpp"
 
 using namespace fs2;
+static_assert(kMaxRanks <= fs2comm::kShmMaxRanks, "shm transport rank table");
 
 namespace {
 
@@ -879,9 +880,9 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         if (rc) return fail(rc);
     }
     if (G > 1 || cfg->sharded_path) {
-        rc = (cfg->comm_mode == FS2_COMM_LOCAL)
-                 ? fs2comm::create_local(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
-                 : fs2comm::create_rccl(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err);
+        rc = (cfg->comm_mode == FS2_COMM_LOCAL) ? fs2comm::create_local(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
+             : (cfg->comm_mode == FS2_COMM_SHM) ? fs2comm::create_shm(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
+                                                 : fs2comm::create_rccl(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err);
         if (rc) return fail(rc);
     }
     if (hipStreamSynchronize(h->stream) != hipSuccess)
@@ -1111,9 +1112,14 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         up.map = h->map();
         const bool first = k0 == 0, last = up.last_pass != 0;
         const bool cand = up.filter && up.blk1 > up.blk0;
+        // a shard without particles launches nothing: its profiled intervals are
+        // recorded empty here (fold_one reads every event of the set)
+        if (prof && first && up.blk1 <= up.blk0)
+            for (int k : {0, 1, 4}) HIP_TRY(h, hipEventRecord(E[k], s));
         HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
         HIP_TRY(h, launch_update(up, s, (prof && first) ? (cand ? E[4] : E[0]) : nullptr,
                                  (prof && last) ? E[2] : nullptr));
+        if (prof && last && up.blk1 <= up.blk0) HIP_TRY(h, hipEventRecord(E[2], s));
         ++passes;
         // pose/weight/count read + weight/count write; pose write on the move pass
         fixed_bytes += (uint64_t)h->n * (32 + 4 + 8 + 4 + (up.do_move ? 24 : 0));
@@ -1188,6 +1194,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     // weight total over all ranks (fast_slam_2.py:166).  Exact: Python's sum (in
     // particle order) from the update pass's block sums, the chain's units also
     // folding the update counters (k_wsum's other job)
+    if (prof && exact && h->n <= 0) HIP_TRY(h, hipEventRecord(E[5], s));   // launch_chain records nothing
     if (exact) {
         ChainParams cp = h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false);
         cp.cpart = h->cpart;
@@ -1307,6 +1314,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     h->stats_clean = true;
     rc = wait_flag(h, pseq);
     if (rc) return rc;
+    // a stream-ordered transport reports a failed collective only now
+    if (h->tp && (rc = h->tp->status(&h->err))) return rc;
     const DevStats &st = *h->pub_stats;
     if (st.resampled) h->cur = nxt;
     h->cnt_upper = st.max_count;

@@ -11,19 +11,35 @@
 //   LocalTransport  G ranks as threads of one process (device-to-device
 //                   copies + a host barrier).  Exercises every sharded code
 //                   path on a single GPU (tests/test_gpu_sharded.py).
+//   ShmTransport    G ranks as processes of one host (several may share a GPU),
+//                   stream-ordered like RCCL: pinned staging copies around one
+//                   host function per collective that moves the bytes through a
+//                   POSIX shared-memory segment behind a process barrier
+//                   (tests/test_gpu_sharded_procs.py).
 #pragma once
 
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fs2.h"
@@ -47,6 +63,8 @@ class Transport {
     // grouped point-to-point: every rank lists what it sends to and receives from each peer
     virtual int exchange(const std::vector<Xfer> &sends, const std::vector<Xfer> &recvs,
                          hipStream_t s, std::string *err) = 0;
+    // a failure inside a stream-ordered collective (after the call returned), else FS2_OK
+    virtual int status(std::string *) { return FS2_OK; }
 };
 
 // ------------------------------------------------------------------ RCCL ---
@@ -209,6 +227,374 @@ inline int create_local(const uint8_t key[128], int world, int rank, Transport *
     auto *t = new LocalTransport();
     t->grp = g;
     t->r = rank;
+    *out = t;
+    return FS2_OK;
+}
+
+// ------------------------------------------------------------------- shm ---
+//
+// Segment: a header (barriers, per-rank round counts), one all-gather slot per
+// rank and a mailbox per ordered pair of ranks (`chunk` bytes + a 64-byte
+// header naming the transfer's size and round).  A collective is
+//   hipMemcpyAsync  device -> this process's pinned staging
+//   hipLaunchHostFunc  staging -> segment, barrier, segment -> staging, barrier
+//   hipMemcpyAsync  pinned staging -> device
+// on the caller's stream; the host function runs when the stream reaches it,
+// so the bytes it moves are the ones the kernels before it produced, and the
+// kernels after it see what arrived -- the ordering RCCL's kernels give, without
+// a host-side stream sync.  Transfers larger than a mailbox go in rounds; every
+// rank runs max over ranks of its own round count (agreed through the header).
+
+constexpr uint64_t kShmMagic = 0x66733273686d3031ull;   // "fs2shm01"
+constexpr size_t kShmAgCap = 4096;                      // all-gather bytes per rank
+constexpr size_t kShmHeader = 4096;
+constexpr size_t kShmBoxHeader = 64;
+constexpr int kShmMaxRanks = 16;                        // >= fs2::kMaxRanks (static_assert in fs2_api.hip)
+
+struct ShmBarrier {
+    std::atomic<uint32_t> count;
+    std::atomic<uint32_t> gen;
+    char pad[56];
+};
+
+struct ShmHeader {
+    std::atomic<uint64_t> magic;
+    int32_t G;
+    int32_t pad0;
+    uint64_t chunk;
+    std::atomic<uint32_t> failed;          // some rank timed out or saw a size mismatch
+    char pad1[36];
+    ShmBarrier attach;                     // creation
+    ShmBarrier bar;                        // collectives (host functions)
+    std::atomic<int64_t> need[kShmMaxRanks];  // rounds the current exchange needs, per rank
+};
+static_assert(sizeof(ShmHeader) <= kShmHeader, "shm header");
+static_assert(std::atomic<uint32_t>::is_always_lock_free && std::atomic<int64_t>::is_always_lock_free &&
+                  std::atomic<uint64_t>::is_always_lock_free,
+              "process-shared atomics must be lock-free");
+
+struct ShmBox {
+    int64_t total;                         // bytes of the whole transfer
+    int64_t round;
+    char pad[kShmBoxHeader - 16];
+};
+
+inline size_t shm_segment_bytes(int G, size_t chunk) {
+    return kShmHeader + (size_t)G * kShmAgCap + (size_t)G * G * (kShmBoxHeader + chunk);
+}
+
+class ShmTransport : public Transport {
+  public:
+    int G = 1, r = 0;
+    char *seg = nullptr;
+    size_t seg_bytes = 0;
+    ShmHeader *hdr = nullptr;
+    size_t chunk = 0;
+    std::chrono::milliseconds timeout{60000};
+    char *ag_send = nullptr, *ag_recv = nullptr;          // pinned
+    std::vector<char *> xs, xr;                           // pinned, per peer
+    std::vector<size_t> xs_cap, xr_cap;
+    std::mutex fmu;
+    std::string fmsg;                                     // first failure seen by a host function
+    std::atomic<int> failed{0};
+
+    ~ShmTransport() override {
+        if (ag_send) hipHostFree(ag_send);
+        if (ag_recv) hipHostFree(ag_recv);
+        for (char *p : xs) if (p) hipHostFree(p);
+        for (char *p : xr) if (p) hipHostFree(p);
+        if (seg) munmap(seg, seg_bytes);
+    }
+    int world() const override { return G; }
+    int rank() const override { return r; }
+
+    char *slot(int p) const { return seg + kShmHeader + (size_t)p * kShmAgCap; }
+    ShmBox *box(int from, int to) const {
+        return reinterpret_cast<ShmBox *>(seg + kShmHeader + (size_t)G * kShmAgCap +
+                                          ((size_t)from * G + to) * (kShmBoxHeader + chunk));
+    }
+    char *box_data(int from, int to) const { return reinterpret_cast<char *>(box(from, to)) + kShmBoxHeader; }
+
+    // sense-counting barrier over the segment; false when a rank failed or the
+    // wait exceeded the timeout (then every rank's later waits fail at once)
+    bool wait(ShmBarrier &b) {
+        if (hdr->failed.load(std::memory_order_acquire)) return false;
+        const uint32_t g = b.gen.load(std::memory_order_acquire);
+        if (b.count.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)G - 1) {
+            b.count.store(0, std::memory_order_relaxed);
+            b.gen.store(g + 1, std::memory_order_release);
+            return true;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned it = 0;; ++it) {
+            if (b.gen.load(std::memory_order_acquire) != g) return true;
+            if ((it & 255u) == 255u) {
+                if (hdr->failed.load(std::memory_order_acquire)) return false;
+                const auto dt = std::chrono::steady_clock::now() - t0;
+                if (dt > timeout) {
+                    hdr->failed.store(1, std::memory_order_release);
+                    return false;
+                }
+                if (dt > std::chrono::milliseconds(2)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+                else std::this_thread::yield();
+            } else {
+                __builtin_ia32_pause();
+            }
+        }
+    }
+    void note_fail(const char *what) {
+        std::lock_guard<std::mutex> lk(fmu);
+        if (!failed.exchange(1)) fmsg = std::string("shm transport: ") + what;
+        hdr->failed.store(1, std::memory_order_release);
+    }
+    int status(std::string *err) override {
+        if (!failed.load() && !hdr->failed.load(std::memory_order_acquire)) return FS2_OK;
+        std::lock_guard<std::mutex> lk(fmu);
+        if (err) *err = fmsg.empty() ? std::string("shm transport: another rank failed") : fmsg;
+        return FS2_ERR_COMM;
+    }
+
+    int allgather(const void *send, void *recv, size_t bytes, hipStream_t s, std::string *err) override {
+        if (int rc = status(err)) return rc;
+        if (bytes > kShmAgCap) return fail(err, "all-gather larger than its slot");
+        if (hipMemcpyAsync(ag_send, send, bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return fail(err, "all-gather copy to staging");
+        auto *op = new AgOp{this, bytes};
+        if (hipLaunchHostFunc(s, &ShmTransport::ag_host, op) != hipSuccess) {
+            delete op;
+            return fail(err, "hipLaunchHostFunc");
+        }
+        if (hipMemcpyAsync(recv, ag_recv, bytes * G, hipMemcpyHostToDevice, s) != hipSuccess)
+            return fail(err, "all-gather copy from staging");
+        return FS2_OK;
+    }
+
+    int exchange(const std::vector<Xfer> &sends, const std::vector<Xfer> &recvs, hipStream_t s,
+                 std::string *err) override {
+        if (int rc = status(err)) return rc;
+        auto *op = new XOp{this, std::vector<size_t>(G, 0), std::vector<size_t>(G, 0)};
+        int rc = FS2_OK;
+        for (const Xfer &x : sends) {
+            if (x.peer < 0 || x.peer >= G || x.peer == r) rc = fail(err, "exchange peer out of range");
+            else if (x.bytes && !(rc = stage(xs, xs_cap, x.peer, x.bytes, s, err)))
+                op->send[x.peer] = x.bytes;
+            if (rc) break;
+        }
+        for (const Xfer &x : recvs) {
+            if (rc) break;
+            if (x.peer < 0 || x.peer >= G || x.peer == r) rc = fail(err, "exchange peer out of range");
+            else if (x.bytes && !(rc = stage(xr, xr_cap, x.peer, x.bytes, s, err)))
+                op->recv[x.peer] = x.bytes;
+        }
+        if (rc) {
+            delete op;
+            return rc;
+        }
+        for (const Xfer &x : sends)
+            if (x.bytes && hipMemcpyAsync(xs[x.peer], x.buf, x.bytes, hipMemcpyDeviceToHost, s) != hipSuccess) {
+                delete op;
+                return fail(err, "exchange copy to staging");
+            }
+        if (hipLaunchHostFunc(s, &ShmTransport::x_host, op) != hipSuccess) {
+            delete op;
+            return fail(err, "hipLaunchHostFunc");
+        }
+        for (const Xfer &x : recvs)
+            if (x.bytes && hipMemcpyAsync(x.buf, xr[x.peer], x.bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+                return fail(err, "exchange copy from staging");
+        return FS2_OK;
+    }
+
+  private:
+    struct AgOp {
+        ShmTransport *t;
+        size_t bytes;
+    };
+    struct XOp {
+        ShmTransport *t;
+        std::vector<size_t> send, recv;   // bytes per peer
+    };
+    static int fail(std::string *err, const char *what) {
+        if (err) *err = std::string("shm transport: ") + what;
+        return FS2_ERR_COMM;
+    }
+    // pinned staging for one peer; growing drains the stream first (earlier
+    // collectives may still copy through the old buffer)
+    int stage(std::vector<char *> &v, std::vector<size_t> &cap, int p, size_t bytes, hipStream_t s,
+              std::string *err) {
+        if (cap[p] >= bytes) return FS2_OK;
+        if (hipStreamSynchronize(s) != hipSuccess) return fail(err, "stream sync");
+        if (v[p]) hipHostFree(v[p]);
+        v[p] = nullptr;
+        cap[p] = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+        if (hipHostMalloc((void **)&v[p], want, 0) != hipSuccess) return fail(err, "pinned staging allocation");
+        cap[p] = want;
+        return FS2_OK;
+    }
+    static void ag_host(void *u) {
+        AgOp *op = static_cast<AgOp *>(u);
+        ShmTransport *t = op->t;
+        const size_t b = op->bytes;
+        delete op;
+        std::memcpy(t->slot(t->r), t->ag_send, b);
+        if (!t->wait(t->hdr->bar)) return t->note_fail("all-gather rendezvous failed or timed out");
+        for (int p = 0; p < t->G; ++p) std::memcpy(t->ag_recv + (size_t)p * b, t->slot(p), b);
+        if (!t->wait(t->hdr->bar)) t->note_fail("all-gather completion failed or timed out");
+    }
+    static void x_host(void *u) {
+        XOp *op = static_cast<XOp *>(u);
+        ShmTransport *t = op->t;
+        const int G = t->G, me = t->r;
+        const size_t C = t->chunk;
+        int64_t mine = 0;
+        for (int p = 0; p < G; ++p)
+            mine = std::max<int64_t>(mine, (int64_t)((std::max(op->send[p], op->recv[p]) + C - 1) / C));
+        t->hdr->need[me].store(mine, std::memory_order_release);
+        int64_t R = 0;
+        bool ok = t->wait(t->hdr->bar);
+        if (ok) {
+            for (int p = 0; p < G; ++p) R = std::max(R, t->hdr->need[p].load(std::memory_order_acquire));
+            ok = t->wait(t->hdr->bar);     // need[] is rewritten by the next exchange
+        }
+        for (int64_t k = 0; ok && k < R; ++k) {
+            const size_t off = (size_t)k * C;
+            for (int p = 0; p < G; ++p)
+                if (op->send[p] > off) {
+                    ShmBox *bx = t->box(me, p);
+                    bx->total = (int64_t)op->send[p];
+                    bx->round = k;
+                    std::memcpy(t->box_data(me, p), t->xs[p] + off, std::min(C, op->send[p] - off));
+                }
+            if (!(ok = t->wait(t->hdr->bar))) break;
+            for (int q = 0; q < G; ++q)
+                if (op->recv[q] > off) {
+                    const ShmBox *bx = t->box(q, me);
+                    if (bx->total != (int64_t)op->recv[q] || bx->round != k) {
+                        t->note_fail("exchange size mismatch between sender and receiver");
+                        ok = false;
+                        break;
+                    }
+                    std::memcpy(t->xr[q] + off, t->box_data(q, me), std::min(C, op->recv[q] - off));
+                }
+            if (ok) ok = t->wait(t->hdr->bar);
+        }
+        if (!ok) t->note_fail("exchange rendezvous failed or timed out");
+        delete op;
+    }
+};
+
+inline int create_shm(const uint8_t key[128], int world, int rank, Transport **out, std::string *err) {
+    auto bad = [&](const std::string &what) {
+        if (err) *err = "shm transport: " + what;
+        return FS2_ERR_COMM;
+    };
+    if (world < 1 || world > kShmMaxRanks) return bad("world size out of range");
+    char name[64];
+    int k = std::snprintf(name, sizeof name, "/fs2shm.");
+    for (int i = 0; i < 16; ++i) k += std::snprintf(name + k, sizeof name - k, "%02x", key[i]);
+    long tmo_s = 60;
+    if (const char *e = std::getenv("FS2_SHM_TIMEOUT_S")) tmo_s = std::max(1L, std::atol(e));
+    size_t chunk = std::min<size_t>(4u << 20, std::max<size_t>(64u << 10, (256u << 20) / ((size_t)world * world)));
+    if (const char *e = std::getenv("FS2_SHM_CHUNK")) chunk = std::max<size_t>(4096, std::strtoull(e, nullptr, 10));
+    chunk = (chunk + 63) / 64 * 64;
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto deadline = t0 + std::chrono::seconds(tmo_s);
+    int fd = -1;
+    size_t bytes = 0;
+    char *seg = nullptr;
+    if (rank == 0) {
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0) return bad(std::string("shm_open(") + name + ") failed: " + std::strerror(errno));
+        bytes = shm_segment_bytes(world, chunk);
+        if (ftruncate(fd, (off_t)bytes) != 0) {
+            close(fd);
+            shm_unlink(name);
+            return bad("ftruncate failed");
+        }
+        seg = (char *)mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (seg == MAP_FAILED) {
+            shm_unlink(name);
+            return bad("mmap failed");
+        }
+        auto *h = new (seg) ShmHeader();
+        h->G = world;
+        h->chunk = chunk;
+        h->failed.store(0);
+        h->attach.count.store(0);
+        h->attach.gen.store(0);
+        h->bar.count.store(0);
+        h->bar.gen.store(0);
+        for (auto &v : h->need) v.store(0);
+        h->magic.store(kShmMagic, std::memory_order_release);
+    } else {
+        while ((fd = shm_open(name, O_RDWR, 0)) < 0) {
+            if (std::chrono::steady_clock::now() > deadline) return bad("rank 0's segment never appeared");
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        }
+        // the header first (rank 0 may still be sizing the segment), then all of it
+        struct stat sb {};
+        while (fstat(fd, &sb) != 0 || (size_t)sb.st_size < kShmHeader) {
+            if (std::chrono::steady_clock::now() > deadline) {
+                close(fd);
+                return bad("segment never sized");
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        char *hp = (char *)mmap(nullptr, kShmHeader, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (hp == MAP_FAILED) {
+            close(fd);
+            return bad("mmap failed");
+        }
+        auto *h = reinterpret_cast<ShmHeader *>(hp);
+        while (h->magic.load(std::memory_order_acquire) != kShmMagic) {
+            if (std::chrono::steady_clock::now() > deadline) {
+                munmap(hp, kShmHeader);
+                close(fd);
+                return bad("segment never initialised");
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        const int G0 = h->G;
+        chunk = h->chunk;
+        munmap(hp, kShmHeader);
+        if (G0 != world) {
+            close(fd);
+            return bad("world size differs from rank 0's");
+        }
+        bytes = shm_segment_bytes(world, chunk);
+        seg = (char *)mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (seg == MAP_FAILED) return bad("mmap failed");
+    }
+    auto *t = new ShmTransport();
+    t->G = world;
+    t->r = rank;
+    t->seg = seg;
+    t->seg_bytes = bytes;
+    t->hdr = reinterpret_cast<ShmHeader *>(seg);
+    t->chunk = chunk;
+    t->timeout = std::chrono::milliseconds(tmo_s * 1000);
+    t->xs.assign(world, nullptr);
+    t->xr.assign(world, nullptr);
+    t->xs_cap.assign(world, 0);
+    t->xr_cap.assign(world, 0);
+    if (hipHostMalloc((void **)&t->ag_send, kShmAgCap, 0) != hipSuccess ||
+        hipHostMalloc((void **)&t->ag_recv, kShmAgCap * world, 0) != hipSuccess) {
+        t->hdr->failed.store(1);
+        if (rank == 0) shm_unlink(name);
+        delete t;
+        return bad("pinned staging allocation failed");
+    }
+    // every rank mapped the segment: its name is no longer needed (nothing stays
+    // behind in /dev/shm, whatever happens to the processes later)
+    const bool ok = t->wait(t->hdr->attach);
+    if (rank == 0) shm_unlink(name);
+    if (!ok) {
+        delete t;
+        return bad("ranks did not all attach in time");
+    }
     *out = t;
     return FS2_OK;
 }

@@ -26,6 +26,9 @@ __host__ __device__ inline double plan_u(double u0, int64_t m, int64_t N) {
 // the real-arithmetic estimate and step to it (a step or two at most, bounded
 // by a binary search fallback).
 __host__ __device__ inline int64_t plan_first_above(double v, double u0, int64_t N) {
+    // a NaN prefix: `u > NaN` is false for every u, so the reference's loop stops
+    // at the particle whose running sum turned NaN and it fills every later output
+    if (v != v) return N;
     const double est = (v - u0) * (double)N;
     int64_t m = (est < 0.0) ? 0 : (est >= (double)N ? N : (int64_t)est + 1);
     for (int it = 0; it < 8; ++it) {

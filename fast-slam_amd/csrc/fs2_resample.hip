@@ -289,6 +289,9 @@ __device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
     const double ne = (sq < 1.0 / ng) ? ng : 1.0 / sq;
     st->sumsq = sq;
     st->n_eff = ne;
+    // fs2.h error_flags bit 1: a weight (hence the total) is not finite; the
+    // rule then never fires (NaN < N/2 is false), as in the reference
+    if (!isfinite(st->total) || !isfinite(sq)) st->error_flags |= 2;
     st->resampled = ne < ng / 2.0 ? 1 : 0;
     // tree sums: a decision this close to the threshold may differ from the
     // reference's summation order

@@ -30,6 +30,7 @@ FS2_HOST = 0
 FS2_DEVICE = 1
 FS2_COMM_RCCL = 0
 FS2_COMM_LOCAL = 1
+FS2_COMM_SHM = 2
 
 
 class fs2_config(C.Structure):

@@ -59,7 +59,8 @@ class FastSLAM2:
         cfg.world_size = int(world_size)
         if comm_id is not None:
             C.memmove(cfg.comm_id, comm_id, 128)
-        cfg.comm_mode = {"rccl": nat.FS2_COMM_RCCL, "local": nat.FS2_COMM_LOCAL}[comm_mode]
+        cfg.comm_mode = {"rccl": nat.FS2_COMM_RCCL, "local": nat.FS2_COMM_LOCAL,
+                         "shm": nat.FS2_COMM_SHM}[comm_mode]
         cfg.sharded_path = 1 if sharded_path else 0
         cfg.page_pool = int(page_pool)          # initial pool sizes (0: defaults; fs2.h)
         cfg.record_pool = int(record_pool)
@@ -133,8 +134,15 @@ class FastSLAM2:
         """iterate() with explicit inputs: meas [M][2] (distance, yaw); observed [M][2]
         robot-frame points (None: computed in libfs2); noise [N_local] motion draws and
         u0 the resample start (None: Philox on the device).  Returns (pose, stats)."""
-        meas = np.asarray(meas, dtype=np.float64).reshape(-1, 2)
+        if not getattr(self, "_h", None) or not self._hv:
+            raise nat.FS2Error(nat.FS2_ERR_ARG, "step() on a closed FastSLAM2 handle")
+        meas = nat.f64(meas).reshape(-1, 2)
         M = meas.shape[0]
+        obs = None
+        if observed is not None:
+            obs = nat.f64(observed).reshape(-1, 2)
+            if obs.shape[0] != M:
+                raise ValueError(f"observed has {obs.shape[0]} points for {M} measurements")
         if M > self._mcap:
             self._mcap = max(M, 2 * self._mcap, 8)
             self._mbuf = np.empty((self._mcap, 2))
@@ -144,8 +152,8 @@ class FastSLAM2:
         oa = None
         if M:
             self._mbuf[:M] = meas
-            if observed is not None:
-                self._obuf[:M] = np.asarray(observed, dtype=np.float64).reshape(-1, 2)
+            if obs is not None:
+                self._obuf[:M] = obs
                 oa = self._obuf_addr
         nz = None
         if noise is not None:
@@ -264,6 +272,7 @@ class FastSLAM2:
         nat.check(self._lib.fs2_synchronize(self._h), self._h)
 
     def close(self):
+        self._hv = None                         # step()'s raw address: never reused once freed
         if getattr(self, "_h", None):
             self._lib.fs2_destroy(self._h)
             self._h = None

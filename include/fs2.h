@@ -59,7 +59,10 @@ enum { FS2_HOST = 0, FS2_DEVICE = 1 };   /* where caller buffers live */
 /* How sharded ranks (world_size > 1) talk. */
 enum {
     FS2_COMM_RCCL = 0,      /* one process per GPU, RCCL over xGMI; comm_id from fs2_comm_unique_id */
-    FS2_COMM_LOCAL = 1      /* ranks are threads of one process (testing); comm_id is a group key */
+    FS2_COMM_LOCAL = 1,     /* ranks are threads of one process (testing); comm_id is a group key */
+    FS2_COMM_SHM = 2        /* ranks are processes on one host (any GPUs, several may share one):
+                               stream-ordered collectives through a POSIX shared-memory segment
+                               named from comm_id (a random group key, e.g. 128 urandom bytes) */
 };
 
 typedef struct fs2_handle fs2_handle;

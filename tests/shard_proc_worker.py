@@ -1,0 +1,67 @@
+"""One rank of the multi-process sharded scan (tests/test_gpu_sharded_procs.py).
+
+  python shard_proc_worker.py G RANK N L SEED SCANS KEYHEX OUT.npz
+
+Runs FastSLAM2 rank RANK of G with the stream-ordered shared-memory transport
+(FS2_COMM_SHM) on cuda:0 over the workload of test_gpu_sharded.py, and saves
+per scan what the parent compares with a single handle: decisions, estimates,
+N_eff, reduce_ambiguous, associations, and the final local state.
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "fast-slam_amd"))
+
+import numpy as np  # noqa: E402
+
+
+def workload(N, L, seed):
+    import fs2_synthetic as syn
+    wl = syn.Workload(N, L, seed=seed)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    lm[:, :, 2] = lm[:, :, 5] = 0.01        # peaked likelihoods: resampling moves particles across shards
+    return wl, x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm
+
+
+def main(argv):
+    G, rank, N, L, seed, scans = (int(a) for a in argv[:6])
+    key = bytes.fromhex(argv[6])
+    out = argv[7]
+    import torch  # noqa: F401  -- one HIP runtime in the process
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    configure()
+    wl, x, y, yaw, w, cnt, lm = workload(N, L, seed)
+    cap = L + 4 * scans + 8
+    h = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap, rank=rank,
+                              world_size=G, comm_id=key, comm_mode="shm", verbose=False)
+    a, b = h.first_global, h.first_global + h.n_local
+    h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+    h.set_profiling(True)
+    rec = {k: [] for k in ("resampled", "best_index", "pose", "n_eff", "reduce_amb", "n_recv")}
+    assoc = []
+    for s in range(scans):
+        rot, tr = syn.odometry(s)
+        pose, st = h.step(rot, tr, wl.measurements(s))
+        rec["resampled"].append(st.resampled)
+        rec["best_index"].append(st.best_index)
+        rec["pose"].append(pose)
+        rec["n_eff"].append(st.n_eff)
+        rec["reduce_amb"].append(st.reduce_ambiguous)
+        assoc.append(h.associations())
+        print(f"rank {rank} scan {s} resampled {st.resampled}", flush=True)
+    xs, ys, yaws, ws, cnts, lms = h.get_state(lm_cap=cap)
+    prof = h.profile()
+    h.close()
+    np.savez(out, first=a, count=b - a, assoc=np.stack(assoc), x=xs, y=ys, yaw=yaws, w=ws, cnt=cnts, lm=lms,
+             sent_particles=prof["sent_particles"], sent_rows=prof["sent_rows"], sent_pages=prof["sent_pages"],
+             migrations=prof["migrations"], **{k: np.array(v) for k, v in rec.items() if k != "n_recv"})
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

@@ -98,9 +98,9 @@ def test_sharded_matches_single(G, N, L):
     # transfers: each destination gets each distinct page once, so once particles
     # share ancestors the pages sent are fewer than the rows they fill
     prof = [h.profile() for h in shards]
-    if sum(p["migrations"] for p in prof) >= 2:
-        assert sum(p["sent_particles"] for p in prof) > 0
-        assert sum(p["sent_pages"] for p in prof) < sum(p["sent_rows"] for p in prof)
+    assert sum(p["migrations"] for p in prof) >= 2, "the case must move particles across shards twice"
+    assert sum(p["sent_particles"] for p in prof) > 0
+    assert sum(p["sent_pages"] for p in prof) < sum(p["sent_rows"] for p in prof)
     for h in shards + [single]:
         h.close()
 

@@ -1,0 +1,84 @@
+"""The whole sharded scan across processes (one GPU, G = 2 and 3 processes).
+
+Each rank is its own process (tests/shard_proc_worker.py) with the
+stream-ordered shared-memory transport (FS2_COMM_SHM): its collectives are a
+copy to pinned staging, one host function on the stream behind a process
+barrier, and a copy back -- no host-side stream sync, so the scan's kernels,
+mid-scan posts and host waits follow the stream ordering RCCL ranks rely on
+(the in-process transport of test_gpu_sharded.py synchronises around every
+collective and hides it).  Reference semantics at stake: normalise, N_eff and
+the low-variance resample across shards (fast_slam_2.py:161-199,212-223).
+
+The parent compares every scan with a single handle in this process on the same
+inputs: resample decisions, estimate index and pose, N_eff, associations, and at
+the end every particle's state within 1e-9; reduce_ambiguous is 0 on every rank
+and scan (no decision the shard order could flip), at least two resamples move
+particles across shards.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("G,N,L,scans", [(2, 6000, 40, 8), (3, 10007, 30, 8)])
+def test_sharded_processes_match_single(G, N, L, scans, tmp_path):
+    import torch  # noqa: F401
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    from shard_proc_worker import workload
+    configure()
+    key = os.urandom(128).hex()
+    env = dict(os.environ, FS2_SHM_CHUNK=str(64 << 10), FS2_SHM_TIMEOUT_S="40")   # small mailboxes: rounds
+    outs = [str(tmp_path / f"rank{r}.npz") for r in range(G)]
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "shard_proc_worker.py"), str(G), str(r),
+                               str(N), str(L), "21", str(scans), key, outs[r]],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(G)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-4000:]}"
+    ranks = [np.load(o) for o in outs]
+
+    wl, x, y, yaw, w, cnt, lm = workload(N, L, 21)
+    cap = L + 4 * scans + 8
+    single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap,
+                                   verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    resamples = 0
+    for s in range(scans):
+        rot, tr = syn.odometry(s)
+        pose1, st1 = single.step(rot, tr, wl.measurements(s))
+        for r, d in enumerate(ranks):
+            assert d["resampled"][s] == st1.resampled, (r, s)
+            assert d["best_index"][s] == st1.best_index, (r, s)
+            assert np.allclose(d["pose"][s], pose1, rtol=1e-9, atol=1e-12), (r, s)
+            assert np.isclose(d["n_eff"][s], st1.n_eff, rtol=1e-9), (r, s)
+            assert d["reduce_amb"][s] == 0, (r, s)
+        assert np.array_equal(single.associations(), np.concatenate([d["assoc"][s] for d in ranks], axis=1)), s
+        resamples += st1.resampled
+    s1 = single.get_state(lm_cap=cap)
+    for d in ranks:
+        a, b = int(d["first"]), int(d["first"]) + int(d["count"])
+        assert np.array_equal(s1[4][a:b], d["cnt"])
+        for k, name in enumerate(("x", "y", "yaw", "w")):
+            assert np.allclose(s1[k][a:b], d[name], rtol=1e-9, atol=1e-15), name
+        assert np.allclose(s1[5][a:b], d["lm"], rtol=1e-9, atol=1e-12)
+    single.close()
+    assert resamples >= 2
+    assert sum(int(d["migrations"]) for d in ranks) >= 2, "particles must cross shards at least twice"
+    assert sum(int(d["sent_pages"]) for d in ranks) < sum(int(d["sent_rows"]) for d in ranks)
