@@ -1866,6 +1866,39 @@ int fs2_mahalanobis(int32_t device, const double *a, const double *b, const doub
     return FS2_OK;
 }
 
+int fs2_debug_philox(int32_t device, int64_t n, const uint32_t *ctr, const uint32_t *key, uint32_t *out) {
+    if (n < 0 || (n > 0 && (!ctr || !key || !out))) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_philox: bad arguments");
+    if (n == 0) return FS2_OK;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t bc = al16((size_t)n * 16), bk = al16((size_t)n * 8);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 2 * bc + bk, &sc);
+    if (rc) return rc;
+    uint32_t *dc = (uint32_t *)sc->buf, *dk = (uint32_t *)(sc->buf + bc), *dout = (uint32_t *)(sc->buf + bc + bk);
+    SHIP(hipMemcpyAsync(dc, ctr, (size_t)n * 16, hipMemcpyHostToDevice, sc->stream));
+    SHIP(hipMemcpyAsync(dk, key, (size_t)n * 8, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_debug_philox(n, dc, dk, dout, sc->stream));
+    SHIP(hipMemcpyAsync(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
+    return FS2_OK;
+}
+
+int fs2_debug_normals(int32_t device, uint64_t seed, uint64_t stream, uint64_t first, int64_t n, double *out) {
+    if (n < 0 || (n > 0 && !out)) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_normals: bad arguments");
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const int64_t chunk = 1 << 24;
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, (size_t)std::min(n, chunk) * 8 + 16, &sc);
+    if (rc) return rc;
+    for (int64_t o = 0; o < n; o += chunk) {
+        const int64_t k = std::min(chunk, n - o);
+        SHIP(launch_debug_normals(seed, stream, first + (uint64_t)o, k, (double *)sc->buf, sc->stream));
+        SHIP(hipMemcpyAsync(out + o, sc->buf, (size_t)k * 8, hipMemcpyDeviceToHost, sc->stream));
+        SHIP(hipStreamSynchronize(sc->stream));
+    }
+    return FS2_OK;
+}
+
 #ifdef FS2_PHASE_TIMING
 // timing builds only (not in include/fs2.h): summed per-wave s_memtime cycles of
 // the k_update phases since the last reset

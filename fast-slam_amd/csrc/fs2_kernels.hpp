@@ -506,6 +506,13 @@ hipError_t cluster_points(const double2 *pts, int64_t n, double eps, int64_t min
 hipError_t gather_map_points(MapRef map, const int32_t *cnt, int64_t n, double2 **pts_out, int64_t *npts,
                              hipStream_t s);
 
+// test hooks of the device generator (fs2_device.hpp): raw Philox4x32-10 blocks
+// (counter c[4 i..], key k[2 i..]) and the motion sample's normals of (seed, stream)
+// at indices first .. first + n - 1
+hipError_t launch_debug_philox(int64_t n, const uint32_t *ctr, const uint32_t *key, uint32_t *out, hipStream_t s);
+hipError_t launch_debug_normals(uint64_t seed, uint64_t stream, uint64_t first, int64_t n, double *out,
+                                hipStream_t s);
+
 hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt,
                       int32_t n_tgt, int32_t max_iter, double thr, double *R, double *t,
                       int32_t *iters, hipStream_t s);

@@ -881,6 +881,38 @@ hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0, hi
     return hipGetLastError();
 }
 
+// ------------------------------------------------------ generator test hooks --
+
+__global__ __launch_bounds__(kBlock) void k_debug_philox(int64_t n, const uint32_t *ctr, const uint32_t *key,
+                                                         uint32_t *out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const U4 r = philox(U4{ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]}, key[2 * i], key[2 * i + 1]);
+    out[4 * i] = r.x;
+    out[4 * i + 1] = r.y;
+    out[4 * i + 2] = r.z;
+    out[4 * i + 3] = r.w;
+}
+
+__global__ __launch_bounds__(kBlock) void k_debug_normals(uint64_t seed, uint64_t stream, uint64_t first, int64_t n,
+                                                          double *out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = philox_normal(seed, stream, first + (uint64_t)i);
+}
+
+hipError_t launch_debug_philox(int64_t n, const uint32_t *ctr, const uint32_t *key, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_philox, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, ctr, key,
+                       out);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_normals(uint64_t seed, uint64_t stream, uint64_t first, int64_t n, double *out,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_normals, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, seed, stream,
+                       first, n, out);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------- normalise & N_eff --
 
 // Weight total (Python builtin sum in particle order in sequential mode) in

@@ -171,6 +171,8 @@ SIGNATURES = [
                                              C.POINTER(C.c_int64)]),
     ("fs2_frontend", C.c_int, [C.c_int32, C.c_int32, _vp, _vp, C.c_int32, _dp, C.c_int32, C.c_int32,
                                C.POINTER(fs2_frontend_out)]),
+    ("fs2_debug_philox", C.c_int, [C.c_int32, C.c_int64, _vp, _vp, _vp]),
+    ("fs2_debug_normals", C.c_int, [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, _vp]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("fs2_plan_ranges", C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double, _vp, _vp]),
     ("fs2_plan_sends", C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),

@@ -275,6 +275,18 @@ int fs2_associate(int32_t device, const double observed[2], const double *lm, in
 int fs2_mahalanobis(int32_t device, const double *a, const double *b, const double *cov,
                     int32_t K, double *out);
 
+/* Test hooks of the device generator that replaces the reference's
+ * np.random draws when rng="device" (fast_slam_2.py:79,81 motion noise, :183
+ * resample start): Philox4x32-10 (Salmon et al., Random123) and the motion
+ * sample's standard normals (Box-Muller on one Philox block per draw; particle
+ * g of scan s draws normal (seed, stream = s, index = g), scaled by the noise).
+ * fs2_debug_philox: n blocks, counter ctr[4 i .. 4 i + 3], key key[2 i, 2 i + 1]
+ * -> out[4 i ..].  fs2_debug_normals: indices first .. first + n - 1 into out.
+ * Host buffers. */
+int fs2_debug_philox(int32_t device, int64_t n, const uint32_t *ctr, const uint32_t *key, uint32_t *out);
+int fs2_debug_normals(int32_t device, uint64_t seed, uint64_t stream, uint64_t first, int64_t n,
+                      double *out);
+
 /* ---------------------------------------------------------- multi-GPU ---- */
 
 /* Replaces GeometryUtils.cluster_points (utils/geometry_utils.py:26-62), i.e.

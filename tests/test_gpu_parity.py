@@ -370,6 +370,49 @@ def test_config2_n100k_l200(fs):
     f.close()
 
 
+def test_config2_exact_mode_sequence(fs):
+    """BASELINE config 2 (N = 1e5, L = 200) in the reduction mode bench.py runs it
+    (reduce="auto": the reference's summation orders bit for bit above 4096
+    particles), 8 scans with injected draws against the oracle: associations,
+    resample decisions, N_eff, estimates, weights and maps every scan; at least
+    one resample (fast_slam_2.py:161-199,212-223)."""
+    import fs2_synthetic as syn
+    from oracle import oracle as orc
+    N, L, S = 100_000, 200, 8
+    wl = syn.Workload(N, L, seed=6)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    cap = L + 4 * S + 8
+    f = fs.FastSLAM2(N, reduce="auto", record_assoc=True, landmark_capacity=cap, verbose=False)
+    f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, cap)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    del lm
+    rng = np.random.default_rng(31)
+    resamples = 0
+    for s in range(S):
+        rot, tr = syn.odometry(s)
+        ms = wl.measurements(s)
+        nz = rng.normal(0, 0.001 if rot else 0.0055, N)
+        u0 = rng.uniform(0, 1.0 / N)
+        pose, st = f.step(rot, tr, ms, None, nz, u0)
+        opose, oassoc, ors, one = o.iterate(rot, tr, ms, nz, u0)
+        assert np.array_equal(f.associations(), oassoc), s
+        assert bool(st.resampled) == ors, s
+        assert st.n_eff == one, s                           # exact mode: bit for bit
+        assert np.allclose(pose, opose, rtol=RTOL, atol=1e-12), s
+        assert st.ambiguous == 0 and st.reduce_ambiguous == 0, s
+        resamples += st.resampled
+        _, _, _, wg, cg, _ = f.get_state(lm_cap=0)
+        assert np.array_equal(cg, o.cnt), s
+        assert np.allclose(wg, o.w, rtol=RTOL, atol=0), s
+    assert resamples >= 1
+    xg, yg, yawg, wg, cg, lmg = f.get_state(lm_cap=cap)
+    assert np.allclose(xg, o.x, rtol=RTOL, atol=1e-12) and np.allclose(yawg, o.yaw, rtol=RTOL, atol=1e-12)
+    assert np.allclose(lmg, o.lm, rtol=RTOL, atol=1e-12)
+    f.close()
+
+
 def test_candidate_list_overflow(fs):
     """More than kMaxCand (16) candidate slots per particle: 40 landmarks crowd the
     first measurement's point while a far measurement matches nothing, so the
