@@ -309,7 +309,43 @@ def robustness(args, f, L, first_scan):
     out["no_gate_filter"]["note"] = "grid map, every slot's fp64 record read (no mirrors, no page boxes)"
     g.close()
     out["sharded_local_g2"] = sharded_local(args, L, n)
+    out["sharded_local_g8"] = sharded_local(args, L, n, G=8)
+    out["dropin_iterate"] = dropin(args, L, n)
     return out
+
+
+def dropin(args, L, n, scans=8, warm=2):
+    """What a reference caller gets: FastSLAM2.iterate(rotation, translation,
+    list[Measurement]) (fast_slam_2.py:33, called at jde_robots_main.py:38) with
+    numpy's global legacy RNG -- N normals drawn on the host per scan, and the
+    resample start, exactly as the reference draws them (Q4/Q5) -- on a handle of
+    the headline size.  host_rng_ms: np.random.normal of N values alone."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from fast_slam_2.models.measurement import Measurement
+    np.random.seed(args.seed)
+    f = fast_slam_2.FastSLAM2(n, rng="numpy", seed=args.seed, landmark_capacity=L + scans + 8, verbose=False)
+    populate(f, n, L, args.seed, 0)
+    meas = [[Measurement(float(d), float(b)) for d, b in syn.scan_measurements(L, s, args.seed)]
+            for s in range(scans)]
+    for s in range(warm):
+        f.iterate(*syn.odometry(s), meas[s])
+    t0 = time.perf_counter()
+    res = 0
+    for s in range(warm, scans):
+        f.iterate(*syn.odometry(s), meas[s])
+        res += f.last_stats.resampled
+    dt = time.perf_counter() - t0
+    f.close()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        np.random.normal(0, 0.0055, size=n)
+    rng_ms = (time.perf_counter() - t1) / 3 * 1e3
+    k = scans - warm
+    return {"value": n * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k, "resamples": res,
+            "host_rng_ms": rng_ms,
+            "note": "FastSLAM2.iterate() with numpy's legacy RNG (the reference's draws, bit for bit): "
+                    "host-RNG bound -- N legacy-MT19937 normals per scan on one host core"}
 
 
 def sharded_local(args, L, n_total, G=2, scans=9, warm=3):

@@ -1151,6 +1151,14 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     rp.flip_margin = flip_margin;
     rp.part_w = exact ? h->part_w : nullptr;
     rp.np_leaf = exact ? h->np_leaf : nullptr;
+    // exact mode on one GPU: normalise and numpy's chunk trees in one pass
+    // (k_normalize_chunks); FS2_TAIL=split keeps k_normalize + k_finalize's trees (A/B)
+    static const bool split_tail = [] {
+        const char *e = std::getenv("FS2_TAIL");
+        return e && std::strcmp(e, "split") == 0;
+    }();
+    rp.chunked = (exact && !sh && !split_tail) ? 1 : 0;
+    if (rp.chunked) rp.nparts = rp.n_np;
     rp.np_tail = exact ? h->np_tail : nullptr;
     rp.u0_host = u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
@@ -1213,7 +1221,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         HIP_TRY(h, launch_global_total(rp, s));
     }
     // normalise (:161-175), local prefix of the normalised weights, this rank's record
-    HIP_TRY(h, launch_normalize(rp, s));
+    HIP_TRY(h, rp.chunked ? launch_normalize_chunks(rp, s) : launch_normalize(rp, s));
     // sharded ranks need their prefix end in the record; one GPU needs the
     // prefix only when the rule fires (computed below, kernels exit otherwise)
     if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));

@@ -79,16 +79,33 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     }
     {
         // estimates of the chain at this workgroup's four 256-term block starts:
-        // the block sums before them in any order (the margin bounds every order)
+        // the block sums before them in any order (the margin bounds every order).
+        // Every load is issued before any add (four per thread and round), and the
+        // workgroup's own four block sums come with them: one memory latency, not
+        // one per loop step.
         const int64_t nb0 = (int64_t)blockIdx.x * 4;
+        const int t = threadIdx.x;
+        const double own = (t < 4 && nb0 + t < P.nb) ? P.bsum[nb0 + t] : 0.0;
         double v = 0.0;
-        for (int64_t j = threadIdx.x; j < nb0; j += 1024) v += P.bsum[j];
+        for (int64_t j0 = 0; j0 < nb0; j0 += 4096) {
+            double x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t j = j0 + t + 1024 * u;
+                x[u] = (j < nb0) ? P.bsum[j] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v += x[u];
+        }
         const double base = block_sum<1024>(v, s_red);
-        if (threadIdx.x == 0) {
-            double e = base;
-            for (int c = 0; c < 4; ++c) {
-                s_bp[c] = e;
-                if (nb0 + c < P.nb) e += P.bsum[nb0 + c];
+        if (t < 64) {
+            const double b0 = bcast(own, 0), b1 = bcast(own, 1), b2 = bcast(own, 2);
+            if (t < 4) {
+                double e = base;
+                if (t > 0) e += b0;
+                if (t > 1) e += b1;
+                if (t > 2) e += b2;
+                s_bp[t] = e;
             }
         }
         __syncthreads();

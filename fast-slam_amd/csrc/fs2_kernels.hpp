@@ -289,6 +289,8 @@ struct ReduceParams {
     double *np_part;         // exact: numpy chunk sums of w'^2 (k_finalize, beyond its LDS stage)
     int32_t n_np;            // their count
     double *np_leaf;         // exact: numpy's 128-element leaves of the full chunks (k_normalize)
+    int32_t chunked;         // exact: k_normalize_chunks left np.sum's chunk terms in np_part and
+                             // the partials per 8192-weight chunk (nparts = n_np)
     const NpTailPlan *np_tail;   // exact: the partial last chunk's tree (null: none)
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
@@ -427,6 +429,9 @@ hipError_t launch_candidates(const UpdateParams &p, hipStream_t s, hipEvent_t e0
 hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s, hipEvent_t e0 = nullptr);
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s);
+// exact mode: normalise + numpy's Sigma w'^2 per 8192-weight chunk + chunk partials
+// (then k_finalize with ReduceParams.chunked)
+hipError_t launch_normalize_chunks(const ReduceParams &p, hipStream_t s);
 hipError_t launch_global_total(const ReduceParams &p, hipStream_t s);
 hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s);
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s);

@@ -131,7 +131,11 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
         }
     };
     load_parts(threadIdx.x);
-    if (P.exact) {
+    if (P.exact && P.chunked) {
+        // k_normalize_chunks left every chunk's term: staged for thread 0's sum in order
+        const int nl = min(P.n_np, kNpStage);
+        for (int k = threadIdx.x; k < nl; k += 1024) s_np[k] = P.np_part[k];
+    } else if (P.exact) {
         // numpy's chunk sums: each full chunk's 64 leaves (k_normalize) as a balanced
         // tree in order (a wave per chunk, xor butterflies; 16 chunks' loads in
         // flight) on waves 0..14, the partial last chunk by numpy's recursion on

@@ -1016,6 +1016,132 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
     }
 }
 
+// Exact mode, one 8192-weight numpy chunk per 1024-thread workgroup (8
+// consecutive weights per thread, loaded and stored as 64-byte runs): normalise
+// (fast_slam_2.py:161-175) and, in the same pass, the chunk's term of
+// np.sum(weights ** 2) (:219) by numpy's own tree -- 64 leaves of 128 (8
+// accumulators of 16 squares added in order, combined ((r0 + r1) + (r2 + r3)) +
+// ((r4 + r5) + (r6 + r7))), the leaves paired as a balanced tree in order (DPP,
+// as k_finalize did before) -- or, for a partial last chunk, numpy's recursion
+// (np_tail).  Also per chunk: the first maximum and the largest map (np_part,
+// part_best_*, part_maxcnt: k_finalize reads n_np entries) and the sum of every
+// 256 weights (part_w: the resample chain's block estimates).  One pass over
+// the weights instead of k_normalize + k_finalize's leaf trees.
+__global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P) {
+    __shared__ double s_sq[1024 * 8];            // squares, thread-major (numpy's leaf order)
+    __shared__ double s_leaf[64];
+    __shared__ double s_bv[16];
+    __shared__ int64_t s_bi[16];
+    __shared__ int s_mc[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * kNpChunk;
+    const int64_t e0 = c0 + 8 * (int64_t)t;
+    const int64_t n = P.n;
+    const bool full = c0 + kNpChunk <= n;
+    const double total = P.stats->total;
+    double w[8];
+    int cn[8];
+    if (e0 + 8 <= n) {
+        const double2 *wp = reinterpret_cast<const double2 *>(P.w + e0);
+        const int4 *cp = reinterpret_cast<const int4 *>(P.cnt + e0);
+        const double2 a = wp[0], b = wp[1], c = wp[2], d = wp[3];
+        const int4 x = cp[0], y = cp[1];
+        w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y; w[4] = c.x; w[5] = c.y; w[6] = d.x; w[7] = d.y;
+        cn[0] = x.x; cn[1] = x.y; cn[2] = x.z; cn[3] = x.w; cn[4] = y.x; cn[5] = y.y; cn[6] = y.z; cn[7] = y.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            w[j] = (e0 + j < n) ? P.w[e0 + j] : 0.0;
+            cn[j] = (e0 + j < n) ? P.cnt[e0 + j] : 0;
+        }
+    }
+    double ws = 0.0, bv = -INFINITY;
+    int64_t bi = INT64_MAX;
+    int mc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const bool live = e0 + j < n;
+        double v = w[j];
+        if (total < P.floor) v = 1.0 / (double)P.n_global;
+        else v = (v < P.floor) ? v : v / total;
+        w[j] = live ? v : 0.0;
+        ws += w[j];
+        if (live && v > bv) {                    // ascending index: the first maximum stays
+            bv = v;
+            bi = e0 + j;
+        }
+        mc = max(mc, live ? cn[j] : 0);
+        s_sq[8 * t + j] = w[j] * w[j];
+    }
+    if (e0 + 8 <= n) {
+        double2 *wp = reinterpret_cast<double2 *>(P.w + e0);
+        wp[0] = make_double2(w[0], w[1]);
+        wp[1] = make_double2(w[2], w[3]);
+        wp[2] = make_double2(w[4], w[5]);
+        wp[3] = make_double2(w[6], w[7]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (e0 + j < n) P.w[e0 + j] = w[j];
+    }
+    // the resample chain's estimate of each 256-weight block (32 threads)
+    {
+        double v = ws;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+        const int64_t blk = c0 / kBlock + (t >> 5);
+        if ((t & 31) == 0 && blk * kBlock < n && P.part_w) P.part_w[blk] = v;
+    }
+    wave_argmax(bv, bi);
+    mc = wave_max_i(mc);
+    if (lane == 0) {
+        s_bv[wid] = bv;
+        s_bi[wid] = bi;
+        s_mc[wid] = mc;
+    }
+    __syncthreads();                             // s_sq, s_bv written (global w' too)
+    double chunk = 0.0;
+    if (full) {
+        // accumulator k of leaf L: its squares 8 q + k, q = 0..15, added in order
+        if (t < 512) {
+            const int L = t >> 3, k = t & 7;
+            const double *q0 = s_sq + (16 * L) * 8 + k;
+            double r = q0[0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) r += q0[8 * q];
+            r += __shfl_xor(r, 1, 64);
+            r += __shfl_xor(r, 2, 64);
+            r += __shfl_xor(r, 4, 64);
+            if (k == 0) s_leaf[L] = r;
+        }
+        __syncthreads();
+        if (wid == 0) chunk = lane63(dpp_scan(s_leaf[lane], 0.0, [](double a, double b) { return a + b; }));
+    } else if (wid == 0 && P.np_tail) {
+        chunk = np_pairwise_wave(P.w + c0, P.np_tail);   // this workgroup's own stores, after the barrier
+    }
+    if (t == 0) {
+        double v = s_bv[0];
+        int64_t ix = s_bi[0];
+        int m = s_mc[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            argmax_combine(v, ix, s_bv[k], s_bi[k]);
+            m = max(m, s_mc[k]);
+        }
+        P.np_part[blockIdx.x] = chunk;
+        P.part_best_w[blockIdx.x] = v;
+        P.part_best_i[blockIdx.x] = ix;
+        P.part_maxcnt[blockIdx.x] = m;
+    }
+}
+
+hipError_t launch_normalize_chunks(const ReduceParams &p, hipStream_t s) {
+    const unsigned grid = (unsigned)((p.n + kNpChunk - 1) / kNpChunk);
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_normalize_chunks, dim3(grid), dim3(1024), 0, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
     const unsigned grid = (unsigned)((p.n + kBlock - 1) / kBlock);
     if (grid == 0) return hipSuccess;
