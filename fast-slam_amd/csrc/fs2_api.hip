@@ -127,7 +127,7 @@ struct fs2_handle {
     int32_t *rank_d = nullptr, *rank_e = nullptr;
     int64_t *iblk = nullptr;
     int cap = 0, max_cap = kMaxSlots;
-    double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr;
+    double *wpart = nullptr, *part_sq = nullptr, *part_best_w = nullptr, *part_pose = nullptr;
     unsigned long long *cpart = nullptr;   // update-pass block counters [kNumCounters][nblocks]
     int64_t *part_best_i = nullptr;
     unsigned long long *part_slots = nullptr;   // gather: slots per output workgroup
@@ -684,6 +684,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
     hipFree(h->sout); hipFree(h->np_leaf); hipFree(h->part_w); hipFree(h->np_part); hipFree(h->np_tail);
     hipFree(h->urec); hipFree(h->sentry);
+    hipFree(h->part_pose);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -768,6 +769,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->cpart, nb * 8 * kNumCounters) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
+    ok &= alloc((void **)&h->part_pose, nb * 24) == hipSuccess;
     ok &= alloc((void **)&h->part_best_i, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_slots, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_maxcnt, nb * 4) == hipSuccess;
@@ -1158,7 +1160,8 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         return e && std::strcmp(e, "split") == 0;
     }();
     rp.chunked = (exact && !sh && !split_tail) ? 1 : 0;
-    if (rp.chunked) rp.nparts = rp.n_np;
+    if (rp.chunked) rp.nparts = normalize_chunk_parts(h->n);
+    rp.part_pose = h->part_pose;
     rp.np_tail = exact ? h->np_tail : nullptr;
     rp.u0_host = u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
@@ -1233,7 +1236,7 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
         rp.pub_flag = h->pub_flag_dev;
         rp.pub_seq = pseq;
     }
-    HIP_TRY(h, launch_finalize(rp, s));
+    HIP_TRY(h, rp.chunked ? launch_finalize_chunked(rp, s) : launch_finalize(rp, s));
     if (sh) {
         {
             CommTimer ct(h);
@@ -1918,6 +1921,14 @@ int fs2_debug_phase_times(uint64_t out[8], int32_t reset) {
 extern "C" int fs2_debug_chain_times(uint64_t out[8], int32_t reset) {
     return fs2::debug_chain_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess ? FS2_OK
                                                                                                     : FS2_ERR_HIP;
+}
+extern "C" int fs2_debug_tail_times(uint64_t out[32], int32_t reset) {
+    unsigned long long a[32], b[32], c[32];
+    if (fs2::debug_tail_times_update(a, reset) != hipSuccess || fs2::debug_tail_times_exact(b, reset) != hipSuccess ||
+        fs2::debug_tail_times_resample(c, reset) != hipSuccess)
+        return FS2_ERR_HIP;
+    for (int k = 0; k < 32; ++k) out[k] = a[k] + b[k] + c[k];
+    return FS2_OK;
 }
 extern "C" int fs2_debug_finalize_times(uint64_t out[8], int32_t reset) {
     return fs2::debug_fin_times(reinterpret_cast<unsigned long long *>(out), reset) == hipSuccess ? FS2_OK

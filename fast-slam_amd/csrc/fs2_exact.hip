@@ -72,6 +72,8 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     __shared__ double s_red[16], s_bp[4];
     __shared__ unsigned long long s_c[16][kNumCounters];
     if (P.lazy && lazy_skip(P)) return;
+    FS2_TS_DECL;
+    FS2_TS(0, 0);
     const int64_t ngroups = (P.n + 1023) / 1024;
     if (blockIdx.x >= ngroups) {     // the update pass's counters (total mode)
         fold_counters(P.cpart, P.ncpart, P.cstats, (int)(blockIdx.x - ngroups), s_c);
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         }
         __syncthreads();
     }
+    FS2_TS(0, 1);
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int64_t i = (int64_t)blockIdx.x * 1024 + t;
     const int64_t k = (int64_t)blockIdx.x * kChainGroup + wid;
@@ -208,6 +211,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
             }
         }
     }
+    FS2_TS(0, 2);
     if (lane == 0) {
         s_D[wid] = D;
         s_f[wid] = listed;
@@ -234,6 +238,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
             P.bM[blockIdx.x] = mask;
         }
     }
+    FS2_TS(0, 3);
 }
 
 __device__ __forceinline__ int seg_len(int32_t m) { return m & 0x7f; }
@@ -274,9 +279,6 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     __shared__ int s_nseq;
     __shared__ unsigned long long s_dtot;
     __shared__ double s_terms[kWalkStage][kUnit];     // term-by-term units of a batch: terms, then values
-    __shared__ double s_val[64][kChainSegs];           // the batch's segment values (wave 0)
-    __shared__ double s_run[64];                       // the translation run ahead of each
-    __shared__ int32_t s_inf[64], s_q[64];
     if (P.lazy && lazy_skip(P)) return;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
 #ifdef FS2_PHASE_TIMING
@@ -382,21 +384,24 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
         }
         __syncthreads();
         if (wid == 0) {
-            // the batch's table in LDS: each unit's segment values and the exact
-            // translation run ahead of it (from the previous listed unit's table
-            // entries, one lane back; the batch before for lane 0)
+            // the batch's table in registers, one unit per lane: its segment values
+            // and the exact translation run ahead of it (from the previous listed
+            // unit's table entries, one lane back; the batch before for lane 0).  The
+            // serial walk below reads them with readlane (scalar operands of the
+            // adds), not through LDS: one dependent fp64 add per step.
+            double rv[kChainSegs];
+#pragma unroll
+            for (int u = 0; u < kChainSegs; ++u) rv[u] = 0.0;
             if (ol < nseq && !(info & 2)) {
                 const UnitRec rr = P.urec[q];
 #pragma unroll
-                for (int u = 0; u < kChainSegs; ++u) s_val[lane][u] = rr.val[u];
+                for (int u = 0; u < kChainSegs; ++u) rv[u] = rr.val[u];
             }
             const unsigned long long gp = __shfl_up(g, 1, 64);
             const int Ep = __shfl_up(En, 1, 64);
             const unsigned long long gb = (lane == 0) ? gprev : gp;
             const int Eb = (lane == 0) ? Eprev : Ep;
-            s_run[lane] = (ol > 0 && ol < nseq) ? (double)(long long)(g - gb) * unit_ulp(Eb) : 0.0;
-            s_inf[lane] = info;
-            s_q[lane] = (int32_t)q;
+            const double run = (ol > 0 && ol < nseq) ? (double)(long long)(g - gb) * unit_ulp(Eb) : 0.0;
             gprev = bcast_i64((long long)g, nb - 1);
             Eprev = __builtin_amdgcn_readlane(En, nb - 1);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -406,11 +411,11 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
             double my_entry = 0.0, my_out = 0.0;      // lane j keeps unit o0 + j's values
             int r = 0;                                // term-by-term units seen
             for (int j = 0; j < nb; ++j) {
-                const int32_t infoj = s_inf[j];
-                s = s + s_run[j];                     // the translation run between (exact)
+                const int32_t infoj = __builtin_amdgcn_readlane(info, j);
+                s = s + bcast(run, j);                // the translation run between (exact)
                 if (lane == j) my_entry = s;
                 if (infoj & 2) {
-                    const int64_t qj = s_q[j];
+                    const int64_t qj = (int64_t)__builtin_amdgcn_readlane((int)q, j);
 #ifdef FS2_PHASE_TIMING
                     if (t == 0) atomicAdd(&g_chain[6], 1ull);
 #endif
@@ -430,14 +435,11 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
                 } else {
                     // one add per segment (unit 0: the value after it, set)
                     const int ns = unit_nseg(infoj);
-                    double v[kChainSegs];
-#pragma unroll
-                    for (int u = 0; u < kChainSegs; ++u) v[u] = s_val[j][u];
-                    if (s_q[j] == 0) s = v[0];
+                    if (__builtin_amdgcn_readlane((int)q, j) == 0) s = bcast(rv[0], j);
                     else {
 #pragma unroll
                         for (int u = 0; u < kChainSegs; ++u)
-                            if (u < ns) s = s + v[u];
+                            if (u < ns) s = s + bcast(rv[u], j);
                     }
                 }
                 if (lane == j) my_out = s;
@@ -567,5 +569,9 @@ bool np_tail_plan(int64_t n, NpTailPlan *out) {
     }
     return true;
 }
+
+#ifdef FS2_PHASE_TIMING
+FS2_TAIL_READER(debug_tail_times_exact)
+#endif
 
 }  // namespace fs2

@@ -289,8 +289,9 @@ struct ReduceParams {
     double *np_part;         // exact: numpy chunk sums of w'^2 (k_finalize, beyond its LDS stage)
     int32_t n_np;            // their count
     double *np_leaf;         // exact: numpy's 128-element leaves of the full chunks (k_normalize)
-    int32_t chunked;         // exact: k_normalize_chunks left np.sum's chunk terms in np_part and
-                             // the partials per 8192-weight chunk (nparts = n_np)
+    int32_t chunked;         // exact: k_normalize_chunks left np.sum's half-chunk terms in np_part
+                             // and its partials (nparts = normalize_chunk_parts(n))
+    double *part_pose;       // chunked: [3 nparts] pose of each partial's first maximum
     const NpTailPlan *np_tail;   // exact: the partial last chunk's tree (null: none)
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
@@ -429,9 +430,11 @@ hipError_t launch_candidates(const UpdateParams &p, hipStream_t s, hipEvent_t e0
 hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_wsum(const ReduceParams &p, hipStream_t s, hipEvent_t e0 = nullptr);
 hipError_t launch_normalize(const ReduceParams &p, hipStream_t s);
-// exact mode: normalise + numpy's Sigma w'^2 per 8192-weight chunk + chunk partials
-// (then k_finalize with ReduceParams.chunked)
+// exact mode: normalise + numpy's Sigma w'^2 per 4096-weight half chunk (a partial
+// last chunk whole) + per-workgroup partials, then k_finalize_chunked (one wave)
 hipError_t launch_normalize_chunks(const ReduceParams &p, hipStream_t s);
+int32_t normalize_chunk_parts(int64_t n);          // workgroups (partials) of launch_normalize_chunks
+hipError_t launch_finalize_chunked(const ReduceParams &p, hipStream_t s);
 hipError_t launch_global_total(const ReduceParams &p, hipStream_t s);
 hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s);
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s);
@@ -469,6 +472,9 @@ hipError_t debug_phase_times(unsigned long long out[8], int reset);
 hipError_t debug_icp_phase_times(unsigned long long out[4], int reset);
 hipError_t debug_chain_times(unsigned long long out[8], int reset);
 hipError_t debug_fin_times(unsigned long long out[8], int reset);
+hipError_t debug_tail_times_update(unsigned long long out[32], int reset);
+hipError_t debug_tail_times_exact(unsigned long long out[32], int reset);
+hipError_t debug_tail_times_resample(unsigned long long out[32], int reset);
 #endif
 // particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
 // alloc.rbase + p * lm_cap + j

@@ -7,6 +7,36 @@
 
 namespace fs2 {
 
+// Optional stamps of the tail kernels (build with -DFS2_PHASE_TIMING; read with
+// fs2_debug_tail_times): workgroup 0, thread 0, s_memrealtime (100 MHz) deltas
+// summed per slot; slot base + k - 1 gets the time from stamp k - 1 to stamp k.
+#ifdef FS2_PHASE_TIMING
+// one copy per translation unit (no relocatable device code); each unit with
+// stamps defines its reader with FS2_TAIL_READER, fs2_debug_tail_times adds them
+static __device__ unsigned long long g_tail[32];
+#define FS2_TAIL_READER(name)                                                                \
+    hipError_t name(unsigned long long out[32], int reset) {                                 \
+        hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 32); \
+        if (e == hipSuccess && reset) {                                                      \
+            unsigned long long z[32] = {};                                                   \
+            e = hipMemcpyToSymbol(HIP_SYMBOL(g_tail), z, sizeof z);                          \
+        }                                                                                    \
+        return e;                                                                            \
+    }
+#define FS2_TS_DECL unsigned long long ts_last_ = 0
+#define FS2_TS(base, k)                                                                      \
+    do {                                                                                     \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                           \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                  \
+            if ((k) > 0) atomicAdd(&g_tail[(base) + (k) - 1], t_ - ts_last_);               \
+            ts_last_ = t_;                                                                   \
+        }                                                                                    \
+    } while (0)
+#else
+#define FS2_TS_DECL do { } while (0)
+#define FS2_TS(base, k) do { } while (0)
+#endif
+
 // ------------------------------------------------------------ reductions ---
 //
 // Wave scans and reductions on DPP (gfx9 row_shr 1/2/4/8, then row_bcast 15/31):

@@ -131,11 +131,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
         }
     };
     load_parts(threadIdx.x);
-    if (P.exact && P.chunked) {
-        // k_normalize_chunks left every chunk's term: staged for thread 0's sum in order
-        const int nl = min(P.n_np, kNpStage);
-        for (int k = threadIdx.x; k < nl; k += 1024) s_np[k] = P.np_part[k];
-    } else if (P.exact) {
+    if (P.exact) {
         // numpy's chunk sums: each full chunk's 64 leaves (k_normalize) as a balanced
         // tree in order (a wave per chunk, xor butterflies; 16 chunks' loads in
         // flight) on waves 0..14, the partial last chunk by numpy's recursion on
@@ -253,6 +249,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
 }
 
 #ifdef FS2_PHASE_TIMING
+FS2_TAIL_READER(debug_tail_times_resample)
 hipError_t debug_fin_times(unsigned long long out[8], int reset) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin), sizeof(unsigned long long) * 8);
     if (e == hipSuccess && reset) {
@@ -262,6 +259,104 @@ hipError_t debug_fin_times(unsigned long long out[8], int reset) {
     return e;
 }
 #endif
+
+// One GPU, exact mode, after k_normalize_chunks: its partials (half-chunk sums
+// of numpy's Sigma w'^2, first maxima with their poses, largest maps) folded by
+// one wave -- no workgroup barrier, no dependent load -- then the same record,
+// decision, estimate and u0 as k_finalize (fast_slam_2.py:60-67, 201-223), and the
+// publication when the rule did not fire.
+__global__ __launch_bounds__(64) void k_finalize_chunked(const ReduceParams P) {
+    __shared__ double s_np[kNpStage];
+    FS2_TS_DECL;
+    FS2_TS(24, 0);
+    const int lane = threadIdx.x;
+    double bv = -INFINITY, px = 0.0, py = 0.0, pyaw = 0.0;
+    int64_t bi = INT64_MAX;
+    int mc = 0;
+    for (int k0 = 0; k0 < P.nparts; k0 += 256) {
+        double w4[4], x4[4], y4[4], a4[4], s4[4];
+        int64_t i4[4];
+        int m4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + 64 * u + lane;
+            const bool in = k < P.nparts;
+            w4[u] = in ? P.part_best_w[k] : -INFINITY;
+            i4[u] = in ? P.part_best_i[k] : INT64_MAX;
+            m4[u] = in ? P.part_maxcnt[k] : 0;
+            s4[u] = in ? P.np_part[k] : 0.0;
+            x4[u] = in ? P.part_pose[3 * (int64_t)k] : 0.0;
+            y4[u] = in ? P.part_pose[3 * (int64_t)k + 1] : 0.0;
+            a4[u] = in ? P.part_pose[3 * (int64_t)k + 2] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + 64 * u + lane;
+            if (w4[u] > bv || (w4[u] == bv && i4[u] < bi)) {
+                bv = w4[u];
+                bi = i4[u];
+                px = x4[u];
+                py = y4[u];
+                pyaw = a4[u];
+            }
+            mc = max(mc, m4[u]);
+            if (k < P.nparts && k < kNpStage) s_np[k] = s4[u];
+        }
+    }
+    FS2_TS(24, 1);
+    // first maximum over the wave, its pose carried along (lowest index on ties)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double v2 = __shfl_xor(bv, o, 64), x2 = __shfl_xor(px, o, 64), y2 = __shfl_xor(py, o, 64),
+                     a2 = __shfl_xor(pyaw, o, 64);
+        const int64_t i2 = __shfl_xor(bi, o, 64);
+        if (v2 > bv || (v2 == bv && i2 < bi)) {
+            bv = v2;
+            bi = i2;
+            px = x2;
+            py = y2;
+            pyaw = a2;
+        }
+    }
+    mc = wave_max_i(mc);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __shared__ int s_kept;
+    if (lane == 0) {
+        // np.sum(weights ** 2): chunk c = half 2c + half 2c + 1 (numpy's top node),
+        // a partial last chunk whole; the chunk sums in order
+        const int64_t nfull = P.n / kNpChunk;
+        auto part = [&](int64_t k) -> double { return k < kNpStage ? s_np[k] : P.np_part[k]; };
+        double sq = 0.0;
+        for (int64_t c = 0; c < nfull; ++c) {
+            const double v = part(2 * c) + part(2 * c + 1);
+            sq = (c == 0) ? v : sq + v;
+        }
+        if (P.n % kNpChunk) sq = (nfull == 0) ? part(2 * nfull) : sq + part(2 * nfull);
+        RankRecord r{};
+        r.sumsq = sq;
+        r.best_w = bv;
+        r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.gidx0 + bi;
+        r.pose[0] = px;
+        r.pose[1] = py;
+        r.pose[2] = pyaw;
+        r.t_local = P.stats->t_local;
+        r.max_count = mc;
+        *P.rec = r;
+        global_finalize_impl(P, [&](int) -> const RankRecord & { return r; });
+        s_kept = (P.pub_flag != nullptr && !P.stats->resampled) ? 1 : 0;
+    }
+    FS2_TS(24, 2);
+    __syncthreads();
+    if (s_kept) publish_body(P.stats, P.pub_host, P.pub_flag, P.pub_seq);
+    FS2_TS(24, 3);
+}
+
+hipError_t launch_finalize_chunked(const ReduceParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize_chunked, dim3(1), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
 
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, p);
@@ -368,7 +463,9 @@ __device__ void publish_body(DevStats *stats, DevStats *host_stats, unsigned lon
         reinterpret_cast<uint64_t *>(host_stats)[t] = v;
         s[t] = 0;                    // the next scan's counters start from zero
     }
-    __threadfence_system();
+    // the barrier completes every thread's stores; thread 0's system-scope release
+    // (cumulative) then orders all of them before the flag -- one cache write-back,
+    // not one per thread
     __syncthreads();
     if (t == 0) __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -387,8 +484,7 @@ __global__ __launch_bounds__(256) void k_post(const DevStats *stats, const int64
     const int t = threadIdx.x;
     if (t < W) reinterpret_cast<uint64_t *>(host)[t] = reinterpret_cast<const uint64_t *>(stats)[t];
     for (int k = t; k < nx; k += blockDim.x) reinterpret_cast<int64_t *>(host + sizeof(DevStats))[k] = xmat[k];
-    __threadfence_system();
-    __syncthreads();
+    __syncthreads();                 // then thread 0's system-scope release orders them all
     if (t == 0) __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

@@ -1016,51 +1016,60 @@ __global__ __launch_bounds__(kBlock) void k_normalize(const ReduceParams P) {
     }
 }
 
-// Exact mode, one 8192-weight numpy chunk per 1024-thread workgroup (8
-// consecutive weights per thread, loaded and stored as 64-byte runs): normalise
-// (fast_slam_2.py:161-175) and, in the same pass, the chunk's term of
-// np.sum(weights ** 2) (:219) by numpy's own tree -- 64 leaves of 128 (8
-// accumulators of 16 squares added in order, combined ((r0 + r1) + (r2 + r3)) +
-// ((r4 + r5) + (r6 + r7))), the leaves paired as a balanced tree in order (DPP,
-// as k_finalize did before) -- or, for a partial last chunk, numpy's recursion
-// (np_tail).  Also per chunk: the first maximum and the largest map (np_part,
-// part_best_*, part_maxcnt: k_finalize reads n_np entries) and the sum of every
-// 256 weights (part_w: the resample chain's block estimates).  One pass over
-// the weights instead of k_normalize + k_finalize's leaf trees.
-__global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P) {
-    __shared__ double s_sq[1024 * 8];            // squares, thread-major (numpy's leaf order)
-    __shared__ double s_leaf[64];
-    __shared__ double s_bv[16];
-    __shared__ int64_t s_bi[16];
-    __shared__ int s_mc[16];
+// Exact mode: normalise (fast_slam_2.py:161-175) and, in the same pass, the terms
+// of np.sum(weights ** 2) (:219) by numpy's own trees.  numpy sums 8192-weight
+// chunks pairwise (the chunk sums then in order); an 8192 chunk's tree is the sum
+// of its two 4096 halves, each a balanced tree of 32 leaves of 128 (8 accumulators
+// of 16 squares added in order, combined ((r0 + r1) + (r2 + r3)) + ((r4 + r5) +
+// (r6 + r7))).  So workgroup b < 2 nfull takes half-chunk b (4 weights per thread,
+// loaded and stored as 32-byte runs) and leaves its half sum in np_part[b]; a
+// partial last chunk (numpy's recursion, np_tail) is one workgroup with 8 weights
+// per thread.  Per workgroup also: the first maximum with its pose (part_best_*,
+// part_pose: no dependent load left for k_finalize_chunked), the largest map
+// (part_maxcnt), and the sum of every 256 weights (part_w: the resample chain's
+// block estimates).  One pass over the weights instead of k_normalize + the leaf
+// trees of k_finalize.
+template <int EPT>
+__device__ __forceinline__ void normalize_span(const ReduceParams &P, int64_t e0, bool tree, double *s_sq,
+                                               double *s_leaf, double *s_bv, int64_t *s_bi, int *s_mc,
+                                               double &chunk_out, double (&pose_out)[3]) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int64_t c0 = (int64_t)blockIdx.x * kNpChunk;
-    const int64_t e0 = c0 + 8 * (int64_t)t;
     const int64_t n = P.n;
-    const bool full = c0 + kNpChunk <= n;
+    const int64_t b0 = e0 + (int64_t)EPT * t;            // this thread's first weight
     const double total = P.stats->total;
-    double w[8];
-    int cn[8];
-    if (e0 + 8 <= n) {
-        const double2 *wp = reinterpret_cast<const double2 *>(P.w + e0);
-        const int4 *cp = reinterpret_cast<const int4 *>(P.cnt + e0);
-        const double2 a = wp[0], b = wp[1], c = wp[2], d = wp[3];
-        const int4 x = cp[0], y = cp[1];
-        w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y; w[4] = c.x; w[5] = c.y; w[6] = d.x; w[7] = d.y;
-        cn[0] = x.x; cn[1] = x.y; cn[2] = x.z; cn[3] = x.w; cn[4] = y.x; cn[5] = y.y; cn[6] = y.z; cn[7] = y.w;
+    double w[EPT];
+    int cn[EPT];
+    if (b0 + EPT <= n) {
+        const double2 *wp = reinterpret_cast<const double2 *>(P.w + b0);
+        const int4 *cp = reinterpret_cast<const int4 *>(P.cnt + b0);
+#pragma unroll
+        for (int h = 0; h < EPT / 2; ++h) {
+            const double2 v = wp[h];
+            w[2 * h] = v.x;
+            w[2 * h + 1] = v.y;
+        }
+#pragma unroll
+        for (int h = 0; h < EPT / 4; ++h) {
+            const int4 v = cp[h];
+            cn[4 * h] = v.x;
+            cn[4 * h + 1] = v.y;
+            cn[4 * h + 2] = v.z;
+            cn[4 * h + 3] = v.w;
+        }
     } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            w[j] = (e0 + j < n) ? P.w[e0 + j] : 0.0;
-            cn[j] = (e0 + j < n) ? P.cnt[e0 + j] : 0;
+        for (int j = 0; j < EPT; ++j) {
+            w[j] = (b0 + j < n) ? P.w[b0 + j] : 0.0;
+            cn[j] = (b0 + j < n) ? P.cnt[b0 + j] : 0;
         }
     }
     double ws = 0.0, bv = -INFINITY;
     int64_t bi = INT64_MAX;
     int mc = 0;
+    FS2_TS(16, 1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const bool live = e0 + j < n;
+    for (int j = 0; j < EPT; ++j) {
+        const bool live = b0 + j < n;
         double v = w[j];
         if (total < P.floor) v = 1.0 / (double)P.n_global;
         else v = (v < P.floor) ? v : v / total;
@@ -1068,29 +1077,27 @@ __global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P)
         ws += w[j];
         if (live && v > bv) {                    // ascending index: the first maximum stays
             bv = v;
-            bi = e0 + j;
+            bi = b0 + j;
         }
         mc = max(mc, live ? cn[j] : 0);
-        s_sq[8 * t + j] = w[j] * w[j];
+        if (tree) s_sq[EPT * t + j] = w[j] * w[j];
     }
-    if (e0 + 8 <= n) {
-        double2 *wp = reinterpret_cast<double2 *>(P.w + e0);
-        wp[0] = make_double2(w[0], w[1]);
-        wp[1] = make_double2(w[2], w[3]);
-        wp[2] = make_double2(w[4], w[5]);
-        wp[3] = make_double2(w[6], w[7]);
+    if (b0 + EPT <= n) {
+        double2 *wp = reinterpret_cast<double2 *>(P.w + b0);
+#pragma unroll
+        for (int h = 0; h < EPT / 2; ++h) wp[h] = make_double2(w[2 * h], w[2 * h + 1]);
     } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (e0 + j < n) P.w[e0 + j] = w[j];
+        for (int j = 0; j < EPT; ++j)
+            if (b0 + j < n) P.w[b0 + j] = w[j];
     }
-    // the resample chain's estimate of each 256-weight block (32 threads)
+    // the resample chain's estimate of each 256-weight block (256 / EPT threads)
     {
         double v = ws;
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
-        const int64_t blk = c0 / kBlock + (t >> 5);
-        if ((t & 31) == 0 && blk * kBlock < n && P.part_w) P.part_w[blk] = v;
+        for (int o = 1; o < kBlock / EPT; o <<= 1) v += __shfl_xor(v, o, 64);
+        const int64_t blk = b0 / kBlock;
+        if ((t & (kBlock / EPT - 1)) == 0 && blk * kBlock < n && P.part_w) P.part_w[blk] = v;
     }
     wave_argmax(bv, bi);
     mc = wave_max_i(mc);
@@ -1100,12 +1107,28 @@ __global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P)
         s_mc[wid] = mc;
     }
     __syncthreads();                             // s_sq, s_bv written (global w' too)
+    FS2_TS(16, 2);
+    // the workgroup's first maximum, and its pose requested before the tree below
+    double v = s_bv[0];
+    int64_t ix = s_bi[0];
+    int m = s_mc[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+        argmax_combine(v, ix, s_bv[k], s_bi[k]);
+        m = max(m, s_mc[k]);
+    }
+    if (t == 0 && ix != INT64_MAX) {
+        pose_out[0] = P.x[ix];
+        pose_out[1] = P.y[ix];
+        pose_out[2] = P.yaw[ix];
+    }
     double chunk = 0.0;
-    if (full) {
-        // accumulator k of leaf L: its squares 8 q + k, q = 0..15, added in order
-        if (t < 512) {
+    if (tree) {
+        // accumulator k of leaf L: the leaf's squares 8 q + k, q = 0..15, added in order
+        constexpr int NL = 1024 * EPT / 128;     // leaves
+        if (t < 8 * NL) {
             const int L = t >> 3, k = t & 7;
-            const double *q0 = s_sq + (16 * L) * 8 + k;
+            const double *q0 = s_sq + 128 * L + k;
             double r = q0[0];
 #pragma unroll
             for (int q = 1; q < 16; ++q) r += q0[8 * q];
@@ -1115,28 +1138,50 @@ __global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P)
             if (k == 0) s_leaf[L] = r;
         }
         __syncthreads();
-        if (wid == 0) chunk = lane63(dpp_scan(s_leaf[lane], 0.0, [](double a, double b) { return a + b; }));
+        // the leaves as a balanced tree in order (DPP rows of 16, then row pairs;
+        // lanes past the leaves add +0)
+        if (wid == 0) chunk = lane63(dpp_scan(lane < NL ? s_leaf[lane] : 0.0, 0.0,
+                                              [](double a, double b) { return a + b; }));
     } else if (wid == 0 && P.np_tail) {
-        chunk = np_pairwise_wave(P.w + c0, P.np_tail);   // this workgroup's own stores, after the barrier
+        chunk = np_pairwise_wave(P.w + e0, P.np_tail);   // this workgroup's own stores, after the barrier
     }
+    FS2_TS(16, 3);
     if (t == 0) {
-        double v = s_bv[0];
-        int64_t ix = s_bi[0];
-        int m = s_mc[0];
-#pragma unroll
-        for (int k = 1; k < 16; ++k) {
-            argmax_combine(v, ix, s_bv[k], s_bi[k]);
-            m = max(m, s_mc[k]);
-        }
-        P.np_part[blockIdx.x] = chunk;
+        chunk_out = chunk;
         P.part_best_w[blockIdx.x] = v;
         P.part_best_i[blockIdx.x] = ix;
         P.part_maxcnt[blockIdx.x] = m;
     }
 }
 
+__global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P) {
+    __shared__ double s_sq[1024 * 4];            // squares of the half chunk, in weight order
+    __shared__ double s_leaf[64];
+    __shared__ double s_bv[16];
+    __shared__ int64_t s_bi[16];
+    __shared__ int s_mc[16];
+    FS2_TS_DECL;
+    FS2_TS(16, 0);
+    const int64_t nfull = P.n / kNpChunk;
+    double chunk = 0.0, pose[3] = {0.0, 0.0, 0.0};
+    if ((int64_t)blockIdx.x < 2 * nfull)
+        normalize_span<4>(P, (int64_t)blockIdx.x * (kNpChunk / 2), true, s_sq, s_leaf, s_bv, s_bi, s_mc, chunk, pose);
+    else
+        normalize_span<8>(P, nfull * kNpChunk, false, s_sq, s_leaf, s_bv, s_bi, s_mc, chunk, pose);
+    if (threadIdx.x == 0) {
+        P.np_part[blockIdx.x] = chunk;
+        P.part_pose[3 * (int64_t)blockIdx.x] = pose[0];
+        P.part_pose[3 * (int64_t)blockIdx.x + 1] = pose[1];
+        P.part_pose[3 * (int64_t)blockIdx.x + 2] = pose[2];
+    }
+}
+
+int32_t normalize_chunk_parts(int64_t n) {
+    return (int32_t)(2 * (n / kNpChunk) + ((n % kNpChunk) ? 1 : 0));
+}
+
 hipError_t launch_normalize_chunks(const ReduceParams &p, hipStream_t s) {
-    const unsigned grid = (unsigned)((p.n + kNpChunk - 1) / kNpChunk);
+    const unsigned grid = (unsigned)normalize_chunk_parts(p.n);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(k_normalize_chunks, dim3(grid), dim3(1024), 0, s, p);
     return hipGetLastError();
@@ -1273,6 +1318,10 @@ hipError_t debug_phase_times(unsigned long long out[8], int reset) {
     }
     return e;
 }
+#endif
+
+#ifdef FS2_PHASE_TIMING
+FS2_TAIL_READER(debug_tail_times_update)
 #endif
 
 }  // namespace fs2
