@@ -1066,7 +1066,6 @@ __device__ __forceinline__ void normalize_span(const ReduceParams &P, int64_t e0
     double ws = 0.0, bv = -INFINITY;
     int64_t bi = INT64_MAX;
     int mc = 0;
-    FS2_TS(16, 1);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const bool live = b0 + j < n;
@@ -1107,7 +1106,6 @@ __device__ __forceinline__ void normalize_span(const ReduceParams &P, int64_t e0
         s_mc[wid] = mc;
     }
     __syncthreads();                             // s_sq, s_bv written (global w' too)
-    FS2_TS(16, 2);
     // the workgroup's first maximum, and its pose requested before the tree below
     double v = s_bv[0];
     int64_t ix = s_bi[0];
@@ -1145,7 +1143,6 @@ __device__ __forceinline__ void normalize_span(const ReduceParams &P, int64_t e0
     } else if (wid == 0 && P.np_tail) {
         chunk = np_pairwise_wave(P.w + e0, P.np_tail);   // this workgroup's own stores, after the barrier
     }
-    FS2_TS(16, 3);
     if (t == 0) {
         chunk_out = chunk;
         P.part_best_w[blockIdx.x] = v;
@@ -1168,6 +1165,7 @@ __global__ __launch_bounds__(1024) void k_normalize_chunks(const ReduceParams P)
         normalize_span<4>(P, (int64_t)blockIdx.x * (kNpChunk / 2), true, s_sq, s_leaf, s_bv, s_bi, s_mc, chunk, pose);
     else
         normalize_span<8>(P, nfull * kNpChunk, false, s_sq, s_leaf, s_bv, s_bi, s_mc, chunk, pose);
+    FS2_TS(16, 1);
     if (threadIdx.x == 0) {
         P.np_part[blockIdx.x] = chunk;
         P.part_pose[3 * (int64_t)blockIdx.x] = pose[0];

@@ -47,8 +47,7 @@ def main():
           f"resampling scan)")
     rows = [("k_chain_units: estimate loads + block sum", 0), ("k_chain_units: unit classification", 1),
             ("k_chain_units: group scan + stores", 2),
-            ("k_normalize_chunks: loads", 16), ("k_normalize_chunks: normalise, stores, barrier", 17),
-            ("k_normalize_chunks: pose + numpy half-chunk tree", 18),
+            ("k_normalize_chunks: workgroup 0 (to its partials)", 16),
             ("k_finalize_chunked: partial loads", 24), ("k_finalize_chunked: reductions + record + decision", 25),
             ("k_finalize_chunked: publication", 26)]
     for name, k in rows:
