@@ -205,6 +205,10 @@ def cpu_baseline(L, P, budget_s, seed):
         return n * scans / t_work, scans, t_work
 
     threads = orc.threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = None
     model = "unknown"
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
@@ -215,10 +219,12 @@ def cpu_baseline(L, P, budget_s, seed):
     many, sm, tm = run(n, threads, budget_s / 2)
     orc.set_threads(threads)
     return dict(value=many, unit="particle-updates/s", cores=threads, kind="port",
-                cpu_model=model, host_cpus=os.cpu_count(),
+                cpu_model=model, host_cpus=os.cpu_count(), affinity_cpus=affinity,
                 single_thread_value=one,
                 sample=f"{n} particles x {L} landmarks, M=4, {sm} scans on {threads} OpenMP threads "
-                       f"({tm:.1f} s); 1 thread: 6000 particles, {s1} scans ({t1:.1f} s); "
+                       f"(OMP_NUM_THREADS; {affinity} CPUs in this process's affinity mask of "
+                       f"{os.cpu_count()} on the host) ({tm:.1f} s); 1 thread: 6000 particles, {s1} scans "
+                       f"({t1:.1f} s); "
                        f"C oracle, reference semantics and reference algorithm (first-match linear "
                        f"scan of every map, deep-copied maps on resample): the ratio to the GPU "
                        f"value mixes algorithm (pruning, page sharing) with hardware")

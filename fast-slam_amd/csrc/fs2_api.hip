@@ -165,8 +165,10 @@ struct fs2_handle {
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr;
     uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
-    std::vector<char *> sendbuf, recvbuf;
-    std::vector<size_t> sendcap, recvcap;
+    // the sharded resample's transfers: one send and one receive arena, each
+    // destination's (source's) transfer at an aligned offset
+    char *sarena = nullptr, *rarena = nullptr;
+    size_t scap = 0, rcap = 0;
     int32_t n_recv = 0;                             // particles received by the last resample
 
     // exact-order reductions (fs2_exact.hip)
@@ -379,18 +381,21 @@ static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
     return FS2_OK;
 }
 
-static int ensure_buf(fs2_handle *h, std::vector<char *> &bufs, std::vector<size_t> &caps, int p,
-                      size_t bytes) {
-    if (caps[p] >= bytes) return FS2_OK;
+// An arena of at least `bytes` (grown by half again, the stream drained first:
+// earlier transfers may still use the old one).  Sized at creation for the first
+// resamples, so a timed scan normally never allocates.
+static int ensure_arena(fs2_handle *h, char *&buf, size_t &cap, size_t bytes) {
+    if (cap >= bytes) return FS2_OK;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
-    hipFree(bufs[p]);
-    bufs[p] = nullptr;
-    caps[p] = 0;
-    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 20);
-    HIP_TRY(h, hipMalloc(&bufs[p], want));
-    caps[p] = want;
+    hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+    HIP_TRY(h, hipMalloc(&buf, want));
+    cap = want;
     return FS2_OK;
 }
+static size_t arena_align(size_t b) { return (b + 255) & ~size_t(255); }
 
 // Wait for a post (k_post / k_publish) whose flag reaches seq: spin for up to
 // 50 ms, then fall back to a stream sync, which also reports a fault.
@@ -519,6 +524,17 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     static const bool log_xfer = std::getenv("FS2_XFER_LOG") != nullptr;
     int64_t nsend = 0;
     std::vector<fs2comm::Xfer> sends, recvs;
+    // every destination's transfer at its offset in the send arena, every source's
+    // in the receive arena
+    size_t soff[kMaxRanks + 1] = {}, roff[kMaxRanks + 1] = {};
+    for (int p = 0; p < G; ++p) {
+        const bool so = p != R && at(R, p, 0) > 0, ro = p != R && at(p, R, 0) > 0;
+        soff[p + 1] = soff[p] + (so ? arena_align((size_t)xfer_bytes(at(R, p, 0), at(R, p, 1), at(R, p, 2), at(R, p, 3))) : 0);
+        roff[p + 1] = roff[p] + (ro ? arena_align((size_t)xfer_bytes(at(p, R, 0), at(p, R, 1), at(p, R, 2), at(p, R, 3))) : 0);
+    }
+    rc = ensure_arena(h, h->sarena, h->scap, soff[G]);
+    if (!rc) rc = ensure_arena(h, h->rarena, h->rcap, roff[G]);
+    if (rc) return rc;
     for (int p = 0; p < G; ++p) {
         rs.sbuf[p] = nullptr;
         T.ubase[p + 1] = T.ubase[p] + (p == R ? 0 : at(R, p, 2));
@@ -531,10 +547,8 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
                          (long long)xfer_bytes(K, S, U, C));
         if (p == R || K == 0) continue;
         const size_t bytes = (size_t)xfer_bytes(K, S, U, C);
-        rc = ensure_buf(h, h->sendbuf, h->sendcap, p, bytes);
-        if (rc) return rc;
-        rs.sbuf[p] = h->sendbuf[p];
-        sends.push_back({p, h->sendbuf[p], bytes});
+        rs.sbuf[p] = h->sarena + soff[p];
+        sends.push_back({p, rs.sbuf[p], bytes});
         nsend += K;
     }
     if (nsend > INT32_MAX) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld particles to send", (long long)nsend);
@@ -547,14 +561,13 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         const int64_t K = at(q, R, 0), S = at(q, R, 1), U = at(q, R, 2), C = at(q, R, 3);
         if (!K) continue;
         const size_t bytes = (size_t)xfer_bytes(K, S, U, C);
-        rc = ensure_buf(h, h->recvbuf, h->recvcap, q, bytes);
-        if (rc) return rc;
-        recvs.push_back({q, h->recvbuf[q], bytes});
+        char *rb = h->rarena + roff[q];
+        recvs.push_back({q, rb, bytes});
         RecvPeer &pp = rs.peers[rs.npeers++];
-        pp.hdr = reinterpret_cast<const PackHeader *>(h->recvbuf[q]);
-        pp.idx = reinterpret_cast<const uint32_t *>(h->recvbuf[q] + xfer_idx_off(K));
-        pp.pages = reinterpret_cast<const XferPage *>(h->recvbuf[q] + xfer_page_off(K, S));
-        pp.covs = reinterpret_cast<const double2 *>(h->recvbuf[q] + xfer_cov_off(K, S, U));
+        pp.hdr = reinterpret_cast<const PackHeader *>(rb);
+        pp.idx = reinterpret_cast<const uint32_t *>(rb + xfer_idx_off(K));
+        pp.pages = reinterpret_cast<const XferPage *>(rb + xfer_page_off(K, S));
+        pp.covs = reinterpret_cast<const double2 *>(rb + xfer_cov_off(K, S, U));
         pp.K = (int32_t)K;
         pp.kbase = kbase;
         pp.U = U;
@@ -677,8 +690,8 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
-    for (char *b : h->sendbuf) hipFree(b);
-    for (char *b : h->recvbuf) hipFree(b);
+    hipFree(h->sarena);
+    hipFree(h->rarena);
     hipFree(h->cand); hipFree(h->ncand);
     hipFree(h->uinfo); hipFree(h->uol); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ugl);
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
@@ -861,25 +874,23 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     rc = grow_recs(h, cfg->record_pool > 0 ? cfg->record_pool
                                             : n * h->cap + n * h->cap / 4 + 64 * n + recv_recs + 1024);
     if (rc) return fail(rc);
-    h->sendbuf.assign(G, nullptr);
-    h->recvbuf.assign(G, nullptr);
-    h->sendcap.assign(G, 0);
-    h->recvcap.assign(G, 0);
     if (G > 1) {
         // the sharded resample's buffers, made here rather than in a timed scan: the
-        // dedup table and transfers to / from the neighbouring ranks for a quarter
-        // of the shard with nothing shared (the first resamples)
-        const int64_t K = n / 4 + 1, S = K * h->rows;
+        // dedup table, the send and receive arenas for half the shard with nothing
+        // shared (the first resamples move up to ~40 % of a rank's particles, to up
+        // to three ranks), and the received particles' rows and pages
+        const int64_t K = n / 2 + 1, S = K * h->rows;
         int lg = 10;
         while ((int64_t(1) << lg) < 2 * S && lg < 31) ++lg;
         rc = reserve_xfer_table(h, int64_t(1) << lg, S);
-        const size_t bytes = (size_t)xfer_bytes(K, S, S, 0);
-        for (int p = (int)r - 1; !rc && p <= (int)r + 1; p += 2) {
-            if (p < 0 || p >= G) continue;
-            rc = ensure_buf(h, h->sendbuf, h->sendcap, p, bytes);
-            if (!rc) rc = ensure_buf(h, h->recvbuf, h->recvcap, p, bytes);
-        }
-        if (rc) return fail(rc);
+        const size_t bytes = (size_t)xfer_bytes(K, S, S, 0) + 256 * kMaxRanks;
+        if (!rc) rc = ensure_arena(h, h->sarena, h->scap, bytes);
+        if (!rc) rc = ensure_arena(h, h->rarena, h->rcap, bytes);
+        if (!rc && hipMalloc(&h->rdesc, sizeof(Desc) * (size_t)S) != hipSuccess) rc = FS2_ERR_OOM;
+        if (!rc) h->rdesc_cap = sizeof(Desc) * (size_t)S;
+        if (!rc && hipMalloc(&h->udesc, sizeof(Desc) * (size_t)S) != hipSuccess) rc = FS2_ERR_OOM;
+        if (!rc) h->udesc_cap = sizeof(Desc) * (size_t)S;
+        if (rc) return fail(rc == FS2_ERR_OOM ? set_err(&h->err, rc, "sharded transfer buffers") : rc);
     }
     if (G > 1 || cfg->sharded_path) {
         rc = (cfg->comm_mode == FS2_COMM_LOCAL) ? fs2comm::create_local(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
