@@ -746,8 +746,20 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         return code;
     };
     if (hipSetDevice(cfg->device) != hipSuccess) return fail(set_err(&h->err, FS2_ERR_HIP, "hipSetDevice failed"));
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    // A/B knob (config 4 interference): FS2_MAIN_EXCLUDE_CU=k keeps
+    // the filter's kernels off compute unit k
+    if (const char *e = std::getenv("FS2_MAIN_EXCLUDE_CU")) {
+        hipDeviceProp_t pr{};
+        const int words = hipGetDeviceProperties(&pr, cfg->device) == hipSuccess ? (pr.multiProcessorCount + 31) / 32 : 8;
+        std::vector<uint32_t> mask(words, 0xffffffffu);
+        if (pr.multiProcessorCount % 32) mask[words - 1] = (1u << (pr.multiProcessorCount % 32)) - 1u;
+        const int k = std::atoi(e);
+        if (k >= 0 && k / 32 < words) mask[k / 32] &= ~(1u << (k % 32));
+        if (hipExtStreamCreateWithCUMask(&h->stream, (uint32_t)words, mask.data()) != hipSuccess)
+            return fail(set_err(&h->err, FS2_ERR_HIP, "hipExtStreamCreateWithCUMask failed"));
+    } else if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
+    }
     const int64_t n = std::max<int64_t>(h->n, 1);
     const int64_t nb = (n + kBlock - 1) / kBlock;
     const int64_t nsb = (n + 1023) / 1024;
@@ -1711,6 +1723,12 @@ struct IcpQueue {
 std::mutex g_icpq_mu;
 IcpQueue g_icpq[64];
 
+int cu_mask_words(int32_t device) {
+    hipDeviceProp_t pr{};
+    if (hipGetDeviceProperties(&pr, device) != hipSuccess) return 8;
+    return (pr.multiProcessorCount + 31) / 32;
+}
+
 int icpq_get(int32_t device, IcpQueue **out) {
     if (device < 0 || device >= 64) return set_err(nullptr, FS2_ERR_ARG, "bad device %d", device);
     int ndev = 0;
@@ -1719,7 +1737,16 @@ int icpq_get(int32_t device, IcpQueue **out) {
     SHIP(hipSetDevice(device));
     IcpQueue &q = g_icpq[device];
     if (!q.stream) {
-        SHIP(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+        // A/B knob (config 4 interference): FS2_ICP_CU=k confines the
+        // alignments to compute unit k
+        if (const char *e = std::getenv("FS2_ICP_CU")) {
+            std::vector<uint32_t> mask(cu_mask_words(device), 0u);
+            const int k = std::atoi(e);
+            if (k >= 0 && k / 32 < (int)mask.size()) mask[k / 32] = 1u << (k % 32);
+            SHIP(hipExtStreamCreateWithCUMask(&q.stream, (uint32_t)mask.size(), mask.data()));
+        } else {
+            SHIP(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+        }
         for (IcpSlot &s : q.slot) {
             SHIP(hipHostMalloc((void **)&s.host, 2 * kIcpCloud + 64, hipHostMallocDefault));
             SHIP(hipMalloc(&s.dev, 2 * kIcpCloud + 64));
