@@ -480,27 +480,31 @@ __device__ __forceinline__ uint32_t wave_box_union(uint32_t b) {
     return lo | (hi << 8);
 }
 
-// A workgroup's row boxes in LDS, one array per code (LDS atomics per field).
+// A workgroup's row boxes in LDS as the two packed halves of box_union (lows:
+// x lo | y lo << 16, highs: x hi | y hi << 16): 2 KB for 256 rows.  A merge is a
+// compare-and-swap of the packed min / max, only when the row box grows (rare).
 struct BoxLds {
-    uint32_t xl[kBBoxRows], xh[kBBoxRows], yl[kBBoxRows], yh[kBBoxRows];
+    uint32_t lo[kBBoxRows], hi[kBBoxRows];
 };
 __device__ __forceinline__ void lds_box_set(BoxLds &s, int r, uint32_t b) {
-    s.xl[r] = b & 0xffu;
-    s.xh[r] = (b >> 8) & 0xffu;
-    s.yl[r] = (b >> 16) & 0xffu;
-    s.yh[r] = b >> 24;
+    s.lo[r] = b & kBoxHalf;
+    s.hi[r] = (b >> 8) & kBoxHalf;
 }
-__device__ __forceinline__ uint32_t lds_box_get(const BoxLds &s, int r) {
-    return s.xl[r] | (s.xh[r] << 8) | (s.yl[r] << 16) | (s.yh[r] << 24);
-}
-// grow row r's box to hold b (atomics only when it grows: the row boxes change rarely)
+__device__ __forceinline__ uint32_t lds_box_get(const BoxLds &s, int r) { return s.lo[r] | (s.hi[r] << 8); }
+// grow row r's box to hold b
 __device__ __forceinline__ void lds_box_merge(BoxLds &s, int r, uint32_t b) {
-    const uint32_t cur = lds_box_get(s, r);
-    if (box_union(cur, b) == cur) return;
-    atomicMin(&s.xl[r], b & 0xffu);
-    atomicMax(&s.xh[r], (b >> 8) & 0xffu);
-    atomicMin(&s.yl[r], (b >> 16) & 0xffu);
-    atomicMax(&s.yh[r], b >> 24);
+    const uint32_t blo = b & kBoxHalf, bhi = (b >> 8) & kBoxHalf;
+    uint32_t lo = s.lo[r], hi = s.hi[r];
+    for (uint32_t want = pk_min_u16(lo, blo); want != lo; want = pk_min_u16(lo, blo)) {
+        const uint32_t prev = atomicCAS(&s.lo[r], lo, want);
+        if (prev == lo) break;
+        lo = prev;
+    }
+    for (uint32_t want = pk_max_u16(hi, bhi); want != hi; want = pk_max_u16(hi, bhi)) {
+        const uint32_t prev = atomicCAS(&s.hi[r], hi, want);
+        if (prev == hi) break;
+        hi = prev;
+    }
 }
 
 // Measurements whose band box `s` (page summary or row box) does not lie outside

@@ -309,10 +309,17 @@ template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ Meas s_ms[MAXM];                 // this pass's measurements
     __shared__ double s_lik[MAXM][kBlock];      // per (measurement, lane) likelihood
-    __shared__ int s_idx[MAXM][kBlock];         // per (measurement, lane) association
-    __shared__ uint2 s_cow[kBlock / 64][64 * (MAXM + 1)];   // per wave: (shared page, copy)
+    __shared__ int16_t s_idx[MAXM][kBlock];     // per (measurement, lane) association (slot < 4096, -1, -2)
+    // per wave: the overflow path's per-measurement answers (phase A), then the
+    // page copies' task list (B1) -- the same wave uses them one after the other
+    union WaveScratch {
+        uint2 cow[64 * (MAXM + 1)];             // (shared page, copy)
+        struct {
+            int best[MAXM][64], bpos[MAXM][64];
+        } ov;
+    };
+    __shared__ WaveScratch s_ws[kBlock / 64];
     __shared__ float4 s_mv[MAXM][kBlock];       // new mirrors of the slots phase A modified
-    __shared__ int s_best[MAXM][kBlock], s_bpos[MAXM][kBlock];   // overflow path: per-measurement answer
     __shared__ BoxLds s_bb;                     // this workgroup's row boxes (grown by the writes)
 
 #ifdef FS2_PHASE_TIMING
@@ -325,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     const int64_t n = P.n;
     if (tid < MAXM) s_ms[tid] = Meas{P.meas.d[tid], P.meas.b[tid], P.meas.ox[tid], P.meas.oy[tid]};
 #pragma unroll
-    for (int k = 0; k < MAXM; ++k) s_idx[k][tid] = -2;
+    for (int k = 0; k < MAXM; ++k) s_idx[k][tid] = (int16_t)-2;
     if (P.map.bbox && tid < P.map.rows) lds_box_set(s_bb, tid, P.map.bbox[blk * kBBoxRows + tid]);
     __syncthreads();
 
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             // one EKF site: the matched measurement sees the slot as left by
             // the earlier measurements (fast_slam_2.py:116-153)
             s_lik[km][tid] = ekf_update(s, px, py, pyaw, s_ms[km], R, singular);
-            s_idx[km][tid] = slot;
+            s_idx[km][tid] = (int16_t)slot;
             pend &= ~(1u << km);
             mod = true;
             ok = inv2(s.P, I);
@@ -482,8 +489,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         // (registers are k_update's occupancy limit)
 #pragma unroll
         for (int k = 0; k < MAXM; ++k) {
-            s_best[k][tid] = INT_MAX;
-            s_bpos[k][tid] = -1;
+            s_ws[tid >> 6].ov.best[k][tid & 63] = INT_MAX;
+            s_ws[tid >> 6].ov.bpos[k][tid & 63] = -1;
         }
         int sing = INT_MAX;
         // pre-scan pass over every page (measurements `want`; `skip_mods`: ignore
@@ -514,7 +521,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                     unsigned test = 0u;
 #pragma unroll
                     for (int k = 0; k < MAXM; ++k)
-                        if (((open >> k) & 1u) && slot < s_best[k][tid] &&
+                        if (((open >> k) & 1u) && slot < s_ws[tid >> 6].ov.best[k][tid & 63] &&
                             !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
                             test |= 1u << k;
                     if (!test && !(mirror_s(mv) == 0.0f && slot < sing)) continue;
@@ -531,8 +538,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                             const double qd = quad(I, s_ms[k].ox - s.mx, s_ms[k].oy - s.my);
                             amb += ambiguous(qd, gate2);
                             if (qd >= 0.0 && qd < gate2) {
-                                s_best[k][tid] = slot;
-                                s_bpos[k][tid] = pos;
+                                s_ws[tid >> 6].ov.best[k][tid & 63] = slot;
+                                s_ws[tid >> 6].ov.bpos[k][tid & 63] = pos;
                             }
                         }
                     }
@@ -543,17 +550,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         for (int k = 0; k < MAXM; ++k) {
             if (!((pend >> k) & 1u)) continue;
             int t = -1;                            // the pre-scan answer's slot, if modified since
-            const int pb = s_bpos[k][tid];
+            const int pb = s_ws[tid >> 6].ov.bpos[k][tid & 63];
 #pragma unroll
             for (int q = 0; q < MAXM; ++q)
                 if (q < nmod && pb >= 0 && (int)((mods >> (16 * q)) & 0xffffu) == pb) t = q;
             if (t >= 0) {
                 // rescan this measurement over the unmodified slots
-                s_best[k][tid] = INT_MAX;
-                s_bpos[k][tid] = -1;
+                s_ws[tid >> 6].ov.best[k][tid & 63] = INT_MAX;
+                s_ws[tid >> 6].ov.bpos[k][tid & 63] = -1;
                 scan(1u << k, true);
             }
-            int bk = s_best[k][tid], pk = s_bpos[k][tid];
+            int bk = s_ws[tid >> 6].ov.best[k][tid & 63], pk = s_ws[tid >> 6].ov.bpos[k][tid & 63];
             // the slots modified so far, with their new states
             int tk = -1;
             for (int q = 0; q < nmod; ++q) {
@@ -587,7 +594,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             Slot s = load_rec(map.recs, t2 >= 0 ? sel_u32(t2, frec)
                                                 : mirror_rec(load_mirror(page_of(map, pk, il), pk)));
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, s_ms[k], R, singular);
-            s_idx[k][tid] = bk;
+            s_idx[k][tid] = (int16_t)bk;
             pend &= ~(1u << k);
             if (t2 < 0) {
                 t2 = nmod++;
@@ -654,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 ++cow;
             }
             const uint64_t bm = __ballot(task);
-            if (task) s_cow[wid][T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
+            if (task) s_ws[wid].cow[T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
             T += __popcll(bm);
         }
 #if FS2_B1_DESC_STORE
@@ -676,7 +683,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         auto load_batch = [&](int base, v4i *v, uint32_t *d) {
 #pragma unroll
             for (int u = 0; u < CB; ++u) {
-                const uint2 tk = s_cow[wid][min(base + 8 * u + (lane >> 3), T - 1)];
+                const uint2 tk = s_ws[wid].cow[min(base + 8 * u + (lane >> 3), T - 1)];
                 d[u] = tk.y;
                 v[u] = *reinterpret_cast<const v4i *>(page_ptr(map.pool, tk.x) + off);
             }
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
             if (jh / kPageSlots == arow) ad = merge_summary(ad, mv, map.frame);
             else box_note(jh / kPageSlots, note_write(map, jh, il, mv, false).y);
-            s_idx[k][tid] = c + hit;
+            s_idx[k][tid] = (int16_t)(c + hit);
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
             const Slot s{px + mk.d * cos(pyaw + mk.b), py + mk.d * sin(pyaw + mk.b),
@@ -810,7 +817,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
                 ad = merge_summary(ad, mv, map.frame);
             }
-            s_idx[k][tid] = -1;
+            s_idx[k][tid] = (int16_t)-1;
             ++nap;
             ++appends;
         }
