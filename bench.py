@@ -470,17 +470,31 @@ def main(argv=None):
         if scans_pts is not None and s < total_scans and s not in icp_tickets:
             icp_tickets[s] = fast_slam_2.ICP.submit(scans_pts[s], scans_pts[s + 1])
 
+    icp_host = {"result_ms": 0.0, "submit_ms": 0.0, "odometry_ms": 0.0, "step_ms": 0.0, "scans": 0}
+
     def one_scan(s):
         rot, tr = syn.odometry(s)
         if scans_pts is not None:
+            t0 = time.perf_counter()
             icp_submit(s)
             R, t, _ = icp_tickets.pop(s).result()
+            t1 = time.perf_counter()
             if s + 1 != args.warmup and not args.serial_icp:
                 icp_submit(s + 1)
+            t2 = time.perf_counter()
             # Robot.get_transformation_icp (robot.py:108-120): the commanded linear
             # velocity is nonzero on the driving scans of the odometry pattern
             v = 0.3 if tr != 0 else 0.0
             rot, tr = (float(q) for q in fast_slam_2.Robot.icp_odometry(R, t, v))
+            t3 = time.perf_counter()
+            out = f.step(rot, tr, meas[s])
+            if s >= args.warmup:
+                icp_host["result_ms"] += (t1 - t0) * 1e3
+                icp_host["submit_ms"] += (t2 - t1) * 1e3
+                icp_host["odometry_ms"] += (t3 - t2) * 1e3
+                icp_host["step_ms"] += (time.perf_counter() - t3) * 1e3
+                icp_host["scans"] += 1
+            return out
         return f.step(rot, tr, meas[s])
 
     def barrier():
@@ -648,7 +662,9 @@ def main(argv=None):
                       "pages_opened_per_particle_scan": opened / units,
                       "slots_visited_per_particle_scan": visited / units,
                       "exact_slots_per_particle_scan": exact_slots / units,
-                      "icp_us": icp_us},
+                      "icp_us": icp_us,
+                      "icp_host_ms_per_scan": ({k: v / max(icp_host["scans"], 1) for k, v in icp_host.items()
+                                                if k != "scans"} if scans_pts is not None else None)},
         }
         if migration is not None:
             out["extra"]["migration"] = migration
