@@ -62,6 +62,9 @@ def parse(argv=None):
                          "beside the previous scan's update")
     ap.add_argument("--dry-run", action="store_true",
                     help="with --gpus N > 1 and no WORLD_SIZE: print the ranks' environments, start nothing")
+    ap.add_argument("--probe-side-kernels", type=int, default=0,
+                    help="A/B (config 4 interference): launch this many tiny kernels on a second stream "
+                         "before each scan, as the ICP hand-off does")
     ap.add_argument("--dropin", action="store_true",
                     help="time the drop-in FastSLAM2.iterate() (numpy RNG) beside the device-RNG step")
     return ap.parse_args(argv)
@@ -484,8 +487,15 @@ def main(argv=None):
         rot, tr = (float(q) for q in fast_slam_2.Robot.icp_odometry(R, t, v))
         return rot, tr, (time.perf_counter() - t0) * 1e3
 
+    side = torch.cuda.Stream() if args.probe_side_kernels else None
+    side_x = torch.zeros(64, device="cuda") if side is not None else None
+
     def one_scan(s):
         rot, tr = syn.odometry(s)
+        if side is not None:
+            with torch.cuda.stream(side):
+                for _ in range(args.probe_side_kernels):
+                    side_x.add_(1.0)
         if scans_pts is not None:
             t0 = time.perf_counter()
             fut = icp_tickets.pop(s, None)
