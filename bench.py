@@ -464,19 +464,16 @@ def main(argv=None):
     meas = [np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64)
             for s in range(total_scans)]
 
-    # ICP of scan s+1 runs beside scan s's filter update: a worker thread submits
-    # the alignment, waits for it and turns it into odometry
-    # (Robot.get_transformation_icp, robot.py:108-120) while this thread is inside
-    # step(s) (ctypes releases the GIL), so the hand-off's host time (~0.1 ms of HIP
-    # calls, event wait, numpy) stays off the scan's critical path.  The timed
-    # region's first scan prepares its own, so exactly one alignment per timed
-    # scan runs inside the timing.
-    icp_tickets = {}
+    # ICP of scan s+1 runs beside scan s's filter update: the scan is enqueued
+    # (step_submit: fs2_iterate_submit), then this thread hands the next alignment
+    # to the ICP stream, waits for it and turns it into odometry
+    # (Robot.get_transformation_icp, robot.py:108-120) while the GPU runs the scan,
+    # then completes the scan (step_wait).  The hand-off's host time (~0.1 ms of HIP
+    # calls, event wait, numpy) stays off the GPU's critical path.  The timed
+    # region's first scan prepares its own alignment, so exactly one alignment per
+    # timed scan runs inside the timing.
+    icp_odo = {}
     icp_host = {"wait_ms": 0.0, "prep_ms": 0.0, "scans": 0}
-    icp_pool = None
-    if scans_pts is not None:
-        from concurrent.futures import ThreadPoolExecutor
-        icp_pool = ThreadPoolExecutor(1)
 
     def icp_prepare(s):
         """Odometry of scan s from the alignment of scans s -> s+1 (and its host time)."""
@@ -496,20 +493,23 @@ def main(argv=None):
             with torch.cuda.stream(side):
                 for _ in range(args.probe_side_kernels):
                     side_x.add_(1.0)
-        if scans_pts is not None:
-            t0 = time.perf_counter()
-            fut = icp_tickets.pop(s, None)
-            if fut is None or args.serial_icp:
-                rot, tr, prep = icp_prepare(s)
-            else:
-                rot, tr, prep = fut.result()
-            if s >= args.warmup:
-                icp_host["wait_ms"] += (time.perf_counter() - t0) * 1e3
-                icp_host["prep_ms"] += prep
-                icp_host["scans"] += 1
-            if s + 1 != args.warmup and s + 1 < total_scans and not args.serial_icp:
-                icp_tickets[s + 1] = icp_pool.submit(icp_prepare, s + 1)
-        return f.step(rot, tr, meas[s])
+        if scans_pts is None:
+            return f.step(rot, tr, meas[s])
+        t0 = time.perf_counter()
+        ready = icp_odo.pop(s, None)
+        rot, tr, prep = ready if ready is not None else icp_prepare(s)
+        t1 = time.perf_counter()
+        f.step_submit(rot, tr, meas[s])
+        nxt = None
+        if s + 1 != args.warmup and s + 1 < total_scans and not args.serial_icp:
+            nxt = icp_prepare(s + 1)
+            icp_odo[s + 1] = nxt
+        out = f.step_wait()
+        if s >= args.warmup:
+            icp_host["wait_ms"] += (t1 - t0) * 1e3       # alignment work before this scan could start
+            icp_host["prep_ms"] += nxt[2] if nxt is not None else prep
+            icp_host["scans"] += 1
+        return out
 
     def barrier():
         torch.cuda.synchronize()
@@ -677,10 +677,11 @@ def main(argv=None):
                       "slots_visited_per_particle_scan": visited / units,
                       "exact_slots_per_particle_scan": exact_slots / units,
                       "icp_us": icp_us,
-                      "icp_host_ms_per_scan": ({"waited": icp_host["wait_ms"] / max(icp_host["scans"], 1),
+                      "icp_host_ms_per_scan": ({"before_scan": icp_host["wait_ms"] / max(icp_host["scans"], 1),
                                                 "hand_off": icp_host["prep_ms"] / max(icp_host["scans"], 1),
-                                                "note": "hand_off: submission + alignment + odometry on the worker "
-                                                        "thread; waited: what the scan loop waited for it"}
+                                                "note": "hand_off: submission + alignment + odometry of the next "
+                                                        "scan, done between step_submit and step_wait; before_scan: "
+                                                        "alignment work ahead of a scan's submission"}
                                                if scans_pts is not None else None)},
         }
         if migration is not None:
@@ -689,8 +690,6 @@ def main(argv=None):
             out["extra"]["robustness"] = robustness(args, f, L, total_scans)
         print(json.dumps(out), flush=True)
     f.close()
-    if icp_pool is not None:
-        icp_pool.shutdown(wait=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -149,6 +149,15 @@ struct fs2_handle {
     int64_t assoc_cap = 0;
     int32_t last_m = 0;
     uint64_t scan = 0;
+    // a scan enqueued by fs2_iterate_submit, completed by fs2_iterate_wait
+    struct Pending {
+        bool on = false;
+        unsigned long long seq = 0;
+        bool prof = false;
+        int passes = 0;
+        int32_t m = 0;
+        uint64_t fixed_bytes = 0;
+    } pending;
     int32_t cnt_upper = 0;
     double gate2 = 64.0;
     std::string err;
@@ -934,6 +943,7 @@ int fs2_synchronize(fs2_handle *h) {
 
 int fs2_set_profiling(fs2_handle *h, int32_t enable) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (enable && !h->ev.ok) {
         for (auto &set : h->ev.e)
             for (auto &e : set) HIP_TRY(h, hipEventCreate(&e));
@@ -952,6 +962,7 @@ static int fold_profile(fs2_handle *h);
 int fs2_get_profile(const fs2_handle *hc, fs2_profile *out) {
     if (!hc || !out) return set_err(nullptr, FS2_ERR_ARG, "null argument");
     fs2_handle *h = const_cast<fs2_handle *>(hc);   // the last scan's events are folded in
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     const int rc = fold_profile(h);
     if (rc) return rc;
     *out = h->prof;
@@ -1030,10 +1041,10 @@ static int wait_flag(fs2_handle *h, unsigned long long seq) {
     return FS2_OK;
 }
 
-int fs2_iterate(fs2_handle *h, double rotation, double translation, const double *meas,
-                const double *observed, int32_t M, const double *noise, const double *u0,
-                double out_pose[3], fs2_iter_stats *stats) {
+int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
+                       const double *observed, int32_t M, const double *noise, const double *u0) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan has not been waited for");
     if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     int rc = grow_rows(h, h->cnt_upper + M);
@@ -1346,21 +1357,35 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     else
         HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s, prof ? E[3] : nullptr));
     h->stats_clean = true;
-    rc = wait_flag(h, pseq);
+    h->pending.on = true;
+    h->pending.seq = pseq;
+    h->pending.prof = prof;
+    h->pending.passes = passes;
+    h->pending.m = M;
+    h->pending.fixed_bytes = fixed_bytes;
+    return FS2_OK;
+}
+
+int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (!h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "no submitted scan to wait for");
+    h->pending.on = false;
+    const int M = h->pending.m;
+    int rc = wait_flag(h, h->pending.seq);
     if (rc) return rc;
     // a stream-ordered transport reports a failed collective only now
     if (h->tp && (rc = h->tp->status(&h->err))) return rc;
     const DevStats &st = *h->pub_stats;
-    if (st.resampled) h->cur = nxt;
+    if (st.resampled) h->cur = 1 - h->cur;
     h->cnt_upper = st.max_count;
     h->last_m = M;
     h->scan += 1;
-    if (prof) {
+    if (h->pending.prof) {
         ProfScan &p = h->ev.scan[h->ev.used++];
         p.st = st;
-        p.passes = passes;
+        p.passes = h->pending.passes;
         p.m = M;
-        p.fixed_bytes = fixed_bytes;
+        p.fixed_bytes = h->pending.fixed_bytes;
     }
     if (out_pose) {
         out_pose[0] = st.pose[0];
@@ -1394,8 +1419,17 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
     return FS2_OK;
 }
 
+int fs2_iterate(fs2_handle *h, double rotation, double translation, const double *meas,
+                const double *observed, int32_t M, const double *noise, const double *u0,
+                double out_pose[3], fs2_iter_stats *stats) {
+    const int rc = fs2_iterate_submit(h, rotation, translation, meas, observed, M, noise, u0);
+    if (rc) return rc;
+    return fs2_iterate_wait(h, out_pose, stats);
+}
+
 int fs2_get_assoc(fs2_handle *h, int32_t *idx, int64_t capacity, int32_t *m_out) {
     if (!h || !idx) return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "null argument");
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (!h->cfg.record_assoc) return set_err(&h->err, FS2_ERR_STATE, "record_assoc is off");
     const int64_t need = (int64_t)h->last_m * h->n;
     if (capacity < need) return set_err(&h->err, FS2_ERR_ARG, "assoc buffer too small (%lld < %lld)",
@@ -1417,6 +1451,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
                   const double *yaw, const double *w, const int32_t *cnt, const double *lm,
                   int32_t lm_cap, int32_t where) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (first < 0 || count < 0 || first + count > h->n)
         return set_err(&h->err, FS2_ERR_ARG, "range [%lld, %lld) outside %lld local particles",
                        (long long)first, (long long)(first + count), (long long)h->n);
@@ -1512,6 +1547,7 @@ int fs2_update_known_landmarks(fs2_handle *h, double eps, double min_fraction, d
                                int64_t *n_clusters) {
     if (!h || !n_clusters || (cap > 0 && !centres) || !(eps > 0.0))
         return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_update_known_landmarks: bad arguments");
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (h->cfg.world_size > 1)
         return set_err(&h->err, FS2_ERR_STATE, "update_known_landmarks needs every particle on one rank");
     HIP_TRY(h, hipSetDevice(h->cfg.device));
@@ -1550,6 +1586,7 @@ int fs2_update_known_landmarks(fs2_handle *h, double eps, double min_fraction, d
 int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double *y, double *yaw,
                   double *w, int32_t *cnt, double *lm, int32_t lm_cap, int32_t where) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (first < 0 || count < 0 || first + count > h->n)
         return set_err(&h->err, FS2_ERR_ARG, "range outside local particles");
     HIP_TRY(h, hipSetDevice(h->cfg.device));

@@ -143,6 +143,8 @@ SIGNATURES = [
     ("fs2_last_error", C.c_char_p, [_H]),
     ("fs2_iterate", C.c_int, [_H, C.c_double, C.c_double, _vp, _vp, C.c_int32, _vp, _vp, _dp,
                               C.POINTER(fs2_iter_stats)]),
+    ("fs2_iterate_submit", C.c_int, [_H, C.c_double, C.c_double, _vp, _vp, C.c_int32, _vp, _vp]),
+    ("fs2_iterate_wait", C.c_int, [_H, _dp, C.POINTER(fs2_iter_stats)]),
     ("fs2_get_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,
                                 C.c_int32]),
     ("fs2_set_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,

@@ -85,6 +85,11 @@ class FastSLAM2:
         proto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_double, C.c_double, C.c_void_p, C.c_void_p, C.c_int32,
                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p)
         self._iterate_raw = proto(C.cast(lib.fs2_iterate, C.c_void_p).value)
+        sproto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_double, C.c_double, C.c_void_p, C.c_void_p, C.c_int32,
+                             C.c_void_p, C.c_void_p)
+        self._submit_raw = sproto(C.cast(lib.fs2_iterate_submit, C.c_void_p).value)
+        wproto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p)
+        self._wait_raw = wproto(C.cast(lib.fs2_iterate_wait, C.c_void_p).value)
         self._hv = h.value
         self._mcap = 0
         self._pose = np.empty(3)
@@ -134,6 +139,25 @@ class FastSLAM2:
         """iterate() with explicit inputs: meas [M][2] (distance, yaw); observed [M][2]
         robot-frame points (None: computed in libfs2); noise [N_local] motion draws and
         u0 the resample start (None: Philox on the device).  Returns (pose, stats)."""
+        return self._step(rotation, translation, meas, observed, noise, u0, split=False)
+
+    def step_submit(self, rotation: float, translation: float, meas, observed=None, noise=None, u0=None):
+        """The first half of step(): enqueue the scan and return while the GPU works
+        (libfs2 fs2_iterate_submit).  Finish it with step_wait()."""
+        self._step(rotation, translation, meas, observed, noise, u0, split=True)
+
+    def step_wait(self):
+        """Complete the scan step_submit() enqueued; returns (pose, stats) like step()."""
+        if not getattr(self, "_h", None) or not self._hv:
+            raise nat.FS2Error(nat.FS2_ERR_ARG, "step_wait() on a closed FastSLAM2 handle")
+        rc = self._wait_raw(self._hv, self._pose_addr, self._st_addr)
+        self._particles = None
+        st = nat.fs2_iter_stats.from_buffer_copy(self._st)
+        self.last_stats = st
+        nat.check(rc, self._h)
+        return self._pose.copy(), st
+
+    def _step(self, rotation, translation, meas, observed, noise, u0, split):
         if not getattr(self, "_h", None) or not self._hv:
             raise nat.FS2Error(nat.FS2_ERR_ARG, "step() on a closed FastSLAM2 handle")
         meas = nat.f64(meas).reshape(-1, 2)
@@ -164,6 +188,12 @@ class FastSLAM2:
         if u0 is not None:
             self._u0[0] = float(u0)
             ua = self._u0_addr
+        if split:
+            rc = self._submit_raw(self._hv, float(rotation), float(translation), self._mbuf_addr if M else None, oa,
+                                  M, None if nz is None else nz.ctypes.data, ua)
+            self._particles = None
+            nat.check(rc, self._h)
+            return None
         rc = self._iterate_raw(self._hv, float(rotation), float(translation), self._mbuf_addr if M else None, oa,
                                M, None if nz is None else nz.ctypes.data, ua, self._pose_addr, self._st_addr)
         self._particles = None

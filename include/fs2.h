@@ -188,6 +188,17 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
                 const double *observed, int32_t M, const double *noise, const double *u0,
                 double out_pose[3], fs2_iter_stats *stats);
 
+/* fs2_iterate in two halves: fs2_iterate_submit enqueues the scan (same
+ * arguments; on a sharded handle it also performs the mid-scan exchanges) and
+ * returns while the GPU works; fs2_iterate_wait completes it (pose, stats).  The
+ * caller can do host work in between -- e.g. hand the next scan's ICP alignment
+ * to the GPU (config 4) -- without delaying the scan.  One scan at a time:
+ * submitting again, or reading / writing the state, before the wait fails with
+ * FS2_ERR_STATE. */
+int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
+                       const double *observed, int32_t M, const double *noise, const double *u0);
+int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats);
+
 /* Particle state in the reference's object layout (Particle.x/.y/.yaw/.weight,
  * Particle.landmarks[j] = Landmark(x, y, cov) -- models/particle.py:11-20,
  * models/landmark.py:13-21).  Range [first, first+count) of this rank's local
