@@ -62,6 +62,9 @@ def parse(argv=None):
                          "beside the previous scan's update")
     ap.add_argument("--dry-run", action="store_true",
                     help="with --gpus N > 1 and no WORLD_SIZE: print the ranks' environments, start nothing")
+    ap.add_argument("--icp-offline", action="store_true",
+                    help="A/B (config 4): align every scan before the timed loop and feed the same odometry, "
+                         "so the timed scans run config 4's workload without an alignment beside them")
     ap.add_argument("--probe-side-kernels", type=int, default=0,
                     help="A/B (config 4 interference): launch this many tiny kernels on a second stream "
                          "before each scan, as the ICP hand-off does")
@@ -484,6 +487,8 @@ def main(argv=None):
         rot, tr = (float(q) for q in fast_slam_2.Robot.icp_odometry(R, t, v))
         return rot, tr, (time.perf_counter() - t0) * 1e3
 
+    offline_odo = ({s: icp_prepare(s)[:2] for s in range(total_scans)}
+                   if (scans_pts is not None and args.icp_offline) else None)
     side = torch.cuda.Stream() if args.probe_side_kernels else None
     side_x = torch.zeros(64, device="cuda") if side is not None else None
 
@@ -495,6 +500,8 @@ def main(argv=None):
                     side_x.add_(1.0)
         if scans_pts is None:
             return f.step(rot, tr, meas[s])
+        if args.icp_offline:
+            return f.step(*offline_odo[s], meas[s])
         t0 = time.perf_counter()
         ready = icp_odo.pop(s, None)
         rot, tr, prep = ready if ready is not None else icp_prepare(s)
