@@ -323,6 +323,7 @@ __device__ __forceinline__ void store_rec(char *recs, uint32_t r, const Slot &s)
     __builtin_nontemporal_store((v2d){s.mx, s.my}, qv);
     __builtin_nontemporal_store((v2d){s.P.a00, s.P.a01}, qv + 1);
     __builtin_nontemporal_store((v2d){s.P.a10, s.P.a11}, qv + 2);
+    if constexpr (kRecBytes == 64) __builtin_nontemporal_store((v2d){0.0, 0.0}, qv + 3);   // whole 64 B
 #else
     q[0] = make_double2(s.mx, s.my);
     q[1] = make_double2(s.P.a00, s.P.a01);
