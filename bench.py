@@ -417,6 +417,9 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
             "particles_sent_per_resample": sum(p["sent_particles"] for p in profs) / max(res[0], 1),
             "page_dedup_ratio": (sum(p["sent_rows"] for p in profs) / sum(p["sent_pages"] for p in profs)
                                  if sum(p["sent_pages"] for p in profs) else None),
+            "pages_sent_before_fraction": (sum(p["sent_pages_repeat"] for p in profs) /
+                                           sum(p["sent_pages"] for p in profs)
+                                           if sum(p["sent_pages"] for p in profs) else None),
             "note": f"{G} ranks as threads on one GPU, in-process transport, {n_total} particles in all; "
                     "comm: host time in transport calls and mid-scan waits (a wait includes the collectives "
                     "queued before it)"}

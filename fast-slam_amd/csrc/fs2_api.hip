@@ -110,6 +110,7 @@ struct fs2_handle {
     uint32_t *freel = nullptr;             // free page ids [0, nfree)
     int64_t nfree = 0, cursor = 0;         // free pages listed / reserved since the last collection
     uint8_t *mark = nullptr;               // collection marks, one byte per page
+    uint32_t *sent_mask = nullptr;         // sharded: per page, the ranks it went to since the last collection
     uint8_t epoch = 0;
     int64_t *bcnt = nullptr;               // sweep block counts -> offsets
     int64_t *nfree_dev = nullptr;
@@ -291,6 +292,8 @@ static int collect(fs2_handle *h, bool records) {
         HIP_TRY(h, hipMemcpyAsync(&h->rnfree, h->rnfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         h->rcursor = 0;
     }
+    // page ids are recycled from here on: the transfer probe starts over
+    if (h->sent_mask) HIP_TRY(h, hipMemsetAsync(h->sent_mask, 0, sizeof(uint32_t) * (size_t)h->npool, s));
     HIP_TRY(h, hipStreamSynchronize(s));
     h->cursor = 0;
     h->collections += 1;
@@ -317,6 +320,11 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
     hipFree(h->freel);
     h->freel = nullptr;
     HIP_TRY(h, hipMalloc(&h->freel, sizeof(uint32_t) * (size_t)pages));
+    if (h->cfg.world_size > 1) {
+        hipFree(h->sent_mask);
+        h->sent_mask = nullptr;
+        HIP_TRY(h, hipMalloc(&h->sent_mask, sizeof(uint32_t) * (size_t)pages));
+    }
     hipFree(h->bcnt);
     h->bcnt = nullptr;
     HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int64_t) * (size_t)collect_blocks(pages)));
@@ -480,6 +488,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     std::memcpy(rs.init_cov, h->cfg.init_landmark_cov, sizeof rs.init_cov);
     rs.plan = h->plan;
     rs.xrow = h->xrow;
+    rs.sent_mask = h->sent_mask;
     HIP_TRY(h, launch_pack_count(rs, s));
     int rc;
     auto gather_sizes = [&]() -> int {
@@ -693,6 +702,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->rdesc); hipFree(h->udesc);
     hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
     hipFree(h->xt_eslot); hipFree(h->xt_ulist);
+    hipFree(h->sent_mask);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->ext_dev);
@@ -1380,6 +1390,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     h->cnt_upper = st.max_count;
     h->last_m = M;
     h->scan += 1;
+    if (h->profiling) h->prof.sent_pages_repeat += st.repeat_pages;
     if (h->pending.prof) {
         ProfScan &p = h->ev.scan[h->ev.used++];
         p.st = st;

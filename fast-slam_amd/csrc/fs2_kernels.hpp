@@ -98,6 +98,9 @@ struct DevStats {
     unsigned long long opened;       // pages whose mirrors k_candidates loaded
     unsigned long long ref_visits;   // landmarks the reference's first-match scan reads (j + 1 on a
                                      // match, the map size on an append)
+    unsigned long long repeat_pages; // sharded: distinct pages sent that went to the same rank before
+                                     // (since this rank's last collection; what a receiver-side page
+                                     // cache could skip)
 };
 
 // numpy's np.sum over 8192-element buffers (fs2_exact.hip).  The recursion over a
@@ -364,6 +367,7 @@ struct ResampleParams {
     int64_t *xrow;           // [kXrowWords world] per destination (K, S, U, C, i0, i1)
     char *sbuf[kMaxRanks];   // per destination: the transfer (xfer_bytes)
     XferTable xt;
+    uint32_t *sent_mask;     // [npool] bit p: the page went to rank p since the last collection (probe)
     double init_cov[4];      // the configured initial landmark covariance (compact transfers)
     // received particles
     int32_t npeers;

@@ -1002,6 +1002,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P)
             s_cbase[threadIdx.x] = (uint32_t)atomicAdd(row + 3, (unsigned long long)s_ccnt[threadIdx.x]);
     }
     __syncthreads();
+    unsigned repeats = 0;
     for (int64_t h = c0 + threadIdx.x; h < c0 + kAssignChunk; h += kBlock) {
         const int d = dest(h);
         uint32_t local = 0;
@@ -1012,7 +1013,17 @@ __global__ __launch_bounds__(kBlock) void k_dedup_assign(const ResampleParams P)
             T.uidx[h] = u;
             T.cbase[h] = mask ? s_cbase[d] + atomicAdd(&s_crun[d], (uint32_t)__popc(mask)) : 0u;
             T.ulist[T.ebase[d] + u] = (uint32_t)h;
+            if (P.sent_mask) {
+                // probe: did this page already go to rank d since the last collection?
+                const uint32_t page = (uint32_t)T.key[h] & kIdMask, bit = 1u << d;
+                repeats += (atomicOr(&P.sent_mask[page], bit) & bit) ? 1u : 0u;
+            }
         }
+    }
+    if (P.sent_mask) {
+        __shared__ unsigned long long s_rep[kBlock / 64];
+        const unsigned long long r = block_sum_u64<kBlock>(repeats, s_rep);
+        if (threadIdx.x == 0 && r) atomicAdd(&P.stats->repeat_pages, r);
     }
 }
 

@@ -110,6 +110,7 @@ class fs2_profile(C.Structure):
         ("sent_pages", C.c_uint64),
         ("sent_bytes", C.c_uint64),
         ("migrate_ms", C.c_double),
+        ("sent_pages_repeat", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -149,6 +149,9 @@ typedef struct fs2_profile {
     uint64_t sent_pages;        /* distinct pages those rows name (sent once per destination) */
     uint64_t sent_bytes;        /* transfer bytes (headers, row entries, pages with their records) */
     double migrate_ms;          /* host wall time from the plan to the end of the exchange */
+    uint64_t sent_pages_repeat; /* of sent_pages, those that had gone to the same rank before since
+                                   the sender's last collection (what a receiver-side page cache
+                                   could skip; a probe, nothing is skipped) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */
