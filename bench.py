@@ -60,6 +60,11 @@ def parse(argv=None):
     ap.add_argument("--serial-icp", action="store_true",
                     help="A/B (config 4): align each scan just before its update instead of "
                          "beside the previous scan's update")
+    ap.add_argument("--comm", choices=("rccl", "shm"), default="rccl",
+                    help="libfs2 transport between ranks (shm: POSIX shared memory, any GPUs)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="testing: every rank on GPU 0 (implies --comm shm; the bench's own barrier and "
+                         "timing reduction over gloo)")
     ap.add_argument("--dry-run", action="store_true",
                     help="with --gpus N > 1 and no WORLD_SIZE: print the ranks' environments, start nothing")
     ap.add_argument("--icp-offline", action="store_true",
@@ -111,8 +116,9 @@ def launch_ranks(args, argv):
         print(json.dumps([{k: e[k] for k in RANK_ENV} for e in envs]), flush=True)
         return 0
     have = visible_gpus()
-    if have < n:
-        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this process sees {have}; "
+    need = 1 if args.share_gpu else n
+    if have < need:
+        print(f"bench.py: --gpus {n} needs {need} visible GPUs, this process sees {have}; "
               f"refusing to time fewer ranks than asked", file=sys.stderr, flush=True)
         return 2
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e) for e in envs]
@@ -436,11 +442,21 @@ def main(argv=None):
               file=sys.stderr, flush=True)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:
+        args.comm = "shm"
+    dev = 0 if args.share_gpu else local
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(dev)
+    # the bench's own barrier and timing reduction: RCCL with one GPU per rank, gloo
+    # when ranks share a GPU (RCCL refuses two ranks on one device)
+    host_coll = args.share_gpu
+    tdev = "cpu" if host_coll else "cuda"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if host_coll:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import fast_slam_2
     import fs2_synthetic as syn
     from fast_slam_2 import _native as nat
@@ -451,17 +467,17 @@ def main(argv=None):
     N = n_per_gpu * world
     comm_id = None
     if world > 1:
-        obj = [nat.comm_unique_id() if rank == 0 else None]
+        obj = [(nat.comm_unique_id() if args.comm == "rccl" else os.urandom(128)) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
     total_scans = args.warmup + args.steps
-    f = fast_slam_2.FastSLAM2(N, device=local, rng="device", seed=args.seed, reduce="auto",
+    f = fast_slam_2.FastSLAM2(N, device=dev, rng="device", seed=args.seed, reduce="auto",
                               landmark_capacity=L + total_scans + 8, rank=rank,
                               world_size=world, comm_id=comm_id, verbose=False,
-                              gate_filter=not args.no_gate_filter)
+                              gate_filter=not args.no_gate_filter, comm_mode=args.comm)
     populate(f, f.n_local, L, args.seed, rank)
     scans_pts = None
-    fast_slam_2.ICP.device = local
+    fast_slam_2.ICP.device = dev
     if cfg["icp"]:
         scans_pts = [syn.room_scan((0.03 * s, 0.0, 0.0), cfg["P"], args.seed, s)
                      for s in range(total_scans + 1)]
@@ -560,7 +576,7 @@ def main(argv=None):
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     prof = f.profile()
@@ -568,7 +584,7 @@ def main(argv=None):
     if world > 1:
         # the sharded resample's transfers, summed over the ranks
         keys = ("migrations", "sent_particles", "sent_rows", "sent_pages", "sent_bytes", "migrate_ms", "comm_ms")
-        mt = torch.tensor([float(prof[k]) for k in keys], dtype=torch.float64, device="cuda")
+        mt = torch.tensor([float(prof[k]) for k in keys], dtype=torch.float64, device=tdev)
         dist.all_reduce(mt, op=dist.ReduceOp.SUM)
         tot = dict(zip(keys, mt.tolist()))
         per = max(resamples, 1)
@@ -652,7 +668,9 @@ def main(argv=None):
                        "icp_pipelined": bool(cfg["icp"] and not args.serial_icp),
                        "gate_filter": not args.no_gate_filter, "reduce": "exact" if N > 4096 and world == 1
                        else ("parallel" if world > 1 else "sequential"),
-                       "parallelism": f"particle-shard{world}"},
+                       "parallelism": f"particle-shard{world}",
+                       "transport": args.comm if world > 1 else None,
+                       "ranks_share_gpu": bool(args.share_gpu and world > 1)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "basis": basis,
