@@ -83,6 +83,7 @@ def test_sharded_matches_single(G, N, L):
             assert st.best_index == st1.best_index, s
             assert np.allclose(pose, pose1, rtol=1e-9, atol=1e-12), s
             assert np.isclose(st.n_eff, st1.n_eff, rtol=1e-9), s
+            assert st.reduce_ambiguous == 0, s          # no decision the shard order could flip
         resamples += st1.resampled
         moved += sum(sh.last_stats.resample_slots for sh in shards)
         a1 = single.associations()
