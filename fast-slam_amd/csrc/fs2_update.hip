@@ -72,6 +72,12 @@ __device__ unsigned long long g_phase[8];
 #ifndef FS2_PAGE_PRED
 #define FS2_PAGE_PRED 0
 #endif
+#ifndef FS2_CAND_PAIR
+#define FS2_CAND_PAIR 0        // A/B knob: two rows' pages in flight per wave
+#endif
+#ifndef FS2_PAIR_AHEAD
+#define FS2_PAIR_AHEAD 4       // descriptors in flight with FS2_CAND_PAIR
+#endif
 #ifndef FS2_B1_DESC_STORE
 #define FS2_B1_DESC_STORE 0    // A/B knob: store the owned pages' ids in B1 as well
 #endif
@@ -109,8 +115,11 @@ __device__ __forceinline__ void sort8(uint64_t (&e)[8]) {
     cmpx(e[1], e[2]); cmpx(e[3], e[4]); cmpx(e[5], e[6]);
 }
 
+#ifndef FS2_CAND_WAVES
+#define FS2_CAND_WAVES 0       // A/B knob: minimum waves per SIMD for k_candidates
+#endif
 template <int MAXM>
-__global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
+__global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const UpdateParams P) {
     __shared__ uint64_t s_list[kMaxCand][kBlock];
     __shared__ Band s_band[MAXM];
     __shared__ uint16_t s_rows[kBBoxRows];      // rows the row boxes leave open, ascending
@@ -228,6 +237,70 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
     // row of list entry q (past the end: row 0, a valid address whose load is discarded)
     auto row_at = [&](int q) -> int { return use_bb ? (q < nrows ? (int)s_rows[q] : 0) : min(q, rlast); };
+#if FS2_CAND_PAIR
+    // Rows two at a time: both rows' pages are loaded before either is tested, so
+    // a wave has two page latencies in flight, not one.  A page is loaded as its
+    // mirrors' (x, y, s|slot) words only (12 of 16 bytes: two pages fit in the
+    // registers one float4 page took, plus a third); a listed entry names its
+    // page id and the record ids are read once, after the walk.
+    constexpr int kPairAhead = FS2_PAIR_AHEAD;   // descriptors in flight (pairs of rows)
+    static_assert(kPairAhead % 2 == 0 && kPairAhead >= 2, "whole pairs");
+    Desc dq[kPairAhead];
+#pragma unroll
+    for (int q = 0; q < kPairAhead; ++q) dq[q] = ptrow[(int64_t)row_at(q) * n];
+    auto load3 = [&](uint32_t id, float4 (&mir)[kScanGroup]) {
+        const float *pg = reinterpret_cast<const float *>(page_ptr(map.pool, id));
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u) mir[u] = make_float4(pg[4 * u], pg[4 * u + 1], pg[4 * u + 2], 0.0f);
+    };
+    auto test3 = [&](const float4 (&mir)[kScanGroup], int g, unsigned om, uint32_t pid) {
+        const int j0 = g * kPageSlots;
+#pragma unroll
+        for (int u = 0; u < kScanGroup; ++u) {
+            if (j0 + u < c) {
+                ++visited;
+                const float4 mv = mir[u];
+                const float cx = fabsf(mv.x) * 2.3841858e-7f;
+                const float cy = fabsf(mv.y) * 2.3841858e-7f;
+                bool hit = false;
+#pragma unroll
+                for (int k = 0; k < MAXM; ++k)
+                    if ((om >> k) & 1u)
+                        hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f);
+                if (hit) {
+                    if (nc < kMaxCand) s_list[nc][tid] = cand_entry(mirror_slot(mv), j0 + u, pid & kIdMask);
+                    ++nc;
+                }
+            }
+        }
+    };
+    for (int q = 0; q < nrows; q += 2) {
+        const int ga = row_at(q), gb = row_at(q + 1);
+        if (!__any(ga * kPageSlots < c)) break;      // rows ascend: no lane has more
+        const bool hb = q + 1 < nrows;               // wave-uniform
+        const Desc da = dq[0], db = dq[1];
+#pragma unroll
+        for (int u = 0; u + 2 < kPairAhead; ++u) dq[u] = dq[u + 2];
+        dq[kPairAhead - 2] = ptrow[(int64_t)row_at(q + kPairAhead) * n];
+        dq[kPairAhead - 1] = ptrow[(int64_t)row_at(q + kPairAhead + 1) * n];
+        if (ga * kPageSlots < c) ++groups;
+        if (hb && gb * kPageSlots < c) ++groups;
+        const unsigned oma = open_mask(da, ga);
+        const unsigned omb = hb ? open_mask(db, gb) : 0u;
+        const bool anya = __any(oma), anyb = __any(omb);
+        float4 ma[kScanGroup], mb[kScanGroup];
+        if (anya) load3(oma ? da.x : 0u, ma);
+        if (anyb) load3(omb ? db.x : 0u, mb);
+        if (oma) {
+            ++opened;
+            test3(ma, ga, oma, da.x);
+        }
+        if (omb) {
+            ++opened;
+            test3(mb, gb, omb, db.x);
+        }
+    }
+#else
     Desc dq[kDescAhead];             // descriptors of list entries q .. q + kDescAhead - 1 in flight
 #pragma unroll
     for (int q = 0; q < kDescAhead; ++q) dq[q] = ptrow[(int64_t)row_at(q) * n];
@@ -262,6 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         }
 #endif
     }
+#endif
     if (live) {
         P.ncand[i] = nc;
         if (nc <= kMaxCand) {
@@ -271,6 +345,16 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             uint64_t e[kMaxCand];
 #pragma unroll
             for (int q = 0; q < kMaxCand; ++q) e[q] = (q < nc) ? s_list[q][tid] : ~0ull;
+#if FS2_CAND_PAIR
+            // page id -> the slot's record id (all the list's loads in flight together)
+#pragma unroll
+            for (int q = 0; q < kMaxCand; ++q) {
+                if (q < nc) {
+                    const uint32_t rec = mirror_rec(load_mirror(page_ptr(map.pool, cand_rec(e[q])), cand_pos(e[q])));
+                    e[q] = (e[q] & ~0xffffffffull) | rec;
+                }
+            }
+#endif
             sort8(e);
 #pragma unroll
             for (int q = 0; q < kMaxCand; ++q)
@@ -305,8 +389,13 @@ static __device__ __forceinline__ uint32_t sel_u32(int t, const uint32_t (&a)[K]
 // resolved afterwards in measurement order.  Likelihoods multiply into the
 // weight in measurement order, as the reference does.  Without the gate filter
 // (or past an overflowing candidate list) every slot takes the exact path.
+// FS2_UPDATE_WAVES (A/B knob): minimum waves per SIMD the compiler must fit
+// k_update into (spilling what does not fit); 0 = its own choice (3 at 164 VGPRs)
+#ifndef FS2_UPDATE_WAVES
+#define FS2_UPDATE_WAVES 0
+#endif
 template <int MAXM>
-__global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
+__global__ __launch_bounds__(kBlock, FS2_UPDATE_WAVES) void k_update(const UpdateParams P) {
     __shared__ Meas s_ms[MAXM];                 // this pass's measurements
     __shared__ double s_lik[MAXM][kBlock];      // per (measurement, lane) likelihood
     __shared__ int16_t s_idx[MAXM][kBlock];     // per (measurement, lane) association (slot < 4096, -1, -2)
