@@ -72,20 +72,6 @@ __device__ unsigned long long g_phase[8];
 #ifndef FS2_PAGE_PRED
 #define FS2_PAGE_PRED 0
 #endif
-#ifndef FS2_CAND_X3
-#define FS2_CAND_X3 0          // A/B knob: pages loaded as 12-byte mirror words
-#endif
-#ifndef FS2_CAND_QUEUE
-#define FS2_CAND_QUEUE 0       // A/B knob: open pages queued per wave, read 8 lanes per page
-#endif
-#ifndef FS2_QUEUE_CAP
-#define FS2_QUEUE_CAP 256      // FS2_CAND_QUEUE: queue entries per wave
-#endif
-#ifndef FS2_QUEUE_BATCH
-#define FS2_QUEUE_BATCH 4      // FS2_CAND_QUEUE: load instructions in flight per drain step
-#endif
-constexpr int kQueueCap = FS2_QUEUE_CAP;
-constexpr int kQueueBatch = FS2_QUEUE_BATCH;
 #ifndef FS2_B1_DESC_STORE
 #define FS2_B1_DESC_STORE 0    // A/B knob: store the owned pages' ids in B1 as well
 #endif
@@ -132,10 +118,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
     __shared__ Band s_band[MAXM];
     __shared__ uint16_t s_rows[kBBoxRows];      // rows the row boxes leave open, ascending
     __shared__ int s_wc[kBlock / 64];
-#if FS2_CAND_QUEUE
-    __shared__ uint2 s_queue[kBlock / 64][kQueueCap];   // per wave: open pages (id; lane | row | mask | slots)
-    __shared__ int s_nc[kBlock];                        // per lane: hits listed so far
-#endif
     const int tid = threadIdx.x;
     const int64_t n = P.n;
     const int64_t blk = P.blk0 + blockIdx.x;   // this launch may cover a chunk of the blocks
@@ -249,97 +231,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
     }
     // row of list entry q (past the end: row 0, a valid address whose load is discarded)
     auto row_at = [&](int q) -> int { return use_bb ? (q < nrows ? (int)s_rows[q] : 0) : min(q, rlast); };
-#if FS2_CAND_QUEUE
-    // Two alternating phases per wave.  (1) The descriptor stream only: each
-    // lane tests its rows' page boxes and queues its open pages (page id, lane,
-    // row, measurements, live slots) in the wave's LDS queue, compacted by
-    // ballot.  (2) The queue is drained cooperatively: 8 lanes per page, one
-    // 16-byte mirror each, kQueueBatch pages-of-8 in flight, so a load
-    // instruction touches 8 whole lines (scripts/ubench_lines: random lines read
-    // 8 lanes per line run 2-5x faster than one lane per line) and no lane loads
-    // a dummy page.  A hit goes into its owner's list at an LDS-atomic position;
-    // the list is sorted at the end, so the order of the hits does not matter.
-    const int lane = tid & 63, wid = tid >> 6;
-    const int sub = lane & 7, grp = lane >> 3;
-    s_nc[tid] = 0;
-    Desc dq[kDescAhead];
-#pragma unroll
-    for (int q = 0; q < kDescAhead; ++q) dq[q] = ptrow[(int64_t)row_at(q) * n];
-    int q = 0;
-    bool more = nrows > 0;
-    while (more) {
-        // (1) fill: whole rows while a row's 64 possible entries fit
-        int qn = 0;
-        while (q < nrows && qn + 64 <= kQueueCap) {
-            const int g = row_at(q);
-            if (!__any(g * kPageSlots < c)) {       // rows ascend: no lane has more
-                q = nrows;
-                break;
-            }
-            const Desc d = dq[0];
-#pragma unroll
-            for (int u = 0; u + 1 < kDescAhead; ++u) dq[u] = dq[u + 1];
-            dq[kDescAhead - 1] = ptrow[(int64_t)row_at(q + kDescAhead) * n];
-            ++q;
-            if (g * kPageSlots < c) ++groups;
-            const unsigned om = open_mask(d, g);
-            const uint64_t ob = __ballot(om != 0u);
-            if (om) {
-                const int live_slots = min(c - g * kPageSlots, kPageSlots);
-                s_queue[wid][qn + __popcll(ob & ((1ull << lane) - 1ull))] =
-                    make_uint2(d.x & kIdMask, (unsigned)lane | ((unsigned)g << 6) | (om << 15) |
-                                                  ((unsigned)live_slots << 24));
-                ++opened;
-                visited += (unsigned)live_slots;
-            }
-            qn += __popcll(ob);
-        }
-        more = q < nrows;
-        if (qn == 0) continue;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        // (2) drain: entry t = 8 (b + v) + grp, slot `sub` of its page
-        for (int b = 0; 8 * b < qn; b += kQueueBatch) {
-            float4 mv[kQueueBatch];
-#pragma unroll
-            for (int v = 0; v < kQueueBatch; ++v)
-                if (8 * (b + v) < qn)                     // wave-uniform
-                    mv[v] = load_mirror(page_ptr(map.pool, s_queue[wid][min(8 * (b + v) + grp, qn - 1)].x), sub);
-#pragma unroll
-            for (int v = 0; v < kQueueBatch; ++v) {
-                const int t = 8 * (b + v) + grp;
-                if (8 * (b + v) < qn && t < qn) {
-                    const unsigned meta = s_queue[wid][t].y;
-                    if (sub < (int)(meta >> 24)) {
-                        const unsigned om = (meta >> 15) & 0xffu;
-                        const float cx = fabsf(mv[v].x) * 2.3841858e-7f;   // 2^-22 |x_lm|
-                        const float cy = fabsf(mv[v].y) * 2.3841858e-7f;
-                        bool hit = false;
-#pragma unroll
-                        for (int k = 0; k < MAXM; ++k)
-                            if ((om >> k) & 1u)
-                                hit |= !gate_reject_fast(mv[v], cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
-                                                         P.gate2f);
-                        if (hit) {
-                            const int owner = wid * 64 + (int)(meta & 63u);
-                            const int g = (int)((meta >> 6) & 0x1ffu);
-                            const int pos = atomicAdd(&s_nc[owner], 1);
-                            if (pos < kMaxCand)
-                                s_list[pos][owner] = cand_entry(mirror_slot(mv[v]), g * kPageSlots + sub,
-                                                                mirror_rec(mv[v]));
-                        }
-                    }
-                }
-            }
-        }
-        // the next fill overwrites the queue: the drain's LDS reads come first
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    nc = s_nc[tid];
-#else
     Desc dq[kDescAhead];             // descriptors of list entries q .. q + kDescAhead - 1 in flight
 #pragma unroll
     for (int q = 0; q < kDescAhead; ++q) dq[q] = ptrow[(int64_t)row_at(q) * n];
@@ -366,27 +257,14 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
 #else
         const char *pg = page_ptr(map.pool, om ? d.x : 0u);
         float4 mir[kScanGroup];
-#if FS2_CAND_X3
-        // only the tested words (x, y, s|slot): 12 of each mirror's 16 bytes go
-        // through the vector memory path; a listed entry names the page, its
-        // record id is read after the walk
-        {
-            const float *pf = reinterpret_cast<const float *>(pg);
-            const float pid = __uint_as_float(d.x & kIdMask);
-#pragma unroll
-            for (int u = 0; u < kScanGroup; ++u) mir[u] = make_float4(pf[4 * u], pf[4 * u + 1], pf[4 * u + 2], pid);
-        }
-#else
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
-#endif
         if (om) {
             ++opened;
             test_page(mir, g, om);
         }
 #endif
     }
-#endif
     if (live) {
         P.ncand[i] = nc;
         if (nc <= kMaxCand) {
@@ -396,14 +274,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
             uint64_t e[kMaxCand];
 #pragma unroll
             for (int q = 0; q < kMaxCand; ++q) e[q] = (q < nc) ? s_list[q][tid] : ~0ull;
-#if FS2_CAND_X3
-            // page id -> the slot's record id (the list's loads in flight together)
-#pragma unroll
-            for (int q = 0; q < kMaxCand; ++q)
-                if (q < nc)
-                    e[q] = (e[q] & ~0xffffffffull) |
-                           mirror_rec(load_mirror(page_ptr(map.pool, cand_rec(e[q])), cand_pos(e[q])));
-#endif
             sort8(e);
 #pragma unroll
             for (int q = 0; q < kMaxCand; ++q)
