@@ -180,6 +180,14 @@ struct fs2_handle {
     char *sarena = nullptr, *rarena = nullptr;
     size_t scap = 0, rcap = 0;
     int32_t n_recv = 0;                             // particles received by the last resample
+    // which slice of the global particle order (shard) this rank holds, and the
+    // rank holding each shard.  With equal shards a resample may hand a rank
+    // another shard, the one its own sources fill most (exchange_particles):
+    // `follow`.  first = shard_begin(shard).
+    int32_t shard = 0;
+    int8_t rank_of[kMaxRanks] = {};
+    bool follow = false;
+    uint64_t shard_moves = 0;                       // resamples that changed this rank's shard
 
     // exact-order reductions (fs2_exact.hip)
     int32_t *uinfo = nullptr, *uol = nullptr, *seql = nullptr, *bC = nullptr, *bpc = nullptr;
@@ -248,12 +256,23 @@ CommTimer::~CommTimer() {
 }
 
 // Page-table rows for maps of up to need_slots slots (current buffer kept).
+// Growth after the first sizing is geometric (a quarter more rows, at least 8):
+// maps grow by about one slot per scan, and a growth drains the stream and
+// reallocates both tables (~n * rows * 16 B), so row-by-row growth cost a
+// realloc every few scans of a long run.  Rows past a map's count are never
+// read (every kernel stops at ceil(cnt / 8)), so spare rows cost memory only.
 static int grow_rows(fs2_handle *h, int need_slots) {
     if (need_slots <= h->cap) return FS2_OK;
     if (need_slots > h->max_cap)
         return set_err(&h->err, FS2_ERR_CAPACITY, "map needs %d landmark slots, limit is %d",
                        need_slots, h->max_cap);
-    const int rows = (need_slots + kPageSlots - 1) / kPageSlots;
+    int rows = (need_slots + kPageSlots - 1) / kPageSlots;
+    if (h->rows > 0) {
+        const int geo = h->rows + std::max(h->rows / 4, 8);
+        // (spare rows never switch the workgroup row boxes off)
+        const int lim = std::min(h->max_cap / kPageSlots, rows <= kBBoxRows ? kBBoxRows : INT_MAX);
+        rows = std::max(rows, std::min(geo, lim));
+    }
     const size_t row_bytes = sizeof(Desc) * (size_t)std::max<int64_t>(h->n, 1);
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     for (int b = 0; b < 2; ++b) {
@@ -473,6 +492,45 @@ static int reserve_xfer_table(fs2_handle *h, int64_t cap, int64_t nrows) {
     return FS2_OK;
 }
 
+// The shard each rank keeps after a resample ("output shards follow
+// their sources").  Systematic resampling keeps the global order, so the
+// outputs of shard q are the children of one run of sources; with Q6/Q8's
+// drift that run lies below q, on other ranks, and with shard r pinned to rank
+// r nearly every rank would receive its whole shard.  Shards are the same size,
+// so any one-to-one assignment of shards to ranks balances the work: take the
+// one that keeps the most page-table rows local (the sum over ranks of the rows
+// rank r's sources give shard keep_of[r]; ties keep the current shard, then
+// the lower one).  An exact maximum by a DP over subsets of shards (2^G states,
+// G <= 16), computed alike on every rank from the all-gathered counts.
+template <typename At>
+static void keep_shards(const fs2_handle *h, int G, At at, int keep_of[]) {
+    int shard_of[kMaxRanks];
+    for (int q = 0; q < G; ++q) shard_of[h->rank_of[q]] = q;
+    if (!h->follow) {
+        for (int r = 0; r < G; ++r) keep_of[r] = shard_of[r];
+        return;
+    }
+    auto val = [&](int r, int q) { return 2 * at(r, q, 1) + (q == shard_of[r] ? 1 : 0); };
+    const uint32_t full = (1u << G) - 1u;
+    std::vector<int64_t> dp((size_t)full + 1, -1);
+    std::vector<int8_t> pick((size_t)full + 1, -1);
+    dp[0] = 0;
+    for (uint32_t m = 0; m < full; ++m) {
+        if (dp[m] < 0) continue;
+        const int r = __builtin_popcount(m);      // ranks 0..r-1 are assigned
+        for (int q = 0; q < G; ++q) {
+            if (m & (1u << q)) continue;
+            const uint32_t m2 = m | (1u << q);
+            const int64_t v = dp[m] + val(r, q);
+            if (v > dp[m2]) {
+                dp[m2] = v;
+                pick[m2] = (int8_t)q;
+            }
+        }
+    }
+    for (uint32_t m = full; m; m &= ~(1u << pick[m])) keep_of[__builtin_popcount(m) - 1] = pick[m];
+}
+
 // Sharded resample: plan what goes to every other rank on the device (one run of
 // local particles per destination, fs2_plan.hpp), all-gather the sizes and learn
 // them with a post; find the distinct pages of every destination's rows
@@ -502,15 +560,23 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     rc = gather_sizes();
     if (rc) return rc;
     std::vector<int64_t> mat(posted_xmat(h), posted_xmat(h) + kXrowWords * G * G);
+    // at(rank, shard, field): what rank `from` would send to the outputs of shard `to`
     auto at = [&](int from, int to, int f) { return mat[(size_t)from * kXrowWords * G + kXrowWords * to + f]; };
+    // Which shard each rank keeps (its outputs are filled locally, not sent): every
+    // rank computes the same assignment from the same counts (keep_shards)
+    int keep_of[kMaxRanks], owner[kMaxRanks];
+    keep_shards(h, G, at, keep_of);
+    for (int r = 0; r < G; ++r) owner[keep_of[r]] = r;
+    const int keep = keep_of[R];
+    rs.keep = keep;
     // distinct pages of the rows sent (every rank takes part in the all-gather)
     XferTable &T = rs.xt;
     T = XferTable{};
     T.i_lo = h->n;
     T.i_hi = 0;
     for (int p = 0; p < G; ++p) {
-        T.ebase[p + 1] = T.ebase[p] + (p == R ? 0 : at(R, p, 1));
-        if (p != R && at(R, p, 0) > 0) {
+        T.ebase[p + 1] = T.ebase[p] + (p == keep ? 0 : at(R, p, 1));
+        if (p != keep && at(R, p, 0) > 0) {
             T.i_lo = std::min(T.i_lo, at(R, p, 4));
             T.i_hi = std::max(T.i_hi, at(R, p, 5));
         }
@@ -545,28 +611,30 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     // every destination's transfer at its offset in the send arena, every source's
     // in the receive arena
     size_t soff[kMaxRanks + 1] = {}, roff[kMaxRanks + 1] = {};
+    // soff by destination shard, roff by source rank (sending to shard keep)
     for (int p = 0; p < G; ++p) {
-        const bool so = p != R && at(R, p, 0) > 0, ro = p != R && at(p, R, 0) > 0;
+        const bool so = p != keep && at(R, p, 0) > 0, ro = p != R && at(p, keep, 0) > 0;
         soff[p + 1] = soff[p] + (so ? arena_align((size_t)xfer_bytes(at(R, p, 0), at(R, p, 1), at(R, p, 2), at(R, p, 3))) : 0);
-        roff[p + 1] = roff[p] + (ro ? arena_align((size_t)xfer_bytes(at(p, R, 0), at(p, R, 1), at(p, R, 2), at(p, R, 3))) : 0);
+        roff[p + 1] = roff[p] + (ro ? arena_align((size_t)xfer_bytes(at(p, keep, 0), at(p, keep, 1), at(p, keep, 2),
+                                                                      at(p, keep, 3))) : 0);
     }
     rc = ensure_arena(h, h->sarena, h->scap, soff[G]);
     if (!rc) rc = ensure_arena(h, h->rarena, h->rcap, roff[G]);
     if (rc) return rc;
     for (int p = 0; p < G; ++p) {
         rs.sbuf[p] = nullptr;
-        T.ubase[p + 1] = T.ubase[p] + (p == R ? 0 : at(R, p, 2));
+        T.ubase[p + 1] = T.ubase[p] + (p == keep ? 0 : at(R, p, 2));
         const int64_t K = at(R, p, 0), S = at(R, p, 1), U = at(R, p, 2), C = at(R, p, 3);
-        if (log_xfer && p != R)
+        if (log_xfer)
             std::fprintf(stderr,
-                         "fs2 xfer scan %lld rank %d -> %d: %lld particles, %lld rows, %lld pages, %lld covariances, "
-                         "%lld B\n",
-                         (long long)h->scan, R, p, (long long)K, (long long)S, (long long)U, (long long)C,
-                         (long long)xfer_bytes(K, S, U, C));
-        if (p == R || K == 0) continue;
+                         "fs2 xfer scan %lld rank %d (shard %d -> %d) -> shard %d (rank %d)%s: %lld particles, "
+                         "%lld rows, %lld pages, %lld covariances, %lld B\n",
+                         (long long)h->scan, R, h->shard, keep, p, owner[p], p == keep ? " kept" : "", (long long)K,
+                         (long long)S, (long long)U, (long long)C, (long long)(p == keep ? 0 : xfer_bytes(K, S, U, C)));
+        if (p == keep || K == 0) continue;
         const size_t bytes = (size_t)xfer_bytes(K, S, U, C);
         rs.sbuf[p] = h->sarena + soff[p];
-        sends.push_back({p, rs.sbuf[p], bytes});
+        sends.push_back({owner[p], rs.sbuf[p], bytes});
         nsend += K;
     }
     if (nsend > INT32_MAX) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld particles to send", (long long)nsend);
@@ -576,7 +644,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     int64_t ubase = 0;
     for (int q = 0; q < G; ++q) {
         if (q == R) continue;
-        const int64_t K = at(q, R, 0), S = at(q, R, 1), U = at(q, R, 2), C = at(q, R, 3);
+        const int64_t K = at(q, keep, 0), S = at(q, keep, 1), U = at(q, keep, 2), C = at(q, keep, 3);
         if (!K) continue;
         const size_t bytes = (size_t)xfer_bytes(K, S, U, C);
         char *rb = h->rarena + roff[q];
@@ -603,7 +671,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
     if (h->profiling) {
         uint64_t np = 0, nr = 0, nu = 0, nb = 0;
         for (int p = 0; p < G; ++p) {
-            if (p == R) continue;
+            if (p == keep) continue;
             np += at(R, p, 0);
             nr += at(R, p, 1);
             nu += at(R, p, 2);
@@ -617,6 +685,18 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         h->prof.migrate_ms +=
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
+    // this rank now holds shard keep: its local outputs (the local sources'
+    // outputs inside that shard) are filled relative to the shard's start
+    rs.ao = shard_begin(h->n_global, G, keep);
+    if (h->follow) {
+        ResampleParams r2 = rs;
+        r2.ranges_mode = 2;
+        HIP_TRY(h, launch_resample_ranges(r2, s));
+    }
+    if (keep != h->shard) h->shard_moves += 1;
+    h->shard = keep;
+    h->first = rs.ao;
+    for (int q = 0; q < G; ++q) h->rank_of[q] = (int8_t)owner[q];
     return FS2_OK;
 }
 
@@ -756,6 +836,14 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     const int64_t G = cfg->world_size, r = cfg->rank;
     h->first = (h->n_global * r) / G;
     h->n = (h->n_global * (r + 1)) / G - h->first;
+    h->shard = (int32_t)r;
+    for (int q = 0; q < kMaxRanks; ++q) h->rank_of[q] = (int8_t)(q < G ? q : 0);
+    // shards can change hands only when they are all the same size (buffers are
+    // sized for n); FS2_SHARD_FOLLOW=0 pins shard r to rank r (A/B)
+    {
+        const char *e = std::getenv("FS2_SHARD_FOLLOW");
+        h->follow = G > 1 && h->n_global % G == 0 && !(e && std::strcmp(e, "0") == 0);
+    }
     h->max_cap = cfg->max_landmark_capacity > 0 ? std::min(cfg->max_landmark_capacity, kMaxSlots) : kMaxSlots;
     h->gate2 = gate_to_q(cfg->max_landmark_distance);
     auto fail = [&](int code) {
@@ -1213,6 +1301,8 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rp.stats = h->stats_dev;
     rp.world = G;
     rp.rank = h->cfg.rank;
+    rp.shard = h->shard;
+    std::memcpy(rp.rank_of, h->rank_of, sizeof rp.rank_of);
     rp.rec = h->rec;
     rp.recs = sh ? h->recs : h->rec;
     rp.totals = h->totals;
@@ -1222,6 +1312,11 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rs.n = h->n;
     rs.N = h->n_global;
     rs.a = h->first;
+    rs.ao = h->first;        // the outputs stay in this shard unless exchange_particles moves it
+    rs.keep = h->shard;
+    // a rank that may take another shard learns which one after the plan counts:
+    // its first k_ranges stores the ranges only, the outputs are filled after
+    rs.ranges_mode = (sh && h->follow) ? 1 : 3;
     rs.w = h->w[cur];
     rs.c = h->cbuf;
     rs.bsum = h->bsum;

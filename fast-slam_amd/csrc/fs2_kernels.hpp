@@ -309,6 +309,11 @@ struct ReduceParams {
     const RankRecord *recs;  // all ranks' records (== rec when world == 1)
     const double *totals;    // all ranks' weight totals (world > 1)
     int32_t world, rank;
+    // the shard (slice of the global particle order) this rank holds and the
+    // rank holding each shard: cross-rank sums run in shard order (DESIGN §5,
+    // "output shards follow their sources")
+    int32_t shard;
+    int8_t rank_of[kMaxRanks];
     // one GPU: k_finalize publishes a scan whose rule did not fire (null: never)
     DevStats *pub_host;
     unsigned long long *pub_flag;
@@ -331,7 +336,10 @@ struct ChainView {
 struct ResampleParams {
     int64_t n;
     int64_t N;               // global particles
-    int64_t a;               // global index of local particle 0 (and of local output 0)
+    int64_t a;               // global index of local particle 0 (the sources)
+    int64_t ao;              // global index of local output 0 (the shard kept; == a on one GPU)
+    int32_t keep;            // shard whose outputs this rank keeps (not sent; == shard of a unless reassigned)
+    int32_t ranges_mode;     // k_ranges: bit 0 store mlo / mhi (and count ties), bit 1 fill out_src
     double *w;               // normalised weights (current)
     double *c;               // local inclusive prefix [n]
     double *bsum;            // block sums (prefix)

@@ -27,10 +27,10 @@ constexpr int kScanBlock = kBlock * kScanPer;     // 1024 elements per block
 
 // ------------------------------------------------------- global reductions --
 
-// Weight total over ranks, in rank order (world > 1).
+// Weight total over ranks, in shard order (world > 1; totals are gathered by rank).
 __global__ void k_global_total(const ReduceParams P) {
     double t = 0.0;
-    for (int g = 0; g < P.world; ++g) t = (g == 0) ? P.totals[0] : t + P.totals[g];
+    for (int q = 0; q < P.world; ++q) t = (q == 0) ? P.totals[P.rank_of[0]] : t + P.totals[P.rank_of[q]];
     P.stats->total = t;
 }
 
@@ -364,16 +364,19 @@ hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
 }
 
 // N_eff (fast_slam_2.py:212-223), the N_eff < N/2 rule (:62), the estimate
-// (:201-210), u0 (:183) and this rank's prefix offset, from all records.
+// (:201-210), u0 (:183) and this rank's prefix offset, from all records (held
+// by rank; the sums run in shard order, the first maximum is order-free).
 template <typename RecOf>
 __device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
     DevStats *st = P.stats;
-    double sq = rec(0).sumsq;
-    double bv = rec(0).best_w;
-    int64_t bi = rec(0).best_gidx;
-    int gb = 0;
+    const int g0 = P.rank_of[0];
+    double sq = rec(g0).sumsq;
+    double bv = rec(g0).best_w;
+    int64_t bi = rec(g0).best_gidx;
+    int gb = g0;
     double off = 0.0;
-    for (int g = 1; g < P.world; ++g) {
+    for (int q = 1; q < P.world; ++q) {
+        const int g = P.rank_of[q];
         sq = sq + rec(g).sumsq;
         const double v = rec(g).best_w;
         const int64_t i = rec(g).best_gidx;
@@ -383,7 +386,7 @@ __device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
             gb = g;
         }
     }
-    for (int g = 0; g < P.rank; ++g) off = (g == 0) ? rec(0).t_local : off + rec(g).t_local;
+    for (int q = 0; q < P.shard; ++q) off = (q == 0) ? rec(g0).t_local : off + rec(P.rank_of[q]).t_local;
     const double ng = (double)P.n_global;
     const double ne = (sq < 1.0 / ng) ? ng : 1.0 / sq;
     st->sumsq = sq;
@@ -631,19 +634,22 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
                                                     : ((i == 0) ? off : ((P.a == 0) ? P.c[i - 1] : off + P.c[i - 1])));
         int64_t lo, hi;
         plan_range(g, P.N, prev, cur, u0, lo, hi);
-        P.mlo[i] = (int32_t)lo;
-        P.mhi[i] = (int32_t)hi;
+        if (P.ranges_mode & 1) {
+            P.mlo[i] = (int32_t)lo;
+            P.mhi[i] = (int32_t)hi;
+        }
         // tree prefix: a u_m within the rounding bound of this boundary might fall
         // on the other side of the reference's sequential value
-        if (P.flip_margin > 0.0 && g != P.N - 1) {
+        if ((P.ranges_mode & 1) && P.flip_margin > 0.0 && g != P.N - 1) {
             const int64_t m1 = hi + 1;                  // first output with u > cur
             const double tol = P.flip_margin * cur;
             if ((m1 < P.N && plan_u(u0, m1, P.N) - cur <= tol) || (m1 > 0 && cur - plan_u(u0, m1 - 1, P.N) <= tol))
                 amb = 1;
         }
-        llo = max(lo, P.a);
-        lhi = min(hi, P.a + P.n - 1);
+        llo = max(lo, P.ao);
+        lhi = min(hi, P.ao + P.n - 1);
     }
+    if (!(P.ranges_mode & 2)) llo = INT64_MAX;     // ranges only: no output filled here
     // out_src of the local outputs.  The wave's sources are consecutive and their
     // local output ranges partition one contiguous range in order, so the wave
     // fills that range together, 64 outputs per step (one lane per source would
@@ -678,7 +684,7 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
                 if (wk[mid] <= o) l = mid;
                 else h = mid - 1;
             }
-            P.out_src[o - P.a] = (int32_t)(i - lane + l);
+            P.out_src[o - P.ao] = (int32_t)(i - lane + l);
         }
     }
     if (P.flip_margin > 0.0) {
@@ -755,8 +761,10 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const ResampleParams P) {
 }
 
 // Exclusive scans of the block totals (totals at iblk[2 nblk], iblk[2 nblk + 1]),
-// then per destination its run, bases and transfer size (xrow: particles, rows;
-// zero for this rank and when the rule did not fire).
+// then per destination shard its run, bases and transfer size (xrow: particles,
+// rows; zero when the rule did not fire).  The shard this rank holds is planned
+// too: the host picks which shard each rank keeps from these counts
+// (exchange_particles), and the kept one is then skipped by the packing.
 __global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
     __shared__ long long lds[16];
     const bool fired = P.stats->resampled != 0;
@@ -786,7 +794,7 @@ __global__ __launch_bounds__(1024) void k_pack_bounds(const ResampleParams P) {
     const int p = threadIdx.x;
     if (p >= P.world) return;
     PackPlan pl{};
-    if (fired && p != P.rank) {
+    if (fired) {
         const int64_t pa = shard_begin(P.N, P.world, p), pb = shard_begin(P.N, P.world, p + 1);
         plan_run(P.n, pa, pb, [&](int64_t i) { return (int64_t)P.mlo[i]; }, [&](int64_t i) { return (int64_t)P.mhi[i]; },
                  pl.i0, pl.i1);
@@ -829,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_headers(const ResampleParams P)
     const int64_t e = P.iblk[b] + P.rank_d[i], c = P.iblk[P.nblk + b] + P.rank_e[i];
     for (int p = 0; p < P.world; ++p) {
         const PackPlan &pl = P.plan[p];
-        if (p == P.rank || i < pl.i0 || i >= pl.i1) continue;
+        if (p == P.keep || i < pl.i0 || i >= pl.i1) continue;
         PackHeader h{};
         h.gsrc = P.a + i;
         h.out_lo = (int32_t)max(lo, pl.pa);
@@ -911,7 +919,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_insert(const ResampleParams P)
     const XferTable &T = P.xt;
     const uint32_t mask = (uint32_t)(T.cap - 1);
     for (int p = 0; p < P.world; ++p) {
-        if (p == P.rank) continue;
+        if (p == P.keep) continue;
         const DedupRow r = dedup_row(P, p, i, k);
         if (!r.key || dedup_row(P, p, i - 1, k).key == r.key) continue;
         bool shared = dedup_row(P, p, i + 1, k).key == r.key;
@@ -943,7 +951,7 @@ __global__ __launch_bounds__(kBlock) void k_dedup_follow(const ResampleParams P)
     const XferTable &T = P.xt;
     const uint32_t mask = (uint32_t)(T.cap - 1);
     for (int p = 0; p < P.world; ++p) {
-        if (p == P.rank) continue;
+        if (p == P.keep) continue;
         const DedupRow r = dedup_row(P, p, i, k);
         if (!r.key || dedup_row(P, p, i - 1, k).key != r.key) continue;
         uint32_t h = xt_hash(r.key, T.log2cap);
@@ -1130,7 +1138,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P,
     if (k >= nrecv) return;
     const int p = peer_of(P, k);
     const PackHeader &h = P.peers[p].hdr[k - P.peers[p].kbase];
-    for (int64_t m = h.out_lo; m <= h.out_hi; ++m) P.out_src[m - P.a] = -(k + 1);
+    for (int64_t m = h.out_lo; m <= h.out_hi; ++m) P.out_src[m - P.ao] = -(k + 1);
 }
 
 // Received distinct pages into fresh pages and records: received page u takes
@@ -1258,7 +1266,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             P.oyaw[m] = P.yaw[s];
             w = P.w[s];
             c = P.cnt[s];
-            const int64_t lo = max((int64_t)P.mlo[s], P.a), hi = min((int64_t)P.mhi[s], P.a + n - 1);
+            const int64_t lo = max((int64_t)P.mlo[s], P.ao), hi = min((int64_t)P.mhi[s], P.ao + n - 1);
             keep = (hi == lo) ? 0xffffffffu : kIdMask;
             src = pt_entry(P.map, 0, s);
             stride = n;
@@ -1399,7 +1407,7 @@ __device__ void estimate_body(const ResampleParams &P, int32_t nparts) {
         P.stats->resample_slots = sl;
         RankRecord r = *P.rec;
         r.best_w = bv;
-        r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.a + bi;
+        r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.ao + bi;
         if (bi != INT64_MAX) {
             r.pose[0] = P.ox[bi];
             r.pose[1] = P.oy[bi];

@@ -77,7 +77,6 @@ class FastSLAM2:
         nat.check(lib.fs2_shard_info(h, C.byref(n_local), C.byref(first), C.byref(cap)), h)
         self.num_particles = int(cfg.num_particles)
         self.n_local = int(n_local.value)
-        self.first_global = int(first.value)
         self._particles = None
         self.last_stats = None
         # step(): fs2_iterate through a prototype of plain addresses and buffers
@@ -98,6 +97,17 @@ class FastSLAM2:
         self._st_addr = C.addressof(self._st)
         self._u0 = np.empty(1)
         self._u0_addr = self._u0.ctypes.data
+
+    @property
+    def first_global(self) -> int:
+        """Global index of local particle 0.  Sharded handles with equal shards may
+        take another shard at a resample (the one their sources fill most; DESIGN.md
+        §5), so this is read from libfs2 each time."""
+        if self._h is None:
+            raise nat.FS2Error(nat.FS2_ERR_ARG, "first_global of a closed FastSLAM2 handle")
+        n_local, first, cap = C.c_int64(), C.c_int64(), C.c_int32()
+        nat.check(self._lib.fs2_shard_info(self._h, C.byref(n_local), C.byref(first), C.byref(cap)), self._h)
+        return int(first.value)
 
     # ------------------------------------------------------------------ core
     def iterate(self, rotation: float, translation: float,

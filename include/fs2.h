@@ -221,7 +221,10 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x,
  * Requires cfg.record_assoc. */
 int fs2_get_assoc(fs2_handle *h, int32_t *idx, int64_t capacity, int32_t *m_out);
 
-/* Local shard geometry and current map capacity. */
+/* Local shard geometry and current map capacity.  With world_size > 1 and
+ * num_particles divisible by world_size, a resample may hand this rank another
+ * shard (the one its own sources fill most), so first_global can
+ * change after any scan that resampled: read it after the scan, not once. */
 int fs2_shard_info(const fs2_handle *h, int64_t *n_local, int64_t *first_global,
                    int32_t *capacity);
 

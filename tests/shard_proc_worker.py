@@ -17,49 +17,66 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "fast-slam_amd"))
 import numpy as np  # noqa: E402
 
 
-def workload(N, L, seed):
+def workload(N, L, seed, mode="peaked", G=1):
+    """mode "peaked": peaked likelihoods, so resampling moves particles across
+    shards; "follow": only rank 0's particles carry weight (its first 100 ten
+    times more), so the first scan (no measurements) resamples and rank 0 keeps
+    a higher shard (equal shards follow their sources)."""
     import fs2_synthetic as syn
     wl = syn.Workload(N, L, seed=seed)
     x, y, yaw = wl.poses()
     lm = wl.maps()
-    lm[:, :, 2] = lm[:, :, 5] = 0.01        # peaked likelihoods: resampling moves particles across shards
-    return wl, x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm
+    w = np.full(N, 1.0 / N)
+    if mode == "follow":
+        w = np.zeros(N)
+        w[:N // G] = 1e-3
+        w[:100] = 1e-2
+    else:
+        lm[:, :, 2] = lm[:, :, 5] = 0.01
+    return wl, x, y, yaw, w, np.full(N, L, np.int32), lm
+
+
+def measurements(wl, s, mode):
+    return np.zeros((0, 2)) if (mode == "follow" and s == 0) else wl.measurements(s)
 
 
 def main(argv):
     G, rank, N, L, seed, scans = (int(a) for a in argv[:6])
     key = bytes.fromhex(argv[6])
     out = argv[7]
+    mode = argv[8] if len(argv) > 8 else "peaked"
     import torch  # noqa: F401  -- one HIP runtime in the process
     import fast_slam_2
     import fs2_synthetic as syn
     from gpu_util import configure
     configure()
-    wl, x, y, yaw, w, cnt, lm = workload(N, L, seed)
+    wl, x, y, yaw, w, cnt, lm = workload(N, L, seed, mode, G)
     cap = L + 4 * scans + 8
     h = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap, rank=rank,
                               world_size=G, comm_id=key, comm_mode="shm", verbose=False)
     a, b = h.first_global, h.first_global + h.n_local
     h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
     h.set_profiling(True)
-    rec = {k: [] for k in ("resampled", "best_index", "pose", "n_eff", "reduce_amb", "n_recv")}
+    rec = {k: [] for k in ("resampled", "best_index", "pose", "n_eff", "reduce_amb", "firsts")}
     assoc = []
     for s in range(scans):
         rot, tr = syn.odometry(s)
-        pose, st = h.step(rot, tr, wl.measurements(s))
+        pose, st = h.step(rot, tr, measurements(wl, s, mode))
         rec["resampled"].append(st.resampled)
         rec["best_index"].append(st.best_index)
         rec["pose"].append(pose)
         rec["n_eff"].append(st.n_eff)
         rec["reduce_amb"].append(st.reduce_ambiguous)
         assoc.append(h.associations())
+        rec["firsts"].append(h.first_global)        # a resample may hand this rank another shard
         print(f"rank {rank} scan {s} resampled {st.resampled}", flush=True)
     xs, ys, yaws, ws, cnts, lms = h.get_state(lm_cap=cap)
+    a, b = h.first_global, h.first_global + h.n_local
     prof = h.profile()
     h.close()
     np.savez(out, first=a, count=b - a, assoc=np.stack(assoc), x=xs, y=ys, yaw=yaws, w=ws, cnt=cnts, lm=lms,
              sent_particles=prof["sent_particles"], sent_rows=prof["sent_rows"], sent_pages=prof["sent_pages"],
-             migrations=prof["migrations"], **{k: np.array(v) for k, v in rec.items() if k != "n_recv"})
+             migrations=prof["migrations"], **{k: np.array(v) for k, v in rec.items()})
     return 0
 
 

@@ -40,8 +40,14 @@ def _step_all(handles, rot, tr, ms):
     return out
 
 
+def _ordered(handles):
+    """Handles in the order of the shards they hold (equal shards change hands at
+    resamples: a rank keeps the shard its sources fill most)."""
+    return sorted(handles, key=lambda h: h.first_global)
+
+
 def _gather(handles, cap):
-    parts = [h.get_state(lm_cap=cap) for h in handles]
+    parts = [h.get_state(lm_cap=cap) for h in _ordered(handles)]
     return [np.concatenate([p[k] for p in parts]) for k in range(6)]
 
 
@@ -73,6 +79,7 @@ def test_sharded_matches_single(G, N, L):
         h.set_profiling(True)
     resamples = 0
     moved = 0
+    firsts = {g: {h.first_global} for g, h in enumerate(shards)}
     for s in range(8):
         rot, tr = syn.odometry(s)
         ms = wl.measurements(s)
@@ -86,8 +93,11 @@ def test_sharded_matches_single(G, N, L):
             assert st.reduce_ambiguous == 0, s          # no decision the shard order could flip
         resamples += st1.resampled
         moved += sum(sh.last_stats.resample_slots for sh in shards)
+        for g, h in enumerate(shards):
+            firsts[g].add(h.first_global)
+        assert sorted(h.first_global for h in shards) == [N * g // G for g in range(G)], s
         a1 = single.associations()
-        ag = np.concatenate([h.associations() for h in shards], axis=1)
+        ag = np.concatenate([h.associations() for h in _ordered(shards)], axis=1)
         assert np.array_equal(a1, ag), s
         s1 = single.get_state(lm_cap=cap)
         sg = _gather(shards, cap)
@@ -104,6 +114,84 @@ def test_sharded_matches_single(G, N, L):
     assert sum(p["sent_pages"] for p in prof) < sum(p["sent_rows"] for p in prof)
     for h in shards + [single]:
         h.close()
+
+
+def _follow_case(G, N, L, seed):
+    """Rank 0's particles alone carry weight, its first 100 ten times more than
+    the rest: its sources fill shard 0 with few (heavy) particles and the other
+    shards with many, so with shards following their sources rank 0 keeps a
+    higher shard and the other ranks take the rest (all received)."""
+    import fs2_synthetic as syn
+    wl = syn.Workload(N, L, seed=seed)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    n0 = N // G
+    w = np.zeros(N)
+    w[:n0] = 1e-3
+    w[:100] = 1e-2
+    return wl, x, y, yaw, w, np.full(N, L, np.int32), lm
+
+
+@pytest.mark.parametrize("G,N", [(2, 6000), (4, 8192)])
+def test_shards_follow_sources(G, N, monkeypatch):
+    """A resample hands a rank the shard its own sources fill most (DESIGN §5,
+    "output shards follow their sources"): every scan still equals a single handle,
+    the shards stay a partition of the global order, and fewer particles move than
+    with shard r pinned to rank r (FS2_SHARD_FOLLOW=0, the A/B)."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    configure()
+    L = 16
+    wl, x, y, yaw, w, cnt, lm = _follow_case(G, N, L, 5)
+    cap = L + 24
+    single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=9, landmark_capacity=cap,
+                                   verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    sent = {}
+    for follow in ("1", "0"):
+        monkeypatch.setenv("FS2_SHARD_FOLLOW", follow)
+        key = os.urandom(128)
+        shards = [fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=9, landmark_capacity=cap,
+                                        rank=g, world_size=G, comm_id=key, comm_mode="local", verbose=False)
+                  for g in range(G)]
+        for h in shards:
+            a, b = h.first_global, h.first_global + h.n_local
+            h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+            h.set_profiling(True)
+        if follow == "0":
+            single.close()
+            single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=9, landmark_capacity=cap,
+                                           verbose=False)
+            single.set_state(x, y, yaw, w, cnt, lm)
+        for s in range(3):
+            ms = np.zeros((0, 2)) if s == 0 else wl.measurements(s)
+            pose1, st1 = single.step(0.0, 0.03, ms)
+            outs = _step_all(shards, 0.0, 0.03, ms)
+            if s == 0:
+                assert st1.resampled == 1
+            for pose, st in outs:
+                assert st.resampled == st1.resampled and st.best_index == st1.best_index, s
+                assert np.allclose(pose, pose1, rtol=1e-9, atol=1e-12), s
+                assert st.reduce_ambiguous == 0, s
+            assert sorted(h.first_global for h in shards) == [N * g // G for g in range(G)], s
+            assert np.array_equal(single.associations(),
+                                  np.concatenate([h.associations() for h in _ordered(shards)], axis=1)), s
+            s1 = single.get_state(lm_cap=cap)
+            sg = _gather(shards, cap)
+            assert np.array_equal(s1[4], sg[4]), s
+            for k in range(4):
+                assert np.allclose(s1[k], sg[k], rtol=1e-9, atol=1e-15), (s, k)
+            assert np.allclose(s1[5], sg[5], rtol=1e-9, atol=1e-12), s
+        if follow == "1":
+            assert shards[0].first_global > 0, "rank 0 keeps the higher shard its sources fill most"
+        else:
+            assert [h.first_global for h in shards] == [N * g // G for g in range(G)]
+        sent[follow] = sum(h.profile()["sent_particles"] for h in shards)
+        for h in shards:
+            h.close()
+    single.close()
+    assert 0 < sent["1"] < sent["0"], sent
 
 
 @pytest.mark.parametrize("mode", ["rccl", "local"])
@@ -180,7 +268,7 @@ def test_sharded_long_run_with_collections():
             assert st.resampled == st1.resampled and st.best_index == st1.best_index, s
             assert np.allclose(pose, pose1, rtol=1e-9, atol=1e-12), s
         assert np.array_equal(single.associations(),
-                              np.concatenate([h.associations() for h in shards], axis=1)), s
+                              np.concatenate([h.associations() for h in _ordered(shards)], axis=1)), s
         resamples += st1.resampled
     cap = L + 30 * 4
     s1 = single.get_state(lm_cap=cap)

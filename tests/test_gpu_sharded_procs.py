@@ -27,19 +27,20 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("G,N,L,scans", [(2, 6000, 40, 8), (3, 10007, 30, 8)])
-def test_sharded_processes_match_single(G, N, L, scans, tmp_path):
+@pytest.mark.parametrize("G,N,L,scans,mode", [(2, 6000, 40, 8, "peaked"), (3, 10007, 30, 8, "peaked"),
+                                               (2, 6000, 24, 4, "follow")])
+def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     import torch  # noqa: F401
     import fast_slam_2
     import fs2_synthetic as syn
     from gpu_util import configure
-    from shard_proc_worker import workload
+    from shard_proc_worker import measurements, workload
     configure()
     key = os.urandom(128).hex()
     env = dict(os.environ, FS2_SHM_CHUNK=str(64 << 10), FS2_SHM_TIMEOUT_S="40")   # small mailboxes: rounds
     outs = [str(tmp_path / f"rank{r}.npz") for r in range(G)]
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "shard_proc_worker.py"), str(G), str(r),
-                               str(N), str(L), "21", str(scans), key, outs[r]],
+                               str(N), str(L), "21", str(scans), key, outs[r], mode],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for r in range(G)]
     logs = []
@@ -54,7 +55,7 @@ def test_sharded_processes_match_single(G, N, L, scans, tmp_path):
         assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-4000:]}"
     ranks = [np.load(o) for o in outs]
 
-    wl, x, y, yaw, w, cnt, lm = workload(N, L, 21)
+    wl, x, y, yaw, w, cnt, lm = workload(N, L, 21, mode, G)
     cap = L + 4 * scans + 8
     single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap,
                                    verbose=False)
@@ -62,14 +63,16 @@ def test_sharded_processes_match_single(G, N, L, scans, tmp_path):
     resamples = 0
     for s in range(scans):
         rot, tr = syn.odometry(s)
-        pose1, st1 = single.step(rot, tr, wl.measurements(s))
+        pose1, st1 = single.step(rot, tr, measurements(wl, s, mode))
         for r, d in enumerate(ranks):
             assert d["resampled"][s] == st1.resampled, (r, s)
             assert d["best_index"][s] == st1.best_index, (r, s)
             assert np.allclose(d["pose"][s], pose1, rtol=1e-9, atol=1e-12), (r, s)
             assert np.isclose(d["n_eff"][s], st1.n_eff, rtol=1e-9), (r, s)
             assert d["reduce_amb"][s] == 0, (r, s)
-        assert np.array_equal(single.associations(), np.concatenate([d["assoc"][s] for d in ranks], axis=1)), s
+        # ranks in the order of the shards they hold after scan s (equal shards change hands)
+        order = sorted(ranks, key=lambda d: int(d["firsts"][s]))
+        assert np.array_equal(single.associations(), np.concatenate([d["assoc"][s] for d in order], axis=1)), s
         resamples += st1.resampled
     s1 = single.get_state(lm_cap=cap)
     for d in ranks:
@@ -79,6 +82,10 @@ def test_sharded_processes_match_single(G, N, L, scans, tmp_path):
             assert np.allclose(s1[k][a:b], d[name], rtol=1e-9, atol=1e-15), name
         assert np.allclose(s1[5][a:b], d["lm"], rtol=1e-9, atol=1e-12)
     single.close()
-    assert resamples >= 2
-    assert sum(int(d["migrations"]) for d in ranks) >= 2, "particles must cross shards at least twice"
+    need = 1 if mode == "follow" else 2
+    assert resamples >= need
+    assert sum(int(d["migrations"]) for d in ranks) >= need, "particles must cross shards"
     assert sum(int(d["sent_pages"]) for d in ranks) < sum(int(d["sent_rows"]) for d in ranks)
+    if mode == "follow":     # rank 0 took the higher shard its sources fill most
+        assert int(ranks[0]["firsts"][0]) > 0 and int(ranks[0]["first"]) > 0
+
