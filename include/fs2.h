@@ -217,6 +217,8 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x,
 
 /* Association index per (measurement, local particle) of the last scan,
  * [M][N_local] row-major; -1 = no landmark associated (a new one was appended).
+ * The particles are those of the scan's update pass, before its resample (a
+ * sharded rank: the shard it held before the scan; see fs2_shard_info).
  * Mirrors the return of LandmarkUtils.associate_landmarks (landmark_utils.py:92-117).
  * Requires cfg.record_assoc. */
 int fs2_get_assoc(fs2_handle *h, int32_t *idx, int64_t capacity, int32_t *m_out);

@@ -57,10 +57,11 @@ def main(argv):
     a, b = h.first_global, h.first_global + h.n_local
     h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
     h.set_profiling(True)
-    rec = {k: [] for k in ("resampled", "best_index", "pose", "n_eff", "reduce_amb", "firsts")}
+    rec = {k: [] for k in ("resampled", "best_index", "pose", "n_eff", "reduce_amb", "firsts", "firsts_pre")}
     assoc = []
     for s in range(scans):
         rot, tr = syn.odometry(s)
+        rec["firsts_pre"].append(h.first_global)    # the shard whose particles the associations describe
         pose, st = h.step(rot, tr, measurements(wl, s, mode))
         rec["resampled"].append(st.resampled)
         rec["best_index"].append(st.best_index)

@@ -70,8 +70,9 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
             assert np.allclose(d["pose"][s], pose1, rtol=1e-9, atol=1e-12), (r, s)
             assert np.isclose(d["n_eff"][s], st1.n_eff, rtol=1e-9), (r, s)
             assert d["reduce_amb"][s] == 0, (r, s)
-        # ranks in the order of the shards they hold after scan s (equal shards change hands)
-        order = sorted(ranks, key=lambda d: int(d["firsts"][s]))
+        # ranks in the order of the shards they held during scan s's update pass (the
+        # associations' particles; a resample may then hand a rank another shard)
+        order = sorted(ranks, key=lambda d: int(d["firsts_pre"][s]))
         assert np.array_equal(single.associations(), np.concatenate([d["assoc"][s] for d in order], axis=1)), s
         resamples += st1.resampled
     s1 = single.get_state(lm_cap=cap)
