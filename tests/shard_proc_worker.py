@@ -68,7 +68,10 @@ def main(argv):
         rec["pose"].append(pose)
         rec["n_eff"].append(st.n_eff)
         rec["reduce_amb"].append(st.reduce_ambiguous)
-        assoc.append(h.associations())
+        a = h.associations()
+        pad = np.full((4, h.n_local), -2, np.int32)      # scans without measurements: 0 rows
+        pad[:a.shape[0]] = a
+        assoc.append(pad)
         rec["firsts"].append(h.first_global)        # a resample may hand this rank another shard
         print(f"rank {rank} scan {s} resampled {st.resampled}", flush=True)
     xs, ys, yaws, ws, cnts, lms = h.get_state(lm_cap=cap)

@@ -73,7 +73,8 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
         # ranks in the order of the shards they held during scan s's update pass (the
         # associations' particles; a resample may then hand a rank another shard)
         order = sorted(ranks, key=lambda d: int(d["firsts_pre"][s]))
-        assert np.array_equal(single.associations(), np.concatenate([d["assoc"][s] for d in order], axis=1)), s
+        a1 = single.associations()
+        assert np.array_equal(a1, np.concatenate([d["assoc"][s][:a1.shape[0]] for d in order], axis=1)), s
         resamples += st1.resampled
     s1 = single.get_state(lm_cap=cap)
     for d in ranks:
@@ -86,7 +87,10 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     need = 1 if mode == "follow" else 2
     assert resamples >= need
     assert sum(int(d["migrations"]) for d in ranks) >= need, "particles must cross shards"
-    assert sum(int(d["sent_pages"]) for d in ranks) < sum(int(d["sent_rows"]) for d in ranks)
+    pages, rows = sum(int(d["sent_pages"]) for d in ranks), sum(int(d["sent_rows"]) for d in ranks)
+    # siblings share pages once particles have resampled ancestors ("follow" moves
+    # each particle's own initial map once: nothing shared yet)
+    assert pages < rows if mode == "peaked" else pages <= rows
     if mode == "follow":     # rank 0 took the higher shard its sources fill most
         assert int(ranks[0]["firsts"][0]) > 0 and int(ranks[0]["first"]) > 0
 
