@@ -241,6 +241,16 @@ struct fs2_handle {
     }
 };
 
+// A copy that touches the handle's memory, ordered on its (non-blocking) stream
+// and complete on return.  A plain hipMemcpy between two device buffers may
+// return before the copy ends and is not ordered with that stream, so a kernel
+// or memset the handle enqueues next could overtake it (a chunked export read
+// back zeros that way).
+static hipError_t copy_sync(fs2_handle *h, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, h->stream);
+    return e == hipSuccess ? hipStreamSynchronize(h->stream) : e;
+}
+
 // Host wall time of one transport call or mid-scan wait, into the profile.
 struct CommTimer {
     fs2_handle *h;
@@ -278,7 +288,7 @@ static int grow_rows(fs2_handle *h, int need_slots) {
     for (int b = 0; b < 2; ++b) {
         Desc *p = nullptr;
         HIP_TRY(h, hipMalloc(&p, row_bytes * rows));
-        if (h->pt[b] && b == h->cur) HIP_TRY(h, hipMemcpy(p, h->pt[b], row_bytes * h->rows, hipMemcpyDeviceToDevice));
+        if (h->pt[b] && b == h->cur) HIP_TRY(h, copy_sync(h, p, h->pt[b], row_bytes * h->rows, hipMemcpyDeviceToDevice));
         hipFree(h->pt[b]);
         h->pt[b] = p;
     }
@@ -327,7 +337,7 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     char *pool = nullptr;
     HIP_TRY(h, hipMalloc(&pool, (size_t)pages * kPageBytes));
-    if (h->pool) HIP_TRY(h, hipMemcpy(pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
+    if (h->pool) HIP_TRY(h, copy_sync(h, pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
     hipFree(h->pool);
     h->pool = pool;
     uint8_t *mark = nullptr;
@@ -360,7 +370,7 @@ static int grow_recs(fs2_handle *h, int64_t n) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     char *rp = nullptr;
     HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
-    if (h->rpool) HIP_TRY(h, hipMemcpy(rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
+    if (h->rpool) HIP_TRY(h, copy_sync(h, rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
     hipFree(h->rpool);
     h->rpool = rp;
     uint8_t *mark = nullptr;
@@ -1569,10 +1579,10 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
     HIP_TRY(h, hipStreamSynchronize(s));
     if (count == 0) return FS2_OK;
     const size_t b8 = sizeof(double) * count;
-    if (x) HIP_TRY(h, hipMemcpy(h->x[c] + first, x, b8, kind_in(where)));
-    if (y) HIP_TRY(h, hipMemcpy(h->y[c] + first, y, b8, kind_in(where)));
-    if (yaw) HIP_TRY(h, hipMemcpy(h->yaw[c] + first, yaw, b8, kind_in(where)));
-    if (w) HIP_TRY(h, hipMemcpy(h->w[c] + first, w, b8, kind_in(where)));
+    if (x) HIP_TRY(h, copy_sync(h, h->x[c] + first, x, b8, kind_in(where)));
+    if (y) HIP_TRY(h, copy_sync(h, h->y[c] + first, y, b8, kind_in(where)));
+    if (yaw) HIP_TRY(h, copy_sync(h, h->yaw[c] + first, yaw, b8, kind_in(where)));
+    if (w) HIP_TRY(h, copy_sync(h, h->w[c] + first, w, b8, kind_in(where)));
     if (cnt) {
         std::vector<int32_t> hc(count);
         HIP_TRY(h, hipMemcpy(hc.data(), cnt, sizeof(int32_t) * count,
@@ -1600,7 +1610,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         int rc2 = FS2_OK;
         for (int64_t o = 0; o < count && rc2 == FS2_OK; o += chunk) {
             const int64_t k = std::min(chunk, count - o);
-            hipError_t e = hipMemcpy(stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
+            hipError_t e = copy_sync(h, stage, lm + o * lm_cap * 6, (size_t)k * per, kind_in(where));
             if (e == hipSuccess) e = hipMemcpy(cstage, hc.data() + o, sizeof(int32_t) * k, hipMemcpyHostToDevice);
             // the chunk's layout, from its first map (the filter's page boxes are
             // what it serves; handles without the filter keep slot order)
@@ -1701,11 +1711,11 @@ int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double
     HIP_TRY(h, hipStreamSynchronize(s));
     if (count == 0) return FS2_OK;
     const size_t b8 = sizeof(double) * count;
-    if (x) HIP_TRY(h, hipMemcpy(x, h->x[c] + first, b8, kind_out(where)));
-    if (y) HIP_TRY(h, hipMemcpy(y, h->y[c] + first, b8, kind_out(where)));
-    if (yaw) HIP_TRY(h, hipMemcpy(yaw, h->yaw[c] + first, b8, kind_out(where)));
-    if (w) HIP_TRY(h, hipMemcpy(w, h->w[c] + first, b8, kind_out(where)));
-    if (cnt) HIP_TRY(h, hipMemcpy(cnt, h->cnt[c] + first, sizeof(int32_t) * count, kind_out(where)));
+    if (x) HIP_TRY(h, copy_sync(h, x, h->x[c] + first, b8, kind_out(where)));
+    if (y) HIP_TRY(h, copy_sync(h, y, h->y[c] + first, b8, kind_out(where)));
+    if (yaw) HIP_TRY(h, copy_sync(h, yaw, h->yaw[c] + first, b8, kind_out(where)));
+    if (w) HIP_TRY(h, copy_sync(h, w, h->w[c] + first, b8, kind_out(where)));
+    if (cnt) HIP_TRY(h, copy_sync(h, cnt, h->cnt[c] + first, sizeof(int32_t) * count, kind_out(where)));
     if (lm) {
         if (lm_cap < 0) return set_err(&h->err, FS2_ERR_ARG, "lm_cap < 0");
         std::vector<int32_t> hc(count);
@@ -1722,7 +1732,7 @@ int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double
             hipError_t e = hipMemsetAsync(stage, 0, (size_t)k * per, s);
             if (e == hipSuccess) e = launch_export(stage, first + o, k, lm_cap, h->map(), h->cnt[c], s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e == hipSuccess) e = hipMemcpy(lm + o * lm_cap * 6, stage, (size_t)k * per, kind_out(where));
+            if (e == hipSuccess) e = copy_sync(h, lm + o * lm_cap * 6, stage, (size_t)k * per, kind_out(where));
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state export failed: %s", hipGetErrorString(e));
         }
         hipFree(stage);

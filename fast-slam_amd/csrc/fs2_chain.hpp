@@ -28,6 +28,9 @@ __device__ __forceinline__ long long wave_incl_scan_i64(long long v) {
 __device__ __forceinline__ double unit_ulp(int E) { return ldexp(1.0, E - 52); }
 __device__ __forceinline__ double scaled(double a, int E) { return ldexp(a, 52 - E); }
 __device__ __forceinline__ int unit_binade(int32_t info) { return (info >> 2) - 4096; }
+// binade of a chain value v >= 0 whose grid the chain runs on: values below 2^-1021
+// (zero, subnormals, [2^-1022, 2^-1021)) share the step 2^-1074 = unit_ulp(-1022)
+__device__ __forceinline__ int chain_binade(double v) { return v < 0x1p-1021 ? -1022 : ilogb(v); }
 
 __device__ __forceinline__ long long bcast_i64(long long v, int j) {
     return __double_as_longlong(bcast(__longlong_as_double(v), j));
@@ -91,13 +94,13 @@ __device__ inline double chain_unit(double a, int cnt, double &s, bool first) {
             j0 = jn + 1;
             continue;
         }
-        if (!(s >= 0x1p-1020 && s < 0x1p1020)) {           // outside the regular grid: one step
+        if (!(s >= 0.0 && s < 0x1p1020)) {                 // outside the regular grid: one step
             s = s + bcast(a, j0);
             if (lane == j0) mine = s;
             ++j0;
             continue;
         }
-        const int E = ilogb(s);
+        const int E = chain_binade(s);
         const double u = unit_ulp(E), top = ldexp(1.0, E + 1);
         const double q = active ? scaled(a, E) : 0.0;
         const bool ok = active && a >= 0.0 && q < 0x1p53;    // false for NaN, inf, negative

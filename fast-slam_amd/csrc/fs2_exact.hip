@@ -131,9 +131,13 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         double e_in = s_bp[c4];
         for (int q = 4 * c4; q < wid; ++q) e_in += s_ws[q];
         const double lo = (e_in + (incl - a)) * (1.0 - P.margin), hi = (e_in + incl) * (1.0 + P.margin);
-        bool ok = valid && i != 0 && a >= 0.0 && a < INFINITY && lo >= 0x1p-1020 && hi < 0x1p1020;
-        const int E = ok ? ilogb(lo) : -4096;
-        ok = ok && ilogb(hi) == E;
+        // [0, 2^-1021) -- zero, the subnormals and the lowest normal binade -- is one
+        // grid of step 2^-1074 (binade -1022 below): every add there is exact, so a
+        // run of zero or subnormal weights (a diverged filter's underflowed
+        // likelihoods) is a translation too, not a unit walked term by term
+        bool ok = valid && i != 0 && a >= 0.0 && a < INFINITY && lo >= 0.0 && hi < 0x1p1020;
+        const int E = ok ? chain_binade(lo) : -4096;
+        ok = ok && chain_binade(hi) == E;
         long long r = 0;
         if (ok) {
             const double q = scaled(a, E);          // < 2^53: exact

@@ -8,7 +8,8 @@ with the C oracle's sequential loops bit for bit: the weight total, every
 normalised weight, N_eff, the decision and every resample source.  The cases
 stress what the parallel evaluation has to get right: many binades crossed,
 exact rounding ties (round-half-even depends on the running value), leading
-zeros, a u_m landing exactly on a prefix value, N_eff exactly N/2.  The tree
+zeros, a u_m landing exactly on a prefix value, N_eff exactly N/2, all-zero and
+subnormal weights (one exact grid below 2^-1021).  The tree
 mode (PARALLEL) reports such near-boundary decisions in reduce_ambiguous.
 """
 import numpy as np
@@ -89,6 +90,16 @@ def cases():
         n = 2 * 8192 + tail
         out.append((f"tail_{tail}", rng.random(n) ** 2, 0.3 / n))
     out.append(("cfg3_size", rng.lognormal(0.0, 2.0, 1_000_000), 0.77e-6))
+    # a diverged filter: every likelihood underflowed (the total is 0, the
+    # reference resets the weights to 1/N) -- the chain runs on zeros throughout
+    out.append(("all_zero", np.zeros(1_000_000), 0.5e-6))
+    # the grid below 2^-1021 (subnormals, zeros) and the crossing out of it into
+    # the normal binades, then into the weights that normalise
+    w = rng.integers(0, 1 << 40, 200_003).astype(np.float64) * 2.0 ** -1074
+    w[::7] = 0.0
+    w[120_000:] = rng.random(80_003) * 1e-300
+    w[190_000:] = rng.random(10_003) * 1e-3
+    out.append(("subnormal_grid", w, 0.45 / 200_003))
     return out
 
 
