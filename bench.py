@@ -21,6 +21,7 @@ Default workload: BASELINE config 3, 1e6 particles per GPU x 500 landmarks.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -329,20 +330,23 @@ def robustness(args, f, L, first_scan):
     out["sharded_local_g2"] = sharded_local(args, L, n)
     out["sharded_local_g8"] = sharded_local(args, L, n, G=8)
     out["dropin_iterate"] = dropin(args, L, n)
+    out["dropin_iterate_host_rng"] = dropin(args, L, n, rng="numpy-host")
     return out
 
 
-def dropin(args, L, n, scans=8, warm=2):
+def dropin(args, L, n, scans=8, warm=2, rng="numpy"):
     """What a reference caller gets: FastSLAM2.iterate(rotation, translation,
     list[Measurement]) (fast_slam_2.py:33, called at jde_robots_main.py:38) with
-    numpy's global legacy RNG -- N normals drawn on the host per scan, and the
-    resample start, exactly as the reference draws them (Q4/Q5) -- on a handle of
-    the headline size.  host_rng_ms: np.random.normal of N values alone."""
+    numpy's global legacy RNG -- N normals per scan and the resample start,
+    exactly as the reference draws them (Q4/Q5) -- on a handle of the headline
+    size.  rng="numpy": drawn on the GPU from np.random's state (fs2_mt_draw);
+    "numpy-host": drawn by numpy on the host.  host_rng_ms: np.random.normal of N
+    values alone.  The numpy state after the run is the same either way."""
     import fast_slam_2
     import fs2_synthetic as syn
     from fast_slam_2.models.measurement import Measurement
     np.random.seed(args.seed)
-    f = fast_slam_2.FastSLAM2(n, rng="numpy", seed=args.seed, landmark_capacity=L + scans + 8, verbose=False)
+    f = fast_slam_2.FastSLAM2(n, rng=rng, seed=args.seed, landmark_capacity=L + scans + 8, verbose=False)
     populate(f, n, L, args.seed, 0)
     meas = [[Measurement(float(d), float(b)) for d, b in syn.scan_measurements(L, s, args.seed)]
             for s in range(scans)]
@@ -355,15 +359,17 @@ def dropin(args, L, n, scans=8, warm=2):
         res += f.last_stats.resampled
     dt = time.perf_counter() - t0
     f.close()
+    state_digest = hashlib.sha1(np.random.get_state()[1].tobytes()).hexdigest()[:12]
     t1 = time.perf_counter()
     for _ in range(3):
         np.random.normal(0, 0.0055, size=n)
     rng_ms = (time.perf_counter() - t1) / 3 * 1e3
     k = scans - warm
+    note = ("FastSLAM2.iterate() with numpy's legacy RNG (the reference's draws, bit for bit); "
+            + ("drawn on the GPU from np.random's state (MT19937 + polar method, fs2_mt_draw)" if rng == "numpy"
+               else "drawn by numpy on one host core (host-RNG bound)"))
     return {"value": n * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k, "resamples": res,
-            "host_rng_ms": rng_ms,
-            "note": "FastSLAM2.iterate() with numpy's legacy RNG (the reference's draws, bit for bit): "
-                    "host-RNG bound -- N legacy-MT19937 normals per scan on one host core"}
+            "host_rng_ms": rng_ms, "rng": rng, "numpy_state_sha1": state_digest, "note": note}
 
 
 def sharded_local(args, L, n_total, G=2, scans=9, warm=3):

@@ -18,7 +18,7 @@ LIB = os.path.join(LIB_DIR, "libfs2.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("FS2_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["fs2_api.hip", "fs2_update.hip", "fs2_resample.hip", "fs2_exact.hip", "fs2_pages.hip", "fs2_cluster.hip",
-           "fs2_geometry.hip", "fs2_frontend.hip"]
+           "fs2_geometry.hip", "fs2_frontend.hip", "fs2_mtrng.hip"]
 # every header in csrc/ (a header left out of the hash would let a stale library pass)
 HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp"))
 

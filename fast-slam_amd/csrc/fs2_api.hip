@@ -18,6 +18,7 @@
 #include "fs2_comm.hpp"
 #include "fs2_frontend.hpp"
 #include "fs2_kernels.hpp"
+#include "fs2_mtrng.hpp"
 #include "fs2_plan.hpp"
 
 using namespace fs2;
@@ -146,6 +147,22 @@ struct fs2_handle {
     unsigned long long pub_seq = 0;
     bool stats_clean = false;              // stats_dev is zero (k_publish ran last)
     double *noise_dev = nullptr, *noise_pin = nullptr, *u0_dev = nullptr, *u0_pin = nullptr;
+    // numpy's legacy RandomState on the device (fs2_mt_draw): stream words, block
+    // offsets, results, listed logs, host patches; the next scan uses its draws
+    struct MtWork {
+        uint32_t *raw = nullptr;
+        int64_t raw_cap = 0;
+        int32_t *boff = nullptr;
+        int64_t boff_cap = 0;
+        MtMeta *meta = nullptr, *meta_pin = nullptr;
+        MtAmb *amb = nullptr, *amb_pin = nullptr;
+        int64_t amb_cap = 0;
+        uint32_t *words_pin = nullptr;     // [2 kMtN]: key in, state blocks out
+        int64_t *pidx = nullptr, *pidx_pin = nullptr;
+        double *pval = nullptr, *pval_pin = nullptr;
+        int64_t patch_cap = 0, pval_cap = 0;
+        bool armed = false;
+    } mt;
     int32_t *assoc_dev = nullptr;
     int64_t assoc_cap = 0;
     int32_t last_m = 0;
@@ -815,6 +832,13 @@ static void free_handle(fs2_handle *h) {
     if (h->pub_stats) hipHostFree(h->pub_stats);
     if (h->noise_pin) hipHostFree(h->noise_pin);
     if (h->u0_pin) hipHostFree(h->u0_pin);
+    hipFree(h->mt.raw); hipFree(h->mt.boff); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
+    hipFree(h->mt.pval);
+    if (h->mt.meta_pin) hipHostFree(h->mt.meta_pin);
+    if (h->mt.amb_pin) hipHostFree(h->mt.amb_pin);
+    if (h->mt.words_pin) hipHostFree(h->mt.words_pin);
+    if (h->mt.pidx_pin) hipHostFree(h->mt.pidx_pin);
+    if (h->mt.pval_pin) hipHostFree(h->mt.pval_pin);
     if (h->ev.ok)
         for (auto &set : h->ev.e)
             for (auto &e : set) hipEventDestroy(e);
@@ -1169,6 +1193,11 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     const double flip_margin = (red == FS2_REDUCE_PARALLEL) ? std::ldexp(2.0 * (double)h->n_global + 64.0, -53) : 0.0;
     const bool prof = h->profiling && (h->prof_tick++ % (uint64_t)h->prof_period) == 0;
 
+    // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise / u0
+    const bool drawn = h->mt.armed;
+    if (drawn && (noise || u0))
+        return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
+    h->mt.armed = false;
     if (noise) {
         std::memcpy(h->noise_pin, noise, sizeof(double) * h->n);
         HIP_TRY(h, hipMemcpyAsync(h->noise_dev, h->noise_pin, sizeof(double) * h->n,
@@ -1204,7 +1233,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     up.gidx0 = h->first;
     up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
     up.map = h->map();
-    up.noise = noise ? h->noise_dev : nullptr;
+    up.noise = (noise || drawn) ? h->noise_dev : nullptr;
     up.seed = h->cfg.seed;
     up.scan = h->scan;
     up.sigma = (rotation != 0) ? h->cfg.rotation_noise : h->cfg.translation_noise;
@@ -1267,7 +1296,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         ++passes;
         // pose/weight/count read + weight/count write; pose write on the move pass
         fixed_bytes += (uint64_t)h->n * (32 + 4 + 8 + 4 + (up.do_move ? 24 : 0));
-        if (up.do_move && noise) fixed_bytes += (uint64_t)h->n * 8;
+        if (up.do_move && (noise || drawn)) fixed_bytes += (uint64_t)h->n * 8;
         if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
     }
 
@@ -1305,7 +1334,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (rp.chunked) rp.nparts = normalize_chunk_parts(h->n);
     rp.part_pose = h->part_pose;
     rp.np_tail = exact ? h->np_tail : nullptr;
-    rp.u0_host = u0 ? h->u0_dev : nullptr;
+    rp.u0_host = (u0 || drawn) ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
     rp.stats = h->stats_dev;
@@ -2065,6 +2094,209 @@ int fs2_mahalanobis(int32_t device, const double *a, const double *b, const doub
     SHIP(hipMemcpyAsync(&sing, dsing, 4, hipMemcpyDeviceToHost, sc->stream));
     SHIP(hipStreamSynchronize(sc->stream));
     if (sing) return set_err(nullptr, FS2_ERR_LINALG, "Singular matrix");
+    return FS2_OK;
+}
+
+// ---- numpy's legacy RandomState on the device (fs2_mtrng.hpp / .hip) ----
+
+// grow a device / pinned buffer pair to hold n elements of `esz` bytes (contents dropped)
+static hipError_t mt_grow(void **dev, void **pin, size_t esz, int64_t *cap, int64_t n) {
+    if (n <= *cap) return hipSuccess;
+    const int64_t c = std::max<int64_t>(n, *cap + *cap / 2);
+    if (dev) {
+        hipFree(*dev);
+        *dev = nullptr;
+        hipError_t e = hipMalloc(dev, esz * (size_t)c);
+        if (e != hipSuccess) return e;
+    }
+    if (pin) {
+        if (*pin) hipHostFree(*pin);
+        *pin = nullptr;
+        hipError_t e = hipHostMalloc(pin, esz * (size_t)c, 0);
+        if (e != hipSuccess) return e;
+    }
+    *cap = c;
+    return hipSuccess;
+}
+
+// numpy's state after the stream words before index E were consumed, starting
+// from `in` at in->pos (E == pos: unchanged)
+static int mt_state_at(fs2_handle *h, const fs2_mt_state *in, int64_t E, fs2_mt_state *out) {
+    if (E == in->pos) {
+        std::memcpy(out->key, in->key, sizeof out->key);
+        out->pos = in->pos;
+        return FS2_OK;
+    }
+    const int64_t b = (E - 1) / kMtN;
+    HIP_TRY(h, hipMemcpyAsync(h->mt.words_pin, h->mt.raw + kMtN * b, sizeof(uint32_t) * kMtN,
+                              hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    std::memcpy(out->key, h->mt.words_pin, sizeof out->key);
+    out->pos = (int32_t)(E - kMtN * b);
+    return FS2_OK;
+}
+
+int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
+                fs2_mt_state *after_u0, double *u0_out) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (!in || !after || !after_u0) return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: null state");
+    if (in->pos < 0 || in->pos > kMtN || (in->has_gauss != 0 && in->has_gauss != 1))
+        return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: bad state (pos %d, has_gauss %d)", in->pos, in->has_gauss);
+    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    hipStream_t s = h->stream;
+    auto &mt = h->mt;
+    const int64_t N = h->n_global;
+    const int h0 = (N > 0 && in->has_gauss) ? 1 : 0;
+    const int64_t pos0 = in->pos;
+    const int64_t P = (N > h0) ? (N - h0 + 1) / 2 : 0;     // accepted attempts (pairs) needed
+    // attempts until P successes at p = pi/4: mean P/p, sd sqrt(P(1-p))/p; 12 sd of margin
+    const double mean = (double)P / 0.78539816339744831, sd = std::sqrt((double)P * 0.21460183660255169) / 0.78539816339744831;
+    int64_t A = P ? (int64_t)(mean + 12.0 * sd) + 64 : 0;
+    int64_t amb_cap = P / 8 + 4096;
+    if (!mt.words_pin) HIP_TRY(h, hipHostMalloc((void **)&mt.words_pin, sizeof(uint32_t) * 2 * kMtN, 0));
+    if (!mt.meta) {
+        HIP_TRY(h, hipMalloc((void **)&mt.meta, sizeof(MtMeta)));
+        HIP_TRY(h, hipHostMalloc((void **)&mt.meta_pin, sizeof(MtMeta), 0));
+    }
+    MtMeta meta{};
+    for (int attempt = 0;; ++attempt) {
+        if (attempt == 6) return set_err(&h->err, FS2_ERR_STATE, "fs2_mt_draw: attempts did not converge");
+        // words: the key, then through the block holding the u0 words after the last attempt
+        const int64_t need = pos0 + 4 * A + 2;
+        const int64_t total = std::max<int64_t>(kMtN, (need + kMtN - 1) / kMtN * kMtN);
+        HIP_TRY(h, mt_grow((void **)&mt.raw, nullptr, 4, &mt.raw_cap, total));
+        const int64_t nb = (A + 255) / 256;
+        HIP_TRY(h, mt_grow((void **)&mt.boff, nullptr, 4, &mt.boff_cap, std::max<int64_t>(nb, 1)));
+        int64_t acap = mt.amb_cap;
+        HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, amb_cap));
+        mt.amb_cap = acap;
+        std::memcpy(mt.words_pin, in->key, sizeof(uint32_t) * kMtN);
+        HIP_TRY(h, hipMemcpyAsync(mt.raw, mt.words_pin, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
+        HIP_TRY(h, launch_mt_words(mt.raw, kMtN, total, s));
+        HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
+        HIP_TRY(h, launch_mt_draw(mt.raw, pos0, A, P, N, h0, in->gauss, sigma, h->first, h->n, h->noise_dev,
+                                  mt.boff, mt.meta, mt.amb, (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX), s));
+        HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, mt.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
+        HIP_TRY(h, hipStreamSynchronize(s));
+        meta = *mt.meta_pin;
+        if (P > 0 && meta.accepted < P) {      // (about 1e-30 per draw) more attempts
+            A += A / 4 + 1024;
+            continue;
+        }
+        if (meta.amb_n > mt.amb_cap) {
+            amb_cap = (int64_t)meta.amb_n + 1024;
+            continue;
+        }
+        break;
+    }
+    // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
+    const int64_t na = meta.amb_n;
+    if (na > 0) {
+        HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)na, hipMemcpyDeviceToHost, s));
+        HIP_TRY(h, hipStreamSynchronize(s));
+        HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
+        HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
+        int64_t np = 0;
+        for (int64_t k = 0; k < na; ++k) {
+            const MtAmb &e = mt.amb_pin[k];
+            const double f = mt_polar_f(e.r2, std::log(e.r2));
+            const double g0 = f * e.x2, g1 = f * e.x1;
+            const int64_t o = h0 + 2 * e.rank;
+            if (o >= h->first && o < h->first + h->n) {
+                mt.pidx_pin[np] = o - h->first;
+                mt.pval_pin[np++] = 0.0 + sigma * g0;
+            }
+            if (o + 1 < N) {
+                if (o + 1 >= h->first && o + 1 < h->first + h->n) {
+                    mt.pidx_pin[np] = o + 1 - h->first;
+                    mt.pval_pin[np++] = 0.0 + sigma * g1;
+                }
+            } else {
+                meta.gauss = g1;               // the pair whose second value stays cached
+            }
+        }
+        if (np > 0) {
+            HIP_TRY(h, hipMemcpyAsync(mt.pidx, mt.pidx_pin, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+            HIP_TRY(h, hipMemcpyAsync(mt.pval, mt.pval_pin, sizeof(double) * np, hipMemcpyHostToDevice, s));
+            HIP_TRY(h, launch_mt_patch(h->noise_dev, mt.pidx, mt.pval, np, s));
+        }
+    }
+    // the state after the normals, then after the speculative u0 (two more words)
+    const int64_t E = P > 0 ? pos0 + 4 * (meta.last_attempt + 1) : pos0;
+    int rc = mt_state_at(h, in, E, after);
+    if (rc) return rc;
+    if (N == 0) {
+        after->has_gauss = in->has_gauss;
+        after->gauss = in->gauss;
+    } else if (P == 0) {                       // one normal, the cached one
+        after->has_gauss = 0;
+        after->gauss = 0.0;
+    } else {
+        after->has_gauss = meta.has_gauss;
+        after->gauss = meta.has_gauss ? meta.gauss : 0.0;
+    }
+    // u0 = np.random.uniform(0, 1 / N) = 0 + (1/N - 0) legacy_double (fast_slam_2.py:183)
+    uint32_t wu[2];
+    {
+        // words E and E + 1 (generated: the stream runs through the block of E + 1)
+        fs2_mt_state tmp;
+        rc = mt_state_at(h, in, E + 2, &tmp);
+        if (rc) return rc;
+        std::memcpy(after_u0->key, tmp.key, sizeof tmp.key);
+        after_u0->pos = tmp.pos;
+        after_u0->has_gauss = after->has_gauss;
+        after_u0->gauss = after->gauss;
+        for (int k = 0; k < 2; ++k) {
+            const int64_t j = E + k;
+            if (j < kMtN) {
+                wu[k] = in->key[j];
+            } else {
+                HIP_TRY(h, hipMemcpy(&wu[k], mt.raw + j, 4, hipMemcpyDeviceToHost));
+            }
+        }
+    }
+    const double hi = 1.0 / (double)h->n_global;
+    const double u0 = 0.0 + (hi - 0.0) * mt_double(mt_temper(wu[0]), mt_temper(wu[1]));
+    *h->u0_pin = u0;
+    HIP_TRY(h, hipMemcpyAsync(h->u0_dev, h->u0_pin, 8, hipMemcpyHostToDevice, s));
+    if (u0_out) *u0_out = u0;
+    mt.armed = true;
+    return FS2_OK;
+}
+
+int fs2_debug_noise(fs2_handle *h, double *out) {
+    if (!h || !out) return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_debug_noise: null argument");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    HIP_TRY(h, hipMemcpyAsync(h->noise_pin, h->noise_dev, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    std::memcpy(out, h->noise_pin, sizeof(double) * h->n);
+    return FS2_OK;
+}
+
+int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, int32_t *amb, int32_t on_host) {
+    if (n < 0 || (n > 0 && (!x || !out || !amb))) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_mt_log: bad arguments");
+    if (on_host) {
+        for (int64_t k = 0; k < n; ++k) {
+            bool a = false;
+            out[k] = mt_log(x[k], &a);
+            amb[k] = a ? 1 : 0;
+        }
+        return FS2_OK;
+    }
+    if (n == 0) return FS2_OK;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    const size_t b8 = al16((size_t)n * 8);
+    Scratch *sc = nullptr;
+    int rc = scratch_get(device, 2 * b8 + al16((size_t)n * 4), &sc);
+    if (rc) return rc;
+    double *dx = (double *)sc->buf, *dout = (double *)(sc->buf + b8);
+    int32_t *damb = (int32_t *)(sc->buf + 2 * b8);
+    SHIP(hipMemcpyAsync(dx, x, (size_t)n * 8, hipMemcpyHostToDevice, sc->stream));
+    SHIP(launch_mt_debug_log(dx, n, dout, damb, sc->stream));
+    SHIP(hipMemcpyAsync(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipMemcpyAsync(amb, damb, (size_t)n * 4, hipMemcpyDeviceToHost, sc->stream));
+    SHIP(hipStreamSynchronize(sc->stream));
     return FS2_OK;
 }
 

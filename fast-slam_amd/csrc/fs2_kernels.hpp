@@ -540,6 +540,29 @@ hipError_t launch_debug_philox(int64_t n, const uint32_t *ctr, const uint32_t *k
 hipError_t launch_debug_normals(uint64_t seed, uint64_t stream, uint64_t first, int64_t n, double *out,
                                 hipStream_t s);
 
+// numpy's legacy RandomState on the device (fs2_mtrng.hip): results of one draw,
+// and the attempts whose log the host recomputes with libm
+struct MtMeta {
+    int64_t accepted;        // accepted polar attempts among those evaluated
+    int64_t last_attempt;    // index of the last attempt the draw consumed
+    double gauss;            // cached second value after the draw (has_gauss)
+    int32_t has_gauss;
+    int32_t amb_n;           // attempts listed in MtAmb (may exceed the capacity)
+};
+struct MtAmb {
+    double r2, x1, x2;
+    int64_t rank;            // among the accepted attempts: outputs h0 + 2 rank, + 1
+};
+// raw stream words R[begin, end) from R[begin - 624, begin) (one wave)
+hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t s);
+// N normals legacy_normal(0, sigma) from A attempts at R[pos0 ..] (P pairs needed,
+// h0: gauss0 first), this rank's slice [first, first + n_local) into out
+hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t A, int64_t P, int64_t N, int32_t h0,
+                          double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
+                          int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, hipStream_t s);
+hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n, hipStream_t s);
+hipError_t launch_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb, hipStream_t s);
+
 hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt,
                       int32_t n_tgt, int32_t max_iter, double thr, double *R, double *t,
                       int32_t *iters, hipStream_t s);

@@ -1,0 +1,235 @@
+// fs2_mtrng.hip -- numpy's legacy MT19937 stream and polar Gaussian on the device
+// (fs2_mtrng.hpp): the drop-in iterate()'s motion draws (fast_slam_2.py:79,81)
+// and resample start (:183) bit for bit with np.random, without the host
+// generating N normals per scan.
+//
+//   k_mt_words    one wave: the raw word stream, 227 words per step of the
+//                 recurrence, the ring of the last 851 words in LDS, the loads of
+//                 step s + 1 issued before step s's stores (they read words >= 2
+//                 steps old);
+//   k_mt_count    one lane per polar attempt (4 words): accepted attempts per
+//                 256-attempt block;
+//   k_mt_scan     one workgroup: exclusive offsets of the block counts;
+//   k_mt_normals  one lane per attempt: its rank among the accepted attempts
+//                 gives its two output indices; log in double-double, results
+//                 near a rounding midpoint listed for the host (libm log);
+//   k_mt_patch    the host's recomputed values into the output.
+#include "fs2_kernels.hpp"
+#include "fs2_mtrng.hpp"
+
+namespace fs2 {
+
+__global__ __launch_bounds__(64) void k_mt_words(uint32_t *R, int64_t begin, int64_t end) {
+    __shared__ uint32_t ring[1024];
+    const int lane = threadIdx.x;
+    for (int t = lane; t < kMtN; t += 64) {
+        const int64_t j = begin - kMtN + t;
+        ring[j & 1023] = R[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // lane handles words base + q, q = lane + 64 k < 227; x[j - 227] is its own
+    // value of the previous step
+    uint32_t c[4], a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = lane + 64 * k;
+        const int64_t j = begin + q;
+        c[k] = q < kMtLag ? ring[(j - kMtLag) & 1023] : 0u;
+        a[k] = q < kMtLag ? ring[(j - kMtN) & 1023] : 0u;
+        b[k] = q < kMtLag ? ring[(j - kMtN + 1) & 1023] : 0u;
+    }
+    for (int64_t base = begin; base < end; base += kMtLag) {
+        // next step's operands (words of steps <= s - 1: stored before the last fence)
+        uint32_t na[4], nb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = lane + 64 * k;
+            const int64_t j = base + kMtLag + q;
+            na[k] = q < kMtLag ? ring[(j - kMtN) & 1023] : 0u;
+            nb[k] = q < kMtLag ? ring[(j - kMtN + 1) & 1023] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = lane + 64 * k;
+            const int64_t j = base + q;
+            if (q < kMtLag) {
+                const uint32_t v = mt_next_word(a[k], b[k], c[k]);
+                c[k] = v;
+                ring[j & 1023] = v;
+                if (j < end) R[j] = v;
+            }
+            a[k] = na[k];
+            b[k] = nb[k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+struct MtParams {
+    const uint32_t *R;       // raw stream words x_0 .. (x_0..x_623 = the input key)
+    int64_t pos0;            // stream index of the first word to consume
+    int64_t A;               // attempts evaluated
+    int64_t P;               // accepted attempts needed (pairs)
+    int64_t N;               // normals drawn
+    int32_t h0;              // the first normal is the cached gauss0
+    double gauss0;
+    double sigma;            // legacy_normal(0, sigma)
+    int64_t first, n_local;  // this rank's slice of the N outputs
+    double *out;             // [n_local]
+    int32_t *boff;           // [nb] accepted per block -> exclusive offsets
+    int32_t nb;
+    MtMeta *meta;
+    MtAmb *amb;
+    int32_t amb_cap;
+};
+
+__global__ __launch_bounds__(256) void k_mt_count(const MtParams p) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool ok = false;
+    if (a < p.A) {
+        const uint32_t *w = p.R + p.pos0 + 4 * a;
+        ok = mt_attempt(w[0], w[1], w[2], w[3]).ok;
+    }
+    __shared__ int s_c[4];
+    const uint64_t bal = __ballot(ok);
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) p.boff[blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+}
+
+__global__ __launch_bounds__(1024) void k_mt_scan(const MtParams p) {
+    __shared__ int s_w[16];
+    __shared__ int64_t s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int base = 0; base < p.nb; base += 1024) {
+        const int b = base + threadIdx.x;
+        const int v = b < p.nb ? p.boff[b] : 0;
+        // inclusive wave scan
+        int x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) s_w[wid] = x;
+        __syncthreads();
+        int before = 0;
+        for (int k = 0; k < wid; ++k) before += s_w[k];
+        const int64_t carry = s_carry;
+        if (b < p.nb) p.boff[b] = (int32_t)(carry + before + x - v);
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = carry + before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) p.meta->accepted = s_carry;
+}
+
+__global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    MtAttempt t{0.0, 0.0, 0.0, false};
+    if (a < p.A) {
+        const uint32_t *w = p.R + p.pos0 + 4 * a;
+        t = mt_attempt(w[0], w[1], w[2], w[3]);
+    }
+    __shared__ int s_c[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t bal = __ballot(t.ok);
+    if (lane == 0) s_c[wid] = __popcll(bal);
+    __syncthreads();
+    int before = 0;
+    for (int k = 0; k < wid; ++k) before += s_c[k];
+    const int64_t rank = (int64_t)(p.nb > 0 ? p.boff[blockIdx.x] : 0) + before +
+                         __popcll(bal & ((1ull << lane) - 1ull));
+    if (a == 0 && p.h0) {
+        // the cached value of the previous draw comes first
+        if (p.first == 0 && p.n_local > 0) p.out[0] = 0.0 + p.sigma * p.gauss0;
+    }
+    if (!t.ok || rank >= p.P) return;
+    bool amb = false;
+    const double lg = mt_log(t.r2, &amb);
+    const double f = mt_polar_f(t.r2, lg);
+    const double g0 = f * t.x2, g1 = f * t.x1;
+    const int64_t o = p.h0 + 2 * rank;
+    if (o >= p.first && o < p.first + p.n_local) p.out[o - p.first] = 0.0 + p.sigma * g0;
+    if (o + 1 < p.N) {
+        if (o + 1 >= p.first && o + 1 < p.first + p.n_local) p.out[o + 1 - p.first] = 0.0 + p.sigma * g1;
+    }
+    if (rank == p.P - 1) {
+        p.meta->last_attempt = a;
+        p.meta->has_gauss = (o + 1 < p.N) ? 0 : 1;
+        p.meta->gauss = (o + 1 < p.N) ? 0.0 : g1;
+    }
+    if (amb) {
+        const int k = atomicAdd(&p.meta->amb_n, 1);
+        if (k < p.amb_cap) p.amb[k] = MtAmb{t.r2, t.x1, t.x2, rank};
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < n) out[idx[k]] = val[k];
+}
+
+__global__ __launch_bounds__(256) void k_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    bool a = false;
+    out[k] = mt_log(x[k], &a);
+    amb[k] = a ? 1 : 0;
+}
+
+hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t s) {
+    if (end <= begin) return hipSuccess;
+    hipLaunchKernelGGL(k_mt_words, dim3(1), dim3(64), 0, s, R, begin, end);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t A, int64_t P, int64_t N, int32_t h0,
+                          double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
+                          int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, hipStream_t s) {
+    MtParams p{};
+    p.R = R;
+    p.pos0 = pos0;
+    p.A = A;
+    p.P = P;
+    p.N = N;
+    p.h0 = h0;
+    p.gauss0 = gauss0;
+    p.sigma = sigma;
+    p.first = first;
+    p.n_local = n_local;
+    p.out = out;
+    p.boff = boff;
+    p.nb = (int32_t)((A + 255) / 256);
+    p.meta = meta;
+    p.amb = amb;
+    p.amb_cap = amb_cap;
+    if (p.nb == 0) {
+        hipLaunchKernelGGL(k_mt_normals, dim3(1), dim3(256), 0, s, p);   // the cached value alone
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_mt_count, dim3(p.nb), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_mt_scan, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(k_mt_normals, dim3(p.nb), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mt_patch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, idx, val, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mt_debug_log, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, out, amb);
+    return hipGetLastError();
+}
+
+}  // namespace fs2

@@ -123,6 +123,26 @@ class fs2_frontend_out(C.Structure):
                 ("counts", C.c_void_p)]
 
 
+class fs2_mt_state(C.Structure):
+    """np.random.get_state()'s ('MT19937', key, pos, has_gauss, cached_gaussian)."""
+    _fields_ = [("key", C.c_uint32 * 624), ("pos", C.c_int32), ("has_gauss", C.c_int32),
+                ("gauss", C.c_double)]
+
+    @classmethod
+    def from_numpy(cls, st):
+        name, key, pos, has_gauss, gauss = st
+        if name != "MT19937":
+            raise ValueError(f"numpy bit generator {name!r} is not MT19937")
+        out = cls()
+        C.memmove(out.key, np.ascontiguousarray(key, dtype=np.uint32).ctypes.data, 624 * 4)
+        out.pos, out.has_gauss, out.gauss = int(pos), int(has_gauss), float(gauss)
+        return out
+
+    def to_numpy(self):
+        return ("MT19937", np.frombuffer(bytes(self.key), dtype=np.uint32).copy(), int(self.pos),
+                int(self.has_gauss), float(self.gauss))
+
+
 class FS2Error(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"libfs2 error {code}: {msg}")
@@ -146,6 +166,8 @@ SIGNATURES = [
                               C.POINTER(fs2_iter_stats)]),
     ("fs2_iterate_submit", C.c_int, [_H, C.c_double, C.c_double, _vp, _vp, C.c_int32, _vp, _vp]),
     ("fs2_iterate_wait", C.c_int, [_H, _dp, C.POINTER(fs2_iter_stats)]),
+    ("fs2_mt_draw", C.c_int, [_H, C.POINTER(fs2_mt_state), C.c_double, C.POINTER(fs2_mt_state),
+                              C.POINTER(fs2_mt_state), _dp]),
     ("fs2_get_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,
                                 C.c_int32]),
     ("fs2_set_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,
@@ -176,6 +198,8 @@ SIGNATURES = [
                                C.POINTER(fs2_frontend_out)]),
     ("fs2_debug_philox", C.c_int, [C.c_int32, C.c_int64, _vp, _vp, _vp]),
     ("fs2_debug_normals", C.c_int, [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, _vp]),
+    ("fs2_debug_mt_log", C.c_int, [C.c_int32, _vp, C.c_int64, _vp, _vp, C.c_int32]),
+    ("fs2_debug_noise", C.c_int, [_H, _vp]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("fs2_plan_ranges", C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double, _vp, _vp]),
     ("fs2_plan_sends", C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, _vp, _vp, _vp]),

@@ -9,9 +9,13 @@ Randomness.  By default the motion noise and the resample starting point are
 drawn from numpy's global legacy RandomState exactly as the reference draws
 them (N normals in particle order, then one uniform only if resampling fires,
 SURVEY.md Q4/Q5), so a seeded run reproduces the reference's stream.  The
-uniform is drawn speculatively before the scan and the RNG state is rewound
-when no resample happened.  rng="device" draws both with Philox on the GPU
-instead (no host work per particle; used by bench.py).
+draws are made on the GPU from np.random.get_state() (fs2_mt_draw: MT19937 and
+the polar method bit for bit, a few logs near a rounding midpoint recomputed
+with the host's libm) and numpy's state is advanced to where the reference's
+draws leave it: past the normals, and past the uniform only when resampling
+fired.  rng="numpy-host" draws them with numpy on the host instead (the same
+values, ~10 ms per 1e6 particles); rng="device" draws both with Philox on the
+GPU (not numpy's stream; used by bench.py).
 """
 from __future__ import annotations
 
@@ -64,8 +68,8 @@ class FastSLAM2:
         cfg.sharded_path = 1 if sharded_path else 0
         cfg.page_pool = int(page_pool)          # initial pool sizes (0: defaults; fs2.h)
         cfg.record_pool = int(record_pool)
-        if rng not in ("numpy", "device"):
-            raise ValueError("rng must be 'numpy' or 'device'")
+        if rng not in ("numpy", "numpy-host", "device"):
+            raise ValueError("rng must be 'numpy', 'numpy-host' or 'device'")
         self._rng = rng
         self._verbose = verbose
         h = C.c_void_p()
@@ -97,6 +101,7 @@ class FastSLAM2:
         self._st_addr = C.addressof(self._st)
         self._u0 = np.empty(1)
         self._u0_addr = self._u0.ctypes.data
+        self._mt = [nat.fs2_mt_state() for _ in range(3)]     # in, after the normals, after u0
 
     @property
     def first_global(self) -> int:
@@ -124,8 +129,15 @@ class FastSLAM2:
             obs[k, 1] = m.distance * np.sin(m.yaw)
         noise = u0 = None
         state = None
+        sigma = config.ROTATION_NOISE if rotation != 0 else config.TRANSLATION_NOISE
         if self._rng == "numpy":
-            sigma = config.ROTATION_NOISE if rotation != 0 else config.TRANSLATION_NOISE
+            if self._h is None:
+                raise nat.FS2Error(nat.FS2_ERR_ARG, "iterate on a closed FastSLAM2 handle")
+            mt_in, mt_after, mt_u0 = self._mt
+            C.pointer(mt_in)[0] = nat.fs2_mt_state.from_numpy(np.random.get_state())
+            nat.check(self._lib.fs2_mt_draw(self._h, C.byref(mt_in), float(sigma), C.byref(mt_after),
+                                            C.byref(mt_u0), None), self._h)
+        elif self._rng == "numpy-host":
             noise = np.random.normal(0, sigma, size=self.num_particles)
             noise = np.ascontiguousarray(noise[self.first_global:self.first_global + self.n_local])
             state = np.random.get_state()
@@ -137,7 +149,10 @@ class FastSLAM2:
                                    M, nat.ptr(noise), nat.ptr(u0), nat.dptr(pose), C.byref(st))
         self._particles = None
         self.last_stats = st
-        if state is not None and not st.resampled:
+        if self._rng == "numpy":
+            # the normals are drawn by the move, u0 only when resampling (fast_slam_2.py:79,81,183)
+            np.random.set_state((self._mt[2] if (rc == 0 and st.resampled) else self._mt[1]).to_numpy())
+        elif state is not None and not st.resampled:
             np.random.set_state(state)          # the reference draws u0 only when resampling
         nat.check(rc, self._h)
         if st.resampled and self._verbose:

@@ -202,6 +202,29 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
                        const double *observed, int32_t M, const double *noise, const double *u0);
 int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats);
 
+/* numpy's legacy global RandomState on the device, for the drop-in iterate()
+ * (replaces the host draws np.random.normal(0, ROTATION_NOISE / TRANSLATION_NOISE)
+ * of fast_slam_2.py:79,81 for every particle in order, and the resample start
+ * np.random.uniform(0, 1 / NUM_PARTICLES) of fast_slam_2.py:183).  The state is
+ * np.random.get_state()'s ('MT19937', key, pos, has_gauss, cached_gaussian).
+ * fs2_mt_draw draws the N_global normals legacy_normal(0, sigma) from *in -- this
+ * rank's slice into the handle's noise buffer -- and the speculative u0 after
+ * them; the next fs2_iterate / fs2_iterate_submit (noise and u0 NULL) uses both.
+ * *after is numpy's state after the normals, *after_u0 after the u0 draw too
+ * (the caller keeps it only if the scan resampled, as the reference draws u0 only
+ * then).  Bit for bit with numpy: the MT19937 words, legacy_double, the polar
+ * method's rejections and roundings; log(r2) in double-double on the device, the
+ * few results within 0.025 ulp of a rounding midpoint recomputed with the host's
+ * libm log (glibc's log is within 0.52 ulp, not always correctly rounded). */
+typedef struct fs2_mt_state {
+    uint32_t key[624];
+    int32_t pos;
+    int32_t has_gauss;
+    double gauss;
+} fs2_mt_state;
+int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
+                fs2_mt_state *after_u0, double *u0);
+
 /* Particle state in the reference's object layout (Particle.x/.y/.yaw/.weight,
  * Particle.landmarks[j] = Landmark(x, y, cov) -- models/particle.py:11-20,
  * models/landmark.py:13-21).  Range [first, first+count) of this rank's local
@@ -305,6 +328,14 @@ int fs2_mahalanobis(int32_t device, const double *a, const double *b, const doub
 int fs2_debug_philox(int32_t device, int64_t n, const uint32_t *ctr, const uint32_t *key, uint32_t *out);
 int fs2_debug_normals(int32_t device, uint64_t seed, uint64_t stream, uint64_t first, int64_t n,
                       double *out);
+/* Test hook of fs2_mt_draw's log: out[k] = log(x[k]) rounded from double-double,
+ * amb[k] = 1 where the host recomputes it (within 0.025 ulp of a midpoint);
+ * on_host = 1 runs the same arithmetic on the CPU.  x in (0, 1), host buffers. */
+int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, int32_t *amb,
+                     int32_t on_host);
+/* Test hook: the handle's motion-noise buffer (N_local values: the last scan's
+ * injected draws, or fs2_mt_draw's) into out. */
+int fs2_debug_noise(fs2_handle *h, double *out);
 
 /* ---------------------------------------------------------- multi-GPU ---- */
 

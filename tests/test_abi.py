@@ -37,7 +37,7 @@ def test_struct_layout_matches_header():
     src = open(os.path.join(REPO, "include", "fs2.h")).read()
     for cname, py in [("fs2_config", _native.fs2_config), ("fs2_iter_stats", _native.fs2_iter_stats),
                       ("fs2_profile", _native.fs2_profile),
-                      ("fs2_frontend_out", _native.fs2_frontend_out)]:
+                      ("fs2_frontend_out", _native.fs2_frontend_out), ("fs2_mt_state", _native.fs2_mt_state)]:
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []
@@ -99,7 +99,8 @@ def test_struct_sizes_match_c_compiler():
     import tempfile
     from fast_slam_2 import _native
     structs = [("fs2_config", _native.fs2_config), ("fs2_iter_stats", _native.fs2_iter_stats),
-               ("fs2_profile", _native.fs2_profile), ("fs2_frontend_out", _native.fs2_frontend_out)]
+               ("fs2_profile", _native.fs2_profile), ("fs2_frontend_out", _native.fs2_frontend_out),
+               ("fs2_mt_state", _native.fs2_mt_state)]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fs2.h"', "int main(void) {"]
     for cname, py in structs:
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -31,14 +31,16 @@ def fs():
     configure()
 
 
+@pytest.mark.parametrize("rng", ["numpy", "numpy-host"])
 @pytest.mark.parametrize("name", SEQS)
-def test_iterate_numpy_rng_replays_reference(fs, name):
+def test_iterate_numpy_rng_replays_reference(fs, name, rng):
+    """rng="numpy" draws numpy's stream on the GPU (fs2_mt_draw), "numpy-host" with numpy."""
     from gpu_util import close, configure
     d = np.load(os.path.join(GOLDEN, f"seq_{name}.npz"))
     tr, rot, mn = d["noise_cfg"]
     configure(tr, rot, mn, float(d["gate"]))
     N, cap = int(d["N"]), int(d["cap"])
-    f = fs.FastSLAM2(N, record_assoc=True, landmark_capacity=cap, verbose=False)
+    f = fs.FastSLAM2(N, record_assoc=True, landmark_capacity=cap, verbose=False, rng=rng)
     f.set_state(d["x"][0], d["y"][0], d["yaw"][0], d["w"][0], d["cnt"][0], d["lm"][0])
     np.random.seed(int(d["seed"]))
     for s in range(int(d["S"])):

@@ -1,0 +1,96 @@
+"""numpy's legacy RandomState drawn on the GPU (fs2_mt_draw), the drop-in
+iterate()'s replacement for the reference's host draws
+np.random.normal(0, ROTATION_NOISE / TRANSLATION_NOISE) per particle
+(fast_slam_2/algorithms/fast_slam_2.py:79,81) and np.random.uniform(0, 1/N)
+(:183).  numpy itself is the oracle: the device noise buffer, u0 and the state
+after the normals / after u0 must equal what np.random produces from the same
+state, bit for bit, at sizes from 1 to 4M particles, from states with a cached
+gauss and with pos anywhere in the 624-word block (624 included), over
+consecutive draws."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fs():
+    import torch  # noqa: F401
+    import fast_slam_2
+    yield fast_slam_2
+
+
+def draw(f, sigma):
+    from fast_slam_2 import _native as nat
+    lib = nat.load()
+    st = np.random.get_state()
+    mi, ma, mu, u0 = nat.fs2_mt_state.from_numpy(st), nat.fs2_mt_state(), nat.fs2_mt_state(), C.c_double()
+    nat.check(lib.fs2_mt_draw(f._h, C.byref(mi), sigma, C.byref(ma), C.byref(mu), C.byref(u0)), f._h)
+    out = np.empty(f.n_local)
+    nat.check(lib.fs2_debug_noise(f._h, nat.ptr(out)), f._h)
+    return st, out, ma.to_numpy(), mu.to_numpy(), u0.value
+
+
+def same_state(a, b):
+    return (a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
+            and a[4] == b[4])
+
+
+@pytest.mark.parametrize("N,pre,words", [(1, 0, 0), (1, 1, 0), (2, 1, 3), (7, 0, 312), (1000, 0, 2),
+                                         (1001, 3, 311), (65537, 1, 100), (1000000, 0, 0),
+                                         (1000000, 1, 312), (4194304, 0, 7)])
+def test_mt_draw_matches_numpy(fs, N, pre, words):
+    np.random.seed(1000 * pre + words + N % 997)
+    np.random.normal(size=pre)               # pre odd: a cached gauss
+    np.random.random_sample(words)           # two words each: pos anywhere, 624 included
+    f = fs.FastSLAM2(N, rng="numpy", verbose=False, landmark_capacity=8)
+    for k, sigma in enumerate((0.0055, 0.001, 0.0055)):
+        st, out, after, after_u0, u0 = draw(f, sigma)
+        np.random.set_state(st)
+        ref = np.random.normal(0, sigma, size=N)
+        bad = np.flatnonzero(out != ref)
+        assert len(bad) == 0, (N, k, len(bad), bad[:5], out[bad[:5]], ref[bad[:5]])
+        assert same_state(np.random.get_state(), after), (N, k)
+        ru = np.random.uniform(0, 1 / N)
+        assert ru == u0, (N, k, ru, u0)
+        assert same_state(np.random.get_state(), after_u0), (N, k)
+        # the next scan continues after the normals, or after u0 (a resample)
+        np.random.set_state(after if k % 2 == 0 else after_u0)
+    f.close()
+
+
+def test_iterate_device_draws_equal_host_draws(fs):
+    """Two handles from the same state, one drawing numpy's stream on the GPU, one
+    with numpy on the host: every scan's pose, decision, state and numpy's state
+    afterwards agree bit for bit (resampling scans included)."""
+    import bench
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    configure()
+    N, L, scans = 20000, 40, 8
+    hs = {}
+    for rng in ("numpy", "numpy-host"):
+        f = fs.FastSLAM2(N, rng=rng, verbose=False, landmark_capacity=L + scans + 8)
+        bench.populate(f, N, L, 3, 0)          # the bench's synthetic state (seeded, identical)
+        hs[rng] = f
+    res = {}
+    for rng, f in hs.items():
+        np.random.seed(17)
+        out = []
+        for s in range(scans):
+            rot, tr = syn.odometry(s)
+            ms = [fs.Measurement(float(d), float(b)) for d, b in syn.scan_measurements(L, s, 3)]
+            pose = f.iterate(rot, tr, ms)
+            st = f.last_stats
+            out.append((pose, st.resampled, st.n_eff, f.get_state(lm_cap=L + scans + 8)))
+        res[rng] = (out, np.random.get_state())
+        f.close()
+    a, b = res["numpy"], res["numpy-host"]
+    assert same_state(a[1], b[1])
+    assert sum(o[1] for o in a[0]) >= 1
+    for s, (oa, ob) in enumerate(zip(a[0], b[0])):
+        assert oa[0] == ob[0] and oa[1] == ob[1] and oa[2] == ob[2], s
+        for u, v in zip(oa[3], ob[3]):
+            assert np.array_equal(u, v), s
