@@ -2119,23 +2119,6 @@ static hipError_t mt_grow(void **dev, void **pin, size_t esz, int64_t *cap, int6
     return hipSuccess;
 }
 
-// numpy's state after the stream words before index E were consumed, starting
-// from `in` at in->pos (E == pos: unchanged)
-static int mt_state_at(fs2_handle *h, const fs2_mt_state *in, int64_t E, fs2_mt_state *out) {
-    if (E == in->pos) {
-        std::memcpy(out->key, in->key, sizeof out->key);
-        out->pos = in->pos;
-        return FS2_OK;
-    }
-    const int64_t b = (E - 1) / kMtN;
-    HIP_TRY(h, hipMemcpyAsync(h->mt.words_pin, h->mt.raw + kMtN * b, sizeof(uint32_t) * kMtN,
-                              hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
-    std::memcpy(out->key, h->mt.words_pin, sizeof out->key);
-    out->pos = (int32_t)(E - kMtN * b);
-    return FS2_OK;
-}
-
 int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
                 fs2_mt_state *after_u0, double *u0_out) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
@@ -2222,10 +2205,12 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
             HIP_TRY(h, launch_mt_patch(h->noise_dev, mt.pidx, mt.pval, np, s));
         }
     }
-    // the state after the normals, then after the speculative u0 (two more words)
-    const int64_t E = P > 0 ? pos0 + 4 * (meta.last_attempt + 1) : pos0;
-    int rc = mt_state_at(h, in, E, after);
-    if (rc) return rc;
+    // the state after the normals, then after the speculative u0 (two more words;
+    // k_mt_final left both in meta)
+    std::memcpy(after->key, meta.key_after, sizeof after->key);
+    after->pos = meta.pos_after;
+    std::memcpy(after_u0->key, meta.key_after_u0, sizeof after_u0->key);
+    after_u0->pos = meta.pos_after_u0;
     if (N == 0) {
         after->has_gauss = in->has_gauss;
         after->gauss = in->gauss;
@@ -2236,26 +2221,10 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         after->has_gauss = meta.has_gauss;
         after->gauss = meta.has_gauss ? meta.gauss : 0.0;
     }
+    after_u0->has_gauss = after->has_gauss;
+    after_u0->gauss = after->gauss;
     // u0 = np.random.uniform(0, 1 / N) = 0 + (1/N - 0) legacy_double (fast_slam_2.py:183)
-    uint32_t wu[2];
-    {
-        // words E and E + 1 (generated: the stream runs through the block of E + 1)
-        fs2_mt_state tmp;
-        rc = mt_state_at(h, in, E + 2, &tmp);
-        if (rc) return rc;
-        std::memcpy(after_u0->key, tmp.key, sizeof tmp.key);
-        after_u0->pos = tmp.pos;
-        after_u0->has_gauss = after->has_gauss;
-        after_u0->gauss = after->gauss;
-        for (int k = 0; k < 2; ++k) {
-            const int64_t j = E + k;
-            if (j < kMtN) {
-                wu[k] = in->key[j];
-            } else {
-                HIP_TRY(h, hipMemcpy(&wu[k], mt.raw + j, 4, hipMemcpyDeviceToHost));
-            }
-        }
-    }
+    const uint32_t wu[2] = {meta.w_u0[0], meta.w_u0[1]};
     const double hi = 1.0 / (double)h->n_global;
     const double u0 = 0.0 + (hi - 0.0) * mt_double(mt_temper(wu[0]), mt_temper(wu[1]));
     *h->u0_pin = u0;

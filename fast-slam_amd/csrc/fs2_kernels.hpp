@@ -548,6 +548,11 @@ struct MtMeta {
     double gauss;            // cached second value after the draw (has_gauss)
     int32_t has_gauss;
     int32_t amb_n;           // attempts listed in MtAmb (may exceed the capacity)
+    // numpy's state after the normals and after u0 too (k_mt_final)
+    int64_t E;               // stream index of the first word not consumed by the normals
+    int32_t pos_after, pos_after_u0;
+    uint32_t w_u0[2];        // raw words E, E + 1 (u0)
+    uint32_t key_after[624], key_after_u0[624];
 };
 struct MtAmb {
     double r2, x1, x2;

@@ -26,9 +26,9 @@ __global__ __launch_bounds__(64) void k_mt_words(uint32_t *R, int64_t begin, int
         const int64_t j = begin - kMtN + t;
         ring[j & 1023] = R[j];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // lane handles words base + q, q = lane + 64 k < 227; x[j - 227] is its own
     // value of the previous step
     uint32_t c[4], a[4], b[4];
@@ -63,9 +63,12 @@ __global__ __launch_bounds__(64) void k_mt_words(uint32_t *R, int64_t begin, int
             a[k] = na[k];
             b[k] = nb[k];
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // one wave: its LDS operations complete in order; the wavefront-scope fences
+        // only keep the compiler from moving the next step's loads above these stores
+        // (a workgroup-scope release would also wait for the global stores)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -171,6 +174,24 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
     }
 }
 
+// numpy's state after the draw: the key block holding the last word consumed
+// (pos = words used of it, 624 before the next twist), and the u0 words
+__global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos0, int64_t P, MtMeta *meta) {
+    const int64_t E = P > 0 ? pos0 + 4 * (meta->last_attempt + 1) : pos0;
+    const int64_t b1 = (E == pos0) ? 0 : (E - 1) / kMtN, b2 = (E + 1) / kMtN;
+    for (int t = threadIdx.x; t < kMtN; t += 256) {
+        meta->key_after[t] = R[kMtN * b1 + t];
+        meta->key_after_u0[t] = R[kMtN * b2 + t];
+    }
+    if (threadIdx.x == 0) {
+        meta->E = E;
+        meta->pos_after = (int32_t)(E - kMtN * b1);
+        meta->pos_after_u0 = (int32_t)(E + 2 - kMtN * b2);
+        meta->w_u0[0] = R[E];
+        meta->w_u0[1] = R[E + 1];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k < n) out[idx[k]] = val[k];
@@ -212,11 +233,12 @@ hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t A, int64_t P,
     p.amb_cap = amb_cap;
     if (p.nb == 0) {
         hipLaunchKernelGGL(k_mt_normals, dim3(1), dim3(256), 0, s, p);   // the cached value alone
-        return hipGetLastError();
+    } else {
+        hipLaunchKernelGGL(k_mt_count, dim3(p.nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(k_mt_scan, dim3(1), dim3(1024), 0, s, p);
+        hipLaunchKernelGGL(k_mt_normals, dim3(p.nb), dim3(256), 0, s, p);
     }
-    hipLaunchKernelGGL(k_mt_count, dim3(p.nb), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_mt_scan, dim3(1), dim3(1024), 0, s, p);
-    hipLaunchKernelGGL(k_mt_normals, dim3(p.nb), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_mt_final, dim3(1), dim3(256), 0, s, R, pos0, P, meta);
     return hipGetLastError();
 }
 
