@@ -150,8 +150,19 @@ struct fs2_handle {
     // numpy's legacy RandomState on the device (fs2_mt_draw): stream words, block
     // offsets, results, listed logs, host patches; the next scan uses its draws
     struct MtWork {
-        uint32_t *raw = nullptr;
-        int64_t raw_cap = 0;
+        // two word buffers: the draw reads raw[cur]; the next draw's words are made
+        // ahead into raw[1 - cur] on `side` while the scan runs (the stream does not
+        // depend on how many words a draw consumes)
+        uint32_t *raw[2] = {};
+        int64_t raw_cap[2] = {};
+        int cur = 0;
+        hipStream_t side = nullptr;
+        hipEvent_t ev_words = nullptr, ev_pre = nullptr;
+        bool pre_valid = false;
+        uint32_t pre_key[2][624];          // the states the next draw may start from
+        int32_t pre_spos[2];               // their pos
+        int64_t pre_pos0[2];               // their first word in raw[1 - cur]
+        int64_t pre_total = 0;             // words made ahead in raw[1 - cur]
         int32_t *boff = nullptr;
         int64_t boff_cap = 0;
         MtMeta *meta = nullptr, *meta_pin = nullptr;
@@ -832,7 +843,11 @@ static void free_handle(fs2_handle *h) {
     if (h->pub_stats) hipHostFree(h->pub_stats);
     if (h->noise_pin) hipHostFree(h->noise_pin);
     if (h->u0_pin) hipHostFree(h->u0_pin);
-    hipFree(h->mt.raw); hipFree(h->mt.boff); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
+    if (h->mt.side) hipStreamSynchronize(h->mt.side);
+    hipFree(h->mt.raw[0]); hipFree(h->mt.raw[1]); hipFree(h->mt.boff);
+    if (h->mt.ev_words) hipEventDestroy(h->mt.ev_words);
+    if (h->mt.ev_pre) hipEventDestroy(h->mt.ev_pre);
+    if (h->mt.side) hipStreamDestroy(h->mt.side); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
     hipFree(h->mt.pval);
     if (h->mt.meta_pin) hipHostFree(h->mt.meta_pin);
     if (h->mt.amb_pin) hipHostFree(h->mt.amb_pin);
@@ -2131,7 +2146,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     auto &mt = h->mt;
     const int64_t N = h->n_global;
     const int h0 = (N > 0 && in->has_gauss) ? 1 : 0;
-    const int64_t pos0 = in->pos;
     const int64_t P = (N > h0) ? (N - h0 + 1) / 2 : 0;     // accepted attempts (pairs) needed
     // attempts until P successes at p = pi/4: mean P/p, sd sqrt(P(1-p))/p; 12 sd of margin
     const double mean = (double)P / 0.78539816339744831, sd = std::sqrt((double)P * 0.21460183660255169) / 0.78539816339744831;
@@ -2142,23 +2156,60 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         HIP_TRY(h, hipMalloc((void **)&mt.meta, sizeof(MtMeta)));
         HIP_TRY(h, hipHostMalloc((void **)&mt.meta_pin, sizeof(MtMeta), 0));
     }
+    if (!mt.side) {
+        HIP_TRY(h, hipStreamCreateWithFlags(&mt.side, hipStreamNonBlocking));
+        HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_words, hipEventDisableTiming));
+        HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_pre, hipEventDisableTiming));
+    }
+    // the words made ahead serve this draw if it starts where the last one said
+    // numpy would be (after its normals, or after its u0 too)
+    int64_t pos0 = in->pos;
+    int64_t have = 0;                          // words of the buffer already made
+    if (mt.pre_valid) {
+        for (int k = 0; k < 2 && have == 0; ++k) {
+            if (mt.pre_spos[k] == in->pos && std::memcmp(mt.pre_key[k], in->key, sizeof mt.pre_key[k]) == 0) {
+                mt.cur = 1 - mt.cur;
+                pos0 = mt.pre_pos0[k];
+                have = mt.pre_total;
+            }
+        }
+    }
+    // the side stream's last work (made ahead, or still reading this buffer) first
+    if (mt.pre_valid) HIP_TRY(h, hipStreamWaitEvent(s, mt.ev_pre, 0));
+    mt.pre_valid = false;
     MtMeta meta{};
+    int64_t total = 0;
     for (int attempt = 0;; ++attempt) {
         if (attempt == 6) return set_err(&h->err, FS2_ERR_STATE, "fs2_mt_draw: attempts did not converge");
         // words: the key, then through the block holding the u0 words after the last attempt
         const int64_t need = pos0 + 4 * A + 2;
-        const int64_t total = std::max<int64_t>(kMtN, (need + kMtN - 1) / kMtN * kMtN);
-        HIP_TRY(h, mt_grow((void **)&mt.raw, nullptr, 4, &mt.raw_cap, total));
+        total = std::max<int64_t>(kMtN, (need + kMtN - 1) / kMtN * kMtN);
+        if (have == 0) {
+            HIP_TRY(h, mt_grow((void **)&mt.raw[mt.cur], nullptr, 4, &mt.raw_cap[mt.cur], total));
+            std::memcpy(mt.words_pin, in->key, sizeof(uint32_t) * kMtN);
+            HIP_TRY(h, hipMemcpyAsync(mt.raw[mt.cur], mt.words_pin, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
+            have = kMtN;
+        } else if (total > mt.raw_cap[mt.cur]) {
+            // keep the words made so far
+            uint32_t *nr = nullptr;
+            const int64_t c = std::max<int64_t>(total, mt.raw_cap[mt.cur] + mt.raw_cap[mt.cur] / 2);
+            HIP_TRY(h, hipMalloc((void **)&nr, 4 * (size_t)c));
+            HIP_TRY(h, hipMemcpyAsync(nr, mt.raw[mt.cur], 4 * (size_t)have, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(h, hipStreamSynchronize(s));
+            hipFree(mt.raw[mt.cur]);
+            mt.raw[mt.cur] = nr;
+            mt.raw_cap[mt.cur] = c;
+        }
+        uint32_t *raw = mt.raw[mt.cur];
         const int64_t nb = (A + 255) / 256;
         HIP_TRY(h, mt_grow((void **)&mt.boff, nullptr, 4, &mt.boff_cap, std::max<int64_t>(nb, 1)));
         int64_t acap = mt.amb_cap;
         HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, amb_cap));
         mt.amb_cap = acap;
-        std::memcpy(mt.words_pin, in->key, sizeof(uint32_t) * kMtN);
-        HIP_TRY(h, hipMemcpyAsync(mt.raw, mt.words_pin, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
-        HIP_TRY(h, launch_mt_words(mt.raw, kMtN, total, s));
+        if (total > have) HIP_TRY(h, launch_mt_words(raw, have, total, s));
+        have = std::max(have, total);
         HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
-        HIP_TRY(h, launch_mt_draw(mt.raw, pos0, A, P, N, h0, in->gauss, sigma, h->first, h->n, h->noise_dev,
+        HIP_TRY(h, launch_mt_draw(raw, pos0, (pos0 - in->pos) / kMtN, A, P, N, h0, in->gauss, sigma, h->first, h->n, h->noise_dev,
                                   mt.boff, mt.meta, mt.amb, (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX), s));
         HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, mt.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
         HIP_TRY(h, hipStreamSynchronize(s));
@@ -2223,6 +2274,32 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     }
     after_u0->has_gauss = after->has_gauss;
     after_u0->gauss = after->gauss;
+    {
+        // the next draw's words, made on the side stream while the scan runs: the
+        // other buffer starts at the key block of `after` (kb1), which also holds or
+        // precedes after_u0's (kb2 = kb1 or kb1 + 1)
+        const int64_t E = meta.E;
+        const int64_t kb1 = (E == pos0) ? (pos0 - in->pos) / kMtN : (E - 1) / kMtN;
+        const int64_t kb2 = (E + 1) / kMtN;
+        const int nx = 1 - mt.cur;
+        const int64_t keep = have - kMtN * kb1;        // words made from block kb1 on
+        const int64_t want = std::max<int64_t>(keep, (2 * kMtN + 4 * (A + 2) + 2 + kMtN - 1) / kMtN * kMtN);
+        HIP_TRY(h, mt_grow((void **)&mt.raw[nx], nullptr, 4, &mt.raw_cap[nx], want));
+        HIP_TRY(h, hipEventRecord(mt.ev_words, s));
+        HIP_TRY(h, hipStreamWaitEvent(mt.side, mt.ev_words, 0));
+        HIP_TRY(h, hipMemcpyAsync(mt.raw[nx], mt.raw[mt.cur] + kMtN * kb1, 4 * (size_t)keep,
+                                  hipMemcpyDeviceToDevice, mt.side));
+        HIP_TRY(h, launch_mt_words(mt.raw[nx], keep, want, mt.side));
+        HIP_TRY(h, hipEventRecord(mt.ev_pre, mt.side));
+        std::memcpy(mt.pre_key[0], after->key, sizeof mt.pre_key[0]);
+        std::memcpy(mt.pre_key[1], after_u0->key, sizeof mt.pre_key[1]);
+        mt.pre_spos[0] = after->pos;
+        mt.pre_spos[1] = after_u0->pos;
+        mt.pre_pos0[0] = after->pos;
+        mt.pre_pos0[1] = kMtN * (kb2 - kb1) + after_u0->pos;
+        mt.pre_total = want;
+        mt.pre_valid = true;
+    }
     // u0 = np.random.uniform(0, 1 / N) = 0 + (1/N - 0) legacy_double (fast_slam_2.py:183)
     const uint32_t wu[2] = {meta.w_u0[0], meta.w_u0[1]};
     const double hi = 1.0 / (double)h->n_global;

@@ -176,9 +176,10 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
 
 // numpy's state after the draw: the key block holding the last word consumed
 // (pos = words used of it, 624 before the next twist), and the u0 words
-__global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos0, int64_t P, MtMeta *meta) {
+__global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t P,
+                                                  MtMeta *meta) {
     const int64_t E = P > 0 ? pos0 + 4 * (meta->last_attempt + 1) : pos0;
-    const int64_t b1 = (E == pos0) ? 0 : (E - 1) / kMtN, b2 = (E + 1) / kMtN;
+    const int64_t b1 = (E == pos0) ? b_in : (E - 1) / kMtN, b2 = (E + 1) / kMtN;
     for (int t = threadIdx.x; t < kMtN; t += 256) {
         meta->key_after[t] = R[kMtN * b1 + t];
         meta->key_after_u0[t] = R[kMtN * b2 + t];
@@ -211,7 +212,7 @@ hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t 
     return hipGetLastError();
 }
 
-hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t A, int64_t P, int64_t N, int32_t h0,
+hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t A, int64_t P, int64_t N, int32_t h0,
                           double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
                           int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, hipStream_t s) {
     MtParams p{};
@@ -238,7 +239,7 @@ hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t A, int64_t P,
         hipLaunchKernelGGL(k_mt_scan, dim3(1), dim3(1024), 0, s, p);
         hipLaunchKernelGGL(k_mt_normals, dim3(p.nb), dim3(256), 0, s, p);
     }
-    hipLaunchKernelGGL(k_mt_final, dim3(1), dim3(256), 0, s, R, pos0, P, meta);
+    hipLaunchKernelGGL(k_mt_final, dim3(1), dim3(256), 0, s, R, pos0, b_in, P, meta);
     return hipGetLastError();
 }
 
