@@ -2323,9 +2323,15 @@ int fs2_debug_noise(fs2_handle *h, double *out) {
 int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, int32_t *amb, int32_t on_host) {
     if (n < 0 || (n > 0 && (!x || !out || !amb))) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_mt_log: bad arguments");
     if (on_host) {
+        double thi[kMtLogTab], tlo[kMtLogTab];
+        for (int k = 0; k < kMtLogTab; ++k) {
+            const DD l = mt_log_tab_entry(k);
+            thi[k] = l.hi;
+            tlo[k] = l.lo;
+        }
         for (int64_t k = 0; k < n; ++k) {
             bool a = false;
-            out[k] = mt_log(x[k], &a);
+            out[k] = mt_log(x[k], thi, tlo, &a);
             amb[k] = a ? 1 : 0;
         }
         return FS2_OK;

@@ -3,10 +3,9 @@
 // and resample start (:183) bit for bit with np.random, without the host
 // generating N normals per scan.
 //
-//   k_mt_words    one wave: the raw word stream, 227 words per step of the
-//                 recurrence, the ring of the last 851 words in LDS, the loads of
-//                 step s + 1 issued before step s's stores (they read words >= 2
-//                 steps old);
+//   k_mt_words    one workgroup: the raw word stream, two steps of the
+//                 recurrence (454 words) per pair of barriers, a thread per
+//                 227-strided chain, the last 1024 words in an LDS ring;
 //   k_mt_count    one lane per polar attempt (4 words): accepted attempts per
 //                 256-attempt block;
 //   k_mt_scan     one workgroup: exclusive offsets of the block counts;
@@ -19,56 +18,43 @@
 
 namespace fs2 {
 
-__global__ __launch_bounds__(64) void k_mt_words(uint32_t *R, int64_t begin, int64_t end) {
-    __shared__ uint32_t ring[1024];
-    const int lane = threadIdx.x;
-    for (int t = lane; t < kMtN; t += 64) {
+// Thread q < 227 owns the chain of words base + q, base + q + 227, ... (so
+// x[j - 227] is its own previous word, in a register); x[j - 624] and x[j - 623]
+// come from the LDS ring, a pair read by one ds_read2 (the ring is mirrored:
+// word i at i mod 1024 and i mod 1024 + 1024, so a pair never wraps).  Both are
+// >= 2 steps old, so a phase computes two steps (454 words) between barriers.
+__global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, int64_t end) {
+    __shared__ uint32_t ring[2048];
+    const int q = threadIdx.x;
+    for (int t = q; t < kMtN; t += 256) {
         const int64_t j = begin - kMtN + t;
-        ring[j & 1023] = R[j];
+        const uint32_t v = R[j];
+        ring[j & 1023] = v;
+        ring[(j & 1023) + 1024] = v;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // lane handles words base + q, q = lane + 64 k < 227; x[j - 227] is its own
-    // value of the previous step
-    uint32_t c[4], a[4], b[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int q = lane + 64 * k;
-        const int64_t j = begin + q;
-        c[k] = q < kMtLag ? ring[(j - kMtLag) & 1023] : 0u;
-        a[k] = q < kMtLag ? ring[(j - kMtN) & 1023] : 0u;
-        b[k] = q < kMtLag ? ring[(j - kMtN + 1) & 1023] : 0u;
-    }
-    for (int64_t base = begin; base < end; base += kMtLag) {
-        // next step's operands (words of steps <= s - 1: stored before the last fence)
-        uint32_t na[4], nb[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = lane + 64 * k;
-            const int64_t j = base + kMtLag + q;
-            na[k] = q < kMtLag ? ring[(j - kMtN) & 1023] : 0u;
-            nb[k] = q < kMtLag ? ring[(j - kMtN + 1) & 1023] : 0u;
+    __syncthreads();
+    const bool on = q < kMtLag;
+    uint32_t c = on ? ring[(begin + q - kMtLag) & 1023] : 0u;
+    for (int64_t base = begin; base < end; base += 2 * kMtLag) {
+        const int64_t j0 = base + q, j1 = j0 + kMtLag;
+        if (on) {
+            const uint32_t *p0 = ring + ((j0 - kMtN) & 1023);
+            const uint32_t *p1 = ring + ((j1 - kMtN) & 1023);
+            const uint32_t a0 = p0[0], b0 = p0[1], a1 = p1[0], b1 = p1[1];
+            const uint32_t v0 = mt_next_word(a0, b0, c);
+            const uint32_t v1 = mt_next_word(a1, b1, v0);
+            c = v1;
+            __syncthreads();         // every read of this phase before its writes
+            ring[j0 & 1023] = v0;
+            ring[(j0 & 1023) + 1024] = v0;
+            ring[j1 & 1023] = v1;
+            ring[(j1 & 1023) + 1024] = v1;
+            if (j0 < end) R[j0] = v0;
+            if (j1 < end) R[j1] = v1;
+        } else {
+            __syncthreads();
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = lane + 64 * k;
-            const int64_t j = base + q;
-            if (q < kMtLag) {
-                const uint32_t v = mt_next_word(a[k], b[k], c[k]);
-                c[k] = v;
-                ring[j & 1023] = v;
-                if (j < end) R[j] = v;
-            }
-            a[k] = na[k];
-            b[k] = nb[k];
-        }
-        // one wave: its LDS operations complete in order; the wavefront-scope fences
-        // only keep the compiler from moving the next step's loads above these stores
-        // (a workgroup-scope release would also wait for the global stores)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
     }
 }
 
@@ -141,6 +127,12 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
         t = mt_attempt(w[0], w[1], w[2], w[3]);
     }
     __shared__ int s_c[4];
+    __shared__ double s_thi[kMtLogTab], s_tlo[kMtLogTab];
+    if (threadIdx.x < kMtLogTab) {
+        const DD l = mt_log_tab_entry(threadIdx.x);
+        s_thi[threadIdx.x] = l.hi;
+        s_tlo[threadIdx.x] = l.lo;
+    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t bal = __ballot(t.ok);
     if (lane == 0) s_c[wid] = __popcll(bal);
@@ -155,7 +147,7 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
     }
     if (!t.ok || rank >= p.P) return;
     bool amb = false;
-    const double lg = mt_log(t.r2, &amb);
+    const double lg = mt_log(t.r2, s_thi, s_tlo, &amb);
     const double f = mt_polar_f(t.r2, lg);
     const double g0 = f * t.x2, g1 = f * t.x1;
     const int64_t o = p.h0 + 2 * rank;
@@ -199,16 +191,23 @@ __global__ __launch_bounds__(256) void k_mt_patch(double *out, const int64_t *id
 }
 
 __global__ __launch_bounds__(256) void k_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb) {
+    __shared__ double s_thi[kMtLogTab], s_tlo[kMtLogTab];
+    if (threadIdx.x < kMtLogTab) {
+        const DD l = mt_log_tab_entry(threadIdx.x);
+        s_thi[threadIdx.x] = l.hi;
+        s_tlo[threadIdx.x] = l.lo;
+    }
+    __syncthreads();
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
     bool a = false;
-    out[k] = mt_log(x[k], &a);
+    out[k] = mt_log(x[k], s_thi, s_tlo, &a);
     amb[k] = a ? 1 : 0;
 }
 
 hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t s) {
     if (end <= begin) return hipSuccess;
-    hipLaunchKernelGGL(k_mt_words, dim3(1), dim3(64), 0, s, R, begin, end);
+    hipLaunchKernelGGL(k_mt_words, dim3(1), dim3(256), 0, s, R, begin, end);
     return hipGetLastError();
 }
 

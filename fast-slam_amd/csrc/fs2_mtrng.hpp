@@ -10,7 +10,7 @@
 //   legacy_normal(loc, scale) = loc + scale * legacy_gauss.
 // The word stream is the linear recurrence x[n] = x[n-227] ^ twist(x[n-624], x[n-623])
 // (the in-place twist of the 624-word key restated over the stream), so one
-// wave generates 227 words per step (fs2_mtrng.hip).  Everything but log(r2) is
+// workgroup generates 227 words per step, two steps per barrier pair (fs2_mtrng.hip).  Everything but log(r2) is
 // exact or correctly rounded (IEEE mul / add / div / sqrt), identical on host and
 // device; log is glibc's (error <= 0.52 ulp, not always correctly rounded), so the
 // device evaluates log in double-double and flags the results within 0.025 ulp of
@@ -154,11 +154,48 @@ __host__ __device__ inline DD dd_log(double x) {
     return dd_add(kl, lm);
 }
 
+// The table form used per draw: x = 2^e m, m in [0.75, 1.5), c = 1 + i/128 the
+// nearest table point (i in [-32, 64]; m - c exact), log m = log c + 2 atanh(s),
+// s = (m - c) / (m + c), |s| <= 1/512, seven series terms (s^16 / 15 < 2^-140).
+// c = 1 exactly around m = 1, so a result near 0 (r2 near 1) cancels nothing.
+// log c (double-double) comes from dd_log; host and device compute the same table
+// bit for bit (IEEE operations and exact fma only).
+constexpr int kMtLogTab = 97;
+__host__ __device__ inline DD mt_log_tab_entry(int k) {
+    const double c = 1.0 + (double)(k - 32) / 128.0;
+    return (k == 32) ? DD{0.0, 0.0} : dd_log(c);
+}
+__host__ __device__ inline DD dd_log_tab(double x, const double *thi, const double *tlo) {
+    const uint64_t u = dbits(x);
+    int e = (int)((u >> 52) & 0x7ff) - 1023;
+    double m = dfrom((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);   // [1, 2)
+    if (m >= 1.5) {
+        m = m * 0.5;
+        e += 1;
+    }
+#ifdef __HIP_DEVICE_COMPILE__
+    const double fi = __builtin_rint((m - 1.0) * 128.0);
+#else
+    const double fi = std::rint((m - 1.0) * 128.0);
+#endif
+    const int k = (int)fi + 32;
+    const double c = 1.0 + fi / 128.0;
+    const DD s = dd_div(DD{m - c, 0.0}, dd_two_sum(m, c));
+    const DD t = dd_mul(s, s);
+    DD p = dd_inv(15.0);
+#pragma unroll
+    for (int j = 6; j >= 0; --j) p = dd_add(dd_mul(t, p), dd_inv(2.0 * j + 1.0));
+    const DD lm = dd_add(DD{thi[k], tlo[k]}, dd_mul(dd_mul_d(s, 2.0), p));
+    const double ed = (double)e;
+    const DD kl = dd_add(dd_two_prod(ed, kLn2Hi), DD{ed * kLn2Lo, 0.0});
+    return dd_add(kl, lm);
+}
+
 // log(x) rounded to double, and whether the rounding is not certain to equal
 // glibc's (the double-double value lies within kMtAmbBand ulp of a midpoint, or
 // the result is a power of two, where the ulp changes).  x in (0, 1).
-__host__ __device__ inline double mt_log(double x, bool *amb) {
-    const DD l = dd_log(x);
+__host__ __device__ inline double mt_log(double x, const double *thi, const double *tlo, bool *amb) {
+    const DD l = dd_log_tab(x, thi, tlo);
     const uint64_t au = dbits(l.hi) & 0x7fffffffffffffffull;
     const int ex = (int)(au >> 52);
     const double ulp = dfrom((uint64_t)(ex - 52) << 52);
