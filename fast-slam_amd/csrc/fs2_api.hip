@@ -172,6 +172,8 @@ struct fs2_handle {
         int64_t *pidx = nullptr, *pidx_pin = nullptr;
         double *pval = nullptr, *pval_pin = nullptr;
         int64_t patch_cap = 0, pval_cap = 0;
+        double *tab = nullptr;             // [2][97] log table (device)
+        bool tab_ready = false;
         bool armed = false;
     } mt;
     int32_t *assoc_dev = nullptr;
@@ -848,7 +850,7 @@ static void free_handle(fs2_handle *h) {
     if (h->mt.ev_words) hipEventDestroy(h->mt.ev_words);
     if (h->mt.ev_pre) hipEventDestroy(h->mt.ev_pre);
     if (h->mt.side) hipStreamDestroy(h->mt.side); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
-    hipFree(h->mt.pval);
+    hipFree(h->mt.pval); hipFree(h->mt.tab);
     if (h->mt.meta_pin) hipHostFree(h->mt.meta_pin);
     if (h->mt.amb_pin) hipHostFree(h->mt.amb_pin);
     if (h->mt.words_pin) hipHostFree(h->mt.words_pin);
@@ -2153,6 +2155,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     int64_t amb_cap = P / 8 + 4096;
     if (!mt.words_pin) HIP_TRY(h, hipHostMalloc((void **)&mt.words_pin, sizeof(uint32_t) * 2 * kMtN, 0));
     if (!mt.meta) {
+        HIP_TRY(h, hipMalloc((void **)&mt.tab, sizeof(double) * 2 * kMtLogTab));
         HIP_TRY(h, hipMalloc((void **)&mt.meta, sizeof(MtMeta)));
         HIP_TRY(h, hipHostMalloc((void **)&mt.meta_pin, sizeof(MtMeta), 0));
     }
@@ -2210,7 +2213,9 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         have = std::max(have, total);
         HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
         HIP_TRY(h, launch_mt_draw(raw, pos0, (pos0 - in->pos) / kMtN, A, P, N, h0, in->gauss, sigma, h->first, h->n, h->noise_dev,
-                                  mt.boff, mt.meta, mt.amb, (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX), s));
+                                  mt.boff, mt.meta, mt.amb, (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX),
+                                  mt.tab, mt.tab_ready ? 1 : 0, s));
+        mt.tab_ready = true;
         HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, mt.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
         HIP_TRY(h, hipStreamSynchronize(s));
         meta = *mt.meta_pin;

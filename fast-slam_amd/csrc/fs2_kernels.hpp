@@ -565,7 +565,8 @@ hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t 
 // (the input key is block b_in of R: R[624 b_in + pos] is word pos0)
 hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t A, int64_t P, int64_t N, int32_t h0,
                           double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
-                          int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, hipStream_t s);
+                          int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, double *tab, int32_t tab_ready,
+                          hipStream_t s);   // tab: [2][97] log table, made here unless tab_ready
 hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n, hipStream_t s);
 hipError_t launch_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb, hipStream_t s);
 

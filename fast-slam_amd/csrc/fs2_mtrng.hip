@@ -3,9 +3,9 @@
 // and resample start (:183) bit for bit with np.random, without the host
 // generating N normals per scan.
 //
-//   k_mt_words    one workgroup: the raw word stream, two steps of the
-//                 recurrence (454 words) per pair of barriers, a thread per
-//                 227-strided chain, the last 1024 words in an LDS ring;
+//   k_mt_words    one workgroup: the raw word stream, 623 words (2.7 steps of
+//                 the recurrence) per barrier, a thread per 227-strided chain,
+//                 the last 2048 words in an LDS ring;
 //   k_mt_count    one lane per polar attempt (4 words): accepted attempts per
 //                 256-attempt block;
 //   k_mt_scan     one workgroup: exclusive offsets of the block counts;
@@ -18,41 +18,49 @@
 
 namespace fs2 {
 
-// Thread q < 227 owns the chain of words base + q, base + q + 227, ... (so
-// x[j - 227] is its own previous word, in a register); x[j - 624] and x[j - 623]
-// come from the LDS ring, a pair read by one ds_read2 (the ring is mirrored:
-// word i at i mod 1024 and i mod 1024 + 1024, so a pair never wraps).  Both are
-// >= 2 steps old, so a phase computes two steps (454 words) between barriers.
+// A phase makes the 623 words [base, base + 623): thread q < 227 the words
+// base + q, base + q + 227 and (q < 169) base + q + 454, each one's x[j - 227]
+// being the thread's previous word except the first's (read, like every
+// x[j - 624], x[j - 623], from the LDS ring).  Every word read is older than the
+// phase (623 = 624 - 1 is the most a phase can make), so one barrier per phase
+// orders the ring.  The ring holds 2048 words, mirrored (word i at i mod 2048 and
+// i mod 2048 + 2048) so the pair x[j - 624], x[j - 623] never wraps; a phase reads
+// [base - 624, base) and writes [base, base + 623), never the same slots.
+constexpr int kMtPhase = 2 * kMtLag + (kMtN - 1 - 2 * kMtLag);   // 623
 __global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, int64_t end) {
-    __shared__ uint32_t ring[2048];
+    __shared__ uint32_t ring[4096];
     const int q = threadIdx.x;
     for (int t = q; t < kMtN; t += 256) {
         const int64_t j = begin - kMtN + t;
         const uint32_t v = R[j];
-        ring[j & 1023] = v;
-        ring[(j & 1023) + 1024] = v;
+        ring[j & 2047] = v;
+        ring[(j & 2047) + 2048] = v;
     }
     __syncthreads();
-    const bool on = q < kMtLag;
-    uint32_t c = on ? ring[(begin + q - kMtLag) & 1023] : 0u;
-    for (int64_t base = begin; base < end; base += 2 * kMtLag) {
-        const int64_t j0 = base + q, j1 = j0 + kMtLag;
+    const bool on = q < kMtLag, on2 = q < kMtPhase - 2 * kMtLag;
+    for (int64_t base = begin; base < end; base += kMtPhase) {
+        const int64_t j0 = base + q, j1 = j0 + kMtLag, j2 = j1 + kMtLag;
         if (on) {
-            const uint32_t *p0 = ring + ((j0 - kMtN) & 1023);
-            const uint32_t *p1 = ring + ((j1 - kMtN) & 1023);
+            const uint32_t c0 = ring[(j0 - kMtLag) & 2047];
+            const uint32_t *p0 = ring + ((j0 - kMtN) & 2047);
+            const uint32_t *p1 = ring + ((j1 - kMtN) & 2047);
+            const uint32_t *p2 = ring + ((j2 - kMtN) & 2047);
             const uint32_t a0 = p0[0], b0 = p0[1], a1 = p1[0], b1 = p1[1];
-            const uint32_t v0 = mt_next_word(a0, b0, c);
+            const uint32_t a2 = on2 ? p2[0] : 0u, b2 = on2 ? p2[1] : 0u;
+            const uint32_t v0 = mt_next_word(a0, b0, c0);
             const uint32_t v1 = mt_next_word(a1, b1, v0);
-            c = v1;
-            __syncthreads();         // every read of this phase before its writes
-            ring[j0 & 1023] = v0;
-            ring[(j0 & 1023) + 1024] = v0;
-            ring[j1 & 1023] = v1;
-            ring[(j1 & 1023) + 1024] = v1;
+            ring[j0 & 2047] = v0;
+            ring[(j0 & 2047) + 2048] = v0;
+            ring[j1 & 2047] = v1;
+            ring[(j1 & 2047) + 2048] = v1;
             if (j0 < end) R[j0] = v0;
             if (j1 < end) R[j1] = v1;
-        } else {
-            __syncthreads();
+            if (on2) {
+                const uint32_t v2 = mt_next_word(a2, b2, v1);
+                ring[j2 & 2047] = v2;
+                ring[(j2 & 2047) + 2048] = v2;
+                if (j2 < end) R[j2] = v2;
+            }
         }
         __syncthreads();
     }
@@ -74,7 +82,17 @@ struct MtParams {
     MtMeta *meta;
     MtAmb *amb;
     int32_t amb_cap;
+    const double *tab;       // [2][kMtLogTab] log table (k_mt_table), hi then lo
 };
+
+// the log table of mt_log (host and device compute the same bits)
+__global__ __launch_bounds__(128) void k_mt_table(double *tab) {
+    if (threadIdx.x < kMtLogTab) {
+        const DD l = mt_log_tab_entry(threadIdx.x);
+        tab[threadIdx.x] = l.hi;
+        tab[kMtLogTab + threadIdx.x] = l.lo;
+    }
+}
 
 __global__ __launch_bounds__(256) void k_mt_count(const MtParams p) {
     const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -129,9 +147,8 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
     __shared__ int s_c[4];
     __shared__ double s_thi[kMtLogTab], s_tlo[kMtLogTab];
     if (threadIdx.x < kMtLogTab) {
-        const DD l = mt_log_tab_entry(threadIdx.x);
-        s_thi[threadIdx.x] = l.hi;
-        s_tlo[threadIdx.x] = l.lo;
+        s_thi[threadIdx.x] = p.tab[threadIdx.x];
+        s_tlo[threadIdx.x] = p.tab[kMtLogTab + threadIdx.x];
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t bal = __ballot(t.ok);
@@ -213,8 +230,11 @@ hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t 
 
 hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t A, int64_t P, int64_t N, int32_t h0,
                           double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
-                          int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, hipStream_t s) {
+                          int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, double *tab, int32_t tab_ready,
+                          hipStream_t s) {
     MtParams p{};
+    p.tab = tab;
+    if (!tab_ready) hipLaunchKernelGGL(k_mt_table, dim3(1), dim3(128), 0, s, tab);
     p.R = R;
     p.pos0 = pos0;
     p.A = A;
