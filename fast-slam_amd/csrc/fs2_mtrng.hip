@@ -62,7 +62,10 @@ __global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, in
                 if (j2 < end) R[j2] = v2;
             }
         }
-        __syncthreads();
+        // the phase's LDS writes complete, then the barrier; the global stores stay
+        // in flight (__syncthreads would wait for them too: its workgroup-scope
+        // fence covers global memory)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 }
 
@@ -162,9 +165,26 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
         // the cached value of the previous draw comes first
         if (p.first == 0 && p.n_local > 0) p.out[0] = 0.0 + p.sigma * p.gauss0;
     }
-    if (!t.ok || rank >= p.P) return;
+    const bool use = t.ok && rank < p.P;
     bool amb = false;
-    const double lg = mt_log(t.r2, s_thi, s_tlo, &amb);
+    const double lg = use ? mt_log(t.r2, s_thi, s_tlo, &amb) : 0.0;
+    // the block's listed attempts take consecutive entries: one atomic per block
+    __shared__ int s_a[4];
+    __shared__ int s_abase;
+    const uint64_t abal = __ballot(amb);
+    if (lane == 0) s_a[wid] = __popcll(abal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = s_a[0] + s_a[1] + s_a[2] + s_a[3];
+        s_abase = tot ? atomicAdd(&p.meta->amb_n, tot) : 0;
+    }
+    __syncthreads();
+    if (amb) {
+        int k = s_abase + __popcll(abal & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wid; ++w) k += s_a[w];
+        if (k < p.amb_cap) p.amb[k] = MtAmb{t.r2, t.x1, t.x2, rank};
+    }
+    if (!use) return;
     const double f = mt_polar_f(t.r2, lg);
     const double g0 = f * t.x2, g1 = f * t.x1;
     const int64_t o = p.h0 + 2 * rank;
@@ -176,10 +196,6 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
         p.meta->last_attempt = a;
         p.meta->has_gauss = (o + 1 < p.N) ? 0 : 1;
         p.meta->gauss = (o + 1 < p.N) ? 0.0 : g1;
-    }
-    if (amb) {
-        const int k = atomicAdd(&p.meta->amb_n, 1);
-        if (k < p.amb_cap) p.amb[k] = MtAmb{t.r2, t.x1, t.x2, rank};
     }
 }
 
