@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, in
             const uint32_t *p1 = ring + ((j1 - kMtN) & 2047);
             const uint32_t *p2 = ring + ((j2 - kMtN) & 2047);
             const uint32_t a0 = p0[0], b0 = p0[1], a1 = p1[0], b1 = p1[1];
-            const uint32_t a2 = on2 ? p2[0] : 0u, b2 = on2 ? p2[1] : 0u;
+            const uint32_t a2 = p2[0], b2 = p2[1];   // (read by every thread: one round trip)
             const uint32_t v0 = mt_next_word(a0, b0, c0);
             const uint32_t v1 = mt_next_word(a1, b1, v0);
             ring[j0 & 2047] = v0;
