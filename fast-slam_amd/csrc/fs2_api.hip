@@ -173,6 +173,11 @@ struct fs2_handle {
         double *pval = nullptr, *pval_pin = nullptr;
         int64_t patch_cap = 0, pval_cap = 0;
         double *tab = nullptr;             // [2][97] log table (device)
+        // jump-ahead: G regions of J words made in parallel (J, G fixed per handle)
+        int64_t jJ = 0;
+        int jG = 0;                        // 0: not planned, 1: sequential
+        uint64_t *jpoly = nullptr;         // [G - 1][mt_poly_words()]
+        uint32_t *jwin = nullptr;          // [G - 1][624]
         bool tab_ready = false;
         bool armed = false;
     } mt;
@@ -850,7 +855,7 @@ static void free_handle(fs2_handle *h) {
     if (h->mt.ev_words) hipEventDestroy(h->mt.ev_words);
     if (h->mt.ev_pre) hipEventDestroy(h->mt.ev_pre);
     if (h->mt.side) hipStreamDestroy(h->mt.side); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
-    hipFree(h->mt.pval); hipFree(h->mt.tab);
+    hipFree(h->mt.pval); hipFree(h->mt.tab); hipFree(h->mt.jpoly); hipFree(h->mt.jwin);
     if (h->mt.meta_pin) hipHostFree(h->mt.meta_pin);
     if (h->mt.amb_pin) hipHostFree(h->mt.amb_pin);
     if (h->mt.words_pin) hipHostFree(h->mt.words_pin);
@@ -2136,6 +2141,24 @@ static hipError_t mt_grow(void **dev, void **pin, size_t esz, int64_t *cap, int6
     return hipSuccess;
 }
 
+// the words R[have, total) of a buffer whose R[0, 624) is a key: in parallel
+// regions (jump-ahead) when the buffer is made from its key alone and the draws
+// are large, else one workgroup.  Returns the words made (>= total).
+static int mt_fill(fs2_handle *h, uint32_t *R, int64_t have, int64_t total, hipStream_t s, int64_t *made) {
+    auto &mt = h->mt;
+    *made = std::max(have, total);
+    if (total <= have) return FS2_OK;
+    if (have == kMtN && mt.jG > 1 && total > 3 * mt.jJ) {
+        const int64_t par_end = mt.jG * mt.jJ + 1;
+        HIP_TRY(h, launch_mt_words_parallel(R, par_end, mt.jpoly, mt_poly_words(), mt.jG, mt.jJ, mt.jwin, s));
+        if (total > par_end) HIP_TRY(h, launch_mt_words(R, par_end, total, s));
+        *made = std::max(par_end, total);
+        return FS2_OK;
+    }
+    HIP_TRY(h, launch_mt_words(R, have, total, s));
+    return FS2_OK;
+}
+
 int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
                 fs2_mt_state *after_u0, double *u0_out) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
@@ -2153,6 +2176,25 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     const double mean = (double)P / 0.78539816339744831, sd = std::sqrt((double)P * 0.21460183660255169) / 0.78539816339744831;
     int64_t A = P ? (int64_t)(mean + 12.0 * sd) + 64 : 0;
     int64_t amb_cap = P / 8 + 4096;
+    if (mt.jG == 0) {
+        // regions of ~160 K words (16 for 10^6 particles), J >= 2 x 20 561 (the
+        // jump's operands come first); the polynomials are made once (~0.3 s)
+        const int64_t tn = (2 * kMtN + 4 * (A + 2) + 2 + 2 * kMtN + kMtN - 1) / kMtN * kMtN;
+        const int G = (int)std::min<int64_t>(kMtMaxGen, tn / 160000);
+        mt.jG = 1;
+        if (G >= 2) {
+            const int64_t J = std::max<int64_t>((tn + G - 1) / G, 2 * 20561 + 2 * kMtN);
+            std::vector<uint64_t> gp;
+            if (mt_jump_polys((uint64_t)J, G, gp)) {
+                HIP_TRY(h, hipMalloc((void **)&mt.jpoly, sizeof(uint64_t) * gp.size()));
+                HIP_TRY(h, hipMalloc((void **)&mt.jwin, sizeof(uint32_t) * kMtN * (G - 1)));
+                HIP_TRY(h, hipMemcpy(mt.jpoly, gp.data(), sizeof(uint64_t) * gp.size(), hipMemcpyHostToDevice));
+                mt.jG = G;
+                mt.jJ = J;
+            }
+        }
+    }
+    const int64_t par_words = mt.jG > 1 ? mt.jG * mt.jJ + 1 : 0;   // a parallel fill makes this many
     if (!mt.words_pin) HIP_TRY(h, hipHostMalloc((void **)&mt.words_pin, sizeof(uint32_t) * 2 * kMtN, 0));
     if (!mt.meta) {
         HIP_TRY(h, hipMalloc((void **)&mt.tab, sizeof(double) * 2 * kMtLogTab));
@@ -2188,7 +2230,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         const int64_t need = pos0 + 4 * A + 2;
         total = std::max<int64_t>(kMtN, (need + kMtN - 1) / kMtN * kMtN);
         if (have == 0) {
-            HIP_TRY(h, mt_grow((void **)&mt.raw[mt.cur], nullptr, 4, &mt.raw_cap[mt.cur], total));
+            HIP_TRY(h, mt_grow((void **)&mt.raw[mt.cur], nullptr, 4, &mt.raw_cap[mt.cur], std::max(total, par_words)));
             std::memcpy(mt.words_pin, in->key, sizeof(uint32_t) * kMtN);
             HIP_TRY(h, hipMemcpyAsync(mt.raw[mt.cur], mt.words_pin, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
             have = kMtN;
@@ -2209,8 +2251,12 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         int64_t acap = mt.amb_cap;
         HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, amb_cap));
         mt.amb_cap = acap;
-        if (total > have) HIP_TRY(h, launch_mt_words(raw, have, total, s));
-        have = std::max(have, total);
+        {
+            int64_t made = 0;
+            const int rcf = mt_fill(h, raw, have, total, s, &made);
+            if (rcf) return rcf;
+            have = made;
+        }
         HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
         HIP_TRY(h, launch_mt_draw(raw, pos0, (pos0 - in->pos) / kMtN, A, P, N, h0, in->gauss, sigma, h->first, h->n, h->noise_dev,
                                   mt.boff, mt.meta, mt.amb, (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX),
@@ -2287,14 +2333,21 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         const int64_t kb1 = (E == pos0) ? (pos0 - in->pos) / kMtN : (E - 1) / kMtN;
         const int64_t kb2 = (E + 1) / kMtN;
         const int nx = 1 - mt.cur;
-        const int64_t keep = have - kMtN * kb1;        // words made from block kb1 on
-        const int64_t want = std::max<int64_t>(keep, (2 * kMtN + 4 * (A + 2) + 2 + kMtN - 1) / kMtN * kMtN);
-        HIP_TRY(h, mt_grow((void **)&mt.raw[nx], nullptr, 4, &mt.raw_cap[nx], want));
+        // the key block kb1 and what follows it, then the rest from the key
+        const bool par = mt.jG > 1;
+        const int64_t keep = par ? kMtN : have - kMtN * kb1;
+        int64_t want = std::max<int64_t>(keep, (2 * kMtN + 4 * (A + 2) + 2 + kMtN - 1) / kMtN * kMtN);
+        HIP_TRY(h, mt_grow((void **)&mt.raw[nx], nullptr, 4, &mt.raw_cap[nx], std::max(want, par_words)));
         HIP_TRY(h, hipEventRecord(mt.ev_words, s));
         HIP_TRY(h, hipStreamWaitEvent(mt.side, mt.ev_words, 0));
         HIP_TRY(h, hipMemcpyAsync(mt.raw[nx], mt.raw[mt.cur] + kMtN * kb1, 4 * (size_t)keep,
                                   hipMemcpyDeviceToDevice, mt.side));
-        HIP_TRY(h, launch_mt_words(mt.raw[nx], keep, want, mt.side));
+        {
+            int64_t made = 0;
+            const int rcf = mt_fill(h, mt.raw[nx], keep, want, mt.side, &made);
+            if (rcf) return rcf;
+            want = made;
+        }
         HIP_TRY(h, hipEventRecord(mt.ev_pre, mt.side));
         std::memcpy(mt.pre_key[0], after->key, sizeof mt.pre_key[0]);
         std::memcpy(mt.pre_key[1], after_u0->key, sizeof mt.pre_key[1]);
@@ -2313,6 +2366,12 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     HIP_TRY(h, hipMemcpyAsync(h->u0_dev, h->u0_pin, 8, hipMemcpyHostToDevice, s));
     if (u0_out) *u0_out = u0;
     mt.armed = true;
+    return FS2_OK;
+}
+
+int fs2_debug_mt_jump(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
+    if (!key || !out) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_mt_jump: null argument");
+    if (!mt_jump_host(key, J, out)) return set_err(nullptr, FS2_ERR_STATE, "MT19937 characteristic polynomial not found");
     return FS2_OK;
 }
 

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace fs2 {
 
 constexpr int kBlock = 256;          // 4 waves of 64
@@ -568,6 +570,15 @@ hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t
                           int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, double *tab, int32_t tab_ready,
                           hipStream_t s);   // tab: [2][97] log table, made here unless tab_ready
 hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n, hipStream_t s);
+// jump-ahead (fs2_mtrng.hip): G regions of J words made in parallel (J >= 2 x 20561,
+// G <= kMtMaxGen); g: the polynomials of mt_jump_polys(J, G) ([G - 1][mt_poly_words()]);
+// win: [G - 1][624] scratch.  R[0, 624) is the key; R[624, total) made.
+constexpr int kMtMaxGen = 16;
+hipError_t launch_mt_words_parallel(uint32_t *R, int64_t total, const uint64_t *g, int pw, int G, int64_t J,
+                                    uint32_t *win, hipStream_t s);
+bool mt_jump_polys(uint64_t J, int G, std::vector<uint64_t> &out);
+int mt_poly_words();
+bool mt_jump_host(const uint32_t key[624], uint64_t J, uint32_t out[624]);
 hipError_t launch_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb, hipStream_t s);
 
 hipError_t launch_icp(int32_t B, int32_t P, const double *src, const double *tgt,

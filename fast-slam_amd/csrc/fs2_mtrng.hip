@@ -13,6 +13,9 @@
 //                 gives its two output indices; log in double-double, results
 //                 near a rounding midpoint listed for the host (libm log);
 //   k_mt_patch    the host's recomputed values into the output.
+#include <algorithm>
+#include <vector>
+
 #include "fs2_kernels.hpp"
 #include "fs2_mtrng.hpp"
 
@@ -27,12 +30,13 @@ namespace fs2 {
 // i mod 2048 + 2048) so the pair x[j - 624], x[j - 623] never wraps; a phase reads
 // [base - 624, base) and writes [base, base + 623), never the same slots.
 constexpr int kMtPhase = 2 * kMtLag + (kMtN - 1 - 2 * kMtLag);   // 623
-__global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, int64_t end) {
+// (init: the 624 words before begin)
+__device__ __forceinline__ void mt_words_body(uint32_t *R, int64_t begin, int64_t end, const uint32_t *init) {
     __shared__ uint32_t ring[4096];
     const int q = threadIdx.x;
     for (int t = q; t < kMtN; t += 256) {
         const int64_t j = begin - kMtN + t;
-        const uint32_t v = R[j];
+        const uint32_t v = init[t];
         ring[j & 2047] = v;
         ring[(j & 2047) + 2048] = v;
     }
@@ -67,6 +71,10 @@ __global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, in
         // fence covers global memory)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+}
+
+__global__ __launch_bounds__(256) void k_mt_words(uint32_t *R, int64_t begin, int64_t end) {
+    mt_words_body(R, begin, end, R + begin - kMtN);
 }
 
 struct MtParams {
@@ -287,6 +295,239 @@ hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, i
 hipError_t launch_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_mt_debug_log, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, out, amb);
+    return hipGetLastError();
+}
+
+}  // namespace fs2
+
+// ---------------------------------------------------------------------------
+// Jump-ahead: several workgroups make one draw's words.  Every bit sequence of
+// the stream (bit k of x[n + 1], n >= 0) satisfies the recurrence whose
+// characteristic polynomial phi (degree 19937) is that of the state transition,
+// so with g = x^J mod phi, x[J + w] = XOR_{i : g_i = 1} x[i + w] for w >= 1: the
+// 624 words after index J are a GF(2) combination of the first 20 561 words.
+// phi is found once by Berlekamp-Massey on 2 x 19937 bits of a stream; the
+// polynomials of the region starts J_k = k J are made by products mod phi.
+namespace fs2 {
+namespace {
+
+constexpr int kMtDeg = 19937;
+constexpr int kPW = (kMtDeg + 1 + 63) / 64;       // words of a polynomial of degree <= 19937
+
+typedef std::vector<uint64_t> Poly;
+
+inline int pbit(const uint64_t *p, int64_t i) { return (int)((p[i >> 6] >> (i & 63)) & 1u); }
+
+// q ^= p << sh (q has room)
+inline void xor_shifted(uint64_t *q, const uint64_t *p, int np, int64_t sh) {
+    const int64_t ws = sh >> 6;
+    const int bs = (int)(sh & 63);
+    if (bs == 0) {
+        for (int k = 0; k < np; ++k) q[k + ws] ^= p[k];
+    } else {
+        uint64_t carry = 0;
+        for (int k = 0; k < np; ++k) {
+            q[k + ws] ^= (p[k] << bs) | carry;
+            carry = p[k] >> (64 - bs);
+        }
+        q[np + ws] ^= carry;
+    }
+}
+
+// The stream's characteristic polynomial (degree 19937, bit i = coefficient of x^i).
+const Poly &mt_charpoly() {
+    static const Poly phi = [] {
+        // a stream from an arbitrary key: MSB of x[n + 1], n = 0 .. 2 x 19937 + 63
+        const int64_t nb = 2 * (int64_t)kMtDeg + 64;
+        std::vector<uint32_t> x(nb + kMtN + 2);
+        for (int i = 0; i < kMtN; ++i) x[i] = 0x9e3779b9u * (uint32_t)(i + 1) ^ 0x7f4a7c15u;
+        for (int64_t n = kMtN; n < (int64_t)x.size(); ++n) x[n] = mt_next_word(x[n - 624], x[n - 623], x[n - 227]);
+        // reversed sequence bitset: bit j = s[nb - 1 - j]
+        const int nw = (int)((nb + 63) / 64) + 2;
+        std::vector<uint64_t> rev(nw + kPW + 2, 0);
+        for (int64_t n = 0; n < nb; ++n)
+            if ((x[n + 1] >> 31) & 1u) {
+                const int64_t j = nb - 1 - n;
+                rev[j >> 6] |= 1ull << (j & 63);
+            }
+        // Berlekamp-Massey over GF(2): connection polynomial C (bit i = c_i)
+        const int cw = kPW + 2;
+        std::vector<uint64_t> C(cw + kPW + 4, 0), B(cw + kPW + 4, 0), T;
+        C[0] = B[0] = 1;
+        int64_t L = 0, m = 1;
+        for (int64_t n = 0; n < nb; ++n) {
+            // d = parity(C & (rev >> t)), t = nb - 1 - n: s[n] + sum c_i s[n - i]
+            const int64_t t = nb - 1 - n, tw = t >> 6;
+            const int tb = (int)(t & 63);
+            const int lw = (int)(L >> 6) + 1;
+            uint64_t acc = 0;
+            for (int k = 0; k < lw; ++k) {
+                const uint64_t lo = rev[tw + k], hi = rev[tw + k + 1];
+                const uint64_t wv = tb ? ((lo >> tb) | (hi << (64 - tb))) : lo;
+                acc ^= C[k] & wv;
+            }
+            if (!__builtin_parityll(acc)) {
+                ++m;
+            } else if (2 * L <= n) {
+                T = C;
+                xor_shifted(C.data(), B.data(), cw, m);
+                L = n + 1 - L;
+                B = T;
+                m = 1;
+            } else {
+                xor_shifted(C.data(), B.data(), cw, m);
+                ++m;
+            }
+        }
+        // phi(x) = x^L C(1/x)
+        Poly p(kPW, 0);
+        for (int64_t i = 0; i <= L; ++i)
+            if (pbit(C.data(), i)) {
+                const int64_t j = L - i;
+                p[j >> 6] |= 1ull << (j & 63);
+            }
+        if (L != kMtDeg) p.clear();            // (checked by the caller)
+        return p;
+    }();
+    return phi;
+}
+
+// r (2 kPW words, degree < 2 x 19937) mod phi -> kPW words
+void reduce_mod(std::vector<uint64_t> &r, const Poly &phi) {
+    for (int64_t d = 2 * (int64_t)kMtDeg; d >= kMtDeg; --d)
+        if (pbit(r.data(), d)) xor_shifted(r.data(), phi.data(), kPW, d - kMtDeg);
+    r.resize(kPW);
+}
+
+Poly mulmod(const Poly &a, const Poly &b, const Poly &phi) {
+    std::vector<uint64_t> r(2 * kPW + 2, 0);
+    for (int64_t i = 0; i < kMtDeg; ++i)
+        if (pbit(a.data(), i)) xor_shifted(r.data(), b.data(), kPW, i);
+    reduce_mod(r, phi);
+    return r;
+}
+
+Poly xpow_mod(uint64_t J, const Poly &phi) {
+    Poly r(kPW, 0);
+    r[0] = 1;
+    int top = 63;
+    while (top > 0 && !((J >> top) & 1u)) --top;
+    for (int bt = top; bt >= 0; --bt) {
+        // square: spread the bits
+        std::vector<uint64_t> s(2 * kPW + 2, 0);
+        for (int64_t i = 0; i < kMtDeg; ++i)
+            if (pbit(r.data(), i)) s[(2 * i) >> 6] |= 1ull << ((2 * i) & 63);
+        reduce_mod(s, phi);
+        r = s;
+        if ((J >> bt) & 1u) {
+            std::vector<uint64_t> t(2 * kPW + 2, 0);
+            xor_shifted(t.data(), r.data(), kPW, 1);
+            reduce_mod(t, phi);
+            r = t;
+        }
+    }
+    return r;
+}
+
+}  // namespace
+
+// the jump polynomials of J, 2J, ..., (G-1)J: [G-1][kPW] words into out (false: no phi)
+bool mt_jump_polys(uint64_t J, int G, std::vector<uint64_t> &out) {
+    const Poly &phi = mt_charpoly();
+    if (phi.empty()) return false;
+    out.assign((size_t)(G - 1) * kPW, 0);
+    Poly g1 = xpow_mod(J, phi), gk = g1;
+    for (int k = 1; k < G; ++k) {
+        if (k > 1) gk = mulmod(gk, g1, phi);
+        std::copy(gk.begin(), gk.end(), out.begin() + (size_t)(k - 1) * kPW);
+    }
+    return true;
+}
+int mt_poly_words() { return kPW; }
+
+// host: x[J + 1 .. J + 624] from the key x[0 .. 624) (the device kernels' arithmetic)
+bool mt_jump_host(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
+    std::vector<uint64_t> g;
+    if (!mt_jump_polys(J, 2, g)) return false;
+    std::vector<uint32_t> x(kMtDeg + kMtN + 1);
+    for (int i = 0; i < kMtN; ++i) x[i] = key[i];
+    for (size_t n = kMtN; n < x.size(); ++n) x[n] = mt_next_word(x[n - 624], x[n - 623], x[n - 227]);
+    for (int w = 1; w <= kMtN; ++w) {
+        uint32_t acc = 0;
+        for (int i = 0; i < kMtDeg; ++i)
+            if (pbit(g.data(), i)) acc ^= x[i + w];
+        out[w - 1] = acc;
+    }
+    return true;
+}
+
+// ---- device side ----
+constexpr int kMtJumpChunk = 1024;
+constexpr int kMtBaseWords = kMtDeg + kMtN + 1;    // x[0 .. 20561): the jump's operands
+
+// windows[k - 1][w - 1] ^= XOR over the chunk's i with g_k bit i of x[i + w]
+// (grid: chunks x (G - 1); windows zeroed first)
+__global__ __launch_bounds__(640) void k_mt_jump(const uint32_t *R, const uint64_t *g, int pw, uint32_t *win) {
+    __shared__ uint32_t xs[kMtJumpChunk + kMtN + 1];
+    __shared__ uint64_t gs[kMtJumpChunk / 64];
+    const int k = blockIdx.y;
+    const int i0 = blockIdx.x * kMtJumpChunk;
+    for (int t = threadIdx.x; t < kMtJumpChunk + kMtN + 1; t += blockDim.x) {
+        const int i = i0 + t;
+        xs[t] = i < kMtBaseWords ? R[i] : 0u;
+    }
+    if (threadIdx.x < kMtJumpChunk / 64) {
+        const int wi = (i0 >> 6) + threadIdx.x;
+        gs[threadIdx.x] = wi < pw ? g[(int64_t)k * pw + wi] : 0ull;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t >= kMtN) return;
+    const int w = t + 1;
+    const int n = min(kMtJumpChunk, kMtDeg - i0);
+    uint32_t acc = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t m = 0u - (uint32_t)((gs[i >> 6] >> (i & 63)) & 1ull);
+        acc ^= xs[i + w] & m;
+    }
+    atomicXor(win + (int64_t)k * kMtN + t, acc);
+}
+
+struct MtRegions {
+    int64_t begin[kMtMaxGen], end[kMtMaxGen];
+    int32_t from_win[kMtMaxGen];     // block k > 0: its first 624 words are window k - 1
+};
+
+// block b makes R[begin[b], end[b]) from the 624 words before begin[b] (window
+// b - 1 when from_win, stored into R as well)
+__global__ __launch_bounds__(256) void k_mt_words_multi(uint32_t *R, const uint32_t *win, const MtRegions rg) {
+    const int b = blockIdx.x;
+    const int64_t begin = rg.begin[b], end = rg.end[b];
+    const uint32_t *init = R + begin - kMtN;
+    if (rg.from_win[b]) {
+        init = win + (int64_t)(b - 1) * kMtN;
+        for (int t = threadIdx.x; t < kMtN; t += 256) R[begin - kMtN + t] = init[t];
+    }
+    mt_words_body(R, begin, end, init);
+}
+
+hipError_t launch_mt_words_parallel(uint32_t *R, int64_t total, const uint64_t *g, int pw, int G, int64_t J,
+                                    uint32_t *win, hipStream_t s) {
+    // base words for the jumps, then the G - 1 windows, then the regions
+    hipError_t e = launch_mt_words(R, kMtN, kMtBaseWords, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(win, 0, sizeof(uint32_t) * kMtN * (G - 1), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_mt_jump, dim3((kMtDeg + kMtJumpChunk - 1) / kMtJumpChunk, G - 1), dim3(640), 0, s, R, g,
+                       pw, win);
+    MtRegions rg{};
+    for (int b = 0; b < G; ++b) {
+        const int64_t st = b == 0 ? kMtBaseWords : (int64_t)b * (int64_t)J + 1 + kMtN;   // after window b - 1
+        rg.begin[b] = st;
+        rg.end[b] = b + 1 < G ? (int64_t)(b + 1) * (int64_t)J + 1 : total;
+        rg.from_win[b] = b > 0;
+    }
+    hipLaunchKernelGGL(k_mt_words_multi, dim3(G), dim3(256), 0, s, R, win, rg);
     return hipGetLastError();
 }
 

@@ -336,6 +336,10 @@ int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, in
 /* Test hook: the handle's motion-noise buffer (N_local values: the last scan's
  * injected draws, or fs2_mt_draw's) into out. */
 int fs2_debug_noise(fs2_handle *h, double *out);
+/* Test hook of fs2_mt_draw's jump-ahead: the stream words x[J + 1 .. J + 624]
+ * after the key x[0 .. 624) (J >= 1), as the GF(2) combination of x[1 .. 20561)
+ * given by x^J mod the characteristic polynomial (host arithmetic). */
+int fs2_debug_mt_jump(const uint32_t key[624], uint64_t J, uint32_t out[624]);
 
 /* ---------------------------------------------------------- multi-GPU ---- */
 

@@ -149,3 +149,16 @@ def test_mt_state_struct_round_trip():
     st = np.random.get_state()
     s = nat.fs2_mt_state.from_numpy(st)
     assert states_equal(s.to_numpy(), st)
+
+
+@pytest.mark.parametrize("J", [1, 623, 624, 5000, 123457, 2600000])
+def test_jump_ahead_words(J):
+    """x[J + 1 .. J + 624] from the key by the jump polynomial (Berlekamp-Massey's
+    characteristic polynomial, x^J mod it) equal the sequential stream's."""
+    lib = nat.load()
+    rs = np.random.RandomState(J % 1000)
+    key = rs.randint(0, 2 ** 32, size=624, dtype=np.uint64).astype(np.uint32)
+    out = np.zeros(624, dtype=np.uint32)
+    nat.check(lib.fs2_debug_mt_jump(nat.ptr(key), J, nat.ptr(out)))
+    ref = stream_words(key, J + 625)[J + 1:J + 625]
+    assert np.array_equal(out, ref)
