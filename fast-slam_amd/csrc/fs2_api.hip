@@ -3,8 +3,13 @@
 // the stateless ICP / LineFilter / association helpers.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -12,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fs2.h"
@@ -2121,6 +2127,86 @@ int fs2_mahalanobis(int32_t device, const double *a, const double *b, const doub
 
 // ---- numpy's legacy RandomState on the device (fs2_mtrng.hpp / .hip) ----
 
+// A few host threads for fs2_mt_draw's log recomputations (~5 % of 10^6 attempts
+// per draw): started on first use, one job at a time, the caller takes a share.
+namespace {
+struct HostPool {
+    std::mutex job_mu, mu;
+    std::condition_variable cv, cv_done;
+    std::vector<std::thread> th;
+    const std::function<void(int64_t, int64_t)> *fn = nullptr;
+    int64_t n = 0, chunk = 0;
+    std::atomic<int64_t> next{0};
+    uint64_t gen = 0;
+    int left = 0;
+    bool stop = false;
+    HostPool() {
+        cpu_set_t cs;
+        int ncpu = 4;
+        if (sched_getaffinity(0, sizeof cs, &cs) == 0) ncpu = CPU_COUNT(&cs);
+        const int nw = std::max(0, std::min(7, ncpu / 2 - 1));
+        for (int i = 0; i < nw; ++i) th.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+    void work() {
+        for (;;) {
+            const int64_t k0 = next.fetch_add(chunk);
+            if (k0 >= n) return;
+            (*fn)(k0, std::min(n, k0 + chunk));
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+            }
+            work();
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (--left == 0) cv_done.notify_one();
+            }
+        }
+    }
+    void run(int64_t count, int64_t ch, const std::function<void(int64_t, int64_t)> &f) {
+        std::lock_guard<std::mutex> jl(job_mu);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            fn = &f;
+            n = count;
+            chunk = ch;
+            next.store(0);
+            left = (int)th.size();
+            ++gen;
+        }
+        cv.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu);
+        cv_done.wait(lk, [&] { return left == 0; });
+    }
+};
+}  // namespace
+
+// f over [0, count) in chunks of `chunk`, on the pool when it pays
+static void host_pool_run(int64_t count, int64_t chunk, const std::function<void(int64_t, int64_t)> &f) {
+    if (count <= 2 * chunk) {
+        f(0, count);
+        return;
+    }
+    static HostPool pool;
+    pool.run(count, chunk, f);
+}
+
 // grow a device / pinned buffer pair to hold n elements of `esz` bytes (contents dropped)
 static hipError_t mt_grow(void **dev, void **pin, size_t esz, int64_t *cap, int64_t n) {
     if (n <= *cap) return hipSuccess;
@@ -2282,25 +2368,32 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         HIP_TRY(h, hipStreamSynchronize(s));
         HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
         HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
-        int64_t np = 0;
-        for (int64_t k = 0; k < na; ++k) {
-            const MtAmb &e = mt.amb_pin[k];
-            const double f = mt_polar_f(e.r2, std::log(e.r2));
-            const double g0 = f * e.x2, g1 = f * e.x1;
-            const int64_t o = h0 + 2 * e.rank;
-            if (o >= h->first && o < h->first + h->n) {
-                mt.pidx_pin[np] = o - h->first;
-                mt.pval_pin[np++] = 0.0 + sigma * g0;
-            }
-            if (o + 1 < N) {
-                if (o + 1 >= h->first && o + 1 < h->first + h->n) {
-                    mt.pidx_pin[np] = o + 1 - h->first;
-                    mt.pval_pin[np++] = 0.0 + sigma * g1;
+        // entry k patches outputs 2k, 2k + 1 (index -1: not this rank's); split over
+        // the host pool's threads when there are many
+        const int64_t first = h->first, nl = h->n;
+        double cached = 0.0;
+        bool has_cached = false;
+        auto fix = [&](int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) {
+                const MtAmb &e = mt.amb_pin[k];
+                const double f = mt_polar_f(e.r2, std::log(e.r2));
+                const double g0 = f * e.x2, g1 = f * e.x1;
+                const int64_t o = h0 + 2 * e.rank;
+                const bool in0 = o >= first && o < first + nl;
+                mt.pidx_pin[2 * k] = in0 ? o - first : -1;
+                mt.pval_pin[2 * k] = 0.0 + sigma * g0;
+                const bool in1 = o + 1 < N && o + 1 >= first && o + 1 < first + nl;
+                mt.pidx_pin[2 * k + 1] = in1 ? o + 1 - first : -1;
+                mt.pval_pin[2 * k + 1] = 0.0 + sigma * g1;
+                if (o + 1 >= N) {              // the pair whose second value stays cached (one at most)
+                    cached = g1;
+                    has_cached = true;
                 }
-            } else {
-                meta.gauss = g1;               // the pair whose second value stays cached
             }
-        }
+        };
+        host_pool_run(na, 2048, fix);
+        if (has_cached) meta.gauss = cached;
+        const int64_t np = 2 * na;
         if (np > 0) {
             HIP_TRY(h, hipMemcpyAsync(mt.pidx, mt.pidx_pin, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
             HIP_TRY(h, hipMemcpyAsync(mt.pval, mt.pval_pin, sizeof(double) * np, hipMemcpyHostToDevice, s));

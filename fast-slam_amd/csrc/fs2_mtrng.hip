@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos
 
 __global__ __launch_bounds__(256) void k_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k < n) out[idx[k]] = val[k];
+    if (k < n && idx[k] >= 0) out[idx[k]] = val[k];
 }
 
 __global__ __launch_bounds__(256) void k_mt_debug_log(const double *x, int64_t n, double *out, int32_t *amb) {
