@@ -494,8 +494,8 @@ hipError_t debug_tail_times_update(unsigned long long out[32], int reset);
 hipError_t debug_tail_times_exact(unsigned long long out[32], int reset);
 hipError_t debug_tail_times_resample(unsigned long long out[32], int reset);
 #endif
-// particle p's row k takes page alloc.base + p * rows_each + k, its slot j record
-// alloc.rbase + p * lm_cap + j
+// particle p (of count) row k takes the reserved page alloc.base + k * count + p, its
+// slot j record alloc.rbase + j * count + p (row-major: a wave's row is contiguous)
 // (ext: atomicMax of the float bits of the largest finite |x|, |y| imported; slb
 // lowered to the smallest nonzero mirror s)
 // perm (nullable): maps of exactly perm_len slots are laid out with slot perm[j]

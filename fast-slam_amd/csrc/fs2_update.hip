@@ -1211,8 +1211,9 @@ hipError_t launch_normalize(const ReduceParams &p, hipStream_t s) {
 
 // stage: [count][lm_cap][6] -> maps of particles first .. first+count-1, written
 // into fresh pages and records (row k of particle p takes reserved page
-// p * rows_each + k, slot j reserved record p * lm_cap + j); the pages and
-// records they replace are reclaimed by the next collection.
+// k * count + p, slot j reserved record j * count + p: row-major, so a wave's
+// 64 particles read one row's pages and one slot's records from adjacent ids);
+// the pages and records they replace are reclaimed by the next collection.
 __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const int32_t *cnt_stage,
                                                    int64_t first, int64_t count, int32_t lm_cap,
                                                    MapRef map, PageAlloc alloc, int32_t rows_each,
@@ -1230,11 +1231,13 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         // position j holds slot perm[j] (a spatial layout, fs2_set_state), or slot j
         const int slot = (perm && c == perm_len) ? perm[j] : j;
         const int row = j / kPageSlots;
-        const uint32_t id = alloc.freel[alloc.base + p * rows_each + row];
+        // row-major over the chunk's particles: the pages (and records) a wave reads
+        // for one row (slot) of 64 consecutive particles are adjacent in the pools
+        const uint32_t id = alloc.freel[alloc.base + (int64_t)row * count + p];
         if (j % kPageSlots == 0) pt_entry(map, row, first + p)->x = id | kOwned;
         const double *s = stage + (p * lm_cap + slot) * 6;
         const float4 mv = store_slot(map, page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}},
-                                     alloc.rfreel[alloc.rbase + e], slot);
+                                     alloc.rfreel[alloc.rbase + (int64_t)j * count + p], slot);
         smin = fminf(smin, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
         if (isfinite(mv.x)) amax = fmaxf(amax, fabsf(mv.x));
         if (isfinite(mv.y)) amax = fmaxf(amax, fabsf(mv.y));
