@@ -21,7 +21,9 @@ def workload(N, L, seed, mode="peaked", G=1):
     """mode "peaked": peaked likelihoods, so resampling moves particles across
     shards; "follow": only rank 0's particles carry weight (its first 100 ten
     times more), so the first scan (no measurements) resamples and rank 0 keeps
-    a higher shard (equal shards follow their sources)."""
+    a higher shard (equal shards follow their sources); "numpy":
+    "peaked" through iterate() with numpy's global stream drawn on the device
+    (fs2_mt_draw: every rank draws all N normals and keeps its shard's)."""
     import fs2_synthetic as syn
     wl = syn.Workload(N, L, seed=seed)
     x, y, yaw = wl.poses()
@@ -53,7 +55,9 @@ def main(argv):
     wl, x, y, yaw, w, cnt, lm = workload(N, L, seed, mode, G)
     cap = L + 4 * scans + 8
     h = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap, rank=rank,
-                              world_size=G, comm_id=key, comm_mode="shm", verbose=False)
+                              world_size=G, comm_id=key, comm_mode="shm", verbose=False,
+                              rng="numpy" if mode == "numpy" else "device")
+    np.random.seed(77)
     a, b = h.first_global, h.first_global + h.n_local
     h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
     h.set_profiling(True)
@@ -62,7 +66,12 @@ def main(argv):
     for s in range(scans):
         rot, tr = syn.odometry(s)
         rec["firsts_pre"].append(h.first_global)    # the shard whose particles the associations describe
-        pose, st = h.step(rot, tr, measurements(wl, s, mode))
+        if mode == "numpy":
+            ms = [fast_slam_2.Measurement(float(d), float(b)) for d, b in measurements(wl, s, mode)]
+            pose = np.array(h.iterate(rot, tr, ms))
+            st = h.last_stats
+        else:
+            pose, st = h.step(rot, tr, measurements(wl, s, mode))
         rec["resampled"].append(st.resampled)
         rec["best_index"].append(st.best_index)
         rec["pose"].append(pose)
@@ -80,7 +89,8 @@ def main(argv):
     h.close()
     np.savez(out, first=a, count=b - a, assoc=np.stack(assoc), x=xs, y=ys, yaw=yaws, w=ws, cnt=cnts, lm=lms,
              sent_particles=prof["sent_particles"], sent_rows=prof["sent_rows"], sent_pages=prof["sent_pages"],
-             migrations=prof["migrations"], **{k: np.array(v) for k, v in rec.items()})
+             migrations=prof["migrations"], np_key=np.random.get_state()[1], np_pos=np.random.get_state()[2],
+             **{k: np.array(v) for k, v in rec.items()})
     return 0
 
 

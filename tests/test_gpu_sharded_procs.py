@@ -13,7 +13,9 @@ The parent compares every scan with a single handle in this process on the same
 inputs: resample decisions, estimate index and pose, N_eff, associations, and at
 the end every particle's state within 1e-9; reduce_ambiguous is 0 on every rank
 and scan (no decision the shard order could flip), at least two resamples move
-particles across shards.
+particles across shards.  The "numpy" case runs the drop-in iterate() with
+numpy's global stream drawn on the device (fs2_mt_draw) on every rank, shards
+that move included, and checks numpy's final state too.
 """
 import os
 import subprocess
@@ -28,7 +30,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.mark.parametrize("G,N,L,scans,mode", [(2, 6000, 40, 8, "peaked"), (3, 10007, 30, 8, "peaked"),
-                                               (2, 6000, 24, 4, "follow")])
+                                               (2, 6000, 24, 4, "follow"), (2, 6000, 40, 8, "numpy")])
 def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     import torch  # noqa: F401
     import fast_slam_2
@@ -58,12 +60,18 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     wl, x, y, yaw, w, cnt, lm = workload(N, L, 21, mode, G)
     cap = L + 4 * scans + 8
     single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap,
-                                   verbose=False)
+                                   verbose=False, rng="numpy" if mode == "numpy" else "device")
     single.set_state(x, y, yaw, w, cnt, lm)
+    np.random.seed(77)
     resamples = 0
     for s in range(scans):
         rot, tr = syn.odometry(s)
-        pose1, st1 = single.step(rot, tr, measurements(wl, s, mode))
+        if mode == "numpy":
+            ms = [fast_slam_2.Measurement(float(d), float(b)) for d, b in measurements(wl, s, mode)]
+            pose1 = np.array(single.iterate(rot, tr, ms))
+            st1 = single.last_stats
+        else:
+            pose1, st1 = single.step(rot, tr, measurements(wl, s, mode))
         for r, d in enumerate(ranks):
             assert d["resampled"][s] == st1.resampled, (r, s)
             assert d["best_index"][s] == st1.best_index, (r, s)
@@ -84,6 +92,10 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
             assert np.allclose(s1[k][a:b], d[name], rtol=1e-9, atol=1e-15), name
         assert np.allclose(s1[5][a:b], d["lm"], rtol=1e-9, atol=1e-12)
     single.close()
+    if mode == "numpy":      # every rank left numpy's stream where the single handle did
+        key, pos = np.random.get_state()[1], np.random.get_state()[2]
+        for d in ranks:
+            assert np.array_equal(d["np_key"], key) and int(d["np_pos"]) == pos
     need = 1 if mode == "follow" else 2
     assert resamples >= need
     assert sum(int(d["migrations"]) for d in ranks) >= need, "particles must cross shards"
