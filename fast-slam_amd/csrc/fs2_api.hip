@@ -2335,7 +2335,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     mt.pre_valid = false;
     MtMeta meta{};
     int64_t total = 0;
-    const MtAmb *amb_dev = nullptr;            // where this draw's listed logs are
+    const MtAmb *amb_dev = mt.amb;             // where this draw's listed logs are
     if (spec_k >= 0) {
         auto &sp = mt.spec[spec_k];
         HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, sp.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
@@ -2403,7 +2403,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         }
         break;
     }
-    if (spec_k < 0) amb_dev = mt.amb;          // (the loop may have reallocated it)
     // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
     const int64_t na = meta.amb_n;
     if (na > 0) {
