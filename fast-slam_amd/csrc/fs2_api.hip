@@ -184,23 +184,6 @@ struct fs2_handle {
         int jG = 0;                        // 0: not planned, 1: sequential
         uint64_t *jpoly = nullptr;         // [G - 1][mt_poly_words()]
         uint32_t *jwin = nullptr;          // [G - 1][624]
-        // the next draw made ahead too, for both states it may start from (after
-        // the normals, after u0), unscaled: the draw then only scales, patches and
-        // reads its results
-        struct Spec {
-            double *g = nullptr;
-            int64_t g_cap = 0;
-            int32_t *boff = nullptr;
-            int64_t boff_cap = 0;
-            MtMeta *meta = nullptr;
-            MtAmb *amb = nullptr;
-            int64_t amb_cap = 0;
-            int64_t A = 0;
-        } spec[2];
-        bool spec_valid = false;
-        int64_t spec_first = 0;
-        int32_t spec_hg = 0;
-        double spec_gauss = 0.0;
         bool tab_ready = false;
         bool armed = false;
     } mt;
@@ -879,9 +862,6 @@ static void free_handle(fs2_handle *h) {
     if (h->mt.ev_pre) hipEventDestroy(h->mt.ev_pre);
     if (h->mt.side) hipStreamDestroy(h->mt.side); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
     hipFree(h->mt.pval); hipFree(h->mt.tab); hipFree(h->mt.jpoly); hipFree(h->mt.jwin);
-    for (auto &sp : h->mt.spec) {
-        hipFree(sp.g); hipFree(sp.boff); hipFree(sp.meta); hipFree(sp.amb);
-    }
     if (h->mt.meta_pin) hipHostFree(h->mt.meta_pin);
     if (h->mt.amb_pin) hipHostFree(h->mt.amb_pin);
     if (h->mt.words_pin) hipHostFree(h->mt.words_pin);
@@ -2316,43 +2296,21 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     // numpy would be (after its normals, or after its u0 too)
     int64_t pos0 = in->pos;
     int64_t have = 0;                          // words of the buffer already made
-    int spec_k = -1;                           // the draw made ahead for this state, if any
     if (mt.pre_valid) {
         for (int k = 0; k < 2 && have == 0; ++k) {
             if (mt.pre_spos[k] == in->pos && std::memcmp(mt.pre_key[k], in->key, sizeof mt.pre_key[k]) == 0) {
                 mt.cur = 1 - mt.cur;
                 pos0 = mt.pre_pos0[k];
                 have = mt.pre_total;
-                if (mt.spec_valid && mt.spec_first == h->first && mt.spec_hg == in->has_gauss &&
-                    std::memcmp(&mt.spec_gauss, &in->gauss, sizeof(double)) == 0 && mt.spec[k].A == A)
-                    spec_k = k;
             }
         }
     }
-    mt.spec_valid = false;
     // the side stream's last work (made ahead, or still reading this buffer) first
     if (mt.pre_valid) HIP_TRY(h, hipStreamWaitEvent(s, mt.ev_pre, 0));
     mt.pre_valid = false;
     MtMeta meta{};
     int64_t total = 0;
-    const MtAmb *amb_dev = mt.amb;             // where this draw's listed logs are
-    if (spec_k >= 0) {
-        auto &sp = mt.spec[spec_k];
-        HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, sp.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
-        HIP_TRY(h, hipStreamSynchronize(s));
-        meta = *mt.meta_pin;
-        if ((P == 0 || meta.accepted >= P) && meta.amb_n <= sp.amb_cap) {
-            total = std::max<int64_t>(kMtN, (pos0 + 4 * A + 2 + kMtN - 1) / kMtN * kMtN);
-            HIP_TRY(h, launch_mt_scale(h->noise_dev, sp.g, h->n, sigma, s));
-            amb_dev = sp.amb;
-            int64_t acap = mt.amb_cap;
-            HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, meta.amb_n));
-            mt.amb_cap = acap;
-        } else {
-            spec_k = -1;                       // (short of attempts or listings: made again below)
-        }
-    }
-    for (int attempt = 0; spec_k < 0; ++attempt) {
+    for (int attempt = 0;; ++attempt) {
         if (attempt == 6) return set_err(&h->err, FS2_ERR_STATE, "fs2_mt_draw: attempts did not converge");
         // words: the key, then through the block holding the u0 words after the last attempt
         const int64_t need = pos0 + 4 * A + 2;
@@ -2406,7 +2364,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
     const int64_t na = meta.amb_n;
     if (na > 0) {
-        HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, amb_dev, sizeof(MtAmb) * (size_t)na, hipMemcpyDeviceToHost, s));
+        HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)na, hipMemcpyDeviceToHost, s));
         HIP_TRY(h, hipStreamSynchronize(s));
         HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
         HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
@@ -2483,6 +2441,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
             if (rcf) return rcf;
             want = made;
         }
+        HIP_TRY(h, hipEventRecord(mt.ev_pre, mt.side));
         std::memcpy(mt.pre_key[0], after->key, sizeof mt.pre_key[0]);
         std::memcpy(mt.pre_key[1], after_u0->key, sizeof mt.pre_key[1]);
         mt.pre_spos[0] = after->pos;
@@ -2491,33 +2450,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         mt.pre_pos0[1] = kMtN * (kb2 - kb1) + after_u0->pos;
         mt.pre_total = want;
         mt.pre_valid = true;
-        // the next draw itself, from each of the two states, unscaled (sigma 1)
-        const int h0n = (N > 0 && after->has_gauss) ? 1 : 0;
-        const int64_t Pn = (N > h0n) ? (N - h0n + 1) / 2 : 0;
-        const double mn = (double)Pn / 0.78539816339744831, sdn = std::sqrt((double)Pn * 0.21460183660255169) / 0.78539816339744831;
-        const int64_t An = Pn ? (int64_t)(mn + 12.0 * sdn) + 64 : 0;
-        bool spec_ok = mt.tab_ready;
-        for (int v = 0; v < 2 && spec_ok; ++v) {
-            auto &sp = mt.spec[v];
-            spec_ok = mt.pre_pos0[v] + 4 * An + 2 <= want;
-            if (!spec_ok) break;
-            HIP_TRY(h, mt_grow((void **)&sp.g, nullptr, 8, &sp.g_cap, std::max<int64_t>(h->n, 1)));
-            HIP_TRY(h, mt_grow((void **)&sp.boff, nullptr, 4, &sp.boff_cap, std::max<int64_t>((An + 255) / 256, 1)));
-            HIP_TRY(h, mt_grow((void **)&sp.amb, nullptr, sizeof(MtAmb), &sp.amb_cap, Pn / 8 + 4096));
-            if (!sp.meta) HIP_TRY(h, hipMalloc((void **)&sp.meta, sizeof(MtMeta)));
-            HIP_TRY(h, hipMemsetAsync(sp.meta, 0, sizeof(MtMeta), mt.side));
-            HIP_TRY(h, launch_mt_draw(mt.raw[nx], mt.pre_pos0[v], (mt.pre_pos0[v] - mt.pre_spos[v]) / kMtN, An, Pn, N,
-                                      h0n, after->gauss, 1.0, h->first, h->n, sp.g, sp.boff, sp.meta, sp.amb,
-                                      (int32_t)std::min<int64_t>(sp.amb_cap, INT32_MAX), mt.tab, 1, mt.side));
-            sp.A = An;
-        }
-        if (spec_ok) {
-            mt.spec_valid = true;
-            mt.spec_first = h->first;
-            mt.spec_hg = after->has_gauss;
-            mt.spec_gauss = after->gauss;
-        }
-        HIP_TRY(h, hipEventRecord(mt.ev_pre, mt.side));   // after everything made ahead
     }
     // u0 = np.random.uniform(0, 1 / N) = 0 + (1/N - 0) legacy_double (fast_slam_2.py:183)
     const uint32_t wu[2] = {meta.w_u0[0], meta.w_u0[1]};

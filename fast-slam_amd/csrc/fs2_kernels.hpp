@@ -570,7 +570,6 @@ hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t
                           int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, double *tab, int32_t tab_ready,
                           hipStream_t s);   // tab: [2][97] log table, made here unless tab_ready
 hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n, hipStream_t s);
-hipError_t launch_mt_scale(double *out, const double *g, int64_t n, double sigma, hipStream_t s);
 // jump-ahead (fs2_mtrng.hip): G regions of J words made in parallel (J >= 2 x 20561,
 // G <= kMtMaxGen); g: the polynomials of mt_jump_polys(J, G) ([G - 1][mt_poly_words()]);
 // win: [G - 1][624] scratch.  R[0, 624) is the key; R[624, total) made.

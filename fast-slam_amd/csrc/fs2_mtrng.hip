@@ -226,13 +226,6 @@ __global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos
     }
 }
 
-// out = legacy_normal(0, sigma) of standard normals made ahead (made with sigma 1:
-// 0 + 1 g differs from g only for -0, which 0 + sigma g maps to +0 either way)
-__global__ __launch_bounds__(256) void k_mt_scale(double *out, const double *g, int64_t n, double sigma) {
-    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k < n) out[k] = 0.0 + sigma * g[k];
-}
-
 __global__ __launch_bounds__(256) void k_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k < n && idx[k] >= 0) out[idx[k]] = val[k];
@@ -290,12 +283,6 @@ hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t
         hipLaunchKernelGGL(k_mt_normals, dim3(p.nb), dim3(256), 0, s, p);
     }
     hipLaunchKernelGGL(k_mt_final, dim3(1), dim3(256), 0, s, R, pos0, b_in, P, meta);
-    return hipGetLastError();
-}
-
-hipError_t launch_mt_scale(double *out, const double *g, int64_t n, double sigma, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mt_scale, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, g, n, sigma);
     return hipGetLastError();
 }
 
