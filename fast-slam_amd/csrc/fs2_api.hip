@@ -2288,11 +2288,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         HIP_TRY(h, hipHostMalloc((void **)&mt.meta_pin, sizeof(MtMeta), 0));
     }
     if (!mt.side) {
-        // the words made ahead run beside the scan: lowest priority, so the scan's
-        // workgroups are dispatched first
-        int plo = 0, phi = 0;
-        HIP_TRY(h, hipDeviceGetStreamPriorityRange(&plo, &phi));
-        HIP_TRY(h, hipStreamCreateWithPriority(&mt.side, hipStreamNonBlocking, plo));
+        HIP_TRY(h, hipStreamCreateWithFlags(&mt.side, hipStreamNonBlocking));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_words, hipEventDisableTiming));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_pre, hipEventDisableTiming));
     }

@@ -465,37 +465,32 @@ bool mt_jump_host(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
 constexpr int kMtJumpChunk = 1024;
 constexpr int kMtBaseWords = kMtDeg + kMtN + 1;    // x[0 .. 20561): the jump's operands
 
-// windows[k][w - 1] ^= XOR over the chunk's i with g_(k+1) bit i of x[i + w], for
-// every k (a block per chunk: the x chunk is loaded once; a narrow grid, so the
-// words made ahead for the next draw leave the scan's kernels the GPU).  The
-// windows are zeroed first.
-__global__ __launch_bounds__(640) void k_mt_jump(const uint32_t *R, const uint64_t *g, int pw, int nk, uint32_t *win) {
+// windows[k - 1][w - 1] ^= XOR over the chunk's i with g_k bit i of x[i + w]
+// (grid: chunks x (G - 1); windows zeroed first)
+__global__ __launch_bounds__(640) void k_mt_jump(const uint32_t *R, const uint64_t *g, int pw, uint32_t *win) {
     __shared__ uint32_t xs[kMtJumpChunk + kMtN + 1];
     __shared__ uint64_t gs[kMtJumpChunk / 64];
+    const int k = blockIdx.y;
     const int i0 = blockIdx.x * kMtJumpChunk;
     for (int t = threadIdx.x; t < kMtJumpChunk + kMtN + 1; t += blockDim.x) {
         const int i = i0 + t;
         xs[t] = i < kMtBaseWords ? R[i] : 0u;
     }
+    if (threadIdx.x < kMtJumpChunk / 64) {
+        const int wi = (i0 >> 6) + threadIdx.x;
+        gs[threadIdx.x] = wi < pw ? g[(int64_t)k * pw + wi] : 0ull;
+    }
+    __syncthreads();
     const int t = threadIdx.x;
+    if (t >= kMtN) return;
     const int w = t + 1;
     const int n = min(kMtJumpChunk, kMtDeg - i0);
-    for (int k = 0; k < nk; ++k) {
-        __syncthreads();                    // xs loaded / the previous k's gs read
-        if (threadIdx.x < kMtJumpChunk / 64) {
-            const int wi = (i0 >> 6) + threadIdx.x;
-            gs[threadIdx.x] = wi < pw ? g[(int64_t)k * pw + wi] : 0ull;
-        }
-        __syncthreads();
-        if (t < kMtN) {
-            uint32_t acc = 0;
-            for (int i = 0; i < n; ++i) {
-                const uint32_t m = 0u - (uint32_t)((gs[i >> 6] >> (i & 63)) & 1ull);
-                acc ^= xs[i + w] & m;
-            }
-            atomicXor(win + (int64_t)k * kMtN + t, acc);
-        }
+    uint32_t acc = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t m = 0u - (uint32_t)((gs[i >> 6] >> (i & 63)) & 1ull);
+        acc ^= xs[i + w] & m;
     }
+    atomicXor(win + (int64_t)k * kMtN + t, acc);
 }
 
 struct MtRegions {
@@ -523,8 +518,8 @@ hipError_t launch_mt_words_parallel(uint32_t *R, int64_t total, const uint64_t *
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(win, 0, sizeof(uint32_t) * kMtN * (G - 1), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mt_jump, dim3((kMtDeg + kMtJumpChunk - 1) / kMtJumpChunk), dim3(640), 0, s, R, g, pw, G - 1,
-                       win);
+    hipLaunchKernelGGL(k_mt_jump, dim3((kMtDeg + kMtJumpChunk - 1) / kMtJumpChunk, G - 1), dim3(640), 0, s, R, g,
+                       pw, win);
     MtRegions rg{};
     for (int b = 0; b < G; ++b) {
         const int64_t st = b == 0 ? kMtBaseWords : (int64_t)b * (int64_t)J + 1 + kMtN;   // after window b - 1
