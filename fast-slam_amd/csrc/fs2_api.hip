@@ -2245,18 +2245,8 @@ static int mt_fill(fs2_handle *h, uint32_t *R, int64_t have, int64_t total, hipS
     return FS2_OK;
 }
 
-// FS2_MT_TIMING=1: host time of fs2_mt_draw's phases, printed every 16 draws
-static const bool g_mt_timing = [] {
-    const char *e = std::getenv("FS2_MT_TIMING");
-    return e && e[0] == '1';
-}();
-
 int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
                 fs2_mt_state *after_u0, double *u0_out) {
-    using tclock = std::chrono::steady_clock;
-    const auto t_enter = tclock::now();
-    static double t_acc[5] = {};
-    static int t_n = 0;
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
     if (!in || !after || !after_u0) return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: null state");
     if (in->pos < 0 || in->pos > kMtN || (in->has_gauss != 0 && in->has_gauss != 1))
@@ -2372,13 +2362,10 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         break;
     }
     // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
-    const auto t_meta = tclock::now();
-    auto t_amb = t_meta, t_fix = t_meta;
     const int64_t na = meta.amb_n;
     if (na > 0) {
         HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)na, hipMemcpyDeviceToHost, s));
         HIP_TRY(h, hipStreamSynchronize(s));
-        t_amb = tclock::now();
         HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
         HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
         // entry k patches outputs 2k, 2k + 1 (index -1: not this rank's); split over
@@ -2405,7 +2392,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
             }
         };
         host_pool_run(na, 2048, fix);
-        t_fix = tclock::now();
         if (has_cached) meta.gauss = cached;
         const int64_t np = 2 * na;
         if (np > 0) {
@@ -2473,19 +2459,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     HIP_TRY(h, hipMemcpyAsync(h->u0_dev, h->u0_pin, 8, hipMemcpyHostToDevice, s));
     if (u0_out) *u0_out = u0;
     mt.armed = true;
-    if (g_mt_timing) {
-        const auto t_end = tclock::now();
-        auto us = [](tclock::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
-        t_acc[0] += us(t_meta - t_enter);
-        t_acc[1] += us(t_amb - t_meta);
-        t_acc[2] += us(t_fix - t_amb);
-        t_acc[3] += us(t_end - t_fix);
-        t_acc[4] += (double)na;
-        if (++t_n % 16 == 0) {
-            std::fprintf(stderr, "fs2_mt_draw host us/draw: kernels+meta %.1f  listed-log copy %.1f  recompute %.1f  rest %.1f  (listed %.0f)\n",
-                         t_acc[0] / t_n, t_acc[1] / t_n, t_acc[2] / t_n, t_acc[3] / t_n, t_acc[4] / t_n);
-        }
-    }
     return FS2_OK;
 }
 

@@ -1,5 +1,6 @@
 """Drop-in iterate() at BASELINE config 3 with numpy's stream drawn on the device:
-per-scan wall time, and (FS2_MT_TIMING=1) the host phases of fs2_mt_draw."""
+per-scan wall time.  (profiles/r03_dropin_probe.txt also holds the host phases of
+fs2_mt_draw from a build with FS2_MT_TIMING instrumentation, since removed.)"""
 import os
 import sys
 import time
@@ -9,7 +10,6 @@ import numpy as np
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "fast-slam_amd"))
-os.environ.setdefault("FS2_MT_TIMING", "1")
 import torch  # noqa: F401,E402
 import bench  # noqa: E402
 import fast_slam_2  # noqa: E402
