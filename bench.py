@@ -334,7 +334,7 @@ def robustness(args, f, L, first_scan):
     return out
 
 
-def dropin(args, L, n, scans=8, warm=2, rng="numpy"):
+def dropin(args, L, n, scans=16, warm=4, rng="numpy"):
     """What a reference caller gets: FastSLAM2.iterate(rotation, translation,
     list[Measurement]) (fast_slam_2.py:33, called at jde_robots_main.py:38) with
     numpy's global legacy RNG -- N normals per scan and the resample start,
