@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <sched.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -2140,6 +2141,7 @@ struct HostPool {
     uint64_t gen = 0;
     int left = 0;
     bool stop = false;
+    pid_t owner = getpid();                    // a forked child has none of the threads
     HostPool() {
         cpu_set_t cs;
         int ncpu = 4;
@@ -2204,6 +2206,10 @@ static void host_pool_run(int64_t count, int64_t chunk, const std::function<void
         return;
     }
     static HostPool pool;
+    if (pool.owner != getpid() || pool.th.empty()) {
+        f(0, count);
+        return;
+    }
     pool.run(count, chunk, f);
 }
 
