@@ -2255,6 +2255,8 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
                 fs2_mt_state *after_u0, double *u0_out) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
     if (!in || !after || !after_u0) return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: null state");
+    if (!(sigma >= 0.0))   // numpy: ValueError for a negative (or NaN) scale
+        return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: scale < 0");
     if (in->pos < 0 || in->pos > kMtN || (in->has_gauss != 0 && in->has_gauss != 1))
         return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: bad state (pos %d, has_gauss %d)", in->pos, in->has_gauss);
     if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
