@@ -98,3 +98,16 @@ def test_iterate_device_draws_equal_host_draws(fs):
         assert oa[0] == ob[0] and oa[1] == ob[1] and oa[2] == ob[2], s
         for u, v in zip(oa[3], ob[3]):
             assert np.array_equal(u, v), s
+
+
+def test_mt_draw_rejects_negative_scale(fs):
+    """numpy's normal raises ValueError for scale < 0; so does the device draw."""
+    from fast_slam_2 import _native as nat
+    lib = nat.load()
+    f = fs.FastSLAM2(64, rng="numpy", verbose=False, landmark_capacity=8)
+    mi = nat.fs2_mt_state.from_numpy(np.random.get_state())
+    ma, mu = nat.fs2_mt_state(), nat.fs2_mt_state()
+    for bad in (-1e-3, float("nan")):
+        with pytest.raises(ValueError):
+            nat.check(lib.fs2_mt_draw(f._h, C.byref(mi), bad, C.byref(ma), C.byref(mu), None), f._h)
+    f.close()
