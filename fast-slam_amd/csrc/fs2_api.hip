@@ -179,15 +179,6 @@ struct fs2_handle {
         int64_t *pidx = nullptr, *pidx_pin = nullptr;
         double *pval = nullptr, *pval_pin = nullptr;
         int64_t patch_cap = 0, pval_cap = 0;
-        // the listed logs' recomputation, deferred to the scan (only k_update reads
-        // the noise, so it runs on the host while k_candidates runs)
-        struct Fix {
-            bool pending = false;
-            int64_t na = 0, N = 0, first = 0, n = 0;
-            int h0 = 0;
-            double sigma = 0.0;
-        } fix;
-        hipEvent_t ev_amb = nullptr;
         double *tab = nullptr;             // [2][97] log table (device)
         // jump-ahead: G regions of J words made in parallel (J, G fixed per handle)
         int64_t jJ = 0;
@@ -870,7 +861,6 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->mt.raw[0]); hipFree(h->mt.raw[1]); hipFree(h->mt.boff);
     if (h->mt.ev_words) hipEventDestroy(h->mt.ev_words);
     if (h->mt.ev_pre) hipEventDestroy(h->mt.ev_pre);
-    if (h->mt.ev_amb) hipEventDestroy(h->mt.ev_amb);
     if (h->mt.side) hipStreamDestroy(h->mt.side); hipFree(h->mt.meta); hipFree(h->mt.amb); hipFree(h->mt.pidx);
     hipFree(h->mt.pval); hipFree(h->mt.tab); hipFree(h->mt.jpoly); hipFree(h->mt.jwin);
     if (h->mt.meta_pin) hipHostFree(h->mt.meta_pin);
@@ -1212,8 +1202,6 @@ static int wait_flag(fs2_handle *h, unsigned long long seq) {
     return FS2_OK;
 }
 
-static int mt_apply_fix(fs2_handle *h, bool drop);   // (fs2_mt_draw's deferred log recomputation)
-
 int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
                        const double *observed, int32_t M, const double *noise, const double *u0) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
@@ -1331,11 +1319,6 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         if (prof && first && up.blk1 <= up.blk0)
             for (int k : {0, 1, 4}) HIP_TRY(h, hipEventRecord(E[k], s));
         HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
-        if (first && drawn) {
-            // the draw's listed logs, recomputed while k_candidates runs
-            const int rcf = mt_apply_fix(h, false);
-            if (rcf) return rcf;
-        }
         HIP_TRY(h, launch_update(up, s, (prof && first) ? (cand ? E[4] : E[0]) : nullptr,
                                  (prof && last) ? E[2] : nullptr));
         if (prof && last && up.blk1 <= up.blk0) HIP_TRY(h, hipEventRecord(E[2], s));
@@ -2268,45 +2251,6 @@ static int mt_fill(fs2_handle *h, uint32_t *R, int64_t have, int64_t total, hipS
     return FS2_OK;
 }
 
-// The deferred recomputation of a draw's listed logs: libm's log for each, the
-// two outputs it feeds patched into the noise (on the handle's stream, before
-// k_update).  drop: only wait for the list's copy (a new draw replaces the noise).
-static int mt_apply_fix(fs2_handle *h, bool drop) {
-    auto &mt = h->mt;
-    if (!mt.fix.pending) return FS2_OK;
-    mt.fix.pending = false;
-    HIP_TRY(h, hipEventSynchronize(mt.ev_amb));
-    if (drop) return FS2_OK;
-    const int64_t na = mt.fix.na, N = mt.fix.N, first = mt.fix.first, nl = mt.fix.n;
-    const int h0 = mt.fix.h0;
-    const double sigma = mt.fix.sigma;
-    HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
-    HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
-    // entry k patches outputs 2k, 2k + 1 (index -1: not this rank's); split over
-    // the host pool's threads when there are many
-    auto fix = [&](int64_t k0, int64_t k1) {
-        for (int64_t k = k0; k < k1; ++k) {
-            const MtAmb &e = mt.amb_pin[k];
-            const double f = mt_polar_f(e.r2, std::log(e.r2));
-            const double g0 = f * e.x2, g1 = f * e.x1;
-            const int64_t o = h0 + 2 * e.rank;
-            const bool in0 = o >= first && o < first + nl;
-            mt.pidx_pin[2 * k] = in0 ? o - first : -1;
-            mt.pval_pin[2 * k] = 0.0 + sigma * g0;
-            const bool in1 = o + 1 < N && o + 1 >= first && o + 1 < first + nl;
-            mt.pidx_pin[2 * k + 1] = in1 ? o + 1 - first : -1;
-            mt.pval_pin[2 * k + 1] = 0.0 + sigma * g1;
-        }
-    };
-    host_pool_run(na, 2048, fix);
-    const int64_t np = 2 * na;
-    hipStream_t s = h->stream;
-    HIP_TRY(h, hipMemcpyAsync(mt.pidx, mt.pidx_pin, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
-    HIP_TRY(h, hipMemcpyAsync(mt.pval, mt.pval_pin, sizeof(double) * np, hipMemcpyHostToDevice, s));
-    HIP_TRY(h, launch_mt_patch(h->noise_dev, mt.pidx, mt.pval, np, s));
-    return FS2_OK;
-}
-
 int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
                 fs2_mt_state *after_u0, double *u0_out) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
@@ -2319,10 +2263,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     hipStream_t s = h->stream;
     auto &mt = h->mt;
-    {
-        const int rcd = mt_apply_fix(h, true);     // an earlier draw's list, never used
-        if (rcd) return rcd;
-    }
     const int64_t N = h->n_global;
     const int h0 = (N > 0 && in->has_gauss) ? 1 : 0;
     const int64_t P = (N > h0) ? (N - h0 + 1) / 2 : 0;     // accepted attempts (pairs) needed
@@ -2359,7 +2299,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         HIP_TRY(h, hipStreamCreateWithFlags(&mt.side, hipStreamNonBlocking));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_words, hipEventDisableTiming));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_pre, hipEventDisableTiming));
-        HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_amb, hipEventDisableTiming));
     }
     // the words made ahead serve this draw if it starts where the last one said
     // numpy would be (after its normals, or after its u0 too)
@@ -2430,23 +2369,45 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         }
         break;
     }
-    // the listed logs: libm's log on the host (what numpy's legacy_gauss calls),
-    // copied now and recomputed by the scan (mt_apply_fix) -- except the cached
-    // gauss of the last pair, which the returned state needs
+    // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
     const int64_t na = meta.amb_n;
     if (na > 0) {
         HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)na, hipMemcpyDeviceToHost, s));
-        HIP_TRY(h, hipEventRecord(mt.ev_amb, s));
-        mt.fix.pending = true;
-        mt.fix.na = na;
-        mt.fix.N = N;
-        mt.fix.first = h->first;
-        mt.fix.n = h->n;
-        mt.fix.h0 = h0;
-        mt.fix.sigma = sigma;
+        HIP_TRY(h, hipStreamSynchronize(s));
+        HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
+        HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
+        // entry k patches outputs 2k, 2k + 1 (index -1: not this rank's); split over
+        // the host pool's threads when there are many
+        const int64_t first = h->first, nl = h->n;
+        double cached = 0.0;
+        bool has_cached = false;
+        auto fix = [&](int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) {
+                const MtAmb &e = mt.amb_pin[k];
+                const double f = mt_polar_f(e.r2, std::log(e.r2));
+                const double g0 = f * e.x2, g1 = f * e.x1;
+                const int64_t o = h0 + 2 * e.rank;
+                const bool in0 = o >= first && o < first + nl;
+                mt.pidx_pin[2 * k] = in0 ? o - first : -1;
+                mt.pval_pin[2 * k] = 0.0 + sigma * g0;
+                const bool in1 = o + 1 < N && o + 1 >= first && o + 1 < first + nl;
+                mt.pidx_pin[2 * k + 1] = in1 ? o + 1 - first : -1;
+                mt.pval_pin[2 * k + 1] = 0.0 + sigma * g1;
+                if (o + 1 >= N) {              // the pair whose second value stays cached (one at most)
+                    cached = g1;
+                    has_cached = true;
+                }
+            }
+        };
+        host_pool_run(na, 2048, fix);
+        if (has_cached) meta.gauss = cached;
+        const int64_t np = 2 * na;
+        if (np > 0) {
+            HIP_TRY(h, hipMemcpyAsync(mt.pidx, mt.pidx_pin, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+            HIP_TRY(h, hipMemcpyAsync(mt.pval, mt.pval_pin, sizeof(double) * np, hipMemcpyHostToDevice, s));
+            HIP_TRY(h, launch_mt_patch(h->noise_dev, mt.pidx, mt.pval, np, s));
+        }
     }
-    if (meta.has_gauss && meta.last_amb)
-        meta.gauss = mt_polar_f(meta.last_r2, std::log(meta.last_r2)) * meta.last_x1;
     // the state after the normals, then after the speculative u0 (two more words;
     // k_mt_final left both in meta)
     std::memcpy(after->key, meta.key_after, sizeof after->key);
@@ -2518,10 +2479,6 @@ int fs2_debug_mt_jump(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
 int fs2_debug_noise(fs2_handle *h, double *out) {
     if (!h || !out) return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_debug_noise: null argument");
     HIP_TRY(h, hipSetDevice(h->cfg.device));
-    {
-        const int rcf = mt_apply_fix(h, false);   // a draw's deferred patches first
-        if (rcf) return rcf;
-    }
     HIP_TRY(h, hipMemcpyAsync(h->noise_pin, h->noise_dev, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     std::memcpy(out, h->noise_pin, sizeof(double) * h->n);

@@ -555,10 +555,6 @@ struct MtMeta {
     int32_t pos_after, pos_after_u0;
     uint32_t w_u0[2];        // raw words E, E + 1 (u0)
     uint32_t key_after[624], key_after_u0[624];
-    // the last accepted attempt, when its log is listed (the cached gauss the
-    // host recomputes at once; the other listed logs wait for fs2_iterate)
-    double last_r2, last_x1;
-    int32_t last_amb, pad;
 };
 struct MtAmb {
     double r2, x1, x2;

@@ -204,9 +204,6 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
         p.meta->last_attempt = a;
         p.meta->has_gauss = (o + 1 < p.N) ? 0 : 1;
         p.meta->gauss = (o + 1 < p.N) ? 0.0 : g1;
-        p.meta->last_r2 = t.r2;
-        p.meta->last_x1 = t.x1;
-        p.meta->last_amb = amb ? 1 : 0;
     }
 }
 
