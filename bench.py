@@ -222,6 +222,12 @@ def cpu_baseline(L, P, budget_s, seed):
         affinity = len(os.sched_getaffinity(0))
     except Exception:
         affinity = None
+    quota = None                  # the cgroup's CPU quota (cpu.max), in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except Exception:
+        pass
     model = "unknown"
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
@@ -232,8 +238,14 @@ def cpu_baseline(L, P, budget_s, seed):
     many, sm, tm = run(n, threads, budget_s / 2)
     orc.set_threads(threads)
     return dict(value=many, unit="particle-updates/s", cores=threads, kind="port",
-                cpu_model=model, host_cpus=os.cpu_count(), affinity_cpus=affinity,
+                cpu_model=model, host_cpus=os.cpu_count(), affinity_cpus=affinity, cgroup_cpu_quota=quota,
                 single_thread_value=one,
+                affinity_linear_projection=(one * affinity if affinity else None),
+                threads_note=("threads = OMP_NUM_THREADS, the CPU share a one-GPU job gets on the GPU pool "
+                              "(its rules fix worker pools at that share although the affinity mask lists "
+                              "every host CPU); affinity_linear_projection = single_thread_value x "
+                              "affinity_cpus, a projection to every CPU of the host, not a measurement"),
+                python_reference_config1=python_reference_record(),
                 sample=f"{n} particles x {L} landmarks, M=4, {sm} scans on {threads} OpenMP threads "
                        f"(OMP_NUM_THREADS; {affinity} CPUs in this process's affinity mask of "
                        f"{os.cpu_count()} on the host) ({tm:.1f} s); 1 thread: 6000 particles, {s1} scans "
@@ -241,6 +253,18 @@ def cpu_baseline(L, P, budget_s, seed):
                        f"C oracle, reference semantics and reference algorithm (first-match linear "
                        f"scan of every map, deep-copied maps on resample): the ratio to the GPU "
                        f"value mixes algorithm (pruning, page sharing) with hardware")
+
+
+def python_reference_record():
+    """The Python reference itself timed at config 1 in the build container
+    (scripts/time_reference_cfg1.py; /root/reference is not on the GPU box)."""
+    p = os.path.join(REPO, "profiles", "r04_reference_cfg1_container.json")
+    try:
+        rec = json.load(open(p))
+    except Exception:
+        return None
+    return {k: rec.get(k) for k in ("host", "reference_ms_per_scan_median", "reference_particle_updates_per_s",
+                                    "oracle_c_particle_updates_per_s")}
 
 
 def pmc_record(workload):
@@ -470,13 +494,138 @@ def main(argv=None):
     cfg = dict(CONFIGS[args.config])
     n_per_gpu = args.particles or cfg["N"]
     L = args.landmarks or cfg["L"]
-    N = n_per_gpu * world
     comm_id = None
     if world > 1:
         obj = [(nat.comm_unique_id() if args.comm == "rccl" else os.urandom(128)) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
-    total_scans = args.warmup + args.steps
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    R = run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, args.steps, args.warmup)
+    f, dt, prof, st = R["handle"], R["dt"], R["prof"], R["st"]
+    N = n_per_gpu * world
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=tdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    migration = None
+    if world > 1:
+        # the sharded resample's transfers, summed over the ranks
+        keys = ("migrations", "sent_particles", "sent_rows", "sent_pages", "sent_bytes", "migrate_ms", "comm_ms")
+        mt = torch.tensor([float(prof[k]) for k in keys], dtype=torch.float64, device=tdev)
+        dist.all_reduce(mt, op=dist.ReduceOp.SUM)
+        tot = dict(zip(keys, mt.tolist()))
+        resamples = R["sums"]["resamples"]
+        per = max(resamples, 1)
+        rs_ms = sorted(m for m, r in R["step_ms"] if r)
+        ot_ms = sorted(m for m, r in R["step_ms"] if not r)
+        migration = {
+            "resamples": resamples,
+            "particles_sent_per_resample": tot["sent_particles"] / per,
+            "rows_sent_per_resample": tot["sent_rows"] / per,
+            "pages_sent_per_resample": tot["sent_pages"] / per,
+            "bytes_sent_per_resample": tot["sent_bytes"] / per,
+            "page_dedup_ratio": tot["sent_rows"] / tot["sent_pages"] if tot["sent_pages"] else None,
+            "host_ms_per_resample_rank_mean": tot["migrate_ms"] / world / per,
+            "comm_ms_per_scan_rank_mean": tot["comm_ms"] / world / args.steps,
+            "scan_ms_resample_median_rank0": rs_ms[len(rs_ms) // 2] if rs_ms else None,
+            "scan_ms_other_median_rank0": ot_ms[len(ot_ms) // 2] if ot_ms else None,
+            "note": "every resample moves the particles whose outputs land on another rank's shard, "
+                    "each destination's distinct pages once; Q6/Q8 (sum of weights > 1) shift "
+                    "outputs toward lower global indices, so the flow is mostly rank p -> p+1.."}
+
+    if rank == 0:
+        K = kernel_summary(prof, cfg, n_per_gpu, L)
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(L, cfg["P"], args.cpu_seconds, args.seed)
+        scan_ms = dt / args.steps * 1e3
+        units = f.n_local * args.steps
+        sums = R["sums"]
+        # SURVEY §8(d)'s accounting: the reference layout's bytes (48 B per landmark
+        # its first-match scan reads, 48 B per updated / appended landmark, 104 B of
+        # particle scalars) at this run's scan rate -- a work rate, not a bandwidth
+        ref_bytes = 48.0 * sums["ref_visits"] + 48.0 * sums["hits_appends"] + 104.0 * units
+        out = {
+            "metric": "particle-updates/s",
+            "value": N * args.steps / dt,
+            "unit": "particle-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": scan_ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8d: 6 m landmark grid, 3 hits + 1 miss per scan, "
+                    "odometry 4x0.03 m then 0.05 rad; device Philox motion noise)",
+            "config": {"workload": cfg["name"], "particles_per_gpu": n_per_gpu,
+                       "particles_total": N, "landmarks": L, "beams": cfg["P"],
+                       "measurements_per_scan": 4, "icp": cfg["icp"],
+                       "icp_pipelined": bool(cfg["icp"] and not args.serial_icp),
+                       "gate_filter": not args.no_gate_filter, "reduce": "exact" if N > 4096 and world == 1
+                       else ("parallel" if world > 1 else "sequential"),
+                       "parallelism": f"particle-shard{world}",
+                       "transport": args.comm if world > 1 else None,
+                       "ranks_share_gpu": bool(args.share_gpu and world > 1)},
+            "roofline": K["roofline"],
+            "cpu_baseline": cpu,
+            "extra": {"scan_device_ms": prof["scan_ms"] / max(prof["scans"], 1),
+                      "update_pass_ms": K["update_pass_ms"],
+                      "kernels": K["kernels"],
+                      "byte_model": K["byte_model"],
+                      "reference_equivalent": {
+                          "bytes_per_scan": ref_bytes / args.steps,
+                          "work_rate_GBs": ref_bytes / dt / 1e9,
+                          "landmark_reads_per_particle_scan": sums["ref_visits"] / units,
+                          "note": "SURVEY §8d bytes of the reference's layout and linear scan at this "
+                                  "run's scan rate; not a bandwidth (pruning and page sharing skip them)"},
+                      "update_pass_bytes": prof["update_bytes"] / max(prof["update_launches"], 1),
+                      "reduce_and_resample_ms": prof["reduce_ms"] / max(prof["scans"], 1),
+                      "resamples": sums["resamples"],
+                      "resample_shared_slots": sums["copied_slots"],
+                      "cow_pages_per_particle_scan": sums["cow"] / units,
+                      "pool_collections": st.collections,
+                      "pool_collections_timed": st.collections - R["coll0"],
+                      "pool_pages": st.pool_pages,
+                      "pages_opened_per_particle_scan": sums["opened"] / units,
+                      "slots_visited_per_particle_scan": sums["visited"] / units,
+                      "exact_slots_per_particle_scan": sums["exact"] / units,
+                      "icp_us": R["icp_us"],
+                      "icp_host_ms_per_scan": R["icp_host"]},
+        }
+        if migration is not None:
+            out["extra"]["migration"] = migration
+        extras = not args.no_extras and world == 1
+        if extras and not cfg["icp"]:
+            out["extra"]["robustness"] = robustness(args, f, L, args.warmup + args.steps)
+        f.close()
+        if extras and args.config == "3" and not (args.particles or args.landmarks):
+            # the other single-GPU BASELINE configs, each on a fresh handle
+            out["extra"]["configs"] = {k: config_line(args, k, world, rank, dev, barrier) for k in ("2", "4")}
+        print(json.dumps(out), flush=True)
+    else:
+        f.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, steps, warmup):
+    """Create and populate a handle for one workload, run `warmup` untimed and
+    `steps` timed scans (config 4: each scan's odometry from the ICP alignment of
+    the next scan pair, run beside the previous scan's update); returns the
+    handle, the timed wall time and the per-scan sums."""
+    import torch
+    import fast_slam_2
+    import fs2_synthetic as syn
+    N = n_per_gpu * world
+    total_scans = warmup + steps
     f = fast_slam_2.FastSLAM2(N, device=dev, rng="device", seed=args.seed, reduce="auto",
                               landmark_capacity=L + total_scans + 8, rank=rank,
                               world_size=world, comm_id=comm_id, verbose=False,
@@ -506,10 +655,10 @@ def main(argv=None):
     def icp_prepare(s):
         """Odometry of scan s from the alignment of scans s -> s+1 (and its host time)."""
         t0 = time.perf_counter()
-        R, t, _ = fast_slam_2.ICP.submit(scans_pts[s], scans_pts[s + 1]).result()
+        Rm, t, _ = fast_slam_2.ICP.submit(scans_pts[s], scans_pts[s + 1]).result()
         # the commanded linear velocity is nonzero on the driving scans of the pattern
         v = 0.3 if syn.odometry(s)[1] != 0 else 0.0
-        rot, tr = (float(q) for q in fast_slam_2.Robot.icp_odometry(R, t, v))
+        rot, tr = (float(q) for q in fast_slam_2.Robot.icp_odometry(Rm, t, v))
         return rot, tr, (time.perf_counter() - t0) * 1e3
 
     offline_odo = ({s: icp_prepare(s)[:2] for s in range(total_scans)}
@@ -533,83 +682,42 @@ def main(argv=None):
         t1 = time.perf_counter()
         f.step_submit(rot, tr, meas[s])
         nxt = None
-        if s + 1 != args.warmup and s + 1 < total_scans and not args.serial_icp:
+        if s + 1 != warmup and s + 1 < total_scans and not args.serial_icp:
             nxt = icp_prepare(s + 1)
             icp_odo[s + 1] = nxt
         out = f.step_wait()
-        if s >= args.warmup:
+        if s >= warmup:
             icp_host["wait_ms"] += (t1 - t0) * 1e3       # alignment work before this scan could start
             icp_host["prep_ms"] += nxt[2] if nxt is not None else prep
             icp_host["scans"] += 1
         return out
 
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     coll0 = 0
-    for s in range(args.warmup):
+    for s in range(warmup):
         _, st0 = one_scan(s)
         coll0 = st0.collections
     # kernel events on every 4th timed scan: a dispatch's start / end events delay
     # the next dispatch by ~4.5 us, which the other scans do not pay
     f.set_profiling(True, every=PROFILE_EVERY)
-    resamples = 0
-    visited = 0
-    copied_slots = 0
-    cow_pages = 0
-    exact_slots = 0
-    opened = 0
-    ref_visits = 0
-    hits_appends = 0
+    sums = dict(resamples=0, visited=0, copied_slots=0, cow=0, exact=0, opened=0, ref_visits=0, hits_appends=0)
     step_ms = []                 # (host ms, resampled) of each timed scan on this rank
     barrier()
     t0 = time.perf_counter()
-    for s in range(args.warmup, total_scans):
+    for s in range(warmup, total_scans):
         t1 = time.perf_counter()
         _, st = one_scan(s)
         step_ms.append(((time.perf_counter() - t1) * 1e3, st.resampled))
-        resamples += st.resampled
-        visited += st.slots_visited
-        copied_slots += st.resample_slots
-        cow_pages += st.cow_pages
-        exact_slots += st.candidates
-        opened += st.pages_opened
-        ref_visits += st.reference_visits
-        hits_appends += st.hits + st.appends
+        sums["resamples"] += st.resampled
+        sums["visited"] += st.slots_visited
+        sums["copied_slots"] += st.resample_slots
+        sums["cow"] += st.cow_pages
+        sums["exact"] += st.candidates
+        sums["opened"] += st.pages_opened
+        sums["ref_visits"] += st.reference_visits
+        sums["hits_appends"] += st.hits + st.appends
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=tdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
     prof = f.profile()
-    migration = None
-    if world > 1:
-        # the sharded resample's transfers, summed over the ranks
-        keys = ("migrations", "sent_particles", "sent_rows", "sent_pages", "sent_bytes", "migrate_ms", "comm_ms")
-        mt = torch.tensor([float(prof[k]) for k in keys], dtype=torch.float64, device=tdev)
-        dist.all_reduce(mt, op=dist.ReduceOp.SUM)
-        tot = dict(zip(keys, mt.tolist()))
-        per = max(resamples, 1)
-        rs_ms = sorted(m for m, r in step_ms if r)
-        ot_ms = sorted(m for m, r in step_ms if not r)
-        migration = {
-            "resamples": resamples,
-            "particles_sent_per_resample": tot["sent_particles"] / per,
-            "rows_sent_per_resample": tot["sent_rows"] / per,
-            "pages_sent_per_resample": tot["sent_pages"] / per,
-            "bytes_sent_per_resample": tot["sent_bytes"] / per,
-            "page_dedup_ratio": tot["sent_rows"] / tot["sent_pages"] if tot["sent_pages"] else None,
-            "host_ms_per_resample_rank_mean": tot["migrate_ms"] / world / per,
-            "comm_ms_per_scan_rank_mean": tot["comm_ms"] / world / args.steps,
-            "scan_ms_resample_median_rank0": rs_ms[len(rs_ms) // 2] if rs_ms else None,
-            "scan_ms_other_median_rank0": ot_ms[len(ot_ms) // 2] if ot_ms else None,
-            "note": "every resample moves the particles whose outputs land on another rank's shard, "
-                    "each destination's distinct pages once; Q6/Q8 (sum of weights > 1) shift "
-                    "outputs toward lower global indices, so the flow is mostly rank p -> p+1.."}
     icp_us = None
     if scans_pts is not None:
         # one alignment through the synchronous call, warm (its stream and scratch
@@ -619,114 +727,96 @@ def main(argv=None):
         for s in range(5):
             fast_slam_2.ICP.get_transformation(scans_pts[s], scans_pts[s + 1])
         icp_us = (time.perf_counter() - t1) / 5 * 1e6
+    host = ({"before_scan": icp_host["wait_ms"] / max(icp_host["scans"], 1),
+             "hand_off": icp_host["prep_ms"] / max(icp_host["scans"], 1),
+             "note": "hand_off: submission + alignment + odometry of the next scan, done between "
+                     "step_submit and step_wait; before_scan: alignment work ahead of a scan's submission"}
+            if scans_pts is not None else None)
+    return {"handle": f, "dt": dt, "prof": prof, "st": st, "coll0": coll0, "sums": sums, "step_ms": step_ms,
+            "icp_us": icp_us, "icp_host": host}
 
-    if rank == 0:
-        launches = max(prof["update_launches"], 1)
-        upd_ms = prof["update_ms"] / launches
-        # per-kernel split of the update pass: start / end events of each dispatch
-        # (hipExtLaunchKernel on the library's stream, libfs2 fold_profile)
-        kern = {}
-        if prof["filter_launches"] > 0:
-            fl = prof["filter_launches"]
-            kern["k_candidates"] = (prof["filter_ms"] / fl, prof["filter_bytes"] / fl)
-            kern["k_update"] = (prof["exact_ms"] / max(prof["exact_launches"], 1),
-                                (prof["update_bytes"] - prof["filter_bytes"]) / fl)
-        else:
-            kern["k_update"] = (upd_ms, prof["update_bytes"] / launches)
-        # the roofline line is for the dominant (longest) kernel: HBM bytes per launch
-        # from the PMC passes on this build (profiles/pmc_<workload>.json), over the
-        # launch's live duration (HIP events on the library's stream, this run)
-        kernel = max(kern, key=lambda k: kern[k][0])
-        ms_launch, alg_bytes = kern[kernel]
-        pmc = pmc_record(cfg["name"]) if n_per_gpu == cfg["N"] and L == cfg["L"] else None
-        traffic = pmc_traffic(pmc, kernel)
-        alg_GBs = alg_bytes / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
-        if traffic is not None and ms_launch > 0:
-            achieved, basis = traffic / (ms_launch * 1e-3) / 1e9, "pmc_hbm_bytes"
-        else:
-            achieved, basis = alg_GBs, "algorithmic_bytes (no PMC record for this build)"
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(L, cfg["P"], args.cpu_seconds, args.seed)
-        scan_ms = dt / args.steps * 1e3
-        units = f.n_local * args.steps
-        # SURVEY §8(d)'s accounting: the reference layout's bytes (48 B per landmark
-        # its first-match scan reads, 48 B per updated / appended landmark, 104 B of
-        # particle scalars) at this run's scan rate -- a work rate, not a bandwidth
-        ref_bytes = 48.0 * ref_visits + 48.0 * hits_appends + 104.0 * units
-        out = {
-            "metric": "particle-updates/s",
-            "value": N * args.steps / dt,
-            "unit": "particle-updates/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": scan_ms,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (SURVEY.md §8d: 6 m landmark grid, 3 hits + 1 miss per scan, "
-                    "odometry 4x0.03 m then 0.05 rad; device Philox motion noise)",
-            "config": {"workload": cfg["name"], "particles_per_gpu": n_per_gpu,
-                       "particles_total": N, "landmarks": L, "beams": cfg["P"],
-                       "measurements_per_scan": 4, "icp": cfg["icp"],
-                       "icp_pipelined": bool(cfg["icp"] and not args.serial_icp),
-                       "gate_filter": not args.no_gate_filter, "reduce": "exact" if N > 4096 and world == 1
-                       else ("parallel" if world > 1 else "sequential"),
-                       "parallelism": f"particle-shard{world}",
-                       "transport": args.comm if world > 1 else None,
-                       "ranks_share_gpu": bool(args.share_gpu and world > 1)},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "basis": basis,
-                         "kernel": kernel, "ms_per_launch": ms_launch,
-                         "pmc_source": None if pmc is None else pmc.get("source"),
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "algorithmic_GBs": alg_GBs},
-            "cpu_baseline": cpu,
-            "extra": {"scan_device_ms": prof["scan_ms"] / max(prof["scans"], 1),
-                      "update_pass_ms": upd_ms,
-                      "kernels": {k: {"ms_per_launch": v[0], "algorithmic_bytes_per_launch": v[1],
-                                      "algorithmic_GBs": v[1] / (v[0] * 1e-3) / 1e9 if v[0] > 0 else 0.0,
-                                      "hbm_bytes_per_launch": pmc_traffic(pmc, k),
-                                      "hbm_GBs": (pmc_traffic(pmc, k) / (v[0] * 1e-3) / 1e9
-                                                  if pmc_traffic(pmc, k) and v[0] > 0 else None)}
-                                  for k, v in kern.items()},
-                      "reference_equivalent": {
-                          "bytes_per_scan": ref_bytes / args.steps,
-                          "work_rate_GBs": ref_bytes / dt / 1e9,
-                          "landmark_reads_per_particle_scan": ref_visits / units,
-                          "note": "SURVEY §8d bytes of the reference's layout and linear scan at this "
-                                  "run's scan rate; not a bandwidth (pruning and page sharing skip them)"},
-                      "update_pass_bytes": prof["update_bytes"] / launches,
-                      "reduce_and_resample_ms": prof["reduce_ms"] / max(prof["scans"], 1),
-                      "resamples": resamples,
-                      "resample_shared_slots": copied_slots,
-                      "cow_pages_per_particle_scan": cow_pages / units,
-                      "pool_collections": st.collections,
-                      "pool_collections_timed": st.collections - coll0,
-                      "pool_pages": st.pool_pages,
-                      "pages_opened_per_particle_scan": opened / units,
-                      "slots_visited_per_particle_scan": visited / units,
-                      "exact_slots_per_particle_scan": exact_slots / units,
-                      "icp_us": icp_us,
-                      "icp_host_ms_per_scan": ({"before_scan": icp_host["wait_ms"] / max(icp_host["scans"], 1),
-                                                "hand_off": icp_host["prep_ms"] / max(icp_host["scans"], 1),
-                                                "note": "hand_off: submission + alignment + odometry of the next "
-                                                        "scan, done between step_submit and step_wait; before_scan: "
-                                                        "alignment work ahead of a scan's submission"}
-                                               if scans_pts is not None else None)},
-        }
-        if migration is not None:
-            out["extra"]["migration"] = migration
-        if not args.no_extras and world == 1 and not cfg["icp"]:
-            out["extra"]["robustness"] = robustness(args, f, L, total_scans)
-        print(json.dumps(out), flush=True)
-    f.close()
-    if world > 1:
-        dist.destroy_process_group()
 
+# Algorithmic byte model of the two update kernels (include/fs2.h
+# fs2_profile): bytes per unit the counters count
+BYTE_MODEL = {
+    "k_candidates": {"descriptor_streamed": 8, "page_opened": 128, "list_entry": 8,
+                     "particle_pass (cnt read, count write)": 8, "row_box_read": 4},
+    "k_update": {"fixed (scalars, free-list ids, counts; per particle, summed)": 1, "list_entry": 8,
+                 "candidate_record": 48, "slot_written (record 48, mirror 16, descriptor r+w 16)": 80,
+                 "page_copied (128 read + 128 write)": 256, "row_box_read_and_written": 8},
+}
+
+
+def kernel_summary(prof, cfg, n_per_gpu, L):
+    """Per-kernel times (HIP events of the dispatches), the algorithmic byte model
+    evaluated from the profile's counters, the PMC HBM bytes of this build when a
+    record exists, and the roofline line of the dominant kernel on both bases."""
+    launches = max(prof["update_launches"], 1)
+    upd_ms = prof["update_ms"] / launches
+    kern = {}
+    fl = prof["filter_launches"]
+    if fl > 0:
+        kern["k_candidates"] = (prof["filter_ms"] / fl, prof["filter_bytes"] / fl)
+        kern["k_update"] = (prof["exact_ms"] / max(prof["exact_launches"], 1),
+                            (prof["update_bytes"] - prof["filter_bytes"]) / fl)
+    else:
+        kern["k_update"] = (upd_ms, prof["update_bytes"] / launches)
+    pmc = pmc_record(cfg["name"]) if n_per_gpu == cfg["N"] and L == cfg["L"] else None
+    model = None
+    if fl > 0:
+        c = {k: prof[f"model_{k}"] / fl for k in ("groups", "opened", "words", "candidates", "written", "cow",
+                                                  "fixed_bytes", "box_bytes")}
+        model = {"units": BYTE_MODEL, "counts_per_launch": c,
+                 "k_candidates_bytes": kern["k_candidates"][1], "k_update_bytes": kern["k_update"][1],
+                 "note": "k_candidates = 8 groups + 128 opened + 8 words + 8 n + 4/12 box_bytes; "
+                         "k_update = fixed_bytes + 8 words + 48 candidates + 80 written + 256 cow + 8/12 box_bytes; "
+                         "reuse = model bytes / PMC HBM bytes (> 1: L2 / MALL hits, e.g. siblings' shared pages)"}
+        for k in ("k_candidates", "k_update"):
+            t = pmc_traffic(pmc, k)
+            model[f"{k}_reuse_vs_pmc"] = (kern[k][1] / t) if t else None
+    kernels = {}
+    for k, v in kern.items():
+        t = pmc_traffic(pmc, k)
+        kernels[k] = {"ms_per_launch": v[0], "algorithmic_bytes_per_launch": v[1],
+                      "algorithmic_GBs": v[1] / (v[0] * 1e-3) / 1e9 if v[0] > 0 else 0.0,
+                      "hbm_bytes_per_launch": t,
+                      "hbm_GBs": (t / (v[0] * 1e-3) / 1e9 if t and v[0] > 0 else None)}
+    # the roofline line is for the dominant (longest) kernel: HBM bytes per launch
+    # from the PMC passes on this build (profiles/pmc_<workload>.json), over the
+    # launch's live duration (HIP events on the library's stream, this run)
+    kernel = max(kern, key=lambda k: kern[k][0])
+    ms_launch, alg_bytes = kern[kernel]
+    traffic = pmc_traffic(pmc, kernel)
+    alg_GBs = alg_bytes / (ms_launch * 1e-3) / 1e9 if ms_launch > 0 else 0.0
+    if traffic is not None and ms_launch > 0:
+        achieved, basis = traffic / (ms_launch * 1e-3) / 1e9, "pmc_hbm_bytes"
+    else:
+        achieved, basis = alg_GBs, "algorithmic_bytes (no PMC record for this build)"
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "basis": basis,
+            "kernel": kernel, "ms_per_launch": ms_launch,
+            "pmc_source": None if pmc is None else pmc.get("source"),
+            "algorithmic_bytes_per_launch": alg_bytes, "algorithmic_GBs": alg_GBs,
+            "frac_algorithmic": alg_GBs / HBM_PEAK_GBS}
+    return {"roofline": roof, "kernels": kernels, "byte_model": model, "update_pass_ms": upd_ms}
+
+
+def config_line(args, key, world, rank, dev, barrier, steps=20, warmup=3):
+    """BASELINE config `key` (2: 1e5 x 200; 4: 1e6 x 500 with the 720-beam ICP
+    beside each update) on a fresh handle: ms per scan, value, the dominant
+    kernel's event time and roofline (PMC basis when this build has a record)."""
+    cfg = dict(CONFIGS[key])
+    R = run_config(args, cfg, cfg["N"], cfg["L"], 1, 0, dev, None, barrier, steps, warmup)
+    R["handle"].close()
+    K = kernel_summary(R["prof"], cfg, cfg["N"], cfg["L"])
+    sums = R["sums"]
+    units = cfg["N"] * steps
+    return {"workload": cfg["name"], "value": cfg["N"] * steps / R["dt"], "ms_per_scan": R["dt"] / steps * 1e3,
+            "steps": steps, "warmup": warmup, "roofline": K["roofline"], "kernels": K["kernels"],
+            "reduce_and_resample_ms": R["prof"]["reduce_ms"] / max(R["prof"]["scans"], 1),
+            "resamples": sums["resamples"], "pages_opened_per_particle_scan": sums["opened"] / units,
+            "cow_pages_per_particle_scan": sums["cow"] / units, "icp_us": R["icp_us"],
+            "icp_host_ms_per_scan": R["icp_host"]}
 
 if __name__ == "__main__":
     main()

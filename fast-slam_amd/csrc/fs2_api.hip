@@ -508,7 +508,12 @@ static int post_and_wait(fs2_handle *h, bool sizes) {
     const unsigned long long seq = ++h->post_seq;
     HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? kXrowWords * G * G : 0, h->post, h->post_flag_dev,
                            seq, h->stream));
-    return wait_seq(h, h->post_flag, seq, "mid-scan statistics");
+    const int rc = wait_seq(h, h->post_flag, seq, "mid-scan statistics");
+    if (rc) return rc;
+    // k_post runs after the collectives queued before it, so a stream-ordered
+    // transport's status is final here: a failed exchange leaves stale staging
+    // bytes in the post, which must not size the resample
+    return h->tp ? h->tp->status(&h->err) : FS2_OK;
 }
 static const DevStats &posted_stats(const fs2_handle *h) { return *reinterpret_cast<const DevStats *>(h->post_host); }
 static const int64_t *posted_xmat(const fs2_handle *h) {
@@ -916,20 +921,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         return code;
     };
     if (hipSetDevice(cfg->device) != hipSuccess) return fail(set_err(&h->err, FS2_ERR_HIP, "hipSetDevice failed"));
-    // A/B knob (config 4 interference): FS2_MAIN_EXCLUDE_CU=k keeps
-    // the filter's kernels off compute unit k
-    if (const char *e = std::getenv("FS2_MAIN_EXCLUDE_CU")) {
-        hipDeviceProp_t pr{};
-        const int words = hipGetDeviceProperties(&pr, cfg->device) == hipSuccess ? (pr.multiProcessorCount + 31) / 32 : 8;
-        std::vector<uint32_t> mask(words, 0xffffffffu);
-        if (pr.multiProcessorCount % 32) mask[words - 1] = (1u << (pr.multiProcessorCount % 32)) - 1u;
-        const int k = std::atoi(e);
-        if (k >= 0 && k / 32 < words) mask[k / 32] &= ~(1u << (k % 32));
-        if (hipExtStreamCreateWithCUMask(&h->stream, (uint32_t)words, mask.data()) != hipSuccess)
-            return fail(set_err(&h->err, FS2_ERR_HIP, "hipExtStreamCreateWithCUMask failed"));
-    } else if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
-    }
     const int64_t n = std::max<int64_t>(h->n, 1);
     const int64_t nb = (n + kBlock - 1) / kBlock;
     const int64_t nsb = (n + 1023) / 1024;
@@ -1152,7 +1145,17 @@ static int fold_one(fs2_handle *h, int set) {
     HIP_TRY(h, hipEventElapsedTime(&a, E[0], E[2]));     // update pass(es)
     HIP_TRY(h, hipEventElapsedTime(&r, E[5], E[3]));     // reduce, resample, publication
     HIP_TRY(h, hipEventElapsedTime(&t, E[0], E[3]));     // the scan on the device
-    if (h->cfg.gate_filter && p.m <= kMaxM) {
+    // the algorithmic byte model (include/fs2.h fs2_profile)
+    const uint64_t n = (uint64_t)h->n, nblk = (uint64_t)h->nblocks();
+    const uint64_t box_rows = h->row_boxes(h->cur) ? (uint64_t)h->rows : 0ull;
+    const bool filt = h->cfg.gate_filter != 0;
+    const uint64_t cand_bytes = filt ? 8ull * st.groups + 128ull * st.opened + 8ull * st.words +
+                                           8ull * n * p.passes + 4ull * box_rows * nblk
+                                     : 0ull;
+    const uint64_t upd_fixed = p.fixed_bytes + (filt ? 4ull * n * p.passes : 0ull) + 8ull * n * (uint64_t)p.m;
+    const uint64_t exact_bytes = upd_fixed + (filt ? 8ull * st.words : 0ull) + 48ull * st.candidates +
+                                 80ull * st.written + 2ull * kPageBytes * st.cow_pages + 8ull * box_rows * nblk;
+    if (filt && p.m <= kMaxM) {
         // k_candidates and, one pass, k_update alone
         HIP_TRY(h, hipEventElapsedTime(&f, E[0], E[1]));
         HIP_TRY(h, hipEventElapsedTime(&x, E[4], E[2]));
@@ -1160,25 +1163,22 @@ static int fold_one(fs2_handle *h, int set) {
         h->prof.exact_ms += x;
         h->prof.filter_launches += 1;
         h->prof.filter_ms += f;
-        // one 8 B descriptor per page, the mirrors of the pages it could not
-        // reject, cnt read + count written (8 B per particle), list entries
-        h->prof.filter_bytes += 16ull * st.visited + sizeof(Desc) * st.groups + 8ull * (uint64_t)h->n +
-                                8ull * st.words;
+        h->prof.filter_bytes += cand_bytes;
+        h->prof.model_groups += st.groups;
+        h->prof.model_opened += st.opened;
+        h->prof.model_words += st.words;
+        h->prof.model_candidates += st.candidates;
+        h->prof.model_written += st.written;
+        h->prof.model_cow += st.cow_pages;
+        h->prof.model_fixed_bytes += upd_fixed;
+        h->prof.model_box_bytes += 12ull * box_rows * nblk;
     }
     h->prof.scans += 1;
     h->prof.update_launches += p.passes;
     h->prof.update_ms += a;
     h->prof.reduce_ms += r;
     h->prof.scan_ms += t;
-    // mirror reads (16 B) per visited slot when filtering, record reads (48 B) per
-    // candidate, slot writes (48 B record + 16 B mirror) and the descriptor of the
-    // written row (read + write), candidate list entries written and read back
-    // (8 B each) and their counts, a descriptor per page group, page copies
-    h->prof.update_bytes += (h->cfg.gate_filter ? 16ull * st.visited + sizeof(Desc) * st.groups +
-                                                      16ull * st.words + 8ull * (uint64_t)h->n * p.passes
-                                                : 0ull) +
-                            48ull * st.candidates + (64ull + 2ull * sizeof(Desc)) * st.written + p.fixed_bytes +
-                            2ull * kPageBytes * st.cow_pages + 8ull * (uint64_t)h->nblocks();
+    h->prof.update_bytes += cand_bytes + exact_bytes;
     if (st.resampled)
         // page-table rows (read + write per page of every output) + scalar gather +
         // plan arrays
@@ -1207,6 +1207,12 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
     if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan has not been waited for");
     if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
+    // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise /
+    // u0; a draw is consumed by this call whatever happens below
+    const bool drawn = h->mt.armed;
+    h->mt.armed = false;
+    if (drawn && (noise || u0))
+        return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     int rc = grow_rows(h, h->cnt_upper + M);
     if (rc) return rc;
@@ -1222,11 +1228,6 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     const double flip_margin = (red == FS2_REDUCE_PARALLEL) ? std::ldexp(2.0 * (double)h->n_global + 64.0, -53) : 0.0;
     const bool prof = h->profiling && (h->prof_tick++ % (uint64_t)h->prof_period) == 0;
 
-    // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise / u0
-    const bool drawn = h->mt.armed;
-    if (drawn && (noise || u0))
-        return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
-    h->mt.armed = false;
     if (noise) {
         std::memcpy(h->noise_pin, noise, sizeof(double) * h->n);
         HIP_TRY(h, hipMemcpyAsync(h->noise_dev, h->noise_pin, sizeof(double) * h->n,
@@ -1354,12 +1355,8 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rp.part_w = exact ? h->part_w : nullptr;
     rp.np_leaf = exact ? h->np_leaf : nullptr;
     // exact mode on one GPU: normalise and numpy's chunk trees in one pass
-    // (k_normalize_chunks); FS2_TAIL=split keeps k_normalize + k_finalize's trees (A/B)
-    static const bool split_tail = [] {
-        const char *e = std::getenv("FS2_TAIL");
-        return e && std::strcmp(e, "split") == 0;
-    }();
-    rp.chunked = (exact && !sh && !split_tail) ? 1 : 0;
+    // (k_normalize_chunks)
+    rp.chunked = (exact && !sh) ? 1 : 0;
     if (rp.chunked) rp.nparts = normalize_chunk_parts(h->n);
     rp.part_pose = h->part_pose;
     rp.np_tail = exact ? h->np_tail : nullptr;
@@ -1631,6 +1628,7 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
                        (long long)first, (long long)(first + count), (long long)h->n);
     if ((cnt == nullptr) != (lm == nullptr) || (lm && lm_cap < 0))
         return set_err(&h->err, FS2_ERR_ARG, "cnt and lm must be given together");
+    h->mt.armed = false;         // a pending fs2_mt_draw was made for the state replaced here
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     hipStream_t s = h->stream;
     const int c = h->cur;
@@ -1763,6 +1761,7 @@ int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double
     if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (first < 0 || count < 0 || first + count > h->n)
         return set_err(&h->err, FS2_ERR_ARG, "range outside local particles");
+    h->mt.armed = false;         // a pending fs2_mt_draw was made for the state replaced here
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     hipStream_t s = h->stream;
     const int c = h->cur;
@@ -1934,12 +1933,6 @@ struct IcpQueue {
 std::mutex g_icpq_mu;
 IcpQueue g_icpq[64];
 
-int cu_mask_words(int32_t device) {
-    hipDeviceProp_t pr{};
-    if (hipGetDeviceProperties(&pr, device) != hipSuccess) return 8;
-    return (pr.multiProcessorCount + 31) / 32;
-}
-
 int icpq_get(int32_t device, IcpQueue **out) {
     if (device < 0 || device >= 64) return set_err(nullptr, FS2_ERR_ARG, "bad device %d", device);
     int ndev = 0;
@@ -1948,16 +1941,7 @@ int icpq_get(int32_t device, IcpQueue **out) {
     SHIP(hipSetDevice(device));
     IcpQueue &q = g_icpq[device];
     if (!q.stream) {
-        // A/B knob (config 4 interference): FS2_ICP_CU=k confines the
-        // alignments to compute unit k
-        if (const char *e = std::getenv("FS2_ICP_CU")) {
-            std::vector<uint32_t> mask(cu_mask_words(device), 0u);
-            const int k = std::atoi(e);
-            if (k >= 0 && k / 32 < (int)mask.size()) mask[k / 32] = 1u << (k % 32);
-            SHIP(hipExtStreamCreateWithCUMask(&q.stream, (uint32_t)mask.size(), mask.data()));
-        } else {
-            SHIP(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
-        }
+        SHIP(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
         for (IcpSlot &s : q.slot) {
             SHIP(hipHostMalloc((void **)&s.host, 2 * kIcpCloud + 64, hipHostMallocDefault));
             SHIP(hipMalloc(&s.dev, 2 * kIcpCloud + 64));

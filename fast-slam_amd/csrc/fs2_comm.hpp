@@ -498,8 +498,11 @@ inline int create_shm(const uint8_t key[128], int world, int rank, Transport **o
     size_t chunk = std::min<size_t>(4u << 20, std::max<size_t>(64u << 10, (256u << 20) / ((size_t)world * world)));
     if (const char *e = std::getenv("FS2_SHM_CHUNK")) chunk = std::max<size_t>(4096, std::strtoull(e, nullptr, 10));
     chunk = (chunk + 63) / 64 * 64;
+    // creation waits for every rank to start (a process importing its runtime may
+    // take a while), so it allows at least a minute whatever the collective timeout
+    const long attach_s = std::max(tmo_s, 60L);
     const auto t0 = std::chrono::steady_clock::now();
-    const auto deadline = t0 + std::chrono::seconds(tmo_s);
+    const auto deadline = t0 + std::chrono::seconds(attach_s);
     int fd = -1;
     size_t bytes = 0;
     char *seg = nullptr;
@@ -575,7 +578,7 @@ inline int create_shm(const uint8_t key[128], int world, int rank, Transport **o
     t->seg_bytes = bytes;
     t->hdr = reinterpret_cast<ShmHeader *>(seg);
     t->chunk = chunk;
-    t->timeout = std::chrono::milliseconds(tmo_s * 1000);
+    t->timeout = std::chrono::milliseconds(attach_s * 1000);
     t->xs.assign(world, nullptr);
     t->xr.assign(world, nullptr);
     t->xs_cap.assign(world, 0);
@@ -590,6 +593,7 @@ inline int create_shm(const uint8_t key[128], int world, int rank, Transport **o
     // every rank mapped the segment: its name is no longer needed (nothing stays
     // behind in /dev/shm, whatever happens to the processes later)
     const bool ok = t->wait(t->hdr->attach);
+    t->timeout = std::chrono::milliseconds(tmo_s * 1000);
     if (rank == 0) shm_unlink(name);
     if (!ok) {
         delete t;

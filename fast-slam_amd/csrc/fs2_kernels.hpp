@@ -35,11 +35,7 @@ constexpr int kMaxCand = 8;          // candidate slots listed per particle and 
 // less conservative than the slot tests it replaces (page_reject); a page with
 // an s = 0 slot gets an unbounded box (never rejected).
 constexpr int kPageBytes = 128;
-#ifndef FS2_REC_BYTES
-#define FS2_REC_BYTES 48       // A/B knob: 64 aligns every record to half a 128-byte line
-#endif
-constexpr int kRecBytes = FS2_REC_BYTES;
-static_assert(kRecBytes == 48 || kRecBytes == 64, "record stride");
+constexpr int kRecBytes = 48;   // 64-byte records measured slower (profiles/r03_ab_rec64.txt)
 constexpr uint32_t kOwned = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7fffffffu;
 constexpr uint32_t kRecIdLimit = 0xffffffffu;   // record ids are uint32 (mirror .w, free lists)

@@ -312,23 +312,14 @@ __device__ __forceinline__ Slot load_rec(const char *recs, uint32_t r) {
     return Slot{a.x, a.y, M2{b.x, b.y, c.x, c.y}};
 }
 
-#ifndef FS2_NT_REC
-#define FS2_NT_REC 1           // record stores non-temporal (written once per kernel; A/B: k_update -5%)
-#endif
+// Record stores are non-temporal: written once per kernel, read in a later scan
+// (k_update -5 %).
 __device__ __forceinline__ void store_rec(char *recs, uint32_t r, const Slot &s) {
-    double2 *q = reinterpret_cast<double2 *>(recs + (int64_t)r * kRecBytes);
-#if FS2_NT_REC
     typedef double v2d __attribute__((ext_vector_type(2)));
-    v2d *qv = reinterpret_cast<v2d *>(q);
+    v2d *qv = reinterpret_cast<v2d *>(recs + (int64_t)r * kRecBytes);
     __builtin_nontemporal_store((v2d){s.mx, s.my}, qv);
     __builtin_nontemporal_store((v2d){s.P.a00, s.P.a01}, qv + 1);
     __builtin_nontemporal_store((v2d){s.P.a10, s.P.a11}, qv + 2);
-    if constexpr (kRecBytes == 64) __builtin_nontemporal_store((v2d){0.0, 0.0}, qv + 3);   // whole 64 B
-#else
-    q[0] = make_double2(s.mx, s.my);
-    q[1] = make_double2(s.P.a00, s.P.a01);
-    q[2] = make_double2(s.P.a10, s.P.a11);
-#endif
 }
 
 // Slot j of a page: its mirror names the record.
@@ -551,15 +542,13 @@ __device__ __forceinline__ bool page_reject(uint32_t sum, const SumFrame &f, flo
 // then s * fma(lx, lx, ly^2) >= slb lx^2 (1 - 2^-24)^2 > gate2f.  Likewise in y.
 // A page summary box lying entirely beyond fx + Rx or fx - Rx holds only such
 // slots (a bounded box has finite mirrors with s > 0; kSumOpen is never outside),
-// so the page is rejected for that measurement from its 8-bit codes alone;
-// a slot is rejected when |fl(fx - x)| >= float(Rx) rounded up (finite, s > 0).
+// so the page is rejected for that measurement from its 8-bit codes alone.
 // Every margin only widens the band, so no slot the slot test keeps is dropped.
 struct Band {
     uint32_t cx, cy;   // (a | b << 8): box outside iff low code > a or high code < b
-    float rx, ry;      // slot outside iff s > 0 and finite |fx - x| >= rx (or the same in y)
 };
 
-__device__ __forceinline__ Band band_none() { return Band{0xffu, 0xffu, INFINITY, INFINITY}; }
+__device__ __forceinline__ Band band_none() { return Band{0xffu, 0xffu}; }
 
 // code thresholds of the band [f - R, f + R] on the summary grid: a box with
 // lo(xl) >= f + R (xl >= A) or hi(xh) <= f - R (xh <= B) is outside
@@ -581,14 +570,7 @@ __device__ inline Band gate_band(float fx, float fy, float fe, float slb, float 
     Band b;
     b.cx = band_codes(fx, Rx, fr);
     b.cy = band_codes(fy, Ry, fr);
-    b.rx = (isfinite(Rx) && isfinite(fx)) ? __double2float_ru(Rx * (1.0 + 0x1p-20)) : INFINITY;
-    b.ry = (isfinite(Ry) && isfinite(fy)) ? __double2float_ru(Ry * (1.0 + 0x1p-20)) : INFINITY;
     return b;
-}
-
-__device__ __forceinline__ bool slot_outside_band(const float4 &m, float fx, float fy, float rx, float ry) {
-    const float ax = fabsf(fx - m.x), ay = fabsf(fy - m.y);
-    return mirror_s(m) > 0.0f && ((ax >= rx && ax < INFINITY) || (ay >= ry && ay < INFINITY));
 }
 
 // the page's summary after slot j (mirror mv) was written; returns the new descriptor

@@ -56,32 +56,11 @@ __device__ unsigned long long g_phase[8];
 // can therefore never match and are never modified; k_update visits exactly the
 // listed ones.  A list longer than kMaxCand stores its first kMaxCand entries
 // and k_update resumes with an exact scan after the last stored one.
-// A/B knobs (profiles/r01_v13_ab_k_candidates.txt): deeper descriptor prefetch,
-// the Euclidean box test on pages that pass the bands, and the band pre-test
-// on slots of open pages all measured slower than the defaults (more SGPRs,
-// fewer waves, divergent branches for little rejection gained).
-#ifndef FS2_DESC_AHEAD
-#define FS2_DESC_AHEAD 2
-#endif
-#ifndef FS2_PAGE_REFINE
-#define FS2_PAGE_REFINE 0
-#endif
-#ifndef FS2_SLOT_BAND
-#define FS2_SLOT_BAND 0
-#endif
-#ifndef FS2_PAGE_PRED
-#define FS2_PAGE_PRED 0
-#endif
-#ifndef FS2_B1_DESC_STORE
-#define FS2_B1_DESC_STORE 0    // A/B knob: store the owned pages' ids in B1 as well
-#endif
-#ifndef FS2_NT_COPY
-#define FS2_NT_COPY 0          // A/B knob: copy-on-write page stores non-temporal
-#endif
-#ifndef FS2_COPY_BATCH
-#define FS2_COPY_BATCH 8
-#endif
-constexpr int kDescAhead = FS2_DESC_AHEAD;   // page descriptors a lane keeps in flight
+// Measured slower and removed (profiles/r01_v13_ab_k_candidates.txt, history):
+// deeper descriptor prefetch, the Euclidean box test on pages that pass the
+// bands, the band pre-test on slots of open pages, predicated page loads.
+constexpr int kDescAhead = 2;      // page descriptors a lane keeps in flight
+constexpr int kCopyBatch = 8;      // copy-on-write pages per lane and batch (8 lanes per page)
 
 static_assert(kMaxCand == 8, "sort8 sorts the candidate list");
 
@@ -109,11 +88,8 @@ __device__ __forceinline__ void sort8(uint64_t (&e)[8]) {
     cmpx(e[1], e[2]); cmpx(e[3], e[4]); cmpx(e[5], e[6]);
 }
 
-#ifndef FS2_CAND_WAVES
-#define FS2_CAND_WAVES 0       // A/B knob: minimum waves per SIMD for k_candidates
-#endif
 template <int MAXM>
-__global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const UpdateParams P) {
+__global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ uint64_t s_list[kMaxCand][kBlock];
     __shared__ Band s_band[MAXM];
     __shared__ uint16_t s_rows[kBBoxRows];      // rows the row boxes leave open, ascending
@@ -141,12 +117,9 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
     }
     __syncthreads();
     uint32_t bc[MAXM];               // (x a, x b, y a, y b) code thresholds, one byte each
-    float rx[MAXM], ry[MAXM];
 #pragma unroll
     for (int k = 0; k < MAXM; ++k) {
         bc[k] = __builtin_amdgcn_readfirstlane(s_band[k].cx | (s_band[k].cy << 16));
-        rx[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_band[k].rx)));
-        ry[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_band[k].ry)));
     }
     // the list lives in LDS until the walk ends: (record id << 16 | slot) per
     // entry (a global store inside the walk would serialise the prefetch, since
@@ -165,16 +138,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
         if (g * kPageSlots < c) {
             const uint32_t s = d.y;
             om = box_open_mask<MAXM>(s, bc, P.m);
-#if FS2_PAGE_REFINE
-            // the box survived the bands: the full (Euclidean) box test
-            if (om) {
-#pragma unroll
-                for (int k = 0; k < MAXM; ++k)
-                    if (((om >> k) & 1u) &&
-                        page_reject(s, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
-                        om &= ~(1u << k);
-            }
-#endif
         }
         return om;
     };
@@ -192,9 +155,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
 #pragma unroll
                 for (int k = 0; k < MAXM; ++k) {
                     if ((om >> k) & 1u) {
-#if FS2_SLOT_BAND
-                        if (slot_outside_band(mv, P.meas.fx[k], P.meas.fy[k], rx[k], ry[k])) continue;
-#endif
                         hit |= !gate_reject_fast(mv, cx, cy, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k],
                                                  P.gate2f);
                     }
@@ -244,17 +204,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
         if (g * kPageSlots < c) ++groups;
         const unsigned om = open_mask(d, g);
         if (!__any(om)) continue;
-#if FS2_PAGE_PRED
-        // only lanes whose page is open load it
-        if (om) {
-            const char *pg = page_ptr(map.pool, d.x);
-            float4 mir[kScanGroup];
-#pragma unroll
-            for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
-            ++opened;
-            test_page(mir, g, om);
-        }
-#else
         const char *pg = page_ptr(map.pool, om ? d.x : 0u);
         float4 mir[kScanGroup];
 #pragma unroll
@@ -263,7 +212,6 @@ __global__ __launch_bounds__(kBlock, FS2_CAND_WAVES) void k_candidates(const Upd
             ++opened;
             test_page(mir, g, om);
         }
-#endif
     }
     if (live) {
         P.ncand[i] = nc;
@@ -308,13 +256,8 @@ static __device__ __forceinline__ uint32_t sel_u32(int t, const uint32_t (&a)[K]
 // resolved afterwards in measurement order.  Likelihoods multiply into the
 // weight in measurement order, as the reference does.  Without the gate filter
 // (or past an overflowing candidate list) every slot takes the exact path.
-// FS2_UPDATE_WAVES (A/B knob): minimum waves per SIMD the compiler must fit
-// k_update into (spilling what does not fit); 0 = its own choice (3 at 164 VGPRs)
-#ifndef FS2_UPDATE_WAVES
-#define FS2_UPDATE_WAVES 0
-#endif
 template <int MAXM>
-__global__ __launch_bounds__(kBlock, FS2_UPDATE_WAVES) void k_update(const UpdateParams P) {
+__global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     __shared__ Meas s_ms[MAXM];                 // this pass's measurements
     __shared__ double s_lik[MAXM][kBlock];      // per (measurement, lane) likelihood
     __shared__ int16_t s_idx[MAXM][kBlock];     // per (measurement, lane) association (slot < 4096, -1, -2)
@@ -672,11 +615,6 @@ __global__ __launch_bounds__(kBlock, FS2_UPDATE_WAVES) void k_update(const Updat
             if (task) s_ws[wid].cow[T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
             T += __popcll(bm);
         }
-#if FS2_B1_DESC_STORE
-#pragma unroll
-        for (int t = 0; t < NR; ++t)
-            if (t < nrows && canon[t] == t) pt_entry(map, rrow[t], il)->x = rdesc[t].x;
-#endif
         // (the owned pages' descriptors reach memory with their summaries: B2 stores
         // the modified rows, the appends the partly filled row; nothing reads them
         // from memory before)
@@ -685,7 +623,7 @@ __global__ __launch_bounds__(kBlock, FS2_UPDATE_WAVES) void k_update(const Updat
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int off = (lane & 7) * 16;
-        constexpr int CB = FS2_COPY_BATCH;   // pages per lane and batch (8 lanes per page)
+        constexpr int CB = kCopyBatch;
         v4i va[CB];                   // clang vector type: HIP's int4 struct defeats SROA here
         uint32_t da[CB];
         auto load_batch = [&](int base, v4i *v, uint32_t *d) {
@@ -699,11 +637,7 @@ __global__ __launch_bounds__(kBlock, FS2_UPDATE_WAVES) void k_update(const Updat
         auto store_batch = [&](const v4i *v, const uint32_t *d) {
 #pragma unroll
             for (int u = 0; u < CB; ++u) {
-#if FS2_NT_COPY
-                __builtin_nontemporal_store(v[u], reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off));
-#else
                 *reinterpret_cast<v4i *>(page_ptr(map.pool, d[u]) + off) = v[u];
-#endif
             }
         };
         for (int base = 0; base < T; base += 8 * CB) {
@@ -725,16 +659,7 @@ __global__ __launch_bounds__(kBlock, FS2_UPDATE_WAVES) void k_update(const Updat
 #pragma unroll
                 for (int u = 0; u < NR; ++u)
                     if (u == canon[t]) id = rdesc[u].x;
-#if FS2_NT_COPY
-                {
-                    const float4 mv = s_mv[t][tid];
-                    __builtin_nontemporal_store((v4i){(int)__float_as_uint(mv.x), (int)__float_as_uint(mv.y),
-                                                      (int)__float_as_uint(mv.z), (int)__float_as_uint(mv.w)},
-                                                reinterpret_cast<v4i *>(page_ptr(map.pool, id)) + (j & (kPageSlots - 1)));
-                }
-#else
                 reinterpret_cast<float4 *>(page_ptr(map.pool, id))[j & (kPageSlots - 1)] = s_mv[t][tid];
-#endif
             }
         }
         nrec = nmod;

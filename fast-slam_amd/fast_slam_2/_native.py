@@ -111,6 +111,14 @@ class fs2_profile(C.Structure):
         ("sent_bytes", C.c_uint64),
         ("migrate_ms", C.c_double),
         ("sent_pages_repeat", C.c_uint64),
+        ("model_groups", C.c_uint64),
+        ("model_opened", C.c_uint64),
+        ("model_words", C.c_uint64),
+        ("model_candidates", C.c_uint64),
+        ("model_written", C.c_uint64),
+        ("model_cow", C.c_uint64),
+        ("model_fixed_bytes", C.c_uint64),
+        ("model_box_bytes", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -152,6 +152,23 @@ typedef struct fs2_profile {
     uint64_t sent_pages_repeat; /* of sent_pages, those that had gone to the same rank before since
                                    the sender's last collection (what a receiver-side page cache
                                    could skip; a probe, nothing is skipped) */
+    /* The counters of the algorithmic byte model, summed over the
+     * timed candidate / exact launches, so that filter_bytes and update_bytes can be
+     * recomputed from them:
+     *   k_candidates: 8 B per streamed descriptor + 128 B per opened page + 8 B per
+     *                 list entry + 8 B per particle and pass + 4 B per row box read;
+     *   k_update:     model_fixed_bytes (particle scalars, free-list ids, counts)
+     *                 + 8 B per list entry + 48 B per candidate record + 80 B per
+     *                 written slot (record 48, mirror 16, descriptor read + write 16)
+     *                 + 256 B per copied page + 8 B per row box read and written. */
+    uint64_t model_groups;      /* descriptors streamed */
+    uint64_t model_opened;      /* pages whose 128-byte mirror line was loaded */
+    uint64_t model_words;       /* candidate list entries */
+    uint64_t model_candidates;  /* fp64 records read by the exact pass */
+    uint64_t model_written;     /* slots written (modified + appended) */
+    uint64_t model_cow;         /* pages copied before their first write */
+    uint64_t model_fixed_bytes; /* k_update's per-particle bytes (scalars, ids, counts) */
+    uint64_t model_box_bytes;   /* row-box bytes (k_candidates reads, k_update reads + writes) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */

@@ -63,6 +63,25 @@ def main(argv):
     h.set_profiling(True)
     rec = {k: [] for k in ("resampled", "best_index", "pose", "n_eff", "reduce_amb", "firsts", "firsts_pre")}
     assoc = []
+    if mode == "stall":
+        # the last rank arrives late at scan 1: with FS2_SHM_TIMEOUT_S below the
+        # delay every rank's scan must fail with FS2_ERR_COMM, nothing stale used
+        import time
+        from fast_slam_2._native import FS2Error
+        err = (0, -1, "")
+        for s in range(scans):
+            if s == 1 and rank == G - 1:
+                time.sleep(float(os.environ.get("FS2_TEST_STALL_S", "8")))
+            rot, tr = syn.odometry(s)
+            try:
+                h.step(rot, tr, measurements(wl, s, mode))
+            except FS2Error as e:
+                err = (e.code, s, str(e))
+                break
+        h.close()
+        np.savez(out, err_code=err[0], err_scan=err[1], err_msg=err[2])
+        print(f"rank {rank} error {err}", flush=True)
+        return 0
     for s in range(scans):
         rot, tr = syn.odometry(s)
         rec["firsts_pre"].append(h.first_global)    # the shard whose particles the associations describe

@@ -106,3 +106,33 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     if mode == "follow":     # rank 0 took the higher shard its sources fill most
         assert int(ranks[0]["firsts"][0]) > 0 and int(ranks[0]["first"]) > 0
 
+
+
+def test_shm_timeout_is_a_clean_comm_error(tmp_path):
+    """A rank that never reaches a collective: the others' stream-ordered
+    collectives time out, and the scan reports FS2_ERR_COMM before any stale
+    staging bytes could size the resample (post_and_wait checks the
+    transport status); the late rank fails at once on the marked segment."""
+    G = 2
+    key = os.urandom(128).hex()
+    env = dict(os.environ, FS2_SHM_TIMEOUT_S="2", FS2_TEST_STALL_S="8")
+    outs = [str(tmp_path / f"rank{r}.npz") for r in range(G)]
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "shard_proc_worker.py"), str(G), str(r),
+                               "4000", "24", "21", "4", key, outs[r], "stall"],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(G)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-4000:]}"
+    for r in range(G):
+        d = np.load(outs[r])
+        assert int(d["err_code"]) == -6, (r, str(d["err_msg"]))      # FS2_ERR_COMM
+        assert int(d["err_scan"]) == 1, r
+        assert "shm transport" in str(d["err_msg"]), str(d["err_msg"])
