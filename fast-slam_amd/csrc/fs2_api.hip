@@ -239,6 +239,16 @@ struct fs2_handle {
     double *sout = nullptr, *part_w = nullptr, *np_part = nullptr, *np_leaf = nullptr, *sentry = nullptr;
     NpTailPlan *np_tail = nullptr;         // device: numpy's tree over the partial last chunk (null: none)
     UnitRec *urec = nullptr;
+    // exact-order reductions across shards (sharded EXACT mode): this rank's chain
+    // ops and all ranks', this rank's reduction record and all ranks', the tree
+    // estimate of the chain before this shard, each listed unit's first op, and
+    // numpy's plan of the global partial last chunk
+    bool xsh_ok = false;
+    ChainSummary *dch_send = nullptr, *dch_recv = nullptr;
+    RankRecordX *recx = nullptr, *recxs = nullptr;
+    double *est_base = nullptr;
+    int32_t *uop = nullptr;
+    NpTailPlan *np_tail_g = nullptr;
 
     MapRef map() const {
         return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb, row_boxes(cur)};
@@ -249,7 +259,10 @@ struct fs2_handle {
     // the reduction order in force (FS2_REDUCE_*, AUTO resolved)
     int reduce() const {
         const int mode = cfg.reduce_mode;
-        if (tp) return mode == FS2_REDUCE_SEQUENTIAL ? FS2_REDUCE_SEQUENTIAL : FS2_REDUCE_PARALLEL;
+        if (tp) {
+            if (mode == FS2_REDUCE_SEQUENTIAL) return FS2_REDUCE_SEQUENTIAL;
+            return (mode != FS2_REDUCE_PARALLEL && xsh_ok) ? FS2_REDUCE_EXACT : FS2_REDUCE_PARALLEL;
+        }
         if (mode != FS2_REDUCE_AUTO) return mode;
         return n_global <= 4096 ? FS2_REDUCE_SEQUENTIAL : FS2_REDUCE_EXACT;
     }
@@ -278,7 +291,9 @@ struct fs2_handle {
         p.stats = stats_dev;
         // recursive summation of n terms >= 0: |chain - exact| <= gamma_n exact; the
         // block estimates add gamma_{n/256 + 30}; doubled, plus slack for the scaling
-        p.margin = std::ldexp(2.0 * (double)n + 8192.0, -53);
+        // (sharded: the whole chain's length, the shards' estimates included)
+        p.margin = std::ldexp(2.0 * (double)n_global + 8192.0, -53);
+        p.chain_first = 1;
         return p;
     }
 };
@@ -853,6 +868,8 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
     hipFree(h->sout); hipFree(h->np_leaf); hipFree(h->part_w); hipFree(h->np_part); hipFree(h->np_tail);
     hipFree(h->urec); hipFree(h->sentry);
+    hipFree(h->dch_send); hipFree(h->dch_recv); hipFree(h->recx); hipFree(h->recxs); hipFree(h->est_base);
+    hipFree(h->uop); hipFree(h->np_tail_g);
     hipFree(h->part_pose);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
@@ -1033,6 +1050,33 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
             if (hipMalloc(&h->np_tail, sizeof plan) != hipSuccess ||
                 hipMemcpy(h->np_tail, &plan, sizeof plan, hipMemcpyHostToDevice) != hipSuccess)
                 return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
+        }
+    }
+    if (G > 1) {
+        // exact reductions across shards: every shard holds at least one numpy chunk
+        // (a chunk is then cut by at most one shard boundary) and at most kShardChunks
+        // whole chunks, and the global partial chunk's plan fits an edge record
+        NpTailPlan gp;
+        const bool gpart = np_tail_plan(h->n_global, &gp);
+        const int64_t min_shard = h->n_global / G, max_shard = (h->n_global + G - 1) / G;
+        h->xsh_ok = min_shard >= kNpChunk && max_shard / kNpChunk + 1 <= kShardChunks && (!gpart || gp.nl <= 128);
+        if (cfg->reduce_mode == FS2_REDUCE_EXACT && !h->xsh_ok)
+            return fail(set_err(&h->err, FS2_ERR_ARG,
+                                "exact reductions across %d shards need >= %d particles per shard (%lld)",
+                                (int)G, kNpChunk, (long long)min_shard));
+        if (h->xsh_ok) {
+            const int64_t nu = (n + 63) / 64;      // chain units (kUnit)
+            bool ok2 = hipMalloc(&h->dch_send, sizeof(ChainSummary)) == hipSuccess &&
+                       hipMalloc(&h->dch_recv, sizeof(ChainSummary) * G) == hipSuccess &&
+                       hipMalloc(&h->recx, sizeof(RankRecordX)) == hipSuccess &&
+                       hipMalloc(&h->recxs, sizeof(RankRecordX) * G) == hipSuccess &&
+                       hipMalloc(&h->est_base, sizeof(double)) == hipSuccess &&
+                       hipMalloc(&h->uop, sizeof(int32_t) * (size_t)std::max<int64_t>(nu, 1)) == hipSuccess;
+            if (ok2 && gpart)
+                ok2 = hipMalloc(&h->np_tail_g, sizeof gp) == hipSuccess &&
+                      hipMemcpy(h->np_tail_g, &gp, sizeof gp, hipMemcpyHostToDevice) == hipSuccess;
+            if (ok2) ok2 = hipMemset(h->recx, 0, sizeof(RankRecordX)) == hipSuccess;
+            if (!ok2) return fail(set_err(&h->err, FS2_ERR_OOM, "sharded reduction buffers"));
         }
     }
     int rc = grow_rows(h, std::max(cfg->landmark_capacity, 1));
@@ -1409,8 +1453,9 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     // weight total over all ranks (fast_slam_2.py:166).  Exact: Python's sum (in
     // particle order) from the update pass's block sums, the chain's units also
     // folding the update counters (k_wsum's other job)
-    if (prof && exact && h->n <= 0) HIP_TRY(h, hipEventRecord(E[5], s));   // launch_chain records nothing
-    if (exact) {
+    const bool xsh = sh && exact;            // exact orders across shards
+    if (prof && exact && !xsh && h->n <= 0) HIP_TRY(h, hipEventRecord(E[5], s));   // launch_chain records nothing
+    if (exact && !xsh) {
         ChainParams cp = h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false);
         cp.cpart = h->cpart;
         cp.ncpart = (int32_t)h->nblocks();
@@ -1419,19 +1464,51 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     } else {
         HIP_TRY(h, launch_wsum(rp, s, prof ? E[5] : nullptr));
     }
+    // a sharded rank's chain ops (xsh): its units classified against the tree
+    // prefix of the shards before it, exported as exact adds
+    auto chain_ops = [&](ChainParams cp, const double *est) -> int {
+        cp.chain_first = h->shard == 0 ? 1 : 0;
+        cp.force_list0 = 1;
+        cp.est_base = est;
+        cp.ops_out = h->dch_send;
+        cp.uop = h->uop;
+        HIP_TRY(h, launch_chain_export(cp, s));
+        CommTimer ct(h);
+        return h->tp->allgather(h->dch_send, h->dch_recv, sizeof(ChainSummary), s, &h->err);
+    };
     if (sh) {
         {
             CommTimer ct(h);
             rc = h->tp->allgather(&h->stats_dev->total, h->totals, sizeof(double), s, &h->err);
         }
         if (rc) return rc;
+        rp.est_base = xsh ? h->est_base : nullptr;
         HIP_TRY(h, launch_global_total(rp, s));
+        if (xsh) {
+            // Python's sum over the global order: every rank folds all shards' ops
+            rc = chain_ops(h->chain(h->w[cur], h->wpart, nullptr, nullptr, false), h->est_base);
+            if (rc) return rc;
+            HIP_TRY(h, launch_chain_fold(h->dch_recv, G, h->shard, h->rank_of, &h->stats_dev->total, nullptr,
+                                         h->stats_dev, s));
+        }
     }
-    // normalise (:161-175), local prefix of the normalised weights, this rank's record
-    HIP_TRY(h, rp.chunked ? launch_normalize_chunks(rp, s) : launch_normalize(rp, s));
-    // sharded ranks need their prefix end in the record; one GPU needs the
-    // prefix only when the rule fires (computed below, kernels exit otherwise)
-    if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    if (xsh) {
+        // normalise (tree partials for the estimates), numpy's Sigma w'^2 over the
+        // global chunks, this rank's record, all records, the decision
+        rp.exact = 0;
+        rp.np_leaf = nullptr;
+        rp.part_w = h->part_w;
+        rp.t_from_parts = 1;
+        rp.rec = &h->recx->base;
+        HIP_TRY(h, launch_normalize(rp, s));
+        HIP_TRY(h, launch_np_shard(h->w[cur], h->n, h->first, h->n_global, h->np_tail_g, h->recx, s));
+    } else {
+        // normalise (:161-175), local prefix of the normalised weights, this rank's record
+        HIP_TRY(h, rp.chunked ? launch_normalize_chunks(rp, s) : launch_normalize(rp, s));
+        // sharded ranks need their prefix end in the record; one GPU needs the
+        // prefix only when the rule fires (computed below, kernels exit otherwise)
+        if (sh) HIP_TRY(h, launch_prefix(rs, seq ? 1 : 0, s));
+    }
     // one GPU: k_finalize publishes a scan whose rule did not fire, before the
     // lazy resample kernels (they run while the host returns)
     const unsigned long long pseq = ++h->pub_seq;
@@ -1444,13 +1521,14 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (sh) {
         {
             CommTimer ct(h);
-            rc = h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
+            rc = xsh ? h->tp->allgather(h->recx, h->recxs, sizeof(RankRecordX), s, &h->err)
+                     : h->tp->allgather(h->rec, h->recs, sizeof(RankRecord), s, &h->err);
         }
         if (rc) return rc;
     }
     // N_eff (:212-223), resample rule (:62), estimate (:201-210), u0 (:183); on
     // one GPU k_finalize did this already
-    if (sh) HIP_TRY(h, launch_global_finalize(rp, s));
+    if (sh) HIP_TRY(h, xsh ? launch_global_finalize_x(rp, h->recxs, h->np_tail_g, s) : launch_global_finalize(rp, s));
     if (!sh) {
         rs.lazy = 1;
         if (exact)   // the resample's running sum (fast_slam_2.py:184-193), bit-exact
@@ -1468,6 +1546,20 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         run_resample = posted_stats(h).resampled != 0;
     }
     if (run_resample) {
+        if (xsh) {
+            // the running sum over the global order (fast_slam_2.py:184-193): every
+            // rank folds all shards' ops for the exact value before its first
+            // particle, then walks its own units from there
+            ChainParams cp = h->chain(h->w[cur], h->part_w, h->cbuf, nullptr, false);
+            rc = chain_ops(cp, &h->stats_dev->offset);
+            if (rc) return rc;
+            HIP_TRY(h, launch_chain_fold(h->dch_recv, G, h->shard, h->rank_of, nullptr, &h->stats_dev->offset,
+                                         h->stats_dev, s));
+            cp.chain_first = h->shard == 0 ? 1 : 0;
+            cp.force_list0 = 1;
+            cp.s_entry = &h->stats_dev->offset;
+            HIP_TRY(h, launch_chain_walk_from(cp, s));
+        }
         // every local output is written below: the output ranges of the local
         // sources (k_ranges) and of the received ones (k_scatter_recv) partition them
         HIP_TRY(h, launch_resample_ranges(rs, s));

@@ -135,6 +135,49 @@ __device__ __forceinline__ double chain_unit_entry(const ChainView &V, int64_t k
 
 // ------------------------------------------------------- numpy sum of w^2 --
 
+// numpy's pairwise_sum leaf (loops_utils.h.src, n <= 128) of the squares of x(0 ..
+// len - 1), one thread: n < 8 sequential from 0; else 8 accumulators over the
+// full 8-groups, combined ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then
+// the rest in order.
+template <typename X>
+__device__ inline double np_leaf_seq(X x, int len) {
+    if (len < 8) {
+        double res = 0.0;
+        for (int i = 0; i < len; ++i) res += x(i) * x(i);
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = x(k) * x(k);
+    const int full = len - len % 8;
+    for (int i = 8; i < full; i += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += x(i + k) * x(i + k);
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int i = full; i < len; ++i) res += x(i) * x(i);
+    return res;
+}
+
+// The leaves of a numpy chunk of m elements (m = kNpChunk: 64 leaves of 128;
+// else the partial chunk's plan).
+__device__ __forceinline__ int np_chunk_leaves(int m, const NpTailPlan *pl) { return m == kNpChunk ? 64 : pl->nl; }
+__device__ __forceinline__ int np_leaf_off(int m, const NpTailPlan *pl, int k) { return m == kNpChunk ? 128 * k : pl->off[k]; }
+__device__ __forceinline__ int np_leaf_len(int m, const NpTailPlan *pl, int k) { return m == kNpChunk ? 128 : pl->len[k]; }
+
+// The chunk's sum from its leaf values node[0 .. nl) (overwritten): a balanced tree
+// in order for a full chunk, the plan's post-order nodes for a partial one.  One thread.
+__device__ inline double np_chunk_combine(double *node, int m, const NpTailPlan *pl) {
+    if (m == kNpChunk) {
+        for (int w = 1; w < 64; w <<= 1)
+            for (int k = 0; k < 64; k += 2 * w) node[k] = node[k] + node[k + w];
+        return node[0];
+    }
+    const int nl = pl->nl;
+    for (int q = 0; q + 1 < nl; ++q) node[nl + q] = node[pl->a[q]] + node[pl->b[q]];
+    return node[2 * nl - 2];
+}
+
 // numpy's recursion over n < 8192 elements (n > 128: halves at n/2 rounded down
 // to a multiple of 8; leaves of <= 128).
 // One wave: numpy's pairwise sum of x[i]^2 over the partial chunk planned by pl.

@@ -246,7 +246,7 @@ inline int create_local(const uint8_t key[128], int world, int rank, Transport *
 // rank runs max over ranks of its own round count (agreed through the header).
 
 constexpr uint64_t kShmMagic = 0x66733273686d3031ull;   // "fs2shm01"
-constexpr size_t kShmAgCap = 4096;                      // all-gather bytes per rank
+constexpr size_t kShmAgCap = 16384;                     // all-gather bytes per rank (ChainSummary, RankRecordX)
 constexpr size_t kShmHeader = 4096;
 constexpr size_t kShmBoxHeader = 64;
 constexpr int kShmMaxRanks = 16;                        // >= fs2::kMaxRanks (static_assert in fs2_api.hip)

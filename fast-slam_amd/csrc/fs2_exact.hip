@@ -99,7 +99,8 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) v += x[u];
         }
-        const double base = block_sum<1024>(v, s_red);
+        // (sharded: plus the tree prefix of the shards before this one)
+        const double base = block_sum<1024>(v, s_red) + (P.est_base ? *P.est_base : 0.0);
         if (t < 64) {
             const double b0 = bcast(own, 0), b1 = bcast(own, 1), b2 = bcast(own, 2);
             if (t < 4) {
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         // grid of step 2^-1074 (binade -1022 below): every add there is exact, so a
         // run of zero or subnormal weights (a diverged filter's underflowed
         // likelihoods) is a translation too, not a unit walked term by term
-        bool ok = valid && i != 0 && a >= 0.0 && a < INFINITY && lo >= 0.0 && hi < 0x1p1020;
+        bool ok = valid && !(i == 0 && P.chain_first) && a >= 0.0 && a < INFINITY && lo >= 0.0 && hi < 0x1p1020;
         const int E = ok ? chain_binade(lo) : -4096;
         ok = ok && chain_binade(hi) == E;
         long long r = 0;
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         }
         const unsigned long long vmask = __ballot(valid);
         const int E0 = __builtin_amdgcn_readfirstlane(E);
-        if (k == 0) {
+        if (k == 0 && P.chain_first) {
             // the chain's first unit: its entry is known, so its values are evaluated
             // here; the walk only sets the value after it
             listed = 1;
@@ -166,7 +167,9 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
                 P.udelta[k] = 0;
                 P.urec[k] = rec;
             }
-        } else if (__ballot(ok && E == E0) == vmask) {     // one translation
+        } else if (!(k == 0 && P.force_list0) && __ballot(ok && E == E0) == vmask) {     // one translation
+            // (a sharded rank lists its unit 0: the walk and the ranges need a listed
+            // unit before every translation, and the chain enters there from another rank)
             D = (unsigned long long)wave_sum_i64(r);
             if (lane == 0) {
                 P.uinfo[k] = (E0 + 4096) << 2;
@@ -277,6 +280,81 @@ __device__ unsigned long long g_chain[8];
 #define FS2_CHAIN_STAMP(k) do { } while (0)
 #endif
 
+// Sharded ranks: this shard's chain as a list of fp64 adds (ChainSummary), exact
+// for its true entry value: per listed unit (in order) the translation run before
+// it (one add of D ulp(E), exact inside binade E) and its own adds -- one per
+// segment, or every term of a unit evaluated term by term (and of the chain's
+// first unit: 0 + a_0 = a_0, Python's sum starting from 0); then the run after the
+// last one.  Wave 0; each listed unit's first op index into P.uop.
+__device__ void chain_export(const ChainParams &P, int nseq, int64_t nu, unsigned long long dtot) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    ChainSummary *S = P.ops_out;
+    int base = 0;
+    unsigned long long gprev = 0;
+    int Eprev = 0;
+    for (int o0 = 0; o0 < nseq; o0 += 64) {
+        const int ol = o0 + lane;
+        const bool in = ol < nseq;
+        int64_t q = 0;
+        int32_t info = 0;
+        unsigned long long g = 0;
+        int En = 0;
+        if (in) {
+            q = P.seql[ol];
+            info = P.uinfo[q];
+            g = P.bpd[q / kChainGroup] + P.ugl[q];
+            En = (q + 1 < nu) ? unit_binade(P.uinfo[q + 1]) : 0;
+        }
+        const unsigned long long gp = __shfl_up(g, 1, 64);
+        const int Ep = __shfl_up(En, 1, 64);
+        const unsigned long long gb = (lane == 0) ? gprev : gp;
+        const int Eb = (lane == 0) ? Eprev : Ep;
+        const double run = (in && ol > 0) ? (double)(long long)(g - gb) * unit_ulp(Eb) : 0.0;
+        const int cnt = in ? (int)min<int64_t>(kUnit, P.n - q * kUnit) : 0;
+        const bool terms = in && ((info & 2) || (q == 0 && P.chain_first));
+        const int nrun = (run != 0.0) ? 1 : 0;
+        const int nops = in ? nrun + (terms ? cnt : unit_nseg(info)) : 0;
+        const long long incl = wave_incl_scan_i64(nops);
+        const int off = base + (int)(incl - nops);
+        if (in) {
+            P.uop[ol] = off + nrun;
+            int k = off;
+            if (nrun) {
+                if (k < kChainOpsCap) S->ops[k] = run;
+                ++k;
+            }
+            if (!terms) {
+                const UnitRec rr = P.urec[q];
+                const int ns = unit_nseg(info);
+#pragma unroll
+                for (int u = 0; u < kChainSegs; ++u)
+                    if (u < ns && k + u < kChainOpsCap) S->ops[k + u] = rr.val[u];
+            }
+        }
+        // the terms of units evaluated term by term: the wave copies them unit by unit
+        for (unsigned long long tm = __ballot(terms); tm; tm &= tm - 1) {
+            const int j = (int)__builtin_ctzll(tm);
+            const int64_t qj = (int64_t)__builtin_amdgcn_readlane((int)q, j);
+            const int oj = __builtin_amdgcn_readlane(off + nrun, j), cj = __builtin_amdgcn_readlane(cnt, j);
+            if (lane < cj && oj + lane < kChainOpsCap) S->ops[oj + lane] = P.a[qj * kUnit + lane];
+        }
+        const int nb = min(64, nseq - o0);
+        base += (int)bcast_i64(incl, 63);
+        gprev = bcast_i64((long long)g, nb - 1);
+        Eprev = __builtin_amdgcn_readlane(En, nb - 1);
+    }
+    if (lane == 0) {
+        int k = base;
+        const double run = (double)(long long)(dtot - gprev) * unit_ulp(Eprev);
+        if (run != 0.0) {
+            if (k < kChainOpsCap) S->ops[k] = run;
+            ++k;
+        }
+        S->nops = k;
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     __shared__ unsigned long long s_d[2][16];
     __shared__ int s_c[2][16];
@@ -347,6 +425,10 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     __syncthreads();
     const int nseq = s_nseq;
     FS2_CHAIN_STAMP(1);
+    if (P.ops_out) {                 // sharded: export this shard's ops instead of walking
+        chain_export(P, nseq, nu, s_dtot);
+        return;
+    }
 #ifdef FS2_PHASE_TIMING
     if (t == 0) {
         atomicAdd(&g_chain[4], 1ull);
@@ -356,7 +438,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     // (2) 64 listed units at a time: every wave loads their table entries (one
     // per lane); the term-by-term ones have their terms staged in LDS by all
     // waves; wave 0 walks; then the staged values are written out
-    double s = 0.0;                                // the running value (wave 0)
+    double s = P.s_entry ? *P.s_entry : 0.0;       // the running value (wave 0)
     unsigned long long gprev = 0;
     int Eprev = 0;
     for (int o0 = 0; o0 < nseq; o0 += 64) {
@@ -425,13 +507,13 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
 #endif
                     const int cnt = (int)min<int64_t>(kUnit, P.n - qj * kUnit);
                     if (r < kWalkStage) {
-                        const double mine = chain_unit(s_terms[r][lane], cnt, s, qj == 0);
+                        const double mine = chain_unit(s_terms[r][lane], cnt, s, qj == 0 && P.chain_first);
                         s_terms[r][lane] = mine;
                     } else {                          // beyond the stage: from memory
                         const int64_t i = qj * kUnit + lane;
                         const double a = (i < P.n) ? P.a[i] : 0.0;
                         const double e = s;
-                        const double mine = chain_unit(a, cnt, s, qj == 0);
+                        const double mine = chain_unit(a, cnt, s, qj == 0 && P.chain_first);
                         if (P.c && lane < cnt) P.c[i] = mine;
                         if (P.c && qj > 0 && lane == 0) P.c[qj * kUnit - 1] = e;
                     }
@@ -439,7 +521,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
                 } else {
                     // one add per segment (unit 0: the value after it, set)
                     const int ns = unit_nseg(infoj);
-                    if (__builtin_amdgcn_readlane((int)q, j) == 0) s = bcast(rv[0], j);
+                    if (__builtin_amdgcn_readlane((int)q, j) == 0 && P.chain_first) s = bcast(rv[0], j);
                     else {
 #pragma unroll
                         for (int u = 0; u < kChainSegs; ++u)
@@ -481,7 +563,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     for (int o = wid; o < nseq; o += 16) {
         const int64_t q = P.seql[o];
         const int32_t info = P.uinfo[q];
-        if ((info & 2) || q == 0) continue;              // written above / by k_chain_units
+        if ((info & 2) || (q == 0 && P.chain_first)) continue;   // written above / by k_chain_units
         const UnitRec r = P.urec[q];
         double sg = P.sentry[o];
         const int cnt = (int)min<int64_t>(kUnit, P.n - q * kUnit);
@@ -525,6 +607,61 @@ hipError_t launch_chain(const ChainParams &p, hipStream_t s, hipEvent_t e0) {
     return hipGetLastError();
 }
 
+hipError_t launch_chain_export(const ChainParams &p, hipStream_t s) {
+    if (p.n <= 0) {
+        hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
+        return hipGetLastError();
+    }
+    const unsigned ng = (unsigned)((p.n + 1023) / 1024);
+    hipLaunchKernelGGL(k_chain_units, dim3(ng), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_walk_from(const ChainParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(1024), 0, s, p);
+    return hipGetLastError();
+}
+
+// One wave: every shard's ops in shard order (serial fp64 adds, read 64 at a time).
+__global__ __launch_bounds__(64) void k_chain_fold(const ChainSummary *all, int32_t world, int32_t shard,
+                                                    ShardOrder order, double *total, double *entry,
+                                                    DevStats *stats) {
+    const int lane = threadIdx.x;
+    double s = 0.0, at = 0.0;
+    bool over = false;
+    for (int q = 0; q < world && !over; ++q) {
+        const ChainSummary &S = all[order.r[q]];
+        if (q == shard) at = s;
+        const int n = S.nops;
+        if (n > kChainOpsCap) {
+            over = true;
+            break;
+        }
+        for (int k0 = 0; k0 < n; k0 += 64) {
+            const double v = (k0 + lane < n) ? S.ops[k0 + lane] : 0.0;
+            const int nb = min(64, n - k0);
+            for (int j = 0; j < nb; ++j) s = s + bcast(v, j);
+        }
+    }
+    if (lane == 0) {
+        if (over) {
+            stats->reduce_amb += 1;          // the tree estimates stay: counted, never hidden
+        } else {
+            if (total) *total = s;
+            if (entry) *entry = at;
+        }
+    }
+}
+
+hipError_t launch_chain_fold(const ChainSummary *all, int32_t world, int32_t shard, const int8_t *rank_of,
+                             double *total, double *entry, DevStats *stats, hipStream_t s) {
+    ShardOrder o{};
+    for (int q = 0; q < world && q < kMaxRanks; ++q) o.r[q] = rank_of[q];
+    hipLaunchKernelGGL(k_chain_fold, dim3(1), dim3(64), 0, s, all, world, shard, o, total, entry, stats);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------- numpy sum of w^2 --
 
 #ifdef FS2_PHASE_TIMING
@@ -539,6 +676,100 @@ hipError_t debug_chain_times(unsigned long long out[8], int reset) {
 #endif
 
 int64_t np_sumsq_chunks(int64_t n) { return (n + kNpChunk - 1) / kNpChunk; }
+
+// Sharded exact mode: numpy's chunks of np.sum(w'^2) in the GLOBAL order that
+// overlap this shard [first, first + n), one workgroup each.  A chunk held whole
+// is summed here (its leaves by 8 lanes each, then its tree); the chunk cut by the
+// shard's first (last) boundary is described in rx->head (rx->tail): the sums of
+// the leaves held whole, the raw weights of the leaf the boundary cuts
+// (k_global_finalize_x completes it with the neighbour's half).  Shards hold at
+// least one chunk's worth of particles, so a chunk is cut at most once.
+__global__ __launch_bounds__(1024) void k_np_shard(const double *w, int64_t n, int64_t first, int64_t N,
+                                                   const NpTailPlan *gtail, RankRecordX *rx) {
+    __shared__ double s_w[kNpChunk];
+    __shared__ double s_leaf[kNpMaxLeaves];
+    const int t = threadIdx.x;
+    const int64_t c0 = first / kNpChunk, c1 = (first + n - 1) / kNpChunk;
+    const int64_t c = c0 + blockIdx.x;
+    const int64_t cs = c * kNpChunk;
+    const int m = (int)min<int64_t>(kNpChunk, N - cs);
+    const int lo = (int)(max(first, cs) - cs), hi = (int)(min(first + n, cs + m) - cs);
+    for (int e = t; e < kNpChunk; e += 1024) s_w[e] = (e >= lo && e < hi) ? w[cs + e - first] : 0.0;
+    __syncthreads();
+    const int nl = np_chunk_leaves(m, gtail);
+    // every leaf held whole: 8 lanes per leaf (numpy's 8 accumulators), one leaf
+    // per 8 lanes and round
+    for (int L0 = 0; L0 < nl; L0 += 128) {
+        const int L = L0 + (t >> 3), k = t & 7;
+        const bool in = L < nl;
+        const int off = in ? np_leaf_off(m, gtail, L) : 0, len = in ? np_leaf_len(m, gtail, L) : 0;
+        const bool whole = in && off >= lo && off + len <= hi;
+        double r = 0.0;
+        const int full = len - len % 8;
+        if (whole && len >= 8) {
+            r = s_w[off + k] * s_w[off + k];
+            for (int i = 8 + k; i < full; i += 8) r += s_w[off + i] * s_w[off + i];
+        }
+        r += __shfl_xor(r, 1, 64);
+        r += __shfl_xor(r, 2, 64);
+        r += __shfl_xor(r, 4, 64);
+        if (whole && k == 0) {
+            double res = (len < 8) ? 0.0 : r;
+            for (int i = (len < 8) ? 0 : full; i < len; ++i) res += s_w[off + i] * s_w[off + i];
+            s_leaf[L] = res;
+        }
+    }
+    __syncthreads();
+    const int64_t cw0 = (first % kNpChunk == 0) ? c0 : c0 + 1;   // first chunk held whole
+    if (lo == 0 && hi == m) {
+        if (t == 0) rx->sums[c - cw0] = np_chunk_combine(s_leaf, m, gtail);
+    }
+    if (t == 0 && blockIdx.x == 0) {
+        const int64_t cl = ((first + n) % kNpChunk == 0 || first + n == N) ? c1 : c1 - 1;   // last held whole
+        rx->first_chunk = (int32_t)cw0;
+        rx->nsums = (int32_t)max<int64_t>(0, cl - cw0 + 1);
+    }
+    // the edges (thread 0: at most 128 leaves and 127 raw weights each)
+    if (t == 0) {
+        const bool head = c == c0 && lo > 0, tail = c == c1 && hi < m;
+        if (blockIdx.x == 0 && !head) rx->head.chunk = -1;
+        if (c == c1 && !tail) rx->tail.chunk = -1;
+        for (int side = 0; side < 2; ++side) {
+            if (!(side == 0 ? head : tail)) continue;
+            NpEdge &E = side == 0 ? rx->head : rx->tail;
+            const int p = side == 0 ? lo : hi;      // the cut, chunk-relative
+            int kc = 0;
+            while (kc + 1 < nl && np_leaf_off(m, gtail, kc + 1) <= p) ++kc;
+            const int off = np_leaf_off(m, gtail, kc), len = np_leaf_len(m, gtail, kc);
+            const bool inside = p > off && p < off + len;
+            E.chunk = (int32_t)c;
+            E.cut = inside ? kc : -1;
+            if (side == 0) {                         // leaves from the cut on
+                const int l0 = (p >= off + len) ? kc + 1 : (inside ? kc + 1 : kc);
+                E.leaf0 = l0;
+                E.nleaf = nl - l0;
+                E.rfrom = inside ? p - off : 0;
+                E.nraw = inside ? off + len - p : 0;
+            } else {                                 // leaves before the cut
+                const int l1 = inside ? kc : ((p >= off + len) ? kc + 1 : kc);
+                E.leaf0 = 0;
+                E.nleaf = l1;
+                E.rfrom = 0;
+                E.nraw = inside ? p - off : 0;
+            }
+            for (int j = 0; j < E.nleaf; ++j) E.leaf[j] = s_leaf[E.leaf0 + j];
+            for (int j = 0; j < E.nraw; ++j) E.raw[j] = s_w[off + E.rfrom + j];
+        }
+    }
+}
+
+hipError_t launch_np_shard(const double *w, int64_t n, int64_t first, int64_t n_global, const NpTailPlan *gtail,
+                           RankRecordX *rx, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t c0 = first / kNpChunk, c1 = (first + n - 1) / kNpChunk;
+    hipLaunchKernelGGL(k_np_shard, dim3((unsigned)(c1 - c0 + 1)), dim3(1024), 0, s, w, n, first, n_global, gtail, rx);
+    return hipGetLastError();
+}
 
 // numpy's pairwise_sum recursion (loops_utils.h.src) over the partial last chunk
 // of n elements: n > 128 splits at n2 = n / 2 rounded down to a multiple of 8;

@@ -124,6 +124,52 @@ struct RankRecord {
     int32_t pad;
 };
 
+constexpr int kMaxRanks = 16;
+
+// ---- exact-order reductions across shards (fs2_exact.hip) ----
+//
+// Python's sum over the global particle order, split over G shards: each rank
+// classifies its chain units against an estimate of the global prefix (its
+// shard's offset from the all-gathered tree totals) and exports its chain as a
+// list of fp64 adds ("ops": one per translation run, one per segment, one per
+// term of a unit evaluated term by term) that is exact for its true entry value.
+// Every rank folds all ranks' ops in shard order: the exact total, and the exact
+// chain value at its own first element, from which it walks its own units.
+constexpr int kChainOpsCap = 2046;
+struct ShardOrder {
+    int8_t r[kMaxRanks];     // rank holding shard q
+};
+struct ChainSummary {
+    int32_t nops;            // ops of this rank (> kChainOpsCap: overflow, not folded)
+    int32_t pad[3];
+    double ops[kChainOpsCap];
+};
+static_assert(sizeof(ChainSummary) == 16384, "ChainSummary layout");
+
+// numpy's np.sum(w'^2) over the global order: 8192-element chunks (the last one
+// partial: NpTailPlan of n_global), the chunk sums added in order.  A chunk cut by
+// a shard boundary is described by both ranks: the leaves each holds whole (their
+// sums) and the raw elements of the leaf the boundary cuts (< 128).
+constexpr int kShardChunks = 1024;          // whole chunks per rank (larger shards: tree mode)
+struct NpEdge {
+    int32_t chunk;           // global chunk index (-1: none)
+    int32_t leaf0, nleaf;    // leaves [leaf0, leaf0 + nleaf) of the chunk's plan held whole
+    int32_t cut;             // the leaf the boundary cuts (-1: the cut lies between leaves)
+    int32_t rfrom, nraw;     // raw elements [rfrom, rfrom + nraw) of leaf `cut` (leaf-relative)
+    int32_t pad[2];
+    double leaf[128];        // sums of leaves leaf0 ..
+    double raw[128];
+};
+struct RankRecordX {
+    RankRecord base;
+    int32_t nsums;           // chunks held whole, in order
+    int32_t first_chunk;     // global index of the first of them
+    int32_t pad[14];
+    NpEdge head, tail;       // the chunk cut by this shard's first / last boundary
+    double sums[kShardChunks];
+};
+static_assert(sizeof(RankRecordX) <= 16384, "RankRecordX fits an all-gather slot");
+
 // A transfer to one rank (fs2_resample.hip, "packing"): K particle headers (64 B
 // each), then one 32-bit entry per page-table row of each particle (S rows,
 // padded to 64 B), then the U distinct pages those rows name, then C
@@ -168,8 +214,6 @@ struct PackHeader {
     double x, y, yaw, w;
     int64_t pad;
 };
-
-constexpr int kMaxRanks = 16;
 
 // What this rank sends to one destination (k_pack_bounds): the run [i0, i1) of
 // local particles whose outputs may reach its shard [pa, pb), the exclusive
@@ -300,6 +344,8 @@ struct ReduceParams {
     const NpTailPlan *np_tail;   // exact: the partial last chunk's tree (null: none)
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
+    int32_t t_from_parts;    // k_finalize: t_local = tree sum of part_w (sharded exact mode)
+    double *est_base;        // k_global_total: the tree prefix of the shards before this one (nullable)
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
     uint64_t seed, scan;
     DevStats *stats;
@@ -422,8 +468,36 @@ struct ChainParams {
     double *total;           // nullable: the final value
     const DevStats *stats;
     double margin;           // relative bound on |estimate - chain| (doubled)
+    // sharded ranks (exact mode): the chain's first element is local element 0 only
+    // on the first shard; the estimates start from *est_base (the tree prefix of the
+    // shards before); local unit 0 is always listed; k_chain_walk exports the ops
+    // (ops_out) instead of walking, or walks from *s_entry
+    int32_t chain_first;
+    int32_t force_list0;
+    const double *est_base;
+    ChainSummary *ops_out;
+    const double *s_entry;
+    int32_t *uop;            // [nu] export: each listed unit's first op (by ordinal)
 };
 hipError_t launch_chain(const ChainParams &p, hipStream_t s, hipEvent_t e0 = nullptr);
+// sharded exact mode: the local units and their ops (k_chain_units + k_chain_walk export)
+hipError_t launch_chain_export(const ChainParams &p, hipStream_t s);
+// fold every rank's ops in shard order (all: [world] summaries, by rank): the total
+// into *total (nullable), the value before this rank's first element into *entry
+// (nullable)
+// (an overflowing summary writes nothing -- the tree estimates stay -- and counts
+// one reduce_amb)
+hipError_t launch_chain_fold(const ChainSummary *all, int32_t world, int32_t shard, const int8_t *rank_of,
+                             double *total, double *entry, DevStats *stats, hipStream_t s);
+// walk the local units from *p.s_entry (prefix mode: sentry / sout / c)
+hipError_t launch_chain_walk_from(const ChainParams &p, hipStream_t s);
+// numpy's Sigma w'^2 of this shard's chunks into *rx (sums of whole chunks, edges)
+hipError_t launch_np_shard(const double *w, int64_t n, int64_t first, int64_t n_global, const NpTailPlan *gtail,
+                           RankRecordX *rx, hipStream_t s);
+// all ranks' RankRecordX (by rank): N_eff from the exact Sigma w'^2, decision,
+// estimate, u0, tree offset (sharded exact mode's k_global_finalize)
+hipError_t launch_global_finalize_x(const ReduceParams &p, const RankRecordX *all, const NpTailPlan *gtail,
+                                    hipStream_t s);
 // numpy np.sum(w ** 2): 8192-element chunks (k_normalize leaves, k_finalize trees);
 // the partial last chunk's tree (NpTailPlan, fs2_chain.hpp) planned on the host
 bool np_tail_plan(int64_t n, NpTailPlan *out);

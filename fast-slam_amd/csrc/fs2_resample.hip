@@ -30,7 +30,10 @@ constexpr int kScanBlock = kBlock * kScanPer;     // 1024 elements per block
 // Weight total over ranks, in shard order (world > 1; totals are gathered by rank).
 __global__ void k_global_total(const ReduceParams P) {
     double t = 0.0;
-    for (int q = 0; q < P.world; ++q) t = (q == 0) ? P.totals[P.rank_of[0]] : t + P.totals[P.rank_of[q]];
+    for (int q = 0; q < P.world; ++q) {
+        if (q == P.shard && P.est_base) *P.est_base = t;     // sharded exact: the chain's estimate base
+        t = (q == 0) ? P.totals[P.rank_of[0]] : t + P.totals[P.rank_of[q]];
+    }
     P.stats->total = t;
 }
 
@@ -64,7 +67,7 @@ __device__ double pairwise_sq(const double *a, int64_t n) {
 }
 
 template <typename RecOf>
-__device__ void global_finalize_impl(const ReduceParams &P, RecOf rec);
+__device__ void global_finalize_impl(const ReduceParams &P, RecOf rec, const double *sq_exact = nullptr);
 
 // This rank's record: sum w'^2, first maximum, its pose, normalised total (on
 // one GPU also the global decision, k_global_finalize's work).
@@ -104,10 +107,11 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     // the normalise partials: every thread's loads issued first, so that their
     // latency overlaps the numpy trees below
     constexpr int PL = 4;
-    double s4[PL], w4[PL];
+    double s4[PL], w4[PL], t4[PL];
     int64_t i4[PL];
     int m4[PL];
-    double sq = 0.0;
+    double sq = 0.0, tw = 0.0;
+    __shared__ double s_tw, lds_t[16];
     double bv = -INFINITY;
     int64_t bi = INT64_MAX;
     int mc = 0;
@@ -117,6 +121,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
             const int k = k0 + 1024 * u;
             const bool in = k < P.nparts;
             s4[u] = in ? P.part_sq[k] : 0.0;
+            t4[u] = (in && P.t_from_parts) ? P.part_w[k] : 0.0;
             w4[u] = in ? P.part_best_w[k] : -INFINITY;
             i4[u] = in ? P.part_best_i[k] : INT64_MAX;
             m4[u] = in ? P.part_maxcnt[k] : 0;
@@ -126,6 +131,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
             sq += s4[u];
+            tw += t4[u];
             argmax_combine(bv, bi, w4[u], i4[u]);
             mc = max(mc, m4[u]);
         }
@@ -175,9 +181,11 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
     FS2_FIN(2);
     // the three block reductions behind one barrier (wave trees on DPP)
     sq = wave_sum(sq);
+    tw = wave_sum(tw);
     wave_argmax(bv, bi);
     mc = wave_max_i(mc);
     if (lane == 0) {
+        lds_t[wid] = tw;
         lds_d[wid] = sq;
         s_bv[wid] = bv;
         lds_l[wid] = bi;
@@ -190,12 +198,15 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
         bv = s_bv[0];
         bi = lds_l[0];
         mc = lds_i[0];
+        tw = lds_t[0];
 #pragma unroll
         for (int k = 1; k < 16; ++k) {
             sq += lds_d[k];
+            tw += lds_t[k];
             argmax_combine(bv, bi, s_bv[k], lds_l[k]);
             mc = max(mc, lds_i[k]);
         }
+        s_tw = tw;
     }
     FS2_FIN(4);
     if (threadIdx.x == 0) {
@@ -229,6 +240,9 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
             r.pose[2] = P.yaw[bi];
         }
         r.t_local = P.stats->t_local;
+        // sharded exact mode: a tree estimate of this shard's normalised total (the
+        // resample chain's estimate base; no local prefix is formed)
+        if (P.t_from_parts) r.t_local = s_tw;
         r.max_count = mc;
         *P.rec = r;
         FS2_FIN(6);
@@ -367,7 +381,7 @@ hipError_t launch_finalize(const ReduceParams &p, hipStream_t s) {
 // (:201-210), u0 (:183) and this rank's prefix offset, from all records (held
 // by rank; the sums run in shard order, the first maximum is order-free).
 template <typename RecOf>
-__device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
+__device__ void global_finalize_impl(const ReduceParams &P, RecOf rec, const double *sq_exact) {
     DevStats *st = P.stats;
     const int g0 = P.rank_of[0];
     double sq = rec(g0).sumsq;
@@ -387,6 +401,7 @@ __device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
         }
     }
     for (int q = 0; q < P.shard; ++q) off = (q == 0) ? rec(g0).t_local : off + rec(P.rank_of[q]).t_local;
+    if (sq_exact) sq = *sq_exact;
     const double ng = (double)P.n_global;
     const double ne = (sq < 1.0 / ng) ? ng : 1.0 / sq;
     st->sumsq = sq;
@@ -417,6 +432,53 @@ __device__ void global_finalize_impl(const ReduceParams &P, RecOf rec) {
 
 __global__ void k_global_finalize(const ReduceParams P) {
     global_finalize_impl(P, [&](int g) -> const RankRecord & { return P.recs[g]; });
+}
+
+// Sharded exact mode: np.sum(w'^2) over the global order (fast_slam_2.py:219) from
+// every shard's chunk sums, the chunks cut by shard boundaries completed from both
+// neighbours' edges (the cut leaf from their raw weights), added in order; then
+// the rest of k_global_finalize.  One thread.
+__global__ void k_global_finalize_x(const ReduceParams P, const RankRecordX *all, const NpTailPlan *gtail) {
+    double node[2 * kNpMaxLeaves];
+    double sq = 0.0;
+    bool any = false;
+    auto add = [&](double v) {
+        sq = any ? sq + v : v;
+        any = true;
+    };
+    for (int q = 0; q < P.world; ++q) {
+        const RankRecordX &X = all[P.rank_of[q]];
+        if (q > 0 && X.head.chunk >= 0) {
+            const NpEdge &T = all[P.rank_of[q - 1]].tail, &H = X.head;
+            const int64_t cs = (int64_t)H.chunk * kNpChunk;
+            const int m = (int)min<int64_t>(kNpChunk, P.n_global - cs);
+            const int nl = np_chunk_leaves(m, gtail);
+            bool ok = T.chunk == H.chunk;
+            for (int k = 0; k < nl; ++k) {
+                if (k >= T.leaf0 && k < T.leaf0 + T.nleaf) node[k] = T.leaf[k - T.leaf0];
+                else if (k >= H.leaf0 && k < H.leaf0 + H.nleaf) node[k] = H.leaf[k - H.leaf0];
+                else if (k == H.cut && k == T.cut && T.nraw + H.nraw == np_leaf_len(m, gtail, k))
+                    node[k] = np_leaf_seq([&](int i) { return i < T.nraw ? T.raw[i] : H.raw[i - T.nraw]; },
+                                          T.nraw + H.nraw);
+                else ok = false;
+            }
+            if (!ok) {                   // edges that do not fit together: counted, never hidden
+                P.stats->reduce_amb += 1;
+                P.stats->error_flags |= 4;
+                node[0] = 0.0;
+                for (int k = 1; k < nl; ++k) node[k] = 0.0;
+            }
+            add(np_chunk_combine(node, m, gtail));
+        }
+        for (int j = 0; j < X.nsums; ++j) add(X.sums[j]);
+    }
+    global_finalize_impl(P, [&](int g) -> const RankRecord & { return all[g].base; }, &sq);
+}
+
+hipError_t launch_global_finalize_x(const ReduceParams &p, const RankRecordX *all, const NpTailPlan *gtail,
+                                    hipStream_t s) {
+    hipLaunchKernelGGL(k_global_finalize_x, dim3(1), dim3(1), 0, s, p, all, gtail);
+    return hipGetLastError();
 }
 
 hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s) {
@@ -614,7 +676,8 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         const int32_t info = (k * kUnit < P.n) ? P.chain.uinfo[k] : 1;
         if (info & 1) {
             cv = (i < P.n) ? P.c[i] : 0.0;
-            cprev = (i > 0 && i - 1 < P.n) ? P.c[i - 1] : 0.0;
+            // (a sharded rank's first element: the chain value before it, k_chain_fold)
+            cprev = (i > 0 && i - 1 < P.n) ? P.c[i - 1] : (i == 0 && P.a > 0 ? P.stats->offset : 0.0);
         } else {
             const int E = unit_binade(info);
             const double u = unit_ulp(E);

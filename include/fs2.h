@@ -45,13 +45,16 @@ enum {
  * sum one particle at a time (:184-193) and sum(w^2) with numpy (:219-223). */
 enum {
     FS2_REDUCE_AUTO = 0,       /* one GPU: SEQUENTIAL up to 4096 particles, EXACT above;
-                                  sharded: PARALLEL (the sum spans ranks) */
+                                  sharded: EXACT when every shard holds >= 8192 particles
+                                  (and <= 8M), else PARALLEL */
     FS2_REDUCE_SEQUENTIAL = 1, /* the reference's summation orders, one lane */
     FS2_REDUCE_PARALLEL = 2,   /* fixed-order trees (deterministic, not the reference's
                                   rounding); fs2_iter_stats.reduce_ambiguous counts the
                                   decisions that rounding could flip */
     FS2_REDUCE_EXACT = 3       /* the reference's summation orders, bit-exact, evaluated by
-                                  parallel kernels (one GPU; sharded handles use PARALLEL) */
+                                  parallel kernels; sharded: across the ranks in the global
+                                  particle order (FS2_ERR_ARG at creation where shards are
+                                  too small: fewer than 8192 particles) */
 };
 
 enum { FS2_HOST = 0, FS2_DEVICE = 1 };   /* where caller buffers live */

@@ -117,6 +117,64 @@ def test_sharded_matches_single(G, N, L):
         h.close()
 
 
+@pytest.mark.parametrize("G,N,L", [(2, 20000, 24), (3, 30011, 20), (4, 40000, 16), (8, 70001, 12)])
+def test_sharded_exact_is_bitwise(G, N, L):
+    """EXACT reductions across shards: Python's sum of the weights
+    and the resample's running sum over the global order (every rank folds all
+    shards' chain ops), numpy's sum(w'^2) over the global 8192-chunks (the chunks a
+    shard boundary cuts completed from both neighbours' edges).  Every scan equals
+    a single GPU handle in exact mode -- itself bit-exact with the reference's
+    orders -- bit for bit: decisions, estimates, N_eff, every weight and pose, every
+    landmark; reduce_ambiguous is 0 (no tree anywhere).  Weights spread over many
+    binades (lognormal) so that the chains cross binades inside and across shards."""
+    import torch  # noqa: F401
+    import fast_slam_2
+    import fs2_synthetic as syn
+    from gpu_util import configure
+    configure()
+    wl = syn.Workload(N, L, seed=23)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    lm[:, :, 2] = lm[:, :, 5] = 0.01
+    wh = np.random.default_rng(5).lognormal(0.0, 2.0, N)
+    w = wh / wh.sum()
+    cnt = np.full(N, L, np.int32)
+    cap = L + 40
+    single = fast_slam_2.FastSLAM2(N, reduce="exact", record_assoc=True, seed=5, landmark_capacity=cap,
+                                   verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    key = os.urandom(128)
+    shards = [fast_slam_2.FastSLAM2(N, reduce="auto", record_assoc=True, seed=5, landmark_capacity=cap, rank=g,
+                                    world_size=G, comm_id=key, comm_mode="local", verbose=False) for g in range(G)]
+    for h in shards:
+        a, b = h.first_global, h.first_global + h.n_local
+        h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+    resamples = 0
+    for s in range(8):
+        rot, tr = syn.odometry(s)
+        ms = wl.measurements(s)
+        pre = _ordered(shards)
+        pose1, st1 = single.step(rot, tr, ms)
+        outs = _step_all(shards, rot, tr, ms)
+        for pose, st in outs:
+            assert st.reduce_ambiguous == 0 and st.error_flags == 0, s
+            assert st.resampled == st1.resampled, s
+            assert st.best_index == st1.best_index, s
+            assert st.n_eff == st1.n_eff, (s, st.n_eff, st1.n_eff)
+            assert st.total_weight == st1.total_weight, (s, st.total_weight, st1.total_weight)
+            assert np.array_equal(pose, pose1), s
+        resamples += st1.resampled
+        a1 = single.associations()
+        assert np.array_equal(a1, np.concatenate([h.associations() for h in pre], axis=1)), s
+        s1 = single.get_state(lm_cap=cap)
+        sg = _gather(shards, cap)
+        for k in range(6):
+            assert np.array_equal(s1[k], sg[k]), (s, k)
+    assert resamples >= 2
+    for h in shards + [single]:
+        h.close()
+
+
 def _follow_case(G, N, L, seed):
     """Rank 0's particles alone carry weight, its first 100 ten times more than
     the rest: its sources fill shard 0 with few (heavy) particles and the other
