@@ -353,6 +353,8 @@ def robustness(args, f, L, first_scan):
     g.close()
     out["sharded_local_g2"] = sharded_local(args, L, n)
     out["sharded_local_g8"] = sharded_local(args, L, n, G=8)
+    # the same with whole pages sent (round 3's transfer; A/B of the page references)
+    out["sharded_local_g8_pages"] = sharded_local(args, L, n, G=8, page_refs="off")
     out["dropin_iterate"] = dropin(args, L, n)
     out["dropin_iterate_host_rng"] = dropin(args, L, n, rng="numpy-host")
     return out
@@ -396,7 +398,7 @@ def dropin(args, L, n, scans=16, warm=4, rng="numpy"):
             "host_rng_ms": rng_ms, "rng": rng, "numpy_state_sha1": state_digest, "note": note}
 
 
-def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
+def sharded_local(args, L, n_total, G=2, scans=9, warm=3, page_refs="auto"):
     """The sharded path (fs2_comm.hpp) with G ranks as threads of this process on
     this GPU (in-process transport: device copies + host barriers), n_total
     particles in all: the per-scan time and the host time inside the transport
@@ -406,7 +408,8 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
     import fs2_synthetic as syn
     key = os.urandom(128)
     hs = [fast_slam_2.FastSLAM2(n_total, rng="device", seed=args.seed, landmark_capacity=L + scans + 8, rank=g,
-                                world_size=G, comm_id=key, comm_mode="local", verbose=False) for g in range(G)]
+                                world_size=G, comm_id=key, comm_mode="local", verbose=False, page_refs=page_refs)
+          for g in range(G)]
     for g, h in enumerate(hs):
         populate(h, h.n_local, L, args.seed, g)
     meas = {s: np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64) for s in range(scans)}
@@ -456,6 +459,10 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3):
             "pages_sent_before_fraction": (sum(p["sent_pages_repeat"] for p in profs) /
                                            sum(p["sent_pages"] for p in profs)
                                            if sum(p["sent_pages"] for p in profs) else None),
+            "page_refs": page_refs != "off",
+            # page_refs: remote pages the update passes copied (each with its 8 records)
+            "localized_pages_per_scan": sum(p["localized_pages"] for p in profs) / k,
+            "localized_bytes_per_scan": sum(p["localized_pages"] for p in profs) * (128 + 8 * 48) / k,
             "note": f"{G} ranks as threads on one GPU, in-process transport, {n_total} particles in all; "
                     "comm: host time in transport calls and mid-scan waits (a wait includes the collectives "
                     "queued before it)"}

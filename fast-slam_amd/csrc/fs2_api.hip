@@ -112,6 +112,7 @@ struct fs2_handle {
     SumFrame frame{-127.0f, 1.0f, 1.0f};         // summary grid (fs2_kernels.hpp), grown by imports
     float ext_seen = 0.0f;                 // largest |x|, |y| imported so far
     float *slb = nullptr;                  // device: lower bound on every nonzero mirror s
+    float *slb_pass = nullptr;             // device: slb at the start of the current update pass
     uint32_t *ext_dev = nullptr;           // device: import extent (float bits)
     size_t rdesc_cap = 0;
     int rows = 0;                          // page-table rows allocated
@@ -244,6 +245,16 @@ struct fs2_handle {
     // estimate of the chain before this shard, each listed unit's first op, and
     // numpy's plan of the global partial last chunk
     bool xsh_ok = false;
+    // page_refs mode (fs2_kernels.hpp PeerMaps): every rank's pools mapped here; the
+    // pages other ranks may reference stay alive through collective collections
+    bool refs = false;                     // the mode is on
+    bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
+    bool refs_live = false;                // a resample has exchanged references (no local collection)
+    PeerMaps peers_host{};
+    PeerMaps *peers_dev = nullptr;
+    uint8_t *ep_dev = nullptr, *epochs_dev = nullptr;     // this rank's / every rank's collection epoch
+    int64_t remote_rows = 0;               // upper bound on row entries naming remote pages (localisations)
+    bool collect_next = false;             // a collective collection before the next scan (published)
     ChainSummary *dch_send = nullptr, *dch_recv = nullptr;
     RankRecordX *recx = nullptr, *recxs = nullptr;
     double *est_base = nullptr;
@@ -251,7 +262,8 @@ struct fs2_handle {
     NpTailPlan *np_tail_g = nullptr;
 
     MapRef map() const {
-        return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb, row_boxes(cur)};
+        return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb, row_boxes(cur),
+                      refs_shared ? peers_dev : nullptr};
     }
     // row boxes of buffer b, while the maps fit them (fs2_kernels.hpp)
     uint32_t *row_boxes(int b) const { return rows <= kBBoxRows ? bbox[b] : nullptr; }
@@ -354,6 +366,13 @@ static int grow_rows(fs2_handle *h, int need_slots) {
     return FS2_OK;
 }
 
+static int refs_short(fs2_handle *h, const char *what) {
+    return set_err(&h->err, FS2_ERR_CAPACITY,
+                   "page_refs mode: the %s pool ran short between collective collections (pools shared with "
+                   "the other ranks cannot grow; size them with page_pool / record_pool)",
+                   what);
+}
+
 // Collect the page pool: every page the current page table does not refer to
 // becomes free (fs2_pages.hip); the reservation cursor restarts.  With
 // `records`, the record pool is collected from the same marks as well.
@@ -386,9 +405,60 @@ static int collect(fs2_handle *h, bool records) {
     return FS2_OK;
 }
 
+// page_refs mode: a collection every rank runs at the same scan (the decision is
+// in the all-gathered records, DevStats.collect_next).  Each rank's epoch reaches
+// every rank (an all-gather, after each reset its marks), every rank marks its own
+// pages and, in their owners' marks, the remote pages its rows name; a second
+// all-gather is the barrier before anyone sweeps.  Records as in collect(): the
+// remote-marked pages mark their records too.
+static int collect_collective(fs2_handle *h) {
+    hipStream_t s = h->stream;
+    const int G = h->cfg.world_size;
+    if (h->epoch == 255) {
+        HIP_TRY(h, hipMemsetAsync(h->mark, 0, (size_t)h->npool, s));
+        h->epoch = 0;
+    }
+    h->epoch += 1;
+    HIP_TRY(h, hipMemsetAsync(h->ep_dev, h->epoch, 1, s));
+    {
+        CommTimer ct(h);
+        const int rc = h->tp->allgather(h->ep_dev, h->epochs_dev, 1, s, &h->err);
+        if (rc) return rc;
+    }
+    HIP_TRY(h, launch_collect_mark(h->map(), h->cnt[h->cur], h->mark, h->epoch, h->epochs_dev, s));
+    {
+        CommTimer ct(h);
+        const int rc = h->tp->allgather(h->ep_dev, h->epochs_dev + kMaxRanks, 1, s, &h->err);
+        if (rc) return rc;
+    }
+    HIP_TRY(h, launch_collect_sweep(h->npool, h->mark, h->epoch, h->bcnt, h->freel, h->nfree_dev, s));
+    HIP_TRY(h, hipMemcpyAsync(&h->nfree, h->nfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (h->nrecs > 0) {
+        if (h->repoch == 255) {
+            HIP_TRY(h, hipMemsetAsync(h->rmark, 0, (size_t)h->nrecs, s));
+            h->repoch = 0;
+        }
+        h->repoch += 1;
+        HIP_TRY(h, launch_collect_records(h->pool, h->npool, h->mark, h->epoch, h->nrecs, h->rmark, h->repoch,
+                                          h->rbcnt, h->rfreel, h->rnfree_dev, s));
+        HIP_TRY(h, hipMemcpyAsync(&h->rnfree, h->rnfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (int rc = h->tp->status(&h->err)) return rc;
+    h->cursor = 0;
+    h->rcursor = 0;
+    h->collections += 1;
+    (void)G;
+    return FS2_OK;
+}
+
 // Pool of `pages` pages (existing pages keep their ids), its free list and marks.
 static int grow_pool(fs2_handle *h, int64_t pages) {
     if (pages <= h->npool) return FS2_OK;
+    if (h->refs_shared) return refs_short(h, "page");
+    if (h->refs && pages > (int64_t)kRefIdMask)
+        return set_err(&h->err, FS2_ERR_CAPACITY, "page_refs mode: %lld pages exceed the %u local page ids",
+                       (long long)pages, kRefIdMask);
     if (pages > (int64_t)kIdMask)
         return set_err(&h->err, FS2_ERR_OOM, "page pool of %lld pages exceeds the id space", (long long)pages);
     HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -421,6 +491,7 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
 // Record pool of `n` records (existing records keep their ids), free list, marks.
 static int grow_recs(fs2_handle *h, int64_t n) {
     if (n <= h->nrecs) return FS2_OK;
+    if (h->refs_shared) return refs_short(h, "record");
     if (n > (int64_t)kRecIdLimit)
         return set_err(&h->err, FS2_ERR_OOM, "record pool of %lld records exceeds the 32-bit id space",
                        (long long)n);
@@ -451,6 +522,7 @@ static int grow_recs(fs2_handle *h, int64_t n) {
 // reserves its records first: a record collection restarts the page cursor.
 static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
     if (h->cursor + need > h->nfree) {
+        if (h->refs_live) return refs_short(h, "page");
         int rc = collect(h, false);
         if (rc) return rc;
         if (need > h->nfree) {
@@ -467,6 +539,7 @@ static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
 
 static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
     if (h->rcursor + need > h->rnfree) {
+        if (h->refs_live) return refs_short(h, "record");
         int rc = collect(h, true);
         if (rc) return rc;
         if (need > h->rnfree) {
@@ -603,6 +676,92 @@ static void keep_shards(const fs2_handle *h, int G, At at, int keep_of[]) {
     for (uint32_t m = full; m; m &= ~(1u << pick[m])) keep_of[__builtin_popcount(m) - 1] = pick[m];
 }
 
+// page_refs mode, after the sizes: each particle sent is its header and its rows
+// as tagged descriptors (no page dedup, no page content, no second size round).
+static int exchange_refs(fs2_handle *h, ResampleParams &rs, const std::vector<int64_t> &mat, int keep,
+                         const int owner[], std::chrono::steady_clock::time_point t_start) {
+    const int G = h->cfg.world_size, R = h->cfg.rank;
+    hipStream_t s = h->stream;
+    auto at = [&](int from, int to, int f) { return mat[(size_t)from * kXrowWords * G + kXrowWords * to + f]; };
+    static const bool log_xfer = std::getenv("FS2_XFER_LOG") != nullptr;
+    size_t soff[kMaxRanks + 1] = {}, roff[kMaxRanks + 1] = {};
+    for (int p = 0; p < G; ++p) {
+        const bool so = p != keep && at(R, p, 0) > 0, ro = p != R && at(p, keep, 0) > 0;
+        soff[p + 1] = soff[p] + (so ? arena_align((size_t)xfer_ref_bytes(at(R, p, 0), at(R, p, 1))) : 0);
+        roff[p + 1] = roff[p] + (ro ? arena_align((size_t)xfer_ref_bytes(at(p, keep, 0), at(p, keep, 1))) : 0);
+    }
+    int rc = ensure_arena(h, h->sarena, h->scap, soff[G]);
+    if (!rc) rc = ensure_arena(h, h->rarena, h->rcap, roff[G]);
+    if (rc) return rc;
+    std::vector<fs2comm::Xfer> sends, recvs;
+    int64_t nsend = 0;
+    for (int p = 0; p < G; ++p) {
+        rs.sbuf[p] = nullptr;
+        const int64_t K = at(R, p, 0), S = at(R, p, 1);
+        if (log_xfer)
+            std::fprintf(stderr, "fs2 xfer (refs) scan %lld rank %d -> shard %d (rank %d)%s: %lld particles, %lld rows, %lld B\n",
+                         (long long)h->scan, R, p, owner[p], p == keep ? " kept" : "", (long long)K, (long long)S,
+                         (long long)(p == keep ? 0 : xfer_ref_bytes(K, S)));
+        if (p == keep || K == 0) continue;
+        rs.sbuf[p] = h->sarena + soff[p];
+        sends.push_back({owner[p], rs.sbuf[p], (size_t)xfer_ref_bytes(K, S)});
+        nsend += K;
+    }
+    if (nsend > INT32_MAX) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld particles to send", (long long)nsend);
+    HIP_TRY(h, launch_pack_refs(rs, s));
+    rs.npeers = 0;
+    int32_t kbase = 0;
+    for (int q = 0; q < G; ++q) {
+        if (q == R) continue;
+        const int64_t K = at(q, keep, 0), S = at(q, keep, 1);
+        if (!K) continue;
+        char *rb = h->rarena + roff[q];
+        recvs.push_back({q, rb, (size_t)xfer_ref_bytes(K, S)});
+        RecvPeer &pp = rs.peers[rs.npeers++];
+        pp = RecvPeer{};
+        pp.pre = reinterpret_cast<const RefPreamble *>(rb);
+        pp.hdr = reinterpret_cast<const PackHeader *>(rb + 64);
+        pp.refs = reinterpret_cast<const Desc *>(rb + 64 + 64 * K);
+        pp.K = (int32_t)K;
+        pp.kbase = kbase;
+        kbase += (int32_t)K;
+    }
+    {
+        CommTimer ct(h);
+        rc = h->tp->exchange(sends, recvs, s, &h->err);
+    }
+    if (rc) return rc;
+    h->n_recv = kbase;
+    h->u_recv = 0;
+    h->refs_live = true;
+    if (h->profiling) {
+        uint64_t np = 0, nr = 0, nb = 0;
+        for (int p = 0; p < G; ++p) {
+            if (p == keep) continue;
+            np += at(R, p, 0);
+            nr += at(R, p, 1);
+            nb += at(R, p, 0) ? xfer_ref_bytes(at(R, p, 0), at(R, p, 1)) : 0;
+        }
+        h->prof.migrations += np ? 1 : 0;
+        h->prof.sent_particles += np;
+        h->prof.sent_rows += nr;
+        h->prof.sent_bytes += nb;
+        h->prof.migrate_ms +=
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    rs.ao = shard_begin(h->n_global, G, keep);
+    if (h->follow) {
+        ResampleParams r2 = rs;
+        r2.ranges_mode = 2;
+        HIP_TRY(h, launch_resample_ranges(r2, s));
+    }
+    if (keep != h->shard) h->shard_moves += 1;
+    h->shard = keep;
+    h->first = rs.ao;
+    for (int q = 0; q < G; ++q) h->rank_of[q] = (int8_t)owner[q];
+    return FS2_OK;
+}
+
 // Sharded resample: plan what goes to every other rank on the device (one run of
 // local particles per destination, fs2_plan.hpp), all-gather the sizes and learn
 // them with a post; find the distinct pages of every destination's rows
@@ -654,6 +813,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         }
     }
     const int64_t nrows = T.ebase[G];
+    if (h->refs) return exchange_refs(h, rs, mat, keep, owner, t_start);
     if (nrows > 0) {
         int lg = 10;
         while ((int64_t(1) << lg) < 2 * nrows) ++lg;
@@ -846,6 +1006,15 @@ const char *fs2_last_error(const fs2_handle *h) {
 static void free_handle(fs2_handle *h) {
     if (!h) return;
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->refs_shared && h->tp) {
+        // page_refs: no rank frees its pools while another may still read them (an
+        // export of maps naming remote pages): every rank arrives, unmaps the others'
+        // pools, arrives again (a failed transport skips the rendezvous)
+        std::string e;
+        if (h->tp->allgather(h->ep_dev, h->epochs_dev, 1, h->stream, &e) == FS2_OK) hipStreamSynchronize(h->stream);
+        h->tp->unshare();
+        if (h->tp->allgather(h->ep_dev, h->epochs_dev, 1, h->stream, &e) == FS2_OK) hipStreamSynchronize(h->stream);
+    }
     for (int s = 0; s < 2; ++s) {
         hipFree(h->x[s]); hipFree(h->y[s]); hipFree(h->yaw[s]); hipFree(h->w[s]); hipFree(h->cnt[s]);
         hipFree(h->pt[s]);
@@ -857,7 +1026,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->sent_mask);
     hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
-    hipFree(h->slb); hipFree(h->ext_dev);
+    hipFree(h->slb); hipFree(h->slb_pass); hipFree(h->ext_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
@@ -870,6 +1039,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->urec); hipFree(h->sentry);
     hipFree(h->dch_send); hipFree(h->dch_recv); hipFree(h->recx); hipFree(h->recxs); hipFree(h->est_base);
     hipFree(h->uop); hipFree(h->np_tail_g);
+    hipFree(h->peers_dev); hipFree(h->ep_dev); hipFree(h->epochs_dev);
     hipFree(h->part_pose);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
@@ -956,6 +1126,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->nfree_dev, sizeof(int64_t)) == hipSuccess;
     ok &= alloc((void **)&h->rnfree_dev, sizeof(int64_t)) == hipSuccess;
     ok &= alloc((void **)&h->slb, sizeof(float)) == hipSuccess;
+    ok &= alloc((void **)&h->slb_pass, sizeof(float)) == hipSuccess;
     ok &= alloc((void **)&h->ext_dev, sizeof(uint32_t)) == hipSuccess;
     ok &= alloc((void **)&h->mlo, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
@@ -1086,9 +1257,22 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     // rank also room to receive half its shard's maps without sharing (the first
     // resamples, before the particles share ancestors), so that no resample
     // grows a pool (a large hipMalloc and copy: hundreds of ms)
+    // (page_refs mode: the same room serves the pages localised from other ranks)
     const int64_t recv_pages = G > 1 ? n / 2 * h->rows : 0;
     const int64_t recv_recs = G > 1 ? n / 2 * h->rows * kPageSlots : 0;
-    rc = grow_pool(h, cfg->page_pool > 0 ? cfg->page_pool : n * h->rows * 2 + 8 * n + recv_pages + 1024);
+    int64_t npages = cfg->page_pool > 0 ? cfg->page_pool : n * h->rows * 2 + 8 * n + recv_pages + 1024;
+    // page_refs mode (fs2.h): 2..15 ranks, local page ids below 2^27 (the rank tag
+    // above them); a default pool is clamped to the id space while it still holds
+    // the initial maps 1.25 times over, else the mode stays off (auto) or fails (on)
+    if (G > 1 && cfg->page_refs >= 0) {
+        const int64_t lim = (int64_t)kRefIdMask - 1024;
+        if (cfg->page_pool <= 0 && npages > lim && lim >= n * h->rows + n * h->rows / 4 + 8 * n) npages = lim;
+        h->refs = G <= kRefMaxRanks && npages <= lim;
+        if (cfg->page_refs == 1 && !h->refs)
+            return fail(set_err(&h->err, FS2_ERR_ARG, "page_refs: needs 2..%d ranks and a page pool below %lld pages",
+                                kRefMaxRanks, (long long)lim));
+    }
+    rc = grow_pool(h, npages);
     if (rc) return fail(rc);
     rc = grow_recs(h, cfg->record_pool > 0 ? cfg->record_pool
                                             : n * h->cap + n * h->cap / 4 + 64 * n + recv_recs + 1024);
@@ -1116,6 +1300,28 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
              : (cfg->comm_mode == FS2_COMM_SHM) ? fs2comm::create_shm(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err)
                                                  : fs2comm::create_rccl(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err);
         if (rc) return fail(rc);
+    }
+    if (h->refs) {
+        // every rank's page pool, record pool and page marks, mapped here (IPC; the
+        // ranks of one process share pointers); from now on the pools never move
+        void *ptrs[kMaxRanks] = {};
+        if (hipStreamSynchronize(h->stream) != hipSuccess)
+            return fail(set_err(&h->err, FS2_ERR_HIP, "initialisation sync failed"));
+        for (int what = 0; what < 3; ++what) {
+            void *base = what == 0 ? (void *)h->pool : what == 1 ? (void *)h->rpool : (void *)h->mark;
+            rc = h->tp->share(base, ptrs, &h->err);
+            if (rc) return fail(rc);
+            for (int q = 0; q < (int)G; ++q) {
+                if (what == 0) h->peers_host.pool[q] = (char *)ptrs[q];
+                else if (what == 1) h->peers_host.recs[q] = (char *)ptrs[q];
+                else h->peers_host.mark[q] = (uint8_t *)ptrs[q];
+            }
+        }
+        if (hipMalloc(&h->peers_dev, sizeof(PeerMaps)) != hipSuccess ||
+            hipMemcpy(h->peers_dev, &h->peers_host, sizeof(PeerMaps), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMalloc(&h->ep_dev, 64) != hipSuccess || hipMalloc(&h->epochs_dev, 2 * kMaxRanks) != hipSuccess)
+            return fail(set_err(&h->err, FS2_ERR_OOM, "page_refs tables"));
+        h->refs_shared = true;
     }
     if (hipStreamSynchronize(h->stream) != hipSuccess)
         return fail(set_err(&h->err, FS2_ERR_HIP, "initialisation sync failed"));
@@ -1258,7 +1464,15 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (drawn && (noise || u0))
         return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
     HIP_TRY(h, hipSetDevice(h->cfg.device));
-    int rc = grow_rows(h, h->cnt_upper + M);
+    int rc;
+    if (h->refs_shared && h->collect_next) {
+        // page_refs: some rank's pools ran short in the last scan (every rank read the
+        // same records, so every rank collects here, together)
+        rc = collect_collective(h);
+        if (rc) return rc;
+        h->collect_next = false;
+    }
+    rc = grow_rows(h, h->cnt_upper + M);
     if (rc) return rc;
     const int cur = h->cur;
     hipStream_t s = h->stream;
@@ -1326,6 +1540,16 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     up.wpart = h->wpart;
     up.cpart = h->cpart;
     up.stats = h->stats_dev;
+    up.slb_pass = h->slb_pass;
+    // page_refs: this scan may ask for a collective collection before the next one
+    // (its pools' room after this scan's reservations and localisations, at most
+    // the remote row entries, below twice as much again)
+    int32_t want_collect = 0;
+    if (h->refs_live) {
+        const int64_t pneed = (int64_t)std::max(M, 1) * h->n + h->remote_rows;
+        const int64_t rneed = (int64_t)std::max(M, 1) * h->n + (int64_t)kPageSlots * h->remote_rows;
+        want_collect = (h->nfree - h->cursor < 3 * pneed || h->rnfree - h->rcursor < 3 * rneed) ? 1 : 0;
+    }
     int passes = 0;
     uint64_t fixed_bytes = 0;
     for (int32_t k0 = 0; k0 < std::max(M, 1); k0 += kMaxM) {
@@ -1359,6 +1583,28 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         up.map = h->map();
         const bool first = k0 == 0, last = up.last_pass != 0;
         const bool cand = up.filter && up.blk1 > up.blk0;
+        if (h->refs_shared && h->remote_rows > 0 && up.blk1 > up.blk0) {
+            // page_refs: the remote pages this pass could read, localised first (from
+            // the free lists' tails, clear of every reservation this scan makes; a
+            // tail too short fails the scan loudly, fs2.h error_flags bit 3)
+            const int64_t left = (int64_t)std::max(M - k0 - up.m, 0) * h->n;   // later passes' reservations
+            LocalizeParams lp{};
+            lp.pcap = h->nfree - h->cursor - left;
+            lp.rcap = h->rnfree - h->rcursor - left;
+            lp.map = up.map;
+            lp.cnt = up.cnt;
+            lp.n = h->n;
+            lp.nblk = up.nblk;
+            lp.m = up.m;
+            lp.gate2f = up.gate2f;
+            lp.meas = up.meas;
+            lp.freel = h->freel;
+            lp.ftail = h->nfree;
+            lp.rfreel = h->rfreel;
+            lp.rtail = h->rnfree;
+            lp.stats = h->stats_dev;
+            HIP_TRY(h, launch_localize(lp, s));
+        }
         // a shard without particles launches nothing: its profiled intervals are
         // recorded empty here (fold_one reads every event of the set)
         if (prof && first && up.blk1 <= up.blk0)
@@ -1415,6 +1661,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rp.rec = h->rec;
     rp.recs = sh ? h->recs : h->rec;
     rp.totals = h->totals;
+    rp.want_collect = want_collect;
 
     const int nxt = 1 - cur;
     ResampleParams rs{};
@@ -1448,6 +1695,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rs.rec = h->rec;
     rs.flip_margin = flip_margin;
     rs.use_chain = exact ? 1 : 0;
+    rs.refs = h->refs ? 1 : 0;
     rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout};
 
     // weight total over all ranks (fast_slam_2.py:166).  Exact: Python's sum (in
@@ -1638,6 +1886,18 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     // a stream-ordered transport reports a failed collective only now
     if (h->tp && (rc = h->tp->status(&h->err))) return rc;
     const DevStats &st = *h->pub_stats;
+    if (h->refs_shared) {
+        // page_refs: the free lists' tails the localisations took; the remote row
+        // entries left (recounted by a resample's gather); a collective collection next?
+        h->nfree -= (int64_t)st.loc_pages;
+        h->rnfree -= (int64_t)st.loc_recs;
+        h->remote_rows = st.resampled ? (int64_t)st.remote_rows
+                                      : std::max<int64_t>(0, h->remote_rows - (int64_t)st.loc_pages);
+        h->collect_next = st.collect_next != 0;
+        if (h->profiling) {
+            h->prof.localized_pages += st.loc_pages;
+        }
+    }
     if (st.resampled) h->cur = 1 - h->cur;
     h->cnt_upper = st.max_count;
     h->last_m = M;
@@ -1679,6 +1939,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     }
     if (st.error_flags & 1)
         return set_err(&h->err, FS2_ERR_LINALG, "Singular matrix (landmark or observation covariance)");
+    if (st.error_flags & 8) return refs_short(h, "page or record");
     return FS2_OK;
 }
 

@@ -588,11 +588,12 @@ __global__ __launch_bounds__(kBlock) void k_cl_gather_maps(MapRef map, const int
     const int c = cnt[i];
     const int j0 = row * kPageSlots;
     if (j0 >= c) return;
-    const char *pg = page_of(map, j0, i);
+    const uint32_t e = pt_entry(map, row, i)->x;
+    const char *pg = page_ptr_any(map, e), *recs = recs_of(map, e);    // (a remote page: its rank's pools)
     double2 *o = out + off[i];
     for (int j = j0; j < min(c, j0 + kPageSlots); ++j) {      // position j holds slot mirror_slot
         const float4 mv = load_mirror(pg, j);
-        const Slot sl = load_rec(map.recs, mirror_rec(mv));
+        const Slot sl = load_rec(recs, mirror_rec(mv));
         o[mirror_slot(mv)] = make_double2(sl.mx, sl.my);
     }
 }

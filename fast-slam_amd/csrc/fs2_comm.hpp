@@ -65,6 +65,34 @@ class Transport {
                          hipStream_t s, std::string *err) = 0;
     // a failure inside a stream-ordered collective (after the call returned), else FS2_OK
     virtual int status(std::string *) { return FS2_OK; }
+    // page_refs mode, at creation (no collective in flight): every rank's base of one
+    // device allocation (hipMalloc base), mapped into this process -- peers[r] for
+    // rank r, this rank's own base at peers[rank()]; unmapped with the transport
+    virtual int share(void *base, void **peers, std::string *err) = 0;
+    void unshare() { close_handles(); }
+
+  protected:
+    std::vector<void *> opened_;     // IPC mappings to close
+    int open_handles(const std::vector<hipIpcMemHandle_t> &hs, void *base, void **peers, std::string *err) {
+        for (int p = 0; p < (int)hs.size(); ++p) {
+            if (p == rank()) {
+                peers[p] = base;
+                continue;
+            }
+            void *q = nullptr;
+            if (hipIpcOpenMemHandle(&q, hs[p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                if (err) *err = "hipIpcOpenMemHandle failed (page references across ranks)";
+                return FS2_ERR_COMM;
+            }
+            opened_.push_back(q);
+            peers[p] = q;
+        }
+        return FS2_OK;
+    }
+    void close_handles() {
+        for (void *q : opened_) hipIpcCloseMemHandle(q);
+        opened_.clear();
+    }
 };
 
 // ------------------------------------------------------------------ RCCL ---
@@ -87,7 +115,35 @@ class RcclTransport : public Transport {
     ncclComm_t comm = nullptr;
     int G = 1, r = 0;
     ~RcclTransport() override {
+        close_handles();
         if (comm) ncclCommDestroy(comm);
+    }
+    int share(void *base, void **peers, std::string *err) override {
+        hipIpcMemHandle_t mine;
+        if (hipIpcGetMemHandle(&mine, base) != hipSuccess) {
+            if (err) *err = "hipIpcGetMemHandle failed";
+            return FS2_ERR_COMM;
+        }
+        std::vector<hipIpcMemHandle_t> hs(G);
+        char *d = nullptr;
+        hipStream_t s = nullptr;
+        int rc = FS2_OK;
+        if (hipMalloc(&d, sizeof(hipIpcMemHandle_t) * (G + 1)) != hipSuccess ||
+            hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            rc = FS2_ERR_COMM;
+            if (err) *err = "IPC handle exchange buffers";
+        }
+        if (!rc && hipMemcpy(d, &mine, sizeof mine, hipMemcpyHostToDevice) != hipSuccess) rc = FS2_ERR_COMM;
+        if (!rc) {
+            ncclResult_t e = ncclAllGather(d, d + sizeof mine, sizeof mine, ncclUint8, comm, s);
+            if (e != ncclSuccess) rc = nccl_fail(e, err, "ncclAllGather (IPC handles)");
+        }
+        if (!rc && (hipStreamSynchronize(s) != hipSuccess ||
+                    hipMemcpy(hs.data(), d + sizeof mine, sizeof mine * G, hipMemcpyDeviceToHost) != hipSuccess))
+            rc = FS2_ERR_COMM;
+        if (s) hipStreamDestroy(s);
+        hipFree(d);
+        return rc ? rc : open_handles(hs, base, peers, err);
     }
     int world() const override { return G; }
     int rank() const override { return r; }
@@ -203,6 +259,15 @@ class LocalTransport : public Transport {
         return FS2_OK;
     }
 
+    // ranks are threads of this process: the bases themselves
+    int share(void *base, void **peers, std::string *err) override {
+        grp->send_ptr[r] = base;
+        if (!grp->barrier()) return fail(err, "share rendezvous timed out");
+        for (int p = 0; p < grp->G; ++p) peers[p] = const_cast<void *>(grp->send_ptr[p]);
+        if (!grp->barrier()) return fail(err, "share completion timed out");
+        return FS2_OK;
+    }
+
   private:
     static int fail(std::string *err, const char *what) {
         if (err) *err = std::string("local transport: ") + what;
@@ -299,6 +364,7 @@ class ShmTransport : public Transport {
     std::atomic<int> failed{0};
 
     ~ShmTransport() override {
+        close_handles();
         if (ag_send) hipHostFree(ag_send);
         if (ag_recv) hipHostFree(ag_recv);
         for (char *p : xs) if (p) hipHostFree(p);
@@ -352,6 +418,19 @@ class ShmTransport : public Transport {
         std::lock_guard<std::mutex> lk(fmu);
         if (err) *err = fmsg.empty() ? std::string("shm transport: another rank failed") : fmsg;
         return FS2_ERR_COMM;
+    }
+
+    // the handles through the all-gather slots, host-side (creation: nothing in flight)
+    int share(void *base, void **peers, std::string *err) override {
+        if (int rc = status(err)) return rc;
+        hipIpcMemHandle_t mine;
+        if (hipIpcGetMemHandle(&mine, base) != hipSuccess) return fail(err, "hipIpcGetMemHandle failed");
+        std::memcpy(slot(r), &mine, sizeof mine);
+        if (!wait(hdr->bar)) return fail(err, "share rendezvous failed or timed out");
+        std::vector<hipIpcMemHandle_t> hs(G);
+        for (int p = 0; p < G; ++p) std::memcpy(&hs[p], slot(p), sizeof mine);
+        if (!wait(hdr->bar)) return fail(err, "share completion failed or timed out");
+        return open_handles(hs, base, peers, err);
     }
 
     int allgather(const void *send, void *recv, size_t bytes, hipStream_t s, std::string *err) override {

@@ -90,7 +90,7 @@ struct DevStats {
     double t_local;          // sum of this rank's normalised weights (last local prefix)
     int32_t out_min, out_max;   // smallest / largest output index served by a local particle
     int32_t n_recv;          // particles received from other ranks by the resample
-    int32_t pad2;
+    int32_t collect_next;    // page_refs: some rank asked for a collective collection before the next scan
     unsigned long long reduce_amb;   // tree reductions: resample boundaries / the N_eff rule within
                                      // the rounding bound of the reference's summation order
     unsigned long long opened;       // pages whose mirrors k_candidates loaded
@@ -99,6 +99,9 @@ struct DevStats {
     unsigned long long repeat_pages; // sharded: distinct pages sent that went to the same rank before
                                      // (since this rank's last collection; what a receiver-side page
                                      // cache could skip)
+    unsigned long long loc_pages;    // page_refs: remote pages localised (free-list tail consumed)
+    unsigned long long loc_recs;     //            records taken for them
+    unsigned long long remote_rows;  //            a resample's outputs: row entries naming remote pages
 };
 
 // numpy's np.sum over 8192-element buffers (fs2_exact.hip).  The recursion over a
@@ -121,7 +124,7 @@ struct RankRecord {
     double pose[3];
     double t_local;          // local normalised total (prefix end)
     int32_t max_count;
-    int32_t pad;
+    int32_t want_collect;    // page_refs: this rank's pools run short (collective collection next scan)
 };
 
 constexpr int kMaxRanks = 16;
@@ -226,11 +229,24 @@ struct PackPlan {
     int64_t pa, pb;
 };
 
+// page_refs mode: a transfer is this preamble, the K headers, then every row of
+// the particles as a descriptor naming the page where it lives (rank tag)
+struct RefPreamble {
+    float slb;               // the sender's lower bound on its mirrors' s (the receiver lowers its own)
+    float org, cell, icell;  // the sender's summary grid: its boxes' codes are converted outwards
+    int32_t rank;
+    int32_t pad[11];
+};
+static_assert(sizeof(RefPreamble) == 64, "RefPreamble layout");
+__host__ __device__ inline int64_t xfer_ref_bytes(int64_t K, int64_t S) { return 64 + K * 64 + S * 8; }
+
 struct RecvPeer {
     const PackHeader *hdr;   // K headers
     const uint32_t *idx;     // row entries
     const XferPage *pages;   // U distinct pages
     const double2 *covs;     // their covariances that differ from the initial one (2 per)
+    const Desc *refs;        // page_refs mode: the rows' descriptors (tagged)
+    const RefPreamble *pre;  // page_refs mode: the sender's preamble
     int32_t K;               // particles from this peer
     int32_t kbase;           // index of its first particle among all received
     int64_t U;               // distinct pages from this peer
@@ -264,6 +280,30 @@ struct MeasPack {
     float fe[kMaxM];              // >= |ox - fx|, |oy - fy| (rounded up)
 };
 
+// Page references across ranks (sharded "page_refs" mode): a
+// resample sends the page-table rows of the particles that change ranks, not
+// their pages.  A descriptor whose page lives on rank q carries the tag q + 1 in
+// bits kRefShift..30 (never the owned bit: a remote page is never written in
+// place); local pages have tag 0 (local ids < 2^kRefShift in this mode).  Every
+// rank maps every other rank's page pool, record pool and page marks (IPC), and
+// localises a remote page -- copies it and its records into its own pools --
+// before a kernel of the update pass could read it (k_localize: the pages the
+// measurement bands leave open, and the row an append may write), so the update
+// kernels only ever see local pages; the cold readers (export, clustering,
+// collection marks) follow tags through PeerMaps.  A rank keeps the pages other
+// ranks reference alive: collections are collective in this mode (every rank
+// marks its remote references into the owners' marks before anyone sweeps).
+constexpr int kRefShift = 27;
+constexpr uint32_t kRefIdMask = (1u << kRefShift) - 1u;
+constexpr int kRefMaxRanks = 15;
+struct PeerMaps {
+    char *pool[kMaxRanks];           // every rank's page pool (this rank's own included)
+    char *recs[kMaxRanks];           // record pools
+    uint8_t *mark[kMaxRanks];        // page marks (collection)
+};
+__host__ __device__ inline uint32_t ref_tag(uint32_t e) { return (e & 0x80000000u) ? 0u : (e >> kRefShift) & 15u; }
+__host__ __device__ inline uint32_t ref_id(uint32_t e) { return (e & 0x80000000u) ? (e & 0x7fffffffu) : (e & kRefIdMask); }
+
 // The maps of one particle buffer: page pool + page table.
 struct MapRef {
     char *pool;              // page id p at pool + p * kPageBytes
@@ -274,6 +314,7 @@ struct MapRef {
     SumFrame frame;          // summary grid of the descriptors
     float *slb;              // lower bound on every nonzero mirror s (lowered by every write)
     uint32_t *bbox;          // [nblocks][kBBoxRows] workgroup row boxes (null: rows > kBBoxRows)
+    const PeerMaps *peers;   // page_refs mode: every rank's pools (device memory); null otherwise
 };
 
 // Free pages and records reserved for one launch: lane i's t-th new page is
@@ -315,6 +356,10 @@ struct UpdateParams {
     unsigned long long *cpart;   // [kNumCounters][nblk] block counters
     DevStats *stats;
     MeasPack meas;
+    // k_candidates stores the slb its bands used; k_update's overflow scan tests page
+    // boxes with it (exact: its pages' mirrors predate the pass), so it opens no page
+    // those bands rejected -- none that k_localize left remote (page_refs mode)
+    float *slb_pass;
 };
 
 struct ReduceParams {
@@ -345,6 +390,7 @@ struct ReduceParams {
     double flip_margin;      // tree mode: relative rounding bound for reduce_amb (0: off)
     double *part_w;          // [nparts] block sums of the normalised weights (k_normalize)
     int32_t t_from_parts;    // k_finalize: t_local = tree sum of part_w (sharded exact mode)
+    int32_t want_collect;    // into this rank's record (page_refs mode)
     double *est_base;        // k_global_total: the tree prefix of the shards before this one (nullable)
     const double *u0_host;   // nullable: injected u0 value lives here (device copy)
     uint64_t seed, scan;
@@ -424,6 +470,10 @@ struct ResampleParams {
     // received particles
     int32_t npeers;
     RecvPeer peers[kMaxRanks];
+    // page_refs mode: rows travel as tagged descriptors (k_pack_refs / k_unpack_refs),
+    // an output owns a page only when its source fills one output in all (a page sent
+    // by reference must not be written in place on the sender)
+    int32_t refs;
 };
 
 // A 64-term chain unit that is not one translation, as up to kChainSegs
@@ -536,6 +586,28 @@ hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
 hipError_t launch_pack_dedup(const ResampleParams &p, hipStream_t s);
 // headers, row entries and pages into sbuf (sizes from the all-gathered xrow)
 hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s);
+// page_refs mode: preamble, headers and tagged row descriptors into sbuf (transfer bases)
+hipError_t launch_pack_refs(const ResampleParams &p, hipStream_t s);
+// page_refs mode, before an update pass reads the maps: every remote page the
+// measurement bands leave open (and the row an append may write) copied with its
+// records into this rank's pools, from the free lists' tails (DevStats loc_*)
+struct LocalizeParams {
+    MapRef map;
+    const int32_t *cnt;
+    int64_t n;
+    int64_t nblk;
+    int32_t m;
+    float gate2f;
+    MeasPack meas;
+    const uint32_t *freel;
+    int64_t ftail;           // free pages [.., ftail): the k-th localised page is freel[ftail - 1 - k]
+    const uint32_t *rfreel;
+    int64_t rtail;           // records: the k-th localised page's slot j -> rfreel[rtail - 1 - (8 k + j)]
+    int64_t pcap, rcap;      // pages / records the tails may give (past them: error_flags bit 3, the
+                             // pass's update kernels exit at once, the scan fails)
+    DevStats *stats;
+};
+hipError_t launch_localize(const LocalizeParams &p, hipStream_t s);
 // estimate: also this rank's post-resample record (k_estimate); one GPU leaves
 // it to launch_tail_single
 hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStream_t s);
@@ -590,6 +662,12 @@ hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s);
 hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark,
                           uint8_t epoch, int64_t *bcnt, uint32_t *freel, int64_t *nfree_dev,
                           hipStream_t s);
+// the two halves of launch_collect for a collective collection (page_refs mode:
+// every rank marks, a barrier, every rank sweeps); epochs: every rank's epoch
+hipError_t launch_collect_mark(MapRef map, const int32_t *cnt, uint8_t *mark, uint8_t epoch, const uint8_t *epochs,
+                               hipStream_t s);
+hipError_t launch_collect_sweep(int64_t npool, uint8_t *mark, uint8_t epoch, int64_t *bcnt, uint32_t *freel,
+                                int64_t *nfree_dev, hipStream_t s);
 // after launch_collect with the same (mark, epoch): mark every record a live page
 // refers to, then list every unmarked record of [0, nrecs) in rfreel
 hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,

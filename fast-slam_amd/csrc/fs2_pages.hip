@@ -32,19 +32,32 @@ int64_t collect_blocks(int64_t npool) { return (npool + kSweepBlock - 1) / kSwee
 // One lane per particle; its page-table entries are loaded 8 at a time (a mark
 // store may alias them, so one load per iteration would pay a full memory
 // latency per row).
+// page_refs mode (map.peers, epochs: every rank's epoch of this collective
+// collection): a remote page is marked in its owner's marks.
 __global__ __launch_bounds__(kBlock) void k_mark(const MapRef map, const int32_t *cnt, uint8_t *mark,
-                                                 uint8_t epoch) {
+                                                 uint8_t epoch, const uint8_t *epochs) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= map.n) return;
     const int rows = (cnt[i] + kPageSlots - 1) / kPageSlots;
+    bool remote = false;
     for (int r0 = 0; r0 < rows; r0 += 8) {
         uint32_t e[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) e[u] = pt_entry(map, min(r0 + u, rows - 1), i)->x;
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (r0 + u < rows) mark[e[u] & kIdMask] = epoch;
+        for (int u = 0; u < 8; ++u) {
+            if (r0 + u >= rows) continue;
+            const uint32_t t = map.peers ? ref_tag(e[u]) : 0u;
+            if (t) {
+                map.peers->mark[t - 1][ref_id(e[u])] = epochs[t - 1];
+                remote = true;
+            } else {
+                mark[e[u] & kIdMask] = epoch;
+            }
+        }
     }
+    // marks in other ranks' memory reach it before this rank's barrier
+    if (__any(remote)) __threadfence_system();
 }
 
 __device__ __forceinline__ int wave_incl_scan_int(int v) {
@@ -229,12 +242,29 @@ hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t
     return hipGetLastError();
 }
 
+hipError_t launch_collect_mark(MapRef map, const int32_t *cnt, uint8_t *mark, uint8_t epoch, const uint8_t *epochs,
+                               hipStream_t s) {
+    if (map.n > 0)
+        hipLaunchKernelGGL(k_mark, dim3((unsigned)((map.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, map,
+                           cnt, mark, epoch, epochs);
+    return hipGetLastError();
+}
+
+hipError_t launch_collect_sweep(int64_t npool, uint8_t *mark, uint8_t epoch, int64_t *bcnt, uint32_t *freel,
+                                int64_t *nfree_dev, hipStream_t s) {
+    const int64_t nb = collect_blocks(npool);
+    hipLaunchKernelGGL(k_sweep_count, dim3((unsigned)nb), dim3(kBlock), 0, s, mark, npool, epoch, bcnt);
+    hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, nfree_dev);
+    hipLaunchKernelGGL(k_sweep_write, dim3((unsigned)nb), dim3(kBlock), 0, s, mark, npool, epoch, bcnt, freel);
+    return hipGetLastError();
+}
+
 hipError_t launch_collect(MapRef map, const int32_t *cnt, int64_t npool, uint8_t *mark, uint8_t epoch,
                           int64_t *bcnt, uint32_t *freel, int64_t *nfree_dev, hipStream_t s) {
     const int64_t nb = collect_blocks(npool);
     if (map.n > 0)
         hipLaunchKernelGGL(k_mark, dim3((unsigned)((map.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, map,
-                           cnt, mark, epoch);
+                           cnt, mark, epoch, nullptr);
     hipLaunchKernelGGL(k_sweep_count, dim3((unsigned)nb), dim3(kBlock), 0, s, mark, npool, epoch, bcnt);
     hipLaunchKernelGGL(k_sweep_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, nfree_dev);
     hipLaunchKernelGGL(k_sweep_write, dim3((unsigned)nb), dim3(kBlock), 0, s, mark, npool, epoch, bcnt, freel);

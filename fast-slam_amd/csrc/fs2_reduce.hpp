@@ -299,6 +299,18 @@ __device__ __forceinline__ char *page_of(const MapRef &m, int j, int64_t i) {
     return page_ptr(m.pool, pt_entry(m, j / kPageSlots, i)->x);
 }
 
+// Cold readers in page_refs mode (fs2_kernels.hpp PeerMaps): the page a
+// descriptor names on whichever rank holds it, and that rank's record pool (the
+// records a page's mirrors name live with the page).
+__device__ __forceinline__ const char *page_ptr_any(const MapRef &m, uint32_t e) {
+    const uint32_t t = m.peers ? ref_tag(e) : 0u;
+    return t ? m.peers->pool[t - 1] + (int64_t)ref_id(e) * kPageBytes : page_ptr(m.pool, e);
+}
+__device__ __forceinline__ const char *recs_of(const MapRef &m, uint32_t e) {
+    const uint32_t t = m.peers ? ref_tag(e) : 0u;
+    return t ? m.peers->recs[t - 1] : m.recs;
+}
+
 __device__ __forceinline__ float4 load_mirror(const char *page, int j) {
     return reinterpret_cast<const float4 *>(page)[j & (kPageSlots - 1)];
 }
@@ -586,7 +598,7 @@ __device__ __forceinline__ Desc note_write(const MapRef &m, int j, int64_t i, co
 __device__ __forceinline__ void refresh_summary(const MapRef &m, int row, int64_t i, int c) {
     Desc *pe = pt_entry(m, row, i);
     const uint32_t e = pe->x;
-    const float4 *mir = reinterpret_cast<const float4 *>(page_ptr(m.pool, e));
+    const float4 *mir = reinterpret_cast<const float4 *>(page_ptr_any(m, e));   // (page_refs: maybe remote)
     *pe = describe_page(e, mir, min(kPageSlots, c - row * kPageSlots), m.frame);
 }
 

@@ -244,6 +244,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const ReduceParams P) {
         // resample chain's estimate base; no local prefix is formed)
         if (P.t_from_parts) r.t_local = s_tw;
         r.max_count = mc;
+        r.want_collect = P.want_collect;
         *P.rec = r;
         FS2_FIN(6);
         // one GPU: no record exchange (the record from registers)
@@ -415,8 +416,12 @@ __device__ void global_finalize_impl(const ReduceParams &P, RecOf rec, const dou
     if (P.flip_margin > 0.0 && fabs(ne - ng / 2.0) <= P.flip_margin * ng) st->reduce_amb += 1;
     // the largest map on any rank: a resample may bring it here (the receiver
     // sizes its page-table rows for it before unpacking)
-    int mc = rec(0).max_count;
-    for (int g = 1; g < P.world; ++g) mc = max(mc, rec(g).max_count);
+    int mc = rec(0).max_count, wc = rec(0).want_collect;
+    for (int g = 1; g < P.world; ++g) {
+        mc = max(mc, rec(g).max_count);
+        wc |= rec(g).want_collect;
+    }
+    st->collect_next = wc;
     st->max_count = max(st->max_count, mc);
     st->best_index = bi;
     st->best_w = bv;
@@ -1182,17 +1187,100 @@ hipError_t launch_pack_write(const ResampleParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- apply ----
-
-#ifndef FS2_NT_GATHER
-#define FS2_NT_GATHER 1        // the gather's page-table stores non-temporal (A/B: scan -3%)
-#endif
-
 __device__ __forceinline__ int peer_of(const ResampleParams &P, int k) {
     int p = 0;
     while (p + 1 < P.npeers && k >= P.peers[p + 1].kbase) ++p;
     return p;
 }
+
+// page_refs mode: every row of every particle sent, as a descriptor naming the
+// page where it lives (this rank's pages get this rank's tag; a page this rank
+// holds by reference keeps its owner's tag), never owned.  One thread per
+// (particle, row), rows over grid y; thread (0, 0) writes each destination's
+// preamble (this rank's slb and summary grid).
+__global__ __launch_bounds__(kBlock) void k_pack_refs(const ResampleParams P) {
+    const int64_t i = P.xt.i_lo + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int k = blockIdx.y;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < (unsigned)P.world) {
+        const int p = threadIdx.x;
+        if (p != P.keep && P.plan[p].K > 0) {
+            RefPreamble pre{};
+            pre.slb = *P.map.slb;
+            pre.org = P.map.frame.org;
+            pre.cell = P.map.frame.cell;
+            pre.icell = P.map.frame.icell;
+            pre.rank = P.rank;
+            *reinterpret_cast<RefPreamble *>(P.sbuf[p]) = pre;
+        }
+    }
+    if (i >= P.xt.i_hi || i >= P.n) return;
+    const int c = P.cnt[i];
+    if (k * kPageSlots >= c || P.mlo[i] > P.mhi[i]) return;
+    Desc d = *pt_entry(P.map, k, i);
+    const uint32_t t = ref_tag(d.x);
+    d.x = ((t ? t : (uint32_t)P.rank + 1u) << kRefShift) | ref_id(d.x);
+    const int64_t c_i = P.iblk[P.nblk + i / kScanBlock] + P.rank_e[i];
+    for (int p = 0; p < P.world; ++p) {
+        const PackPlan &pl = P.plan[p];
+        if (p == P.keep || i < pl.i0 || i >= pl.i1) continue;
+        reinterpret_cast<Desc *>(P.sbuf[p] + 64 + 64 * pl.K)[c_i - pl.c0 + k] = d;
+    }
+}
+
+hipError_t launch_pack_refs(const ResampleParams &p, hipStream_t s) {
+    const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
+    if (g) {
+        // headers after each destination's preamble
+        ResampleParams ph = p;
+        for (int q = 0; q < p.world; ++q)
+            if (ph.sbuf[q]) ph.sbuf[q] += 64;
+        hipLaunchKernelGGL(k_pack_headers, dim3(g), dim3(kBlock), 0, s, ph);
+    }
+    const int64_t span = p.xt.i_hi - p.xt.i_lo;
+    if (span > 0 && p.map.rows > 0)
+        hipLaunchKernelGGL(k_pack_refs, dim3((unsigned)((span + kBlock - 1) / kBlock), (unsigned)p.map.rows),
+                           dim3(kBlock), 0, s, p);
+    else if (p.world > 0)
+        hipLaunchKernelGGL(k_pack_refs, dim3(1, 1), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
+// A box's codes on another rank's summary grid, re-coded outwards on this one's
+// (the sender's bounds are exact in fp32; sum_lo / sum_hi round outwards).
+__device__ __forceinline__ uint32_t recode_box(uint32_t b, const RefPreamble &pre, const SumFrame &f) {
+    if (b == kSumOpen) return b;
+    const SumFrame g{pre.org, pre.cell, pre.icell};
+    if (g.org == f.org && g.cell == f.cell) return b;
+    return sum_lo(f, sum_lo_val(g, b & 0xffu)) | (sum_hi(f, sum_hi_val(g, (b >> 8) & 0xffu)) << 8) |
+           (sum_lo(f, sum_lo_val(g, (b >> 16) & 0xffu)) << 16) | (sum_hi(f, sum_hi_val(g, b >> 24)) << 24);
+}
+
+// page_refs mode: the received particles' rows (rdesc) from their tagged
+// descriptors -- a page of this rank's comes home untagged (not owned), the
+// boxes re-coded on this rank's grid; slb lowered to each sender's.
+__global__ __launch_bounds__(kBlock) void k_unpack_refs(const ResampleParams P, int32_t nrecv) {
+    const int r = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nrecv) return;
+    const int q = peer_of(P, r);
+    const RecvPeer &pp = P.peers[q];
+    const PackHeader &h = pp.hdr[r - pp.kbase];
+    const RefPreamble pre = *pp.pre;
+    const int rows = (h.cnt + kPageSlots - 1) / kPageSlots;
+    for (int k = lane; k < rows; k += 64) {
+        Desc d = pp.refs[h.soff + k];
+        if (ref_tag(d.x) == (uint32_t)P.rank + 1u) d.x = ref_id(d.x);
+        d.y = recode_box(d.y, pre, P.map.frame);
+        P.rdesc[(int64_t)r * P.map.rows + k] = d;
+    }
+    lower_slb(P.map.slb, pre.slb);
+}
+
+// ---------------------------------------------------------------- apply ----
+
+#ifndef FS2_NT_GATHER
+#define FS2_NT_GATHER 1        // the gather's page-table stores non-temporal (A/B: scan -3%)
+#endif
 
 // outputs filled by received particles
 __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P, int32_t nrecv) {
@@ -1330,7 +1418,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             w = P.w[s];
             c = P.cnt[s];
             const int64_t lo = max((int64_t)P.mlo[s], P.ao), hi = min((int64_t)P.mhi[s], P.ao + n - 1);
-            keep = (hi == lo) ? 0xffffffffu : kIdMask;
+            // (page_refs: only a source with one output in all keeps its pages -- a row
+            // also sent to another rank is referenced there)
+            keep = (P.refs ? P.mlo[s] == P.mhi[s] : hi == lo) ? 0xffffffffu : kIdMask;
             src = pt_entry(P.map, 0, s);
             stride = n;
         } else {
@@ -1360,6 +1450,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     // (one per iteration would pay a full memory latency per row); the loop runs
     // over the wave's longest map so that every lane takes part in the row unions
     const int wrows = wave_max_i(rows);
+    unsigned nremote = 0;            // page_refs: row entries naming another rank's page
     for (int k0 = 0; k0 < wrows; k0 += 8) {
         Desc e[8];
 #pragma unroll
@@ -1368,6 +1459,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         for (int u = 0; u < 8; ++u) {
             if (k0 + u < rows) {
                 e[u].x &= keep;
+                if (P.refs && ref_tag(e[u].x)) ++nremote;
 #if FS2_NT_GATHER
                 __builtin_nontemporal_store(((unsigned long long)e[u].y << 32) | e[u].x,
                                             reinterpret_cast<unsigned long long *>(P.opt + (int64_t)(k0 + u) * n + m));
@@ -1402,6 +1494,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             nsb += s_wc[w];
         }
         if (first) s_sb[off + __popcll(fm & ((1ull << lane) - 1ull))] = s_src[t];
+    }
+    if (P.refs) {
+        const unsigned long long br = block_sum_u64<kBlock>(nremote, lds_u);
+        if (threadIdx.x == 0 && br) atomicAdd(&P.stats->remote_rows, br);
+        __syncthreads();             // lds_u is reused below
     }
     // per-block partials (no same-address atomics), folded by estimate_body
     const unsigned long long bs = block_sum_u64<kBlock>(slots, lds_u);
@@ -1517,10 +1614,16 @@ hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStre
     }
     if (nrecv > 0) {
         hipLaunchKernelGGL(k_scatter_recv, dim3((nrecv + kBlock - 1) / kBlock), dim3(kBlock), 0, s, p, nrecv);
-        if (nu > 0)
-            hipLaunchKernelGGL(k_unpack_pages, dim3((unsigned)((nu * kPageSlots + kBlock - 1) / kBlock)), dim3(kBlock),
-                               0, s, p, nu);
-        hipLaunchKernelGGL(k_unpack_rows, dim3((nrecv + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, s, p, nrecv);
+        if (p.refs) {
+            hipLaunchKernelGGL(k_unpack_refs, dim3((nrecv + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, s, p,
+                               nrecv);
+        } else {
+            if (nu > 0)
+                hipLaunchKernelGGL(k_unpack_pages, dim3((unsigned)((nu * kPageSlots + kBlock - 1) / kBlock)),
+                                   dim3(kBlock), 0, s, p, nu);
+            hipLaunchKernelGGL(k_unpack_rows, dim3((nrecv + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, s, p,
+                               nrecv);
+        }
     }
     hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
     if (estimate) hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);

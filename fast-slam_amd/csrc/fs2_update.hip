@@ -90,6 +90,7 @@ __device__ __forceinline__ void sort8(uint64_t (&e)[8]) {
 
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
+    if (P.stats->error_flags & 8) return;     // page_refs: localisation failed, the scan fails
     __shared__ uint64_t s_list[kMaxCand][kBlock];
     __shared__ Band s_band[MAXM];
     __shared__ uint16_t s_rows[kBBoxRows];      // rows the row boxes leave open, ascending
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const MapRef map = P.map;
     const Desc *ptrow = map.pt + (live ? i : 0);
     const float slb = *map.slb;
+    if (blockIdx.x == 0 && tid == 0 && P.slb_pass) *P.slb_pass = slb;
     const int rlast = map.rows - 1;
     // Each measurement's band (gate_band): a page whose box, or a slot whose
     // mirror, lies beyond it in x or in y is rejected by integer / one-compare
@@ -258,6 +260,7 @@ static __device__ __forceinline__ uint32_t sel_u32(int t, const uint32_t (&a)[K]
 // (or past an overflowing candidate list) every slot takes the exact path.
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
+    if (P.stats->error_flags & 8) return;     // page_refs: localisation failed, the scan fails
     __shared__ Meas s_ms[MAXM];                 // this pass's measurements
     __shared__ double s_lik[MAXM][kBlock];      // per (measurement, lane) likelihood
     __shared__ int16_t s_idx[MAXM][kBlock];     // per (measurement, lane) association (slot < 4096, -1, -2)
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         // slots modified so far are tested with their new states.  A singular
         // covariance counts only below the match, where the reference would meet it.
         const int rows = (c + kPageSlots - 1) / kPageSlots;
-        const float slb = *map.slb;
+        const float slb = P.slb_pass ? *P.slb_pass : *map.slb;
         // each measurement's smallest matching slot and its position live in LDS
         // (registers are k_update's occupancy limit)
 #pragma unroll
@@ -821,6 +824,159 @@ hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0, hi
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ k_localize ---
+//
+// page_refs mode (fs2_kernels.hpp PeerMaps): before an update pass, every row
+// entry naming another rank's page that the pass could read -- its box inside
+// some measurement's band (the pages k_candidates opens and, a fortiori, those
+// k_update's overflow scan opens: page_reject never keeps a page the bands
+// reject) or the partly filled last row (an append writes there) -- is copied
+// into this rank's pools: the 8 mirrors, each live slot's record into a fresh
+// record (its mirror renamed), the page owned by the particle (its own copy).
+// Rows the workgroup row boxes reject are skipped like k_candidates skips them.
+// Pages and records come from the free lists' tails, one atomic per workgroup.
+template <int MAXM>
+__global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
+    __shared__ Band s_band[MAXM];
+    __shared__ uint16_t s_rows[kBBoxRows];
+    __shared__ int s_wc[kBlock / 64];
+    __shared__ unsigned long long s_base;
+    const int tid = threadIdx.x;
+    const int64_t blk = blockIdx.x;
+    const int64_t i = blk * kBlock + tid;
+    const bool live = i < P.n;
+    const MapRef map = P.map;
+    const int c = live ? P.cnt[i] : 0;
+    if (tid < MAXM) {
+        Band b = band_none();
+#pragma unroll
+        for (int k = 0; k < MAXM; ++k)
+            if (tid == k && k < P.m) b = gate_band(P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], *map.slb, P.gate2f, map.frame);
+        s_band[tid] = b;
+    }
+    __syncthreads();
+    uint32_t bc[MAXM];
+#pragma unroll
+    for (int k = 0; k < MAXM; ++k) bc[k] = __builtin_amdgcn_readfirstlane(s_band[k].cx | (s_band[k].cy << 16));
+    const bool use_bb = map.bbox != nullptr;
+    int nrows = map.rows;
+    if (use_bb) {
+        bool pass = false;
+        if (tid < map.rows) pass = box_open_mask<MAXM>(map.bbox[blk * kBBoxRows + tid], bc, P.m) != 0u;
+        const uint64_t bm = __ballot(pass);
+        const int wid = tid >> 6, lane = tid & 63;
+        if (lane == 0) s_wc[wid] = __popcll(bm);
+        __syncthreads();
+        int off = 0;
+        nrows = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            off += (w < wid) ? s_wc[w] : 0;
+            nrows += s_wc[w];
+        }
+        if (pass) s_rows[off + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)tid;
+        __syncthreads();
+    }
+    const int arow = (c % kPageSlots) ? c / kPageSlots : -1;     // an append may write this row
+    auto row_at = [&](int q) -> int { return use_bb ? (int)s_rows[q] : q; };
+    // the row entries of this lane to localise: the open rows' remote pages, then
+    // the append row when it is remote and not among them
+    auto wanted = [&](int r, const Desc &d) -> bool {
+        return r * kPageSlots < c && ref_tag(d.x) != 0u && (box_open_mask<MAXM>(d.y, bc, P.m) != 0u || r == arow);
+    };
+    int need = 0;
+    bool arow_seen = false;
+    if (live) {
+        for (int q = 0; q < nrows; ++q) {
+            const int r = row_at(q);
+            if (r * kPageSlots >= c) continue;
+            const Desc d = *pt_entry(map, r, i);
+            if (wanted(r, d)) {
+                ++need;
+                arow_seen |= r == arow;
+            }
+        }
+        if (arow >= 0 && !arow_seen && ref_tag(pt_entry(map, arow, i)->x) != 0u) ++need;
+    }
+    // this workgroup's pages: one atomic, then each lane's run
+    const int wid = tid >> 6, lane = tid & 63;
+    int incl = need;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    __syncthreads();
+    if (lane == 63) s_wc[wid] = incl;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        woff += (w < wid) ? s_wc[w] : 0;
+        tot += s_wc[w];
+    }
+    if (tid == 0) {
+        s_base = tot ? atomicAdd(&P.stats->loc_pages, (unsigned long long)tot) : 0ull;
+        if (tot) atomicAdd(&P.stats->loc_recs, (unsigned long long)tot * kPageSlots);
+        // the tails would run into this scan's reservations: nothing localised, the
+        // pass's update kernels exit, the scan reports it (never a remote page read
+        // through the local pool)
+        if (tot && ((int64_t)(s_base + tot) > P.pcap || (int64_t)(s_base + tot) * kPageSlots > P.rcap)) {
+            atomicOr(&P.stats->error_flags, 8);
+            s_base = ~0ull;
+        }
+    }
+    __syncthreads();
+    if (!need || s_base == ~0ull) return;
+    int64_t k = (int64_t)s_base + woff + incl - need;            // this lane's first localised page
+    auto localize = [&](int r, Desc d) {
+        const uint32_t t = ref_tag(d.x);
+        const float4 *src = reinterpret_cast<const float4 *>(map.peers->pool[t - 1] + (int64_t)ref_id(d.x) * kPageBytes);
+        const char *srecs = map.peers->recs[t - 1];
+        const uint32_t id = P.freel[P.ftail - 1 - k];
+        const int valid = min(kPageSlots, c - r * kPageSlots);
+        float4 mv[kPageSlots];
+#pragma unroll
+        for (int u = 0; u < kPageSlots; ++u) mv[u] = src[u];
+        Slot sl[kPageSlots];
+#pragma unroll
+        for (int u = 0; u < kPageSlots; ++u) sl[u] = load_rec(srecs, u < valid ? mirror_rec(mv[u]) : mirror_rec(mv[0]));
+        float4 *dst = reinterpret_cast<float4 *>(page_ptr(map.pool, id));
+#pragma unroll
+        for (int u = 0; u < kPageSlots; ++u) {
+            if (u < valid) {
+                const uint32_t rid = P.rfreel[P.rtail - 1 - (kPageSlots * k + u)];
+                double2 *q = reinterpret_cast<double2 *>(map.recs + (int64_t)rid * kRecBytes);
+                q[0] = make_double2(sl[u].mx, sl[u].my);
+                q[1] = make_double2(sl[u].P.a00, sl[u].P.a01);
+                q[2] = make_double2(sl[u].P.a10, sl[u].P.a11);
+                mv[u].w = __uint_as_float(rid);
+            } else {
+                mv[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);         // past the map: no record named
+            }
+            dst[u] = mv[u];
+        }
+        *pt_entry(map, r, i) = make_uint2(id | kOwned, d.y);
+        ++k;
+    };
+    for (int q = 0; q < nrows; ++q) {
+        const int r = row_at(q);
+        if (r * kPageSlots >= c) continue;
+        const Desc d = *pt_entry(map, r, i);
+        if (wanted(r, d)) localize(r, d);
+    }
+    if (arow >= 0 && !arow_seen) {
+        const Desc d = *pt_entry(map, arow, i);
+        if (ref_tag(d.x) != 0u) localize(arow, d);
+    }
+}
+
+hipError_t launch_localize(const LocalizeParams &p, hipStream_t s) {
+    if (p.nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_localize<kMaxM>, dim3((unsigned)p.nblk), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------ generator test hooks --
 
 __global__ __launch_bounds__(kBlock) void k_debug_philox(int64_t n, const uint32_t *ctr, const uint32_t *key,
@@ -1181,8 +1337,10 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
         const int64_t p = e / lm_cap;
         const int j = (int)(e % lm_cap);
         if (j >= cnt[first + p]) continue;
-        const float4 mv = load_mirror(page_of(map, j, first + p), j);    // position j holds slot mirror_slot
-        const Slot s = load_rec(map.recs, mirror_rec(mv));
+        // position j holds slot mirror_slot (a remote page: its rank's pools)
+        const uint32_t pe = pt_entry(map, j / kPageSlots, first + p)->x;
+        const float4 mv = load_mirror(page_ptr_any(map, pe), j);
+        const Slot s = load_rec(recs_of(map, pe), mirror_rec(mv));
         double *d = stage + (p * lm_cap + mirror_slot(mv)) * 6;
         d[0] = s.mx; d[1] = s.my;
         d[2] = s.P.a00; d[3] = s.P.a01; d[4] = s.P.a10; d[5] = s.P.a11;

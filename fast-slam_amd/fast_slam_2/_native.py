@@ -56,6 +56,8 @@ class fs2_config(C.Structure):
         ("sharded_path", C.c_int32),
         ("page_pool", C.c_int64),
         ("record_pool", C.c_int64),
+        ("page_refs", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 
@@ -119,6 +121,7 @@ class fs2_profile(C.Structure):
         ("model_cow", C.c_uint64),
         ("model_fixed_bytes", C.c_uint64),
         ("model_box_bytes", C.c_uint64),
+        ("localized_pages", C.c_uint64),
     ]
 
     def as_dict(self):

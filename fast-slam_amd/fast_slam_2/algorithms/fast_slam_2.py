@@ -42,7 +42,7 @@ class FastSLAM2:
                  landmark_capacity: int = 64, rank: int = 0, world_size: int = 1,
                  comm_id: bytes | None = None, verbose: bool = True, gate_filter: bool = True,
                  comm_mode: str = "rccl", sharded_path: bool = False, page_pool: int = 0,
-                 record_pool: int = 0):
+                 record_pool: int = 0, page_refs: str = "auto"):
         lib = nat.load()
         cfg = nat.default_config()
         cfg.num_particles = int(config.NUM_PARTICLES if num_particles is None else num_particles)
@@ -68,6 +68,8 @@ class FastSLAM2:
         cfg.sharded_path = 1 if sharded_path else 0
         cfg.page_pool = int(page_pool)          # initial pool sizes (0: defaults; fs2.h)
         cfg.record_pool = int(record_pool)
+        # sharded resample: pages by reference ("on"), by content ("off"); fs2.h page_refs
+        cfg.page_refs = {"auto": 0, "on": 1, "off": -1}[page_refs]
         if rng not in ("numpy", "numpy-host", "device"):
             raise ValueError("rng must be 'numpy', 'numpy-host' or 'device'")
         self._rng = rng

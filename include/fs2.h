@@ -97,6 +97,14 @@ typedef struct fs2_config {
                                        frees too little */
     int64_t record_pool;            /* initial slot-record pool (48 B each); 0 = 1.25x the
                                        initial capacity plus 64 per particle */
+    int32_t page_refs;              /* sharded resample: 0 = auto (on for 2..15 ranks), 1 = on,
+                                       -1 = off.  On: a particle that changes ranks travels as its
+                                       page-table row of references to pages on the rank that
+                                       holds them (every rank maps the others' pools, IPC); the
+                                       receiver copies a page when the update pass first needs
+                                       it.  Off: each destination gets each distinct page's
+                                       content */
+    int32_t reserved0;
 } fs2_config;
 
 typedef struct fs2_iter_stats {
@@ -172,6 +180,8 @@ typedef struct fs2_profile {
     uint64_t model_cow;         /* pages copied before their first write */
     uint64_t model_fixed_bytes; /* k_update's per-particle bytes (scalars, ids, counts) */
     uint64_t model_box_bytes;   /* row-box bytes (k_candidates reads, k_update reads + writes) */
+    uint64_t localized_pages;   /* page_refs: remote pages copied into this rank's pools before an
+                                   update pass read them (with their records: 128 + 8 x 48 B each) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */

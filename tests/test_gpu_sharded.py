@@ -175,6 +175,94 @@ def test_sharded_exact_is_bitwise(G, N, L):
         h.close()
 
 
+def _run_sharded(G, N, L, scans, page_refs, seed=21, page_pool=0, record_pool=0):
+    """G local ranks over the peaked workload, each scan checked against a single
+    handle (decisions, estimates, associations; states within 1e-9); returns the
+    ranks' profiles and last stats."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    wl = syn.Workload(N, L, seed=seed)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    lm[:, :, 2] = lm[:, :, 5] = 0.01
+    w = np.full(N, 1.0 / N)
+    cnt = np.full(N, L, np.int32)
+    cap = L + 4 * scans + 8
+    single = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap,
+                                   verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    key = os.urandom(128)
+    shards = [fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap, rank=g,
+                                    world_size=G, comm_id=key, comm_mode="local", verbose=False, page_refs=page_refs,
+                                    page_pool=page_pool, record_pool=record_pool) for g in range(G)]
+    for h in shards:
+        a, b = h.first_global, h.first_global + h.n_local
+        h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+        h.set_profiling(True)
+    resamples = 0
+    for s in range(scans):
+        rot, tr = syn.odometry(s)
+        ms = wl.measurements(s)
+        pre = _ordered(shards)
+        pose1, st1 = single.step(rot, tr, ms)
+        outs = _step_all(shards, rot, tr, ms)
+        for pose, st in outs:
+            assert st.error_flags == 0, s
+            assert st.resampled == st1.resampled and st.best_index == st1.best_index, s
+            assert np.allclose(pose, pose1, rtol=1e-9, atol=1e-12), s
+            assert st.reduce_ambiguous == 0, s
+        resamples += st1.resampled
+        assert np.array_equal(single.associations(), np.concatenate([h.associations() for h in pre], axis=1)), s
+        if s % 4 == 3 or s == scans - 1:
+            s1 = single.get_state(lm_cap=cap)
+            sg = _gather(shards, cap)
+            assert np.array_equal(s1[4], sg[4]), s
+            for k in range(4):
+                assert np.allclose(s1[k], sg[k], rtol=1e-9, atol=1e-15), (s, k)
+            assert np.allclose(s1[5], sg[5], rtol=1e-9, atol=1e-12), s
+    profs = [h.profile() for h in shards]
+    last = [h.last_stats for h in shards]
+    for h in shards + [single]:
+        h.close()
+    return resamples, profs, last
+
+
+@pytest.mark.parametrize("G,N,L", [(2, 6000, 40), (8, 16384, 20)])
+def test_page_refs_vs_whole_pages(G, N, L):
+    """The sharded resample sending page-table rows of references (page_refs, the
+    default) against sending each distinct page's content: both equal the single
+    handle every scan; references move far fewer bytes at the resamples, and the
+    update passes localise the remote pages they open (k_localize)."""
+    from gpu_util import configure
+    configure()
+    r1, on, _ = _run_sharded(G, N, L, 10, "on")
+    r0, off, _ = _run_sharded(G, N, L, 10, "off")
+    assert r1 == r0 >= 2
+    b_on, b_off = sum(p["sent_bytes"] for p in on), sum(p["sent_bytes"] for p in off)
+    assert sum(p["migrations"] for p in on) >= 2
+    assert 0 < b_on * 4 < b_off, (b_on, b_off)
+    assert sum(p["localized_pages"] for p in on) > 0
+    assert sum(p["localized_pages"] for p in off) == 0
+
+
+def test_page_refs_collective_collections():
+    """page_refs with pools just above the maps: after references cross ranks no
+    rank may collect alone (another rank's rows name its pages), so every
+    collection is collective (DevStats.collect_next from the all-gathered records);
+    30 scans with collections and growing maps still equal the single handle."""
+    from gpu_util import configure
+    configure()
+    G, N, L = 3, 4500, 12
+    n = N // G
+    rows = (L + 4 * 30 + 8 + 7) // 8
+    resamples, profs, last = _run_sharded(G, N, L, 30, "on", seed=77, page_pool=n * rows * 2 + 16 * n,
+                                          record_pool=n * rows * 8 * 2 + 64 * n)
+    assert resamples >= 3
+    cols = [st.collections for st in last]
+    assert min(cols) >= 10 and len(set(cols)) == 1, cols      # together, many times
+    assert sum(p["localized_pages"] for p in profs) > 0
+
+
 def _follow_case(G, N, L, seed):
     """Rank 0's particles alone carry weight, its first 100 ten times more than
     the rest: its sources fill shard 0 with few (heavy) particles and the other
