@@ -405,6 +405,30 @@ static int collect(fs2_handle *h, bool records) {
     return FS2_OK;
 }
 
+// page_refs mode, at the first scan (every rank takes part: the ranks of one
+// process are created one after the other, so creation cannot wait for them):
+// every rank's page pool, record pool and page marks, mapped here (IPC; the ranks
+// of one process share pointers).  From now on the pools never move.
+static int share_pools(fs2_handle *h) {
+    const int G = h->cfg.world_size;
+    void *ptrs[kMaxRanks] = {};
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    for (int what = 0; what < 3; ++what) {
+        void *base = what == 0 ? (void *)h->pool : what == 1 ? (void *)h->rpool : (void *)h->mark;
+        CommTimer ct(h);
+        const int rc = h->tp->share(base, ptrs, &h->err);
+        if (rc) return rc;
+        for (int q = 0; q < G; ++q) {
+            if (what == 0) h->peers_host.pool[q] = (char *)ptrs[q];
+            else if (what == 1) h->peers_host.recs[q] = (char *)ptrs[q];
+            else h->peers_host.mark[q] = (uint8_t *)ptrs[q];
+        }
+    }
+    HIP_TRY(h, hipMemcpy(h->peers_dev, &h->peers_host, sizeof(PeerMaps), hipMemcpyHostToDevice));
+    h->refs_shared = true;
+    return FS2_OK;
+}
+
 // page_refs mode: a collection every rank runs at the same scan (the decision is
 // in the all-gathered records, DevStats.collect_next).  Each rank's epoch reaches
 // every rank (an all-gather, after each reset its marks), every rank marks its own
@@ -1006,10 +1030,12 @@ const char *fs2_last_error(const fs2_handle *h) {
 static void free_handle(fs2_handle *h) {
     if (!h) return;
     if (h->stream) hipStreamSynchronize(h->stream);
-    if (h->refs_shared && h->tp) {
+    if (h->refs_shared && h->tp && !h->tp->in_process()) {
         // page_refs: no rank frees its pools while another may still read them (an
         // export of maps naming remote pages): every rank arrives, unmaps the others'
-        // pools, arrives again (a failed transport skips the rendezvous)
+        // pools, arrives again (a failed transport skips the rendezvous).  Ranks that
+        // are threads of one process are closed one by one: their caller closes them
+        // after the last export
         std::string e;
         if (h->tp->allgather(h->ep_dev, h->epochs_dev, 1, h->stream, &e) == FS2_OK) hipStreamSynchronize(h->stream);
         h->tp->unshare();
@@ -1301,28 +1327,10 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
                                                  : fs2comm::create_rccl(cfg->comm_id, (int)G, (int)r, &h->tp, &h->err);
         if (rc) return fail(rc);
     }
-    if (h->refs) {
-        // every rank's page pool, record pool and page marks, mapped here (IPC; the
-        // ranks of one process share pointers); from now on the pools never move
-        void *ptrs[kMaxRanks] = {};
-        if (hipStreamSynchronize(h->stream) != hipSuccess)
-            return fail(set_err(&h->err, FS2_ERR_HIP, "initialisation sync failed"));
-        for (int what = 0; what < 3; ++what) {
-            void *base = what == 0 ? (void *)h->pool : what == 1 ? (void *)h->rpool : (void *)h->mark;
-            rc = h->tp->share(base, ptrs, &h->err);
-            if (rc) return fail(rc);
-            for (int q = 0; q < (int)G; ++q) {
-                if (what == 0) h->peers_host.pool[q] = (char *)ptrs[q];
-                else if (what == 1) h->peers_host.recs[q] = (char *)ptrs[q];
-                else h->peers_host.mark[q] = (uint8_t *)ptrs[q];
-            }
-        }
-        if (hipMalloc(&h->peers_dev, sizeof(PeerMaps)) != hipSuccess ||
-            hipMemcpy(h->peers_dev, &h->peers_host, sizeof(PeerMaps), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMalloc(&h->ep_dev, 64) != hipSuccess || hipMalloc(&h->epochs_dev, 2 * kMaxRanks) != hipSuccess)
-            return fail(set_err(&h->err, FS2_ERR_OOM, "page_refs tables"));
-        h->refs_shared = true;
-    }
+    if (h->refs &&
+        (hipMalloc(&h->peers_dev, sizeof(PeerMaps)) != hipSuccess || hipMalloc(&h->ep_dev, 64) != hipSuccess ||
+         hipMalloc(&h->epochs_dev, 2 * kMaxRanks) != hipSuccess))
+        return fail(set_err(&h->err, FS2_ERR_OOM, "page_refs tables"));
     if (hipStreamSynchronize(h->stream) != hipSuccess)
         return fail(set_err(&h->err, FS2_ERR_HIP, "initialisation sync failed"));
     *out = h;
@@ -1465,6 +1473,10 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     int rc;
+    if (h->refs && !h->refs_shared) {
+        rc = share_pools(h);
+        if (rc) return rc;
+    }
     if (h->refs_shared && h->collect_next) {
         // page_refs: some rank's pools ran short in the last scan (every rank read the
         // same records, so every rank collects here, together)

@@ -70,6 +70,8 @@ class Transport {
     // rank r, this rank's own base at peers[rank()]; unmapped with the transport
     virtual int share(void *base, void **peers, std::string *err) = 0;
     void unshare() { close_handles(); }
+    // ranks are threads of one process (their handles are closed one after another)
+    virtual bool in_process() const { return false; }
 
   protected:
     std::vector<void *> opened_;     // IPC mappings to close
@@ -259,6 +261,7 @@ class LocalTransport : public Transport {
         return FS2_OK;
     }
 
+    bool in_process() const override { return true; }
     // ranks are threads of this process: the bases themselves
     int share(void *base, void **peers, std::string *err) override {
         grp->send_ptr[r] = base;
