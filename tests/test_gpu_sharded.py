@@ -259,7 +259,8 @@ def test_page_refs_collective_collections():
                                           record_pool=n * rows * 8 * 2 + 64 * n)
     assert resamples >= 3
     cols = [st.collections for st in last]
-    assert min(cols) >= 10 and len(set(cols)) == 1, cols      # together, many times
+    # two at creation, then (after references cross ranks) collective ones, together
+    assert min(cols) >= 5 and len(set(cols)) == 1, cols
     assert sum(p["localized_pages"] for p in profs) > 0
 
 
