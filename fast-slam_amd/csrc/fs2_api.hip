@@ -1294,6 +1294,9 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         const int64_t lim = (int64_t)kRefIdMask - 1024;
         if (cfg->page_pool <= 0 && npages > lim && lim >= n * h->rows + n * h->rows / 4 + 8 * n) npages = lim;
         h->refs = G <= kRefMaxRanks && npages <= lim;
+        // pools shared with the peers never grow: room for a few more scans of
+        // reservations between the collective collections
+        if (h->refs && cfg->page_pool <= 0) npages = std::min(lim, npages + 24 * n);
         if (cfg->page_refs == 1 && !h->refs)
             return fail(set_err(&h->err, FS2_ERR_ARG, "page_refs: needs 2..%d ranks and a page pool below %lld pages",
                                 kRefMaxRanks, (long long)lim));
@@ -1301,7 +1304,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     rc = grow_pool(h, npages);
     if (rc) return fail(rc);
     rc = grow_recs(h, cfg->record_pool > 0 ? cfg->record_pool
-                                            : n * h->cap + n * h->cap / 4 + 64 * n + recv_recs + 1024);
+                                            : n * h->cap + n * h->cap / 4 + 64 * n + recv_recs + 1024 +
+                                                  (h->refs ? 24 * n : 0));
     if (rc) return fail(rc);
     if (G > 1) {
         // the sharded resample's buffers, made here rather than in a timed scan: the
@@ -1557,7 +1561,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     // (its pools' room after this scan's reservations and localisations, at most
     // the remote row entries, below twice as much again)
     int32_t want_collect = 0;
-    if (h->refs_live) {
+    if (h->refs) {              // (also before references cross: this scan's resample may send them)
         const int64_t pneed = (int64_t)std::max(M, 1) * h->n + h->remote_rows;
         const int64_t rneed = (int64_t)std::max(M, 1) * h->n + (int64_t)kPageSlots * h->remote_rows;
         want_collect = (h->nfree - h->cursor < 3 * pneed || h->rnfree - h->rcursor < 3 * rneed) ? 1 : 0;
