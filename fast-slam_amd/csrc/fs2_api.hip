@@ -87,6 +87,77 @@ struct ProfEvents {
     int used = 0;            // sets holding a scan not yet folded
 };
 
+// Device memory that grows in place: a virtual range reserved
+// once, physical chunks mapped at its end as the pool grows (hipMemCreate /
+// hipMemMap / hipMemSetAccess), so a growth copies nothing and the pool's address
+// never changes.  Handles whose pools are shared with other ranks by IPC
+// (page_refs) use plain allocations instead.
+struct GrowMem {
+    char *base = nullptr;
+    size_t reserved = 0, mapped = 0, gran = 0;
+    int device = 0;
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
+};
+static hipMemAllocationProp gm_prop(int device) {
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    return prop;
+}
+static bool gm_init(GrowMem &g, int device, size_t max_bytes) {
+    hipMemAllocationProp prop = gm_prop(device);
+    size_t gran = 0;
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran)
+        return false;
+    const size_t r = (max_bytes + gran - 1) / gran * gran;
+    void *p = nullptr;
+    if (hipMemAddressReserve(&p, r, 0, nullptr, 0) != hipSuccess || !p) return false;
+    g.base = static_cast<char *>(p);
+    g.reserved = r;
+    g.gran = gran;
+    g.device = device;
+    return true;
+}
+static hipError_t gm_grow(GrowMem &g, size_t bytes) {
+    const size_t want = (bytes + g.gran - 1) / g.gran * g.gran;
+    if (want <= g.mapped) return hipSuccess;
+    if (want > g.reserved) return hipErrorOutOfMemory;
+    const size_t delta = want - g.mapped;
+    hipMemAllocationProp prop = gm_prop(g.device);
+    hipMemGenericAllocationHandle_t hd{};
+    hipError_t e = hipMemCreate(&hd, delta, &prop, 0);
+    if (e != hipSuccess) return e;
+    e = hipMemMap(g.base + g.mapped, delta, 0, hd, 0);
+    if (e != hipSuccess) {
+        hipMemRelease(hd);
+        return e;
+    }
+    hipMemAccessDesc ad{};
+    ad.location = prop.location;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(g.base + g.mapped, delta, &ad, 1);
+    if (e != hipSuccess) {
+        hipMemUnmap(g.base + g.mapped, delta);
+        hipMemRelease(hd);
+        return e;
+    }
+    g.chunks.push_back({hd, delta});
+    g.mapped = want;
+    return hipSuccess;
+}
+static void gm_free(GrowMem &g) {
+    size_t off = g.mapped;
+    for (auto it = g.chunks.rbegin(); it != g.chunks.rend(); ++it) {
+        off -= it->second;
+        hipMemUnmap(g.base + off, it->second);
+        hipMemRelease(it->first);
+    }
+    g.chunks.clear();
+    if (g.base) hipMemAddressFree(g.base, g.reserved);
+    g = GrowMem{};
+}
+
 }  // namespace
 
 struct fs2_handle {
@@ -99,6 +170,7 @@ struct fs2_handle {
     // landmark pages (fs2_kernels.hpp): pool, page tables A/B, free list
     char *pool = nullptr;
     int64_t npool = 0;                     // pages in the pool
+    GrowMem pool_vm, rpool_vm;             // in-place growth of the page / record pools (base null: hipMalloc)
     Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
     uint32_t *bbox[2] = {};                // [nblocks][kBBoxRows] workgroup row boxes of pt[0] / pt[1]
     Desc *rdesc = nullptr;                 // received particles' rows [n_recv][rows]
@@ -250,11 +322,13 @@ struct fs2_handle {
     bool refs = false;                     // the mode is on
     bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
     bool refs_live = false;                // a resample has exchanged references (no local collection)
+    uint64_t grows = 0;                    // collective pool growths
     PeerMaps peers_host{};
     PeerMaps *peers_dev = nullptr;
     uint8_t *ep_dev = nullptr, *epochs_dev = nullptr;     // this rank's / every rank's collection epoch
     int64_t remote_rows = 0;               // upper bound on row entries naming remote pages (localisations)
-    bool collect_next = false;             // a collective collection before the next scan (published)
+    int32_t collect_next = 0;              // before the next scan: bit 0 a collective collection, bits 1 / 2
+                                           // every rank grows its page / record pool (published)
     ChainSummary *dch_send = nullptr, *dch_recv = nullptr;
     RankRecordX *recx = nullptr, *recxs = nullptr;
     double *est_base = nullptr;
@@ -476,7 +550,35 @@ static int collect_collective(fs2_handle *h) {
     return FS2_OK;
 }
 
+// page_refs mode: every rank grows the pools some rank asked for (the flags are in
+// the all-gathered records), together -- pools shared by IPC cannot grow in place:
+// every rank unmaps the others' pools, a rendezvous, each reallocates its own
+// (page and record ids keep their meaning), and the pools are shared anew.
+static int grow_pool(fs2_handle *h, int64_t pages);
+static int grow_recs(fs2_handle *h, int64_t n);
+static int regrow_collective(fs2_handle *h, bool pages, bool recs) {
+    hipStream_t s = h->stream;
+    HIP_TRY(h, hipStreamSynchronize(s));
+    h->tp->unshare();
+    {
+        CommTimer ct(h);
+        const int rc = h->tp->allgather(h->ep_dev, h->epochs_dev + kMaxRanks, 1, s, &h->err);
+        if (rc) return rc;
+    }
+    HIP_TRY(h, hipStreamSynchronize(s));
+    h->refs_shared = false;
+    int rc = FS2_OK;
+    if (pages) rc = grow_pool(h, std::min<int64_t>(h->npool + h->npool / 2, (int64_t)kRefIdMask - 1024));
+    if (!rc && recs) rc = grow_recs(h, std::min<int64_t>(h->nrecs + h->nrecs / 2, (int64_t)kRecIdLimit));
+    if (rc) return rc;
+    h->grows += 1;
+    return share_pools(h);
+}
+
 // Pool of `pages` pages (existing pages keep their ids), its free list and marks.
+// The new pages are free: their ids join the free list after the entries already
+// listed (no collection).  In place (GrowMem) when the handle's pools are not
+// shared, else allocate and copy.
 static int grow_pool(fs2_handle *h, int64_t pages) {
     if (pages <= h->npool) return FS2_OK;
     if (h->refs_shared) return refs_short(h, "page");
@@ -485,60 +587,99 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
                        (long long)pages, kRefIdMask);
     if (pages > (int64_t)kIdMask)
         return set_err(&h->err, FS2_ERR_OOM, "page pool of %lld pages exceeds the id space", (long long)pages);
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
-    char *pool = nullptr;
-    HIP_TRY(h, hipMalloc(&pool, (size_t)pages * kPageBytes));
-    if (h->pool) HIP_TRY(h, copy_sync(h, pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
-    hipFree(h->pool);
-    h->pool = pool;
+    hipStream_t s = h->stream;
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (!h->pool && !h->refs) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+            gm_init(h->pool_vm, h->cfg.device, std::min<size_t>((size_t)kIdMask * kPageBytes, tot));
+    }
+    if (h->pool_vm.base && (size_t)pages * kPageBytes <= h->pool_vm.reserved) {
+        HIP_TRY(h, gm_grow(h->pool_vm, (size_t)pages * kPageBytes));
+        h->pool = h->pool_vm.base;
+    } else {
+        if (h->pool_vm.base) return set_err(&h->err, FS2_ERR_OOM, "page pool beyond its reserved range");
+        char *pool = nullptr;
+        HIP_TRY(h, hipMalloc(&pool, (size_t)pages * kPageBytes));
+        if (h->pool) HIP_TRY(h, copy_sync(h, pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
+        hipFree(h->pool);
+        h->pool = pool;
+    }
     uint8_t *mark = nullptr;
     HIP_TRY(h, hipMalloc(&mark, (size_t)pages));
     HIP_TRY(h, hipMemset(mark, 0, (size_t)pages));
     hipFree(h->mark);
     h->mark = mark;
     h->epoch = 0;
+    // the free list: the entries listed so far, then the new pages
+    uint32_t *fl = nullptr;
+    HIP_TRY(h, hipMalloc(&fl, sizeof(uint32_t) * (size_t)pages));
+    if (h->freel && h->nfree > 0)
+        HIP_TRY(h, copy_sync(h, fl, h->freel, sizeof(uint32_t) * (size_t)h->nfree, hipMemcpyDeviceToDevice));
     hipFree(h->freel);
-    h->freel = nullptr;
-    HIP_TRY(h, hipMalloc(&h->freel, sizeof(uint32_t) * (size_t)pages));
+    h->freel = fl;
+    HIP_TRY(h, launch_iota_from(h->freel + h->nfree, (uint32_t)h->npool, pages - h->npool, s));
+    h->nfree += pages - h->npool;
     if (h->cfg.world_size > 1) {
         hipFree(h->sent_mask);
         h->sent_mask = nullptr;
         HIP_TRY(h, hipMalloc(&h->sent_mask, sizeof(uint32_t) * (size_t)pages));
+        HIP_TRY(h, hipMemsetAsync(h->sent_mask, 0, sizeof(uint32_t) * (size_t)pages, s));
     }
     hipFree(h->bcnt);
     h->bcnt = nullptr;
     HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int64_t) * (size_t)collect_blocks(pages)));
     h->npool = pages;
-    return collect(h, false);
+    HIP_TRY(h, hipStreamSynchronize(s));
+    return FS2_OK;
 }
 
-// Record pool of `n` records (existing records keep their ids), free list, marks.
+// Record pool of `n` records (existing records keep their ids), free list, marks:
+// like grow_pool.
 static int grow_recs(fs2_handle *h, int64_t n) {
     if (n <= h->nrecs) return FS2_OK;
     if (h->refs_shared) return refs_short(h, "record");
     if (n > (int64_t)kRecIdLimit)
         return set_err(&h->err, FS2_ERR_OOM, "record pool of %lld records exceeds the 32-bit id space",
                        (long long)n);
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
-    char *rp = nullptr;
-    HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
-    if (h->rpool) HIP_TRY(h, copy_sync(h, rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
-    hipFree(h->rpool);
-    h->rpool = rp;
+    hipStream_t s = h->stream;
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (!h->rpool && !h->refs) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+            gm_init(h->rpool_vm, h->cfg.device, std::min<size_t>((size_t)kRecIdLimit * kRecBytes, tot));
+    }
+    if (h->rpool_vm.base && (size_t)n * kRecBytes <= h->rpool_vm.reserved) {
+        HIP_TRY(h, gm_grow(h->rpool_vm, (size_t)n * kRecBytes));
+        h->rpool = h->rpool_vm.base;
+    } else {
+        if (h->rpool_vm.base) return set_err(&h->err, FS2_ERR_OOM, "record pool beyond its reserved range");
+        char *rp = nullptr;
+        HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
+        if (h->rpool) HIP_TRY(h, copy_sync(h, rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
+        hipFree(h->rpool);
+        h->rpool = rp;
+    }
     uint8_t *mark = nullptr;
     HIP_TRY(h, hipMalloc(&mark, (size_t)n));
     HIP_TRY(h, hipMemset(mark, 0, (size_t)n));
     hipFree(h->rmark);
     h->rmark = mark;
     h->repoch = 0;
+    uint32_t *fl = nullptr;
+    HIP_TRY(h, hipMalloc(&fl, sizeof(uint32_t) * (size_t)n));
+    if (h->rfreel && h->rnfree > 0)
+        HIP_TRY(h, copy_sync(h, fl, h->rfreel, sizeof(uint32_t) * (size_t)h->rnfree, hipMemcpyDeviceToDevice));
     hipFree(h->rfreel);
-    h->rfreel = nullptr;
-    HIP_TRY(h, hipMalloc(&h->rfreel, sizeof(uint32_t) * (size_t)n));
+    h->rfreel = fl;
+    HIP_TRY(h, launch_iota_from(h->rfreel + h->rnfree, (uint32_t)h->nrecs, n - h->nrecs, s));
+    h->rnfree += n - h->nrecs;
     hipFree(h->rbcnt);
     h->rbcnt = nullptr;
     HIP_TRY(h, hipMalloc(&h->rbcnt, sizeof(int64_t) * (size_t)collect_blocks(n)));
     h->nrecs = n;
-    return collect(h, true);
+    HIP_TRY(h, hipStreamSynchronize(s));
+    return FS2_OK;
 }
 
 // Reserve `need` free pages (collecting, then growing the pool, when short);
@@ -1050,8 +1191,12 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
     hipFree(h->xt_eslot); hipFree(h->xt_ulist);
     hipFree(h->sent_mask);
-    hipFree(h->pool); hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
-    hipFree(h->rpool); hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
+    if (h->pool_vm.base) gm_free(h->pool_vm);
+    else hipFree(h->pool);
+    if (h->rpool_vm.base) gm_free(h->rpool_vm);
+    else hipFree(h->rpool);
+    hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
+    hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->slb_pass); hipFree(h->ext_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
@@ -1481,12 +1626,18 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         rc = share_pools(h);
         if (rc) return rc;
     }
+    bool collected = false;
     if (h->refs_shared && h->collect_next) {
         // page_refs: some rank's pools ran short in the last scan (every rank read the
-        // same records, so every rank collects here, together)
+        // same records, so every rank collects -- and grows -- here, together)
+        if (h->collect_next & 6) {
+            rc = regrow_collective(h, (h->collect_next & 2) != 0, (h->collect_next & 4) != 0);
+            if (rc) return rc;
+        }
         rc = collect_collective(h);
         if (rc) return rc;
-        h->collect_next = false;
+        h->collect_next = 0;
+        collected = true;
     }
     rc = grow_rows(h, h->cnt_upper + M);
     if (rc) return rc;
@@ -1564,7 +1715,11 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (h->refs) {              // (also before references cross: this scan's resample may send them)
         const int64_t pneed = (int64_t)std::max(M, 1) * h->n + h->remote_rows;
         const int64_t rneed = (int64_t)std::max(M, 1) * h->n + (int64_t)kPageSlots * h->remote_rows;
-        want_collect = (h->nfree - h->cursor < 3 * pneed || h->rnfree - h->rcursor < 3 * rneed) ? 1 : 0;
+        const bool plow = h->nfree - h->cursor < 3 * pneed, rlow = h->rnfree - h->rcursor < 3 * rneed;
+        want_collect = (plow || rlow) ? 1 : 0;
+        // still short right after a collective collection: every rank grows next scan
+        if (collected && plow) want_collect |= 2;
+        if (collected && rlow) want_collect |= 4;
     }
     int passes = 0;
     uint64_t fixed_bytes = 0;
@@ -1909,7 +2064,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         h->rnfree -= (int64_t)st.loc_recs;
         h->remote_rows = st.resampled ? (int64_t)st.remote_rows
                                       : std::max<int64_t>(0, h->remote_rows - (int64_t)st.loc_pages);
-        h->collect_next = st.collect_next != 0;
+        h->collect_next = st.collect_next;
         if (h->profiling) {
             h->prof.localized_pages += st.loc_pages;
         }
@@ -1950,6 +2105,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         stats->new_pages = st.new_pages;
         stats->collections = h->collections;
         stats->pool_pages = (uint64_t)h->npool;
+        stats->pool_records = (uint64_t)h->nrecs;
         stats->pages_opened = st.opened;
         stats->reference_visits = st.ref_visits;
     }

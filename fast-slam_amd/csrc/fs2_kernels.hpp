@@ -655,6 +655,7 @@ hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm
                          MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_fill(double *p, double v, int64_t n, hipStream_t s);
 hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s);
+hipError_t launch_iota_from(uint32_t *p, uint32_t v0, int64_t n, hipStream_t s);   // p[e] = v0 + e
 
 // page pool collection (fs2_pages.hip): mark the pages referenced by the n maps
 // of `map`, then list every unmarked page of [0, npool) in freel; nfree_dev

@@ -1408,6 +1408,17 @@ hipError_t launch_iota(uint32_t *p, int64_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
+__global__ void k_iota_from(uint32_t *p, uint32_t v0, int64_t n) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (int64_t e = t; e < n; e += (int64_t)gridDim.x * kBlock) p[e] = v0 + (uint32_t)e;
+}
+
+hipError_t launch_iota_from(uint32_t *p, uint32_t v0, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_iota_from, dim3(grid_for(n)), dim3(kBlock), 0, s, p, v0, n);
+    return hipGetLastError();
+}
+
 #ifdef FS2_PHASE_TIMING
 hipError_t debug_phase_times(unsigned long long out[8], int reset) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8);

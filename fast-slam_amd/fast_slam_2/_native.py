@@ -83,6 +83,7 @@ class fs2_iter_stats(C.Structure):
         ("pool_pages", C.c_uint64),
         ("pages_opened", C.c_uint64),
         ("reference_visits", C.c_uint64),
+        ("pool_records", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -134,6 +134,7 @@ typedef struct fs2_iter_stats {
     uint64_t reference_visits;  /* landmarks the reference's first-match scan would read:
                                    j + 1 for a match at j, the map size for an append
                                    (landmark_utils.py:103-117; SURVEY §8d's V) */
+    uint64_t pool_records;      /* records in the record pool (48 B each) */
 } fs2_iter_stats;
 
 typedef struct fs2_profile {
