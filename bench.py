@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
     ap.add_argument("--particles", type=int, default=0, help="override particles per GPU")
     ap.add_argument("--landmarks", type=int, default=0, help="override landmarks per particle")
+    ap.add_argument("--map", choices=("grid", "dense"), default="grid",
+                    help="dense: the robustness dense-map workload as the timed one (its PMC record)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=0)
@@ -312,6 +314,23 @@ def timed_scans(f, scans, meas_of, odo_of, warmup):
             "cow_pages_per_particle_scan": sums["cow"] / (n * k), "resamples": sums["resamples"]}
 
 
+def dense_workload(L, seed):
+    """The dense-map variant: L landmarks uniform over the room, each scan's hits
+    near random ones and a miss 30 m outside.  Returns (map [L][2], meas_of)."""
+    import fs2_synthetic as syn
+    rng = np.random.default_rng(seed + 17)
+    hw, hh = syn.ROOM[0] / 2, syn.ROOM[1] / 2
+    dense = np.column_stack([rng.uniform(-hw, hw, L), rng.uniform(-hh, hh, L)])
+
+    def dense_meas(s):
+        r = np.random.default_rng([seed, 900 + s])
+        ks = r.integers(0, L, 3)
+        pts = [dense[k] + r.uniform(-0.3, 0.3, 2) for k in ks] + [np.array([30.0 + s, -30.0])]
+        return np.array([syn.encode(*p) for p in pts])
+
+    return dense, dense_meas
+
+
 def robustness(args, f, L, first_scan):
     """How much of the headline depends on the synthetic map's sparsity and on the
     run length: the same handle 40 scans further (60 in all), a dense
@@ -327,17 +346,7 @@ def robustness(args, f, L, first_scan):
                                      syn.odometry, 0)
     out["long_run_60"]["note"] = f"scans {first_scan}..{first_scan + steps - 1} of the headline handle"
     n = f.n_local
-    # dense map: uniform landmarks, hits near random ones, a miss 30 m outside
-    rng = np.random.default_rng(args.seed + 17)
-    hw, hh = syn.ROOM[0] / 2, syn.ROOM[1] / 2
-    dense = np.column_stack([rng.uniform(-hw, hw, L), rng.uniform(-hh, hh, L)])
-
-    def dense_meas(s):
-        r = np.random.default_rng([args.seed, 900 + s])
-        ks = r.integers(0, L, 3)
-        pts = [dense[k] + r.uniform(-0.3, 0.3, 2) for k in ks] + [np.array([30.0 + s, -30.0])]
-        return np.array([syn.encode(*p) for p in pts])
-
+    dense, dense_meas = dense_workload(L, args.seed)
     scans = list(range(13))
     g = fast_slam_2.FastSLAM2(n, rng="device", seed=args.seed, landmark_capacity=L + 24, verbose=False)
     populate(g, n, L, args.seed, 0, base_map=dense)
@@ -499,6 +508,8 @@ def main(argv=None):
     from fast_slam_2 import _native as nat
 
     cfg = dict(CONFIGS[args.config])
+    if args.map == "dense":
+        cfg["name"] += "_dense"          # (its own PMC record, profiles/pmc_<name>.json)
     n_per_gpu = args.particles or cfg["N"]
     L = args.landmarks or cfg["L"]
     comm_id = None
@@ -637,7 +648,8 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
                               landmark_capacity=L + total_scans + 8, rank=rank,
                               world_size=world, comm_id=comm_id, verbose=False,
                               gate_filter=not args.no_gate_filter, comm_mode=args.comm)
-    populate(f, f.n_local, L, args.seed, rank)
+    dense = dense_workload(L, args.seed) if args.map == "dense" else None
+    populate(f, f.n_local, L, args.seed, rank, base_map=None if dense is None else dense[0])
     scans_pts = None
     fast_slam_2.ICP.device = dev
     if cfg["icp"]:
@@ -645,7 +657,8 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
                      for s in range(total_scans + 1)]
 
     # the scans' measurements are inputs (the front-end's output), made before timing
-    meas = [np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64)
+    meas = [np.ascontiguousarray(syn.scan_measurements(L, s, args.seed) if dense is None else dense[1](s),
+                                 dtype=np.float64)
             for s in range(total_scans)]
 
     # ICP of scan s+1 runs beside scan s's filter update: the scan is enqueued

@@ -160,6 +160,23 @@ static void gm_free(GrowMem &g) {
 
 }  // namespace
 
+// One draw's context, from its start (mt_begin) to its end (mt_end): a
+// synchronous fs2_mt_draw runs both back to back on the handle's stream; a
+// deferred one (fs2_mt_draw_deferred) runs mt_begin on the draw stream and
+// leaves mt_end to the next scan's submit, between k_candidates (which does not
+// read the motion draws) and k_update, so that the host's work on the draw --
+// waiting for the counts, the listed logs, the patches -- overlaps the
+// candidate pass instead of preceding the scan.
+struct MtCtx {
+    fs2_mt_state in;
+    double sigma = 0.0;
+    int64_t N = 0, P = 0, A = 0, amb_cap = 0, pos0 = 0, have = 0, total = 0;
+    int64_t amb_pre = 0;                  // listed logs copied to the host with the counts
+    int h0 = 0;
+    fs2_mt_state *after = nullptr, *after_u0 = nullptr;
+    double *u0_out = nullptr;
+};
+
 struct fs2_handle {
     fs2_config cfg{};
     int64_t n_global = 0, n = 0, first = 0;
@@ -260,6 +277,11 @@ struct fs2_handle {
         uint32_t *jwin = nullptr;          // [G - 1][624]
         bool tab_ready = false;
         bool armed = false;
+        // a deferred draw (fs2_mt_draw_deferred), enqueued on dstream, ended by the next submit
+        hipStream_t dstream = nullptr;
+        hipEvent_t ev_in = nullptr, ev_noise = nullptr;
+        bool deferred = false;
+        MtCtx dc;
     } mt;
     int32_t *assoc_dev = nullptr;
     int64_t assoc_cap = 0;
@@ -1221,6 +1243,12 @@ static void free_handle(fs2_handle *h) {
     if (h->noise_pin) hipHostFree(h->noise_pin);
     if (h->u0_pin) hipHostFree(h->u0_pin);
     if (h->mt.side) hipStreamSynchronize(h->mt.side);
+    if (h->mt.dstream) {
+        hipStreamSynchronize(h->mt.dstream);
+        hipStreamDestroy(h->mt.dstream);
+        hipEventDestroy(h->mt.ev_in);
+        hipEventDestroy(h->mt.ev_noise);
+    }
     hipFree(h->mt.raw[0]); hipFree(h->mt.raw[1]); hipFree(h->mt.boff);
     if (h->mt.ev_words) hipEventDestroy(h->mt.ev_words);
     if (h->mt.ev_pre) hipEventDestroy(h->mt.ev_pre);
@@ -1609,6 +1637,8 @@ static int wait_flag(fs2_handle *h, unsigned long long seq) {
     return FS2_OK;
 }
 
+static int mt_finish(fs2_handle *h);
+
 int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
                        const double *observed, int32_t M, const double *noise, const double *u0) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
@@ -1616,11 +1646,22 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
     // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise /
     // u0; a draw is consumed by this call whatever happens below
-    const bool drawn = h->mt.armed;
+    const bool drawn = h->mt.armed || h->mt.deferred;
     h->mt.armed = false;
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    // a deferred draw ends between k_candidates and k_update below, or on the way out
+    // (its outputs are written whatever this call returns)
+    struct DrawEnd {
+        fs2_handle *h;
+        ~DrawEnd() {
+            if (h->mt.deferred) {
+                mt_finish(h);
+                h->mt.armed = false;
+            }
+        }
+    } draw_end{h};
     if (drawn && (noise || u0))
         return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
-    HIP_TRY(h, hipSetDevice(h->cfg.device));
     int rc;
     if (h->refs && !h->refs_shared) {
         rc = share_pools(h);
@@ -1781,6 +1822,11 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         if (prof && first && up.blk1 <= up.blk0)
             for (int k : {0, 1, 4}) HIP_TRY(h, hipEventRecord(E[k], s));
         HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
+        if (first && h->mt.deferred) {     // the draw's host half while k_candidates runs
+            rc = mt_finish(h);
+            if (rc) return rc;
+            h->mt.armed = false;
+        }
         HIP_TRY(h, launch_update(up, s, (prof && first) ? (cand ? E[4] : E[0]) : nullptr,
                                  (prof && last) ? E[2] : nullptr));
         if (prof && last && up.blk1 <= up.blk0) HIP_TRY(h, hipEventRecord(E[2], s));
@@ -2153,8 +2199,12 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
                        (long long)first, (long long)(first + count), (long long)h->n);
     if ((cnt == nullptr) != (lm == nullptr) || (lm && lm_cap < 0))
         return set_err(&h->err, FS2_ERR_ARG, "cnt and lm must be given together");
-    h->mt.armed = false;         // a pending fs2_mt_draw was made for the state replaced here
     HIP_TRY(h, hipSetDevice(h->cfg.device));
+    {
+        const int rcm = mt_finish(h);    // a pending fs2_mt_draw was made for the state replaced here
+        h->mt.armed = false;
+        if (rcm) return rcm;
+    }
     hipStream_t s = h->stream;
     const int c = h->cur;
     HIP_TRY(h, hipStreamSynchronize(s));
@@ -2286,8 +2336,12 @@ int fs2_get_state(fs2_handle *h, int64_t first, int64_t count, double *x, double
     if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     if (first < 0 || count < 0 || first + count > h->n)
         return set_err(&h->err, FS2_ERR_ARG, "range outside local particles");
-    h->mt.armed = false;         // a pending fs2_mt_draw was made for the state replaced here
     HIP_TRY(h, hipSetDevice(h->cfg.device));
+    {
+        const int rcm = mt_finish(h);    // a pending fs2_mt_draw was made for the state replaced here
+        h->mt.armed = false;
+        if (rcm) return rcm;
+    }
     hipStream_t s = h->stream;
     const int c = h->cur;
     HIP_TRY(h, hipStreamSynchronize(s));
@@ -2760,29 +2814,108 @@ static int mt_fill(fs2_handle *h, uint32_t *R, int64_t have, int64_t total, hipS
     return FS2_OK;
 }
 
-int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
-                fs2_mt_state *after_u0, double *u0_out) {
-    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+// The device draw is numpy's bit for bit only if the host libm's log is within
+// 0.52 ulp (outside the listed midpoint window its result is then forced, and the
+// device's double-double log gives it).  Checked once per process on a fixed
+// sample: the host restatement of the device log (mt_log) against std::log.
+static bool mt_libm_agrees() {
+    static const bool ok = [] {
+        double thi[kMtLogTab], tlo[kMtLogTab];
+        for (int k = 0; k < kMtLogTab; ++k) {
+            const DD l = mt_log_tab_entry(k);
+            thi[k] = l.hi;
+            tlo[k] = l.lo;
+        }
+        uint64_t z = 0x9E3779B97F4A7C15ull;
+        for (int k = 0; k < 8192; ++k) {
+            z = z * 6364136223846793005ull + 1442695040888963407ull;
+            const double x = (double)((z >> 11) + 1) * 0x1p-53;      // (0, 1], like r2
+            bool amb = false;
+            const double d = mt_log(x, thi, tlo, &amb);
+            if (!amb && d != std::log(x)) return false;
+        }
+        return true;
+    }();
+    return ok;
+}
+
+
+// one attempt: the words through the last one it may read, then the draw and
+// its counts (to meta_pin, not yet waited for)
+static int mt_attempt(fs2_handle *h, MtCtx &c, hipStream_t s) {
+    auto &mt = h->mt;
+    const int64_t par_words = mt.jG > 1 ? mt.jG * mt.jJ + 1 : 0;   // a parallel fill makes this many
+    // words: the key, then through the block holding the u0 words after the last attempt
+    const int64_t need = c.pos0 + 4 * c.A + 2;
+    c.total = std::max<int64_t>(kMtN, (need + kMtN - 1) / kMtN * kMtN);
+    if (c.have == 0) {
+        HIP_TRY(h, mt_grow((void **)&mt.raw[mt.cur], nullptr, 4, &mt.raw_cap[mt.cur], std::max(c.total, par_words)));
+        std::memcpy(mt.words_pin, c.in.key, sizeof(uint32_t) * kMtN);
+        HIP_TRY(h, hipMemcpyAsync(mt.raw[mt.cur], mt.words_pin, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
+        c.have = kMtN;
+    } else if (c.total > mt.raw_cap[mt.cur]) {
+        // keep the words made so far
+        uint32_t *nr = nullptr;
+        const int64_t cap = std::max<int64_t>(c.total, mt.raw_cap[mt.cur] + mt.raw_cap[mt.cur] / 2);
+        HIP_TRY(h, hipMalloc((void **)&nr, 4 * (size_t)cap));
+        HIP_TRY(h, hipMemcpyAsync(nr, mt.raw[mt.cur], 4 * (size_t)c.have, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(h, hipStreamSynchronize(s));
+        hipFree(mt.raw[mt.cur]);
+        mt.raw[mt.cur] = nr;
+        mt.raw_cap[mt.cur] = cap;
+    }
+    uint32_t *raw = mt.raw[mt.cur];
+    const int64_t nb = (c.A + 255) / 256;
+    HIP_TRY(h, mt_grow((void **)&mt.boff, nullptr, 4, &mt.boff_cap, std::max<int64_t>(nb, 1)));
+    int64_t acap = mt.amb_cap;
+    HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, c.amb_cap));
+    mt.amb_cap = acap;
+    {
+        int64_t made = 0;
+        const int rcf = mt_fill(h, raw, c.have, c.total, s, &made);
+        if (rcf) return rcf;
+        c.have = made;
+    }
+    HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
+    HIP_TRY(h, launch_mt_draw(raw, c.pos0, (c.pos0 - c.in.pos) / kMtN, c.A, c.P, c.N, c.h0, c.in.gauss, c.sigma, h->first,
+                              h->n, h->noise_dev, mt.boff, mt.meta, mt.amb,
+                              (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX), mt.tab, mt.tab_ready ? 1 : 0, s));
+    mt.tab_ready = true;
+    HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, mt.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
+    return FS2_OK;
+}
+
+static int mt_begin(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after, fs2_mt_state *after_u0,
+                    double *u0_out, hipStream_t s, MtCtx &c) {
     if (!in || !after || !after_u0) return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: null state");
     if (!(sigma >= 0.0))   // numpy: ValueError for a negative (or NaN) scale
         return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: scale < 0");
     if (in->pos < 0 || in->pos > kMtN || (in->has_gauss != 0 && in->has_gauss != 1))
         return set_err(&h->err, FS2_ERR_ARG, "fs2_mt_draw: bad state (pos %d, has_gauss %d)", in->pos, in->has_gauss);
     if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
-    HIP_TRY(h, hipSetDevice(h->cfg.device));
-    hipStream_t s = h->stream;
+    if (!mt_libm_agrees())
+        return set_err(&h->err, FS2_ERR_STATE,
+                       "fs2_mt_draw: this process's libm log is outside the 0.52-ulp bound the device draw relies on "
+                       "(draw with numpy on the host)");
     auto &mt = h->mt;
-    const int64_t N = h->n_global;
-    const int h0 = (N > 0 && in->has_gauss) ? 1 : 0;
-    const int64_t P = (N > h0) ? (N - h0 + 1) / 2 : 0;     // accepted attempts (pairs) needed
+    c = MtCtx{};
+    c.in = *in;
+    c.sigma = sigma;
+    c.after = after;
+    c.after_u0 = after_u0;
+    c.u0_out = u0_out;
+    c.N = h->n_global;
+    c.h0 = (c.N > 0 && in->has_gauss) ? 1 : 0;
+    c.P = (c.N > c.h0) ? (c.N - c.h0 + 1) / 2 : 0;     // accepted attempts (pairs) needed
     // attempts until P successes at p = pi/4: mean P/p, sd sqrt(P(1-p))/p; 12 sd of margin
-    const double mean = (double)P / 0.78539816339744831, sd = std::sqrt((double)P * 0.21460183660255169) / 0.78539816339744831;
-    int64_t A = P ? (int64_t)(mean + 12.0 * sd) + 64 : 0;
-    int64_t amb_cap = P / 8 + 4096;
+    const double mean = (double)c.P / 0.78539816339744831,
+                 sd = std::sqrt((double)c.P * 0.21460183660255169) / 0.78539816339744831;
+    c.A = c.P ? (int64_t)(mean + 12.0 * sd) + 64 : 0;
+    c.amb_cap = c.P / 8 + 4096;
     if (mt.jG == 0) {
         // regions of ~160 K words (16 for 10^6 particles), J >= 2 x 20 561 (the
         // jump's operands come first); the polynomials are made once (~0.3 s)
-        const int64_t tn = (2 * kMtN + 4 * (A + 2) + 2 + 2 * kMtN + kMtN - 1) / kMtN * kMtN;
+        const int64_t tn = (2 * kMtN + 4 * (c.A + 2) + 2 + 2 * kMtN + kMtN - 1) / kMtN * kMtN;
         const int G = (int)std::min<int64_t>(kMtMaxGen, tn / 160000);
         mt.jG = 1;
         if (G >= 2) {
@@ -2797,7 +2930,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
             }
         }
     }
-    const int64_t par_words = mt.jG > 1 ? mt.jG * mt.jJ + 1 : 0;   // a parallel fill makes this many
     if (!mt.words_pin) HIP_TRY(h, hipHostMalloc((void **)&mt.words_pin, sizeof(uint32_t) * 2 * kMtN, 0));
     if (!mt.meta) {
         HIP_TRY(h, hipMalloc((void **)&mt.tab, sizeof(double) * 2 * kMtLogTab));
@@ -2811,83 +2943,57 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     }
     // the words made ahead serve this draw if it starts where the last one said
     // numpy would be (after its normals, or after its u0 too)
-    int64_t pos0 = in->pos;
-    int64_t have = 0;                          // words of the buffer already made
+    c.pos0 = in->pos;
+    c.have = 0;                                // words of the buffer already made
     if (mt.pre_valid) {
-        for (int k = 0; k < 2 && have == 0; ++k) {
+        for (int k = 0; k < 2 && c.have == 0; ++k) {
             if (mt.pre_spos[k] == in->pos && std::memcmp(mt.pre_key[k], in->key, sizeof mt.pre_key[k]) == 0) {
                 mt.cur = 1 - mt.cur;
-                pos0 = mt.pre_pos0[k];
-                have = mt.pre_total;
+                c.pos0 = mt.pre_pos0[k];
+                c.have = mt.pre_total;
             }
         }
     }
     // the side stream's last work (made ahead, or still reading this buffer) first
     if (mt.pre_valid) HIP_TRY(h, hipStreamWaitEvent(s, mt.ev_pre, 0));
     mt.pre_valid = false;
+    return mt_attempt(h, c, s);
+}
+
+static int mt_end(fs2_handle *h, MtCtx &c, hipStream_t s) {
+    auto &mt = h->mt;
+    const int64_t N = c.N, P = c.P;
+    const int h0 = c.h0;
     MtMeta meta{};
-    int64_t total = 0;
-    for (int attempt = 0;; ++attempt) {
-        if (attempt == 6) return set_err(&h->err, FS2_ERR_STATE, "fs2_mt_draw: attempts did not converge");
-        // words: the key, then through the block holding the u0 words after the last attempt
-        const int64_t need = pos0 + 4 * A + 2;
-        total = std::max<int64_t>(kMtN, (need + kMtN - 1) / kMtN * kMtN);
-        if (have == 0) {
-            HIP_TRY(h, mt_grow((void **)&mt.raw[mt.cur], nullptr, 4, &mt.raw_cap[mt.cur], std::max(total, par_words)));
-            std::memcpy(mt.words_pin, in->key, sizeof(uint32_t) * kMtN);
-            HIP_TRY(h, hipMemcpyAsync(mt.raw[mt.cur], mt.words_pin, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
-            have = kMtN;
-        } else if (total > mt.raw_cap[mt.cur]) {
-            // keep the words made so far
-            uint32_t *nr = nullptr;
-            const int64_t c = std::max<int64_t>(total, mt.raw_cap[mt.cur] + mt.raw_cap[mt.cur] / 2);
-            HIP_TRY(h, hipMalloc((void **)&nr, 4 * (size_t)c));
-            HIP_TRY(h, hipMemcpyAsync(nr, mt.raw[mt.cur], 4 * (size_t)have, hipMemcpyDeviceToDevice, s));
-            HIP_TRY(h, hipStreamSynchronize(s));
-            hipFree(mt.raw[mt.cur]);
-            mt.raw[mt.cur] = nr;
-            mt.raw_cap[mt.cur] = c;
-        }
-        uint32_t *raw = mt.raw[mt.cur];
-        const int64_t nb = (A + 255) / 256;
-        HIP_TRY(h, mt_grow((void **)&mt.boff, nullptr, 4, &mt.boff_cap, std::max<int64_t>(nb, 1)));
-        int64_t acap = mt.amb_cap;
-        HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, amb_cap));
-        mt.amb_cap = acap;
-        {
-            int64_t made = 0;
-            const int rcf = mt_fill(h, raw, have, total, s, &made);
-            if (rcf) return rcf;
-            have = made;
-        }
-        HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
-        HIP_TRY(h, launch_mt_draw(raw, pos0, (pos0 - in->pos) / kMtN, A, P, N, h0, in->gauss, sigma, h->first, h->n, h->noise_dev,
-                                  mt.boff, mt.meta, mt.amb, (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX),
-                                  mt.tab, mt.tab_ready ? 1 : 0, s));
-        mt.tab_ready = true;
-        HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, mt.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
+    for (int attempt = 1;; ++attempt) {
         HIP_TRY(h, hipStreamSynchronize(s));
         meta = *mt.meta_pin;
         if (P > 0 && meta.accepted < P) {      // (about 1e-30 per draw) more attempts
-            A += A / 4 + 1024;
-            continue;
+            c.A += c.A / 4 + 1024;
+        } else if (meta.amb_n > mt.amb_cap) {
+            c.amb_cap = (int64_t)meta.amb_n + 1024;
+        } else {
+            break;
         }
-        if (meta.amb_n > mt.amb_cap) {
-            amb_cap = (int64_t)meta.amb_n + 1024;
-            continue;
-        }
-        break;
+        if (attempt == 6) return set_err(&h->err, FS2_ERR_STATE, "fs2_mt_draw: attempts did not converge");
+        c.amb_pre = 0;
+        const int rca = mt_attempt(h, c, s);
+        if (rca) return rca;
     }
     // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
     const int64_t na = meta.amb_n;
     if (na > 0) {
-        HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)na, hipMemcpyDeviceToHost, s));
-        HIP_TRY(h, hipStreamSynchronize(s));
+        if (na > c.amb_pre) {
+            HIP_TRY(h, hipMemcpyAsync(mt.amb_pin + c.amb_pre, mt.amb + c.amb_pre, sizeof(MtAmb) * (size_t)(na - c.amb_pre),
+                                      hipMemcpyDeviceToHost, s));
+            HIP_TRY(h, hipStreamSynchronize(s));
+        }
         HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
         HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
         // entry k patches outputs 2k, 2k + 1 (index -1: not this rank's); split over
         // the host pool's threads when there are many
         const int64_t first = h->first, nl = h->n;
+        const double sigma = c.sigma;
         double cached = 0.0;
         bool has_cached = false;
         auto fix = [&](int64_t k0, int64_t k1) {
@@ -2911,21 +3017,20 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         host_pool_run(na, 2048, fix);
         if (has_cached) meta.gauss = cached;
         const int64_t np = 2 * na;
-        if (np > 0) {
-            HIP_TRY(h, hipMemcpyAsync(mt.pidx, mt.pidx_pin, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
-            HIP_TRY(h, hipMemcpyAsync(mt.pval, mt.pval_pin, sizeof(double) * np, hipMemcpyHostToDevice, s));
-            HIP_TRY(h, launch_mt_patch(h->noise_dev, mt.pidx, mt.pval, np, s));
-        }
+        HIP_TRY(h, hipMemcpyAsync(mt.pidx, mt.pidx_pin, sizeof(int64_t) * np, hipMemcpyHostToDevice, s));
+        HIP_TRY(h, hipMemcpyAsync(mt.pval, mt.pval_pin, sizeof(double) * np, hipMemcpyHostToDevice, s));
+        HIP_TRY(h, launch_mt_patch(h->noise_dev, mt.pidx, mt.pval, np, s));
     }
     // the state after the normals, then after the speculative u0 (two more words;
     // k_mt_final left both in meta)
+    fs2_mt_state *after = c.after, *after_u0 = c.after_u0;
     std::memcpy(after->key, meta.key_after, sizeof after->key);
     after->pos = meta.pos_after;
     std::memcpy(after_u0->key, meta.key_after_u0, sizeof after_u0->key);
     after_u0->pos = meta.pos_after_u0;
     if (N == 0) {
-        after->has_gauss = in->has_gauss;
-        after->gauss = in->gauss;
+        after->has_gauss = c.in.has_gauss;
+        after->gauss = c.in.gauss;
     } else if (P == 0) {                       // one normal, the cached one
         after->has_gauss = 0;
         after->gauss = 0.0;
@@ -2940,13 +3045,14 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
         // other buffer starts at the key block of `after` (kb1), which also holds or
         // precedes after_u0's (kb2 = kb1 or kb1 + 1)
         const int64_t E = meta.E;
-        const int64_t kb1 = (E == pos0) ? (pos0 - in->pos) / kMtN : (E - 1) / kMtN;
+        const int64_t kb1 = (E == c.pos0) ? (c.pos0 - c.in.pos) / kMtN : (E - 1) / kMtN;
         const int64_t kb2 = (E + 1) / kMtN;
         const int nx = 1 - mt.cur;
+        const int64_t par_words = mt.jG > 1 ? mt.jG * mt.jJ + 1 : 0;
         // the key block kb1 and what follows it, then the rest from the key
         const bool par = mt.jG > 1;
-        const int64_t keep = par ? kMtN : have - kMtN * kb1;
-        int64_t want = std::max<int64_t>(keep, (2 * kMtN + 4 * (A + 2) + 2 + kMtN - 1) / kMtN * kMtN);
+        const int64_t keep = par ? kMtN : c.have - kMtN * kb1;
+        int64_t want = std::max<int64_t>(keep, (2 * kMtN + 4 * (c.A + 2) + 2 + kMtN - 1) / kMtN * kMtN);
         HIP_TRY(h, mt_grow((void **)&mt.raw[nx], nullptr, 4, &mt.raw_cap[nx], std::max(want, par_words)));
         HIP_TRY(h, hipEventRecord(mt.ev_words, s));
         HIP_TRY(h, hipStreamWaitEvent(mt.side, mt.ev_words, 0));
@@ -2974,8 +3080,68 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     const double u0 = 0.0 + (hi - 0.0) * mt_double(mt_temper(wu[0]), mt_temper(wu[1]));
     *h->u0_pin = u0;
     HIP_TRY(h, hipMemcpyAsync(h->u0_dev, h->u0_pin, 8, hipMemcpyHostToDevice, s));
-    if (u0_out) *u0_out = u0;
+    if (c.u0_out) *c.u0_out = u0;
+    return FS2_OK;
+}
+
+// completes a deferred draw: its outputs written, the handle's stream ordered
+// after its noise and u0 (armed for the scan unless it failed)
+static int mt_finish(fs2_handle *h) {
+    auto &mt = h->mt;
+    if (!mt.deferred) return FS2_OK;
+    mt.deferred = false;
+    const int rc = mt_end(h, mt.dc, mt.dstream);
+    HIP_TRY(h, hipEventRecord(mt.ev_noise, mt.dstream));
+    HIP_TRY(h, hipStreamWaitEvent(h->stream, mt.ev_noise, 0));
+    if (rc) return rc;
     mt.armed = true;
+    return FS2_OK;
+}
+
+int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
+                fs2_mt_state *after_u0, double *u0_out) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    int rc = mt_finish(h);                     // a deferred draw first (its outputs are written)
+    if (rc) return rc;
+    h->mt.armed = false;
+    MtCtx c;
+    rc = mt_begin(h, in, sigma, after, after_u0, u0_out, h->stream, c);
+    if (rc) return rc;
+    rc = mt_end(h, c, h->stream);
+    if (rc) return rc;
+    h->mt.armed = true;
+    return FS2_OK;
+}
+
+int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
+                         fs2_mt_state *after_u0, double *u0_out) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    auto &mt = h->mt;
+    int rc = mt_finish(h);
+    if (rc) return rc;
+    mt.armed = false;
+    if (!mt.dstream) {
+        HIP_TRY(h, hipStreamCreateWithFlags(&mt.dstream, hipStreamNonBlocking));
+        HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_in, hipEventDisableTiming));
+        HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_noise, hipEventDisableTiming));
+    }
+    // after everything enqueued so far (the last scan still reads the noise and u0)
+    HIP_TRY(h, hipEventRecord(mt.ev_in, h->stream));
+    HIP_TRY(h, hipStreamWaitEvent(mt.dstream, mt.ev_in, 0));
+    MtCtx &c = mt.dc;
+    rc = mt_begin(h, in, sigma, after, after_u0, u0_out, mt.dstream, c);
+    if (rc) return rc;
+    // the listed logs come back with the counts: about 5% of the pairs (a 0.05-ulp
+    // window per log), so a prefix of P/12 holds them all but rarely
+    c.amb_pre = 0;
+    const int64_t pre = std::min<int64_t>(c.P / 12 + 2048, mt.amb_cap);
+    if (pre > 0) {
+        HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)pre, hipMemcpyDeviceToHost, mt.dstream));
+        c.amb_pre = pre;
+    }
+    mt.deferred = true;
     return FS2_OK;
 }
 
@@ -2988,6 +3154,10 @@ int fs2_debug_mt_jump(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
 int fs2_debug_noise(fs2_handle *h, double *out) {
     if (!h || !out) return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_debug_noise: null argument");
     HIP_TRY(h, hipSetDevice(h->cfg.device));
+    {
+        const int rcm = mt_finish(h);
+        if (rcm) return rcm;
+    }
     HIP_TRY(h, hipMemcpyAsync(h->noise_pin, h->noise_dev, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     std::memcpy(out, h->noise_pin, sizeof(double) * h->n);

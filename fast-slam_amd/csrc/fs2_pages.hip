@@ -185,15 +185,11 @@ __global__ __launch_bounds__(kBlock) void k_sweep_write(const uint8_t *mark, int
 // kMarkRecsAhead items per lane with their mark bytes loaded together: most pages
 // are unmarked, and a one-item lane per (page, slot) needed npool/32 workgroups
 // whose dispatch, not the bytes, set the kernel's time.
-#ifndef FS2_MARK_RECS_STRIDE
-#define FS2_MARK_RECS_STRIDE 1
-#endif
 constexpr int kMarkRecsAhead = 4;
 constexpr unsigned kMarkRecsGrid = 4096;
 __global__ __launch_bounds__(kBlock) void k_mark_recs(const char *pool, int64_t npool, const uint8_t *mark,
                                                       uint8_t epoch, int64_t nrecs, uint8_t *rmark,
                                                       uint8_t repoch) {
-#if FS2_MARK_RECS_STRIDE
     const int64_t lanes = npool * kPageSlots;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; t0 < lanes; t0 += kMarkRecsAhead * stride) {
@@ -214,13 +210,6 @@ __global__ __launch_bounds__(kBlock) void k_mark_recs(const char *pool, int64_t 
         for (int u = 0; u < kMarkRecsAhead; ++u)
             if (live[u] && (int64_t)r[u] < nrecs) rmark[r[u]] = repoch;
     }
-#else
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t id = t / kPageSlots;
-    if (id >= npool || mark[id] != epoch) return;
-    const uint32_t r = mirror_rec(load_mirror(pool + id * kPageBytes, (int)(t % kPageSlots)));
-    if ((int64_t)r < nrecs) rmark[r] = repoch;
-#endif
 }
 
 hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t *mark, uint8_t epoch,
@@ -229,10 +218,7 @@ hipError_t launch_collect_records(const char *pool, int64_t npool, const uint8_t
     const int64_t nb = collect_blocks(nrecs);
     const int64_t lanes = npool * kPageSlots;
     if (lanes > 0) {
-        int64_t grid = (lanes + kBlock - 1) / kBlock;
-#if FS2_MARK_RECS_STRIDE
-        grid = std::min<int64_t>(grid, kMarkRecsGrid);
-#endif
+        const int64_t grid = std::min<int64_t>((lanes + kBlock - 1) / kBlock, kMarkRecsGrid);
         hipLaunchKernelGGL(k_mark_recs, dim3((unsigned)grid), dim3(kBlock), 0, s, pool, npool, mark, epoch, nrecs,
                            rmark, repoch);
     }

@@ -180,6 +180,8 @@ SIGNATURES = [
     ("fs2_iterate_wait", C.c_int, [_H, _dp, C.POINTER(fs2_iter_stats)]),
     ("fs2_mt_draw", C.c_int, [_H, C.POINTER(fs2_mt_state), C.c_double, C.POINTER(fs2_mt_state),
                               C.POINTER(fs2_mt_state), _dp]),
+    ("fs2_mt_draw_deferred", C.c_int, [_H, C.POINTER(fs2_mt_state), C.c_double, C.POINTER(fs2_mt_state),
+                                       C.POINTER(fs2_mt_state), _dp]),
     ("fs2_get_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,
                                 C.c_int32]),
     ("fs2_set_state", C.c_int, [_H, C.c_int64, C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int32,

@@ -137,9 +137,14 @@ class FastSLAM2:
                 raise nat.FS2Error(nat.FS2_ERR_ARG, "iterate on a closed FastSLAM2 handle")
             mt_in, mt_after, mt_u0 = self._mt
             C.pointer(mt_in)[0] = nat.fs2_mt_state.from_numpy(np.random.get_state())
-            nat.check(self._lib.fs2_mt_draw(self._h, C.byref(mt_in), float(sigma), C.byref(mt_after),
-                                            C.byref(mt_u0), None), self._h)
-        elif self._rng == "numpy-host":
+            # ended by fs2_iterate below, while its candidate pass runs (mt_after / mt_u0 written then)
+            rc = self._lib.fs2_mt_draw_deferred(self._h, C.byref(mt_in), float(sigma), C.byref(mt_after),
+                                                C.byref(mt_u0), None)
+            if rc == nat.FS2_ERR_STATE and "libm" in nat.last_error(self._h):
+                self._rng = "numpy-host"        # another libm: numpy draws on the host, still exact
+            else:
+                nat.check(rc, self._h)
+        if self._rng == "numpy-host":
             noise = np.random.normal(0, sigma, size=self.num_particles)
             noise = np.ascontiguousarray(noise[self.first_global:self.first_global + self.n_local])
             state = np.random.get_state()

@@ -255,6 +255,15 @@ typedef struct fs2_mt_state {
 } fs2_mt_state;
 int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
                 fs2_mt_state *after_u0, double *u0);
+/* fs2_mt_draw in two halves around the next scan: the draw is enqueued here and
+ * returns at once; the next fs2_iterate / fs2_iterate_submit ends it while its
+ * candidate pass runs (the host's share of the draw -- the counts, the listed
+ * logs, the patches -- then overlaps the GPU instead of preceding the scan) and
+ * writes *after, *after_u0 and *u0 before it returns, whatever it returns; the
+ * three must stay valid until then.  fs2_mt_draw, fs2_set_state, fs2_get_state
+ * and fs2_debug_noise end a pending deferred draw first. */
+int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
+                         fs2_mt_state *after_u0, double *u0);
 
 /* Particle state in the reference's object layout (Particle.x/.y/.yaw/.weight,
  * Particle.landmarks[j] = Landmark(x, y, cov) -- models/particle.py:11-20,

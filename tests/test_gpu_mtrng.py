@@ -7,7 +7,9 @@ after the normals / after u0 must equal what np.random produces from the same
 state, bit for bit, at sizes from 1 to 4M particles, from states with a cached
 gauss and with pos anywhere in the 624-word block (624 included), over
 consecutive draws (the words of the next draw are made ahead on a side stream;
-continuing after the normals or after u0 uses them, a reseed does not)."""
+continuing after the normals or after u0 uses them, a reseed does not), drawn
+synchronously (fs2_mt_draw) or deferred (fs2_mt_draw_deferred, ended by the
+next call that needs it)."""
 import ctypes as C
 
 import numpy as np
@@ -23,14 +25,15 @@ def fs():
     yield fast_slam_2
 
 
-def draw(f, sigma):
+def draw(f, sigma, deferred=False):
     from fast_slam_2 import _native as nat
     lib = nat.load()
     st = np.random.get_state()
     mi, ma, mu, u0 = nat.fs2_mt_state.from_numpy(st), nat.fs2_mt_state(), nat.fs2_mt_state(), C.c_double()
-    nat.check(lib.fs2_mt_draw(f._h, C.byref(mi), sigma, C.byref(ma), C.byref(mu), C.byref(u0)), f._h)
+    fn = lib.fs2_mt_draw_deferred if deferred else lib.fs2_mt_draw
+    nat.check(fn(f._h, C.byref(mi), sigma, C.byref(ma), C.byref(mu), C.byref(u0)), f._h)
     out = np.empty(f.n_local)
-    nat.check(lib.fs2_debug_noise(f._h, nat.ptr(out)), f._h)
+    nat.check(lib.fs2_debug_noise(f._h, nat.ptr(out)), f._h)     # (ends a deferred draw)
     return st, out, ma.to_numpy(), mu.to_numpy(), u0.value
 
 
@@ -51,7 +54,7 @@ def test_mt_draw_matches_numpy(fs, N, pre, words):
         if k == 3:
             np.random.seed(N + 7)            # the caller moves numpy elsewhere: words made ahead are not used
             np.random.random_sample(words % 5)
-        st, out, after, after_u0, u0 = draw(f, sigma)
+        st, out, after, after_u0, u0 = draw(f, sigma, deferred=(k % 2 == 1))
         np.random.set_state(st)
         ref = np.random.normal(0, sigma, size=N)
         bad = np.flatnonzero(out != ref)
@@ -110,4 +113,32 @@ def test_mt_draw_rejects_negative_scale(fs):
     for bad in (-1e-3, float("nan")):
         with pytest.raises(ValueError):
             nat.check(lib.fs2_mt_draw(f._h, C.byref(mi), bad, C.byref(ma), C.byref(mu), None), f._h)
+    f.close()
+
+
+def test_deferred_draw_ends_on_every_path(fs):
+    """A deferred draw writes its outputs whatever ends it: a scan that rejects
+    explicit noise after it (FS2_ERR_ARG), or a state write; the handle works on."""
+    from fast_slam_2 import _native as nat
+    lib = nat.load()
+    N = 4096
+    f = fs.FastSLAM2(N, rng="numpy", verbose=False, landmark_capacity=8)
+    np.random.seed(5)
+    st = np.random.get_state()
+    ref = np.random.normal(0, 0.001, size=N)
+    after_ref = np.random.get_state()
+    for end in ("submit", "set_state"):
+        mi, ma, mu = nat.fs2_mt_state.from_numpy(st), nat.fs2_mt_state(), nat.fs2_mt_state()
+        nat.check(lib.fs2_mt_draw_deferred(f._h, C.byref(mi), 0.001, C.byref(ma), C.byref(mu), None), f._h)
+        if end == "submit":
+            nz = np.zeros(N)
+            rc = lib.fs2_iterate_submit(f._h, 0.0, 0.1, None, None, 0, nat.ptr(nz), None)
+            assert rc == nat.FS2_ERR_ARG
+        else:
+            x, y, yaw, w, c, lm = f.get_state(lm_cap=8)
+            f.set_state(x, y, yaw, w, c, lm)
+        assert same_state(ma.to_numpy(), after_ref), end
+        out = np.empty(N)
+        nat.check(lib.fs2_debug_noise(f._h, nat.ptr(out)), f._h)
+        assert np.array_equal(out, ref), end
     f.close()
