@@ -342,6 +342,8 @@ struct fs2_handle {
     // page_refs mode (fs2_kernels.hpp PeerMaps): every rank's pools mapped here; the
     // pages other ranks may reference stay alive through collective collections
     bool refs = false;                     // the mode is on
+    bool refs_off = false;                 // turned off at the first scan (a rank could not map its peers)
+    bool refuse_maps = false;              // test hook: this rank reports its peer mappings as failed
     bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
     bool refs_live = false;                // a resample has exchanged references (no local collection)
     uint64_t grows = 0;                    // collective pool growths
@@ -505,20 +507,60 @@ static int collect(fs2_handle *h, bool records) {
 // process are created one after the other, so creation cannot wait for them):
 // every rank's page pool, record pool and page marks, mapped here (IPC; the ranks
 // of one process share pointers).  From now on the pools never move.
-static int share_pools(fs2_handle *h) {
+static int share_pools(fs2_handle *h, bool first) {
     const int G = h->cfg.world_size;
+    hipStream_t s = h->stream;
     void *ptrs[kMaxRanks] = {};
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    HIP_TRY(h, hipStreamSynchronize(s));
+    // Every rank takes part in the three exchanges and in the agreement after
+    // them whatever its own mappings did: if some rank cannot map its peers' pools
+    // (no peer access between the devices), the mode turns off on every rank and
+    // the resamples send pages, as they may (no reference has crossed yet).
+    bool ok = true;
+    std::string why;
     for (int what = 0; what < 3; ++what) {
         void *base = what == 0 ? (void *)h->pool : what == 1 ? (void *)h->rpool : (void *)h->mark;
         CommTimer ct(h);
-        const int rc = h->tp->share(base, ptrs, &h->err);
-        if (rc) return rc;
+        std::string e;
+        if (h->tp->share(base, ptrs, &e)) {
+            if (ok) why = e;
+            ok = false;
+            if (int rc = h->tp->status(&h->err)) return rc;     // the transport itself failed
+            continue;
+        }
         for (int q = 0; q < G; ++q) {
             if (what == 0) h->peers_host.pool[q] = (char *)ptrs[q];
             else if (what == 1) h->peers_host.recs[q] = (char *)ptrs[q];
             else h->peers_host.mark[q] = (uint8_t *)ptrs[q];
         }
+    }
+    if (h->refuse_maps && ok) {
+        ok = false;
+        why = "peer mappings refused (fs2_debug_refuse_peer_maps)";
+    }
+    uint8_t all[kMaxRanks] = {};
+    HIP_TRY(h, hipMemsetAsync(h->ep_dev, ok ? 1 : 0, 1, s));
+    {
+        CommTimer ct(h);
+        const int rc = h->tp->allgather(h->ep_dev, h->epochs_dev, 1, s, &h->err);
+        if (rc) return rc;
+    }
+    HIP_TRY(h, hipMemcpyAsync(all, h->epochs_dev, (size_t)G, hipMemcpyDeviceToHost, s));
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (int rc = h->tp->status(&h->err)) return rc;
+    bool every = true;
+    for (int q = 0; q < G; ++q) every &= all[q] == 1;
+    if (!every && !first)             // references have crossed: the grown pools must map
+        return set_err(&h->err, FS2_ERR_COMM, "page_refs: mapping the grown pools failed (%s)",
+                       ok ? "on another rank" : why.c_str());
+    if (!every) {
+        h->tp->unshare();
+        h->refs = false;
+        h->refs_off = true;
+        if (h->cfg.page_refs == 1)
+            return set_err(&h->err, FS2_ERR_COMM, "page_refs on, but %s",
+                           ok ? "another rank could not map its peers' pools" : why.c_str());
+        return FS2_OK;
     }
     HIP_TRY(h, hipMemcpy(h->peers_dev, &h->peers_host, sizeof(PeerMaps), hipMemcpyHostToDevice));
     h->refs_shared = true;
@@ -594,7 +636,7 @@ static int regrow_collective(fs2_handle *h, bool pages, bool recs) {
     if (!rc && recs) rc = grow_recs(h, std::min<int64_t>(h->nrecs + h->nrecs / 2, (int64_t)kRecIdLimit));
     if (rc) return rc;
     h->grows += 1;
-    return share_pools(h);
+    return share_pools(h, false);
 }
 
 // Pool of `pages` pages (existing pages keep their ids), its free list and marks.
@@ -1555,6 +1597,7 @@ int fs2_get_profile(const fs2_handle *hc, fs2_profile *out) {
     const int rc = fold_profile(h);
     if (rc) return rc;
     *out = h->prof;
+    out->page_refs = h->refs_off ? -1 : (h->refs ? 1 : 0);
     return FS2_OK;
 }
 
@@ -1664,7 +1707,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
     int rc;
     if (h->refs && !h->refs_shared) {
-        rc = share_pools(h);
+        rc = share_pools(h, true);
         if (rc) return rc;
     }
     bool collected = false;
@@ -3148,6 +3191,14 @@ int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs
 int fs2_debug_mt_jump(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
     if (!key || !out) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_mt_jump: null argument");
     if (!mt_jump_host(key, J, out)) return set_err(nullptr, FS2_ERR_STATE, "MT19937 characteristic polynomial not found");
+    return FS2_OK;
+}
+
+int fs2_debug_refuse_peer_maps(fs2_handle *h) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (h->refs_shared || h->refs_off)
+        return set_err(&h->err, FS2_ERR_STATE, "fs2_debug_refuse_peer_maps: the pools are mapped already");
+    h->refuse_maps = true;
     return FS2_OK;
 }
 

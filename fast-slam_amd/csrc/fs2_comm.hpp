@@ -116,16 +116,22 @@ class RcclTransport : public Transport {
   public:
     ncclComm_t comm = nullptr;
     int G = 1, r = 0;
+    bool failed_ = false;             // an IPC handle exchange failed: the communicator is unusable
+    int status(std::string *err) override {
+        if (!failed_) return FS2_OK;
+        if (err) *err = "rccl transport: the IPC handle exchange failed";
+        return FS2_ERR_COMM;
+    }
     ~RcclTransport() override {
         close_handles();
         if (comm) ncclCommDestroy(comm);
     }
+    // (a rank whose handle or mappings fail still takes part in the exchange; it
+    // returns the failure, fs2_api's agreement turns the mode off on every rank)
     int share(void *base, void **peers, std::string *err) override {
         hipIpcMemHandle_t mine;
-        if (hipIpcGetMemHandle(&mine, base) != hipSuccess) {
-            if (err) *err = "hipIpcGetMemHandle failed";
-            return FS2_ERR_COMM;
-        }
+        const bool got = hipIpcGetMemHandle(&mine, base) == hipSuccess;
+        if (!got) std::memset(&mine, 0, sizeof mine);
         std::vector<hipIpcMemHandle_t> hs(G);
         char *d = nullptr;
         hipStream_t s = nullptr;
@@ -145,7 +151,15 @@ class RcclTransport : public Transport {
             rc = FS2_ERR_COMM;
         if (s) hipStreamDestroy(s);
         hipFree(d);
-        return rc ? rc : open_handles(hs, base, peers, err);
+        if (rc) {
+            failed_ = true;           // the exchange itself: the communicator is unusable
+            return rc;
+        }
+        if (!got) {
+            if (err) *err = "hipIpcGetMemHandle failed";
+            return FS2_ERR_COMM;
+        }
+        return open_handles(hs, base, peers, err);
     }
     int world() const override { return G; }
     int rank() const override { return r; }

@@ -123,6 +123,7 @@ class fs2_profile(C.Structure):
         ("model_fixed_bytes", C.c_uint64),
         ("model_box_bytes", C.c_uint64),
         ("localized_pages", C.c_uint64),
+        ("page_refs", C.c_int64),
     ]
 
     def as_dict(self):
@@ -213,6 +214,7 @@ SIGNATURES = [
     ("fs2_debug_philox", C.c_int, [C.c_int32, C.c_int64, _vp, _vp, _vp]),
     ("fs2_debug_normals", C.c_int, [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, _vp]),
     ("fs2_debug_mt_log", C.c_int, [C.c_int32, _vp, C.c_int64, _vp, _vp, C.c_int32]),
+    ("fs2_debug_refuse_peer_maps", C.c_int, [_H]),
     ("fs2_debug_noise", C.c_int, [_H, _vp]),
     ("fs2_debug_mt_jump", C.c_int, [_vp, C.c_uint64, _vp]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),

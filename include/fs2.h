@@ -183,6 +183,9 @@ typedef struct fs2_profile {
     uint64_t model_box_bytes;   /* row-box bytes (k_candidates reads, k_update reads + writes) */
     uint64_t localized_pages;   /* page_refs: remote pages copied into this rank's pools before an
                                    update pass read them (with their records: 128 + 8 x 48 B each) */
+    int64_t page_refs;          /* page_refs mode: 1 in effect, 0 off, -1 turned off on every rank at
+                                   the first scan because some rank could not map its peers' pools
+                                   (no peer access between the devices; resamples then send pages) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */
@@ -373,6 +376,11 @@ int fs2_debug_normals(int32_t device, uint64_t seed, uint64_t stream, uint64_t f
  * on_host = 1 runs the same arithmetic on the CPU.  x in (0, 1), host buffers. */
 int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, int32_t *amb,
                      int32_t on_host);
+/* Test hook of page_refs' fallback: this rank reports, at its first scan, that it
+ * could not map its peers' pools (as without peer access between devices); the
+ * mode then turns off on every rank (fs2_profile.page_refs = -1; with page_refs
+ * = 1 the first scan fails instead).  Before the first scan only. */
+int fs2_debug_refuse_peer_maps(fs2_handle *h);
 /* Test hook: the handle's motion-noise buffer (N_local values: the last scan's
  * injected draws, or fs2_mt_draw's) into out. */
 int fs2_debug_noise(fs2_handle *h, double *out);

@@ -77,6 +77,9 @@ def test_sharded_matches_single(G, N, L):
         a, b = h.first_global, h.first_global + h.n_local
         h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
         h.set_profiling(True)
+    from fast_slam_2 import _native as nat
+    for g in refuse:
+        nat.check(shards[g]._lib.fs2_debug_refuse_peer_maps(shards[g]._h), shards[g]._h)
     resamples = 0
     moved = 0
     firsts = {g: {h.first_global} for g, h in enumerate(shards)}
@@ -175,7 +178,7 @@ def test_sharded_exact_is_bitwise(G, N, L):
         h.close()
 
 
-def _run_sharded(G, N, L, scans, page_refs, seed=21, page_pool=0, record_pool=0):
+def _run_sharded(G, N, L, scans, page_refs, seed=21, page_pool=0, record_pool=0, refuse=()):
     """G local ranks over the peaked workload, each scan checked against a single
     handle (decisions, estimates, associations; states within 1e-9); returns the
     ranks' profiles and last stats."""
@@ -199,6 +202,9 @@ def _run_sharded(G, N, L, scans, page_refs, seed=21, page_pool=0, record_pool=0)
         a, b = h.first_global, h.first_global + h.n_local
         h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
         h.set_profiling(True)
+    from fast_slam_2 import _native as nat
+    for g in refuse:
+        nat.check(shards[g]._lib.fs2_debug_refuse_peer_maps(shards[g]._h), shards[g]._h)
     resamples = 0
     for s in range(scans):
         rot, tr = syn.odometry(s)
@@ -243,6 +249,23 @@ def test_page_refs_vs_whole_pages(G, N, L):
     assert 0 < b_on * 4 < b_off, (b_on, b_off)
     assert sum(p["localized_pages"] for p in on) > 0
     assert sum(p["localized_pages"] for p in off) == 0
+
+
+def test_page_refs_fall_back_when_a_rank_cannot_map():
+    """A rank that cannot map its peers' pools at the first scan (no peer access
+    between devices; fs2_debug_refuse_peer_maps) turns page_refs off on every rank:
+    the resamples send pages, every scan still equals the single handle.  With
+    page_refs forced on, the first scan fails on every rank instead of hanging."""
+    from fast_slam_2 import _native as nat
+    from gpu_util import configure
+    configure()
+    G, N, L = 3, 6000, 40
+    r1, fb, _ = _run_sharded(G, N, L, 8, "auto", refuse=(1,))
+    assert r1 >= 2
+    assert [p["page_refs"] for p in fb] == [-1] * G
+    assert sum(p["localized_pages"] for p in fb) == 0 and sum(p["migrations"] for p in fb) >= 2
+    with pytest.raises(nat.FS2Error, match="page_refs on"):
+        _run_sharded(G, N, L, 2, "on", refuse=(2,))
 
 
 def test_page_refs_collective_collections():
