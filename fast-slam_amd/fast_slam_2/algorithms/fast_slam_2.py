@@ -25,6 +25,7 @@ from collections.abc import Sequence
 import numpy as np
 
 from .. import _native as nat
+from .. import _npstate
 from .. import config
 from ..models.landmark import Landmark
 from ..models.measurement import Measurement
@@ -136,7 +137,11 @@ class FastSLAM2:
             if self._h is None:
                 raise nat.FS2Error(nat.FS2_ERR_ARG, "iterate on a closed FastSLAM2 handle")
             mt_in, mt_after, mt_u0 = self._mt
-            C.pointer(mt_in)[0] = nat.fs2_mt_state.from_numpy(np.random.get_state())
+            npv = _npstate.view()                # numpy's state in place (get_state: ~40-70 us)
+            if npv is not None:
+                npv.read(mt_in)
+            else:
+                C.pointer(mt_in)[0] = nat.fs2_mt_state.from_numpy(np.random.get_state())
             # ended by fs2_iterate below, while its candidate pass runs (mt_after / mt_u0 written then)
             rc = self._lib.fs2_mt_draw_deferred(self._h, C.byref(mt_in), float(sigma), C.byref(mt_after),
                                                 C.byref(mt_u0), None)
@@ -158,7 +163,12 @@ class FastSLAM2:
         self.last_stats = st
         if self._rng == "numpy":
             # the normals are drawn by the move, u0 only when resampling (fast_slam_2.py:79,81,183)
-            np.random.set_state((self._mt[2] if (rc == 0 and st.resampled) else self._mt[1]).to_numpy())
+            chosen = self._mt[2] if (rc == 0 and st.resampled) else self._mt[1]
+            npv = _npstate.view()
+            if npv is not None:
+                npv.write(chosen)
+            else:
+                np.random.set_state(chosen.to_numpy())
         elif state is not None and not st.resampled:
             np.random.set_state(state)          # the reference draws u0 only when resampling
         nat.check(rc, self._h)
