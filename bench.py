@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--landmarks", type=int, default=0, help="override landmarks per particle")
     ap.add_argument("--map", choices=("grid", "dense"), default="grid",
                     help="dense: the robustness dense-map workload as the timed one (its PMC record)")
+    ap.add_argument("--profile-every", type=int, default=PROFILE_EVERY,
+                    help="timed scans per scan with kernel events (0: none; the line then lacks kernel times)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=0)
@@ -718,7 +720,8 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
         coll0 = st0.collections
     # kernel events on every 4th timed scan: a dispatch's start / end events delay
     # the next dispatch by ~4.5 us, which the other scans do not pay
-    f.set_profiling(True, every=PROFILE_EVERY)
+    if args.profile_every > 0:
+        f.set_profiling(True, every=args.profile_every)
     sums = dict(resamples=0, visited=0, copied_slots=0, cow=0, exact=0, opened=0, ref_visits=0, hits_appends=0)
     step_ms = []                 # (host ms, resampled) of each timed scan on this rank
     barrier()

@@ -98,6 +98,7 @@ class FastSLAM2:
         self._wait_raw = wproto(C.cast(lib.fs2_iterate_wait, C.c_void_p).value)
         self._hv = h.value
         self._mcap = 0
+        self._grow_meas(8)                      # measurement / observed-point buffers
         self._pose = np.empty(3)
         self._pose_addr = self._pose.ctypes.data
         self._st = nat.fs2_iter_stats()
@@ -105,6 +106,9 @@ class FastSLAM2:
         self._u0 = np.empty(1)
         self._u0_addr = self._u0.ctypes.data
         self._mt = [nat.fs2_mt_state() for _ in range(3)]     # in, after the normals, after u0
+        self._mt_addr = [C.addressof(m) for m in self._mt]
+        dproto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p)
+        self._draw_raw = dproto(C.cast(lib.fs2_mt_draw_deferred, C.c_void_p).value)
 
     @property
     def first_global(self) -> int:
@@ -121,30 +125,31 @@ class FastSLAM2:
     def iterate(self, rotation: float, translation: float,
                 measurements: list[Measurement]) -> tuple[float, float, float]:
         """One FastSLAM step (reference fast_slam_2.py:33-67); returns the estimate pose."""
+        if not getattr(self, "_h", None) or not self._hv:
+            raise nat.FS2Error(nat.FS2_ERR_ARG, "iterate on a closed FastSLAM2 handle")
         M = len(measurements)
-        meas = np.empty((M, 2))
-        obs = np.empty((M, 2))
+        if M > self._mcap:
+            self._grow_meas(M)
+        mb, ob = self._mbuf, self._obuf
         for k, m in enumerate(measurements):
-            meas[k, 0] = m.distance
-            meas[k, 1] = m.yaw
+            d, b = m.distance, m.yaw
+            mb[k, 0] = d
+            mb[k, 1] = b
             # observed robot-frame point, computed as the reference does (:100-103)
-            obs[k, 0] = m.distance * np.cos(m.yaw)
-            obs[k, 1] = m.distance * np.sin(m.yaw)
+            ob[k, 0] = d * np.cos(b)
+            ob[k, 1] = d * np.sin(b)
         noise = u0 = None
         state = None
         sigma = config.ROTATION_NOISE if rotation != 0 else config.TRANSLATION_NOISE
         if self._rng == "numpy":
-            if self._h is None:
-                raise nat.FS2Error(nat.FS2_ERR_ARG, "iterate on a closed FastSLAM2 handle")
-            mt_in, mt_after, mt_u0 = self._mt
+            mt_in = self._mt[0]
             npv = _npstate.view()                # numpy's state in place (get_state: ~40-70 us)
             if npv is not None:
                 npv.read(mt_in)
             else:
                 C.pointer(mt_in)[0] = nat.fs2_mt_state.from_numpy(np.random.get_state())
             # ended by fs2_iterate below, while its candidate pass runs (mt_after / mt_u0 written then)
-            rc = self._lib.fs2_mt_draw_deferred(self._h, C.byref(mt_in), float(sigma), C.byref(mt_after),
-                                                C.byref(mt_u0), None)
+            rc = self._draw_raw(self._hv, self._mt_addr[0], float(sigma), self._mt_addr[1], self._mt_addr[2], None)
             if rc == nat.FS2_ERR_STATE and "libm" in nat.last_error(self._h):
                 self._rng = "numpy-host"        # another libm: numpy draws on the host, still exact
             else:
@@ -153,13 +158,13 @@ class FastSLAM2:
             noise = np.random.normal(0, sigma, size=self.num_particles)
             noise = np.ascontiguousarray(noise[self.first_global:self.first_global + self.n_local])
             state = np.random.get_state()
-            u0 = np.array([np.random.uniform(0, 1 / self.num_particles)])
-        pose = np.empty(3)
-        st = nat.fs2_iter_stats()
-        rc = self._lib.fs2_iterate(self._h, float(rotation), float(translation),
-                                   nat.ptr(meas) if M else None, nat.ptr(obs) if M else None,
-                                   M, nat.ptr(noise), nat.ptr(u0), nat.dptr(pose), C.byref(st))
+            self._u0[0] = np.random.uniform(0, 1 / self.num_particles)
+            u0 = self._u0_addr
+        rc = self._iterate_raw(self._hv, float(rotation), float(translation), self._mbuf_addr if M else None,
+                               self._obuf_addr if M else None, M, None if noise is None else noise.ctypes.data, u0,
+                               self._pose_addr, self._st_addr)
         self._particles = None
+        st = nat.fs2_iter_stats.from_buffer_copy(self._st)
         self.last_stats = st
         if self._rng == "numpy":
             # the normals are drawn by the move, u0 only when resampling (fast_slam_2.py:79,81,183)
@@ -174,7 +179,15 @@ class FastSLAM2:
         nat.check(rc, self._h)
         if st.resampled and self._verbose:
             print("\nRESAMPLING")               # reference fast_slam_2.py:63
+        pose = self._pose
         return float(pose[0]), float(pose[1]), float(pose[2])
+
+    def _grow_meas(self, M):
+        self._mcap = max(M, 2 * self._mcap, 8)
+        self._mbuf = np.empty((self._mcap, 2))
+        self._obuf = np.empty((self._mcap, 2))
+        self._mbuf_addr = self._mbuf.ctypes.data
+        self._obuf_addr = self._obuf.ctypes.data
 
     def step(self, rotation: float, translation: float, meas, observed=None, noise=None,
              u0=None):
@@ -210,11 +223,7 @@ class FastSLAM2:
             if obs.shape[0] != M:
                 raise ValueError(f"observed has {obs.shape[0]} points for {M} measurements")
         if M > self._mcap:
-            self._mcap = max(M, 2 * self._mcap, 8)
-            self._mbuf = np.empty((self._mcap, 2))
-            self._obuf = np.empty((self._mcap, 2))
-            self._mbuf_addr = self._mbuf.ctypes.data
-            self._obuf_addr = self._obuf.ctypes.data
+            self._grow_meas(M)
         oa = None
         if M:
             self._mbuf[:M] = meas

@@ -5,9 +5,12 @@ The page and record pools are virtual ranges reserved at creation, grown by
 mapping physical chunks at their end (hipMemCreate / hipMemMap), so a growth
 copies nothing: a scan that grows the record pool costs a collection and a
 mapping, not an allocate-and-copy of the whole pool (round 3: ~20 ms for 35 GB).
-A handle whose record pool starts just above its maps grows it within the run;
-every scan is compared with the C oracle, and no scan takes more than 1 ms
-longer than the median of its neighbours.
+A handle whose record pool starts just above its maps grows it within the run:
+every measurement is a miss far from the maps (four new landmarks per particle
+and scan, no weight change, no resample to share records), so the live records
+grow by 4 N per scan and the pool must grow several times.  Every scan is
+compared with the C oracle, and no scan takes more than 1 ms longer than the
+median of its neighbours.
 """
 import time
 
@@ -41,7 +44,8 @@ def test_record_pool_grows_in_place():
     ms_each, recs = [], []
     for s in range(S):
         rot, tr = syn.odometry(s)
-        ms = wl.measurements(s)
+        # four misses, 20+ m from the maps and from each other
+        ms = np.array([[100.0 + 10.0 * s + 20.0 * k, 0.25 * k + 0.01 * s] for k in range(4)])
         nz = rng.normal(0, 0.001 if rot else 0.0055, N)
         u0 = rng.uniform(0, 1.0 / N)
         t0 = time.perf_counter()
@@ -57,7 +61,7 @@ def test_record_pool_grows_in_place():
     assert np.allclose(flm, o.lm, rtol=1e-9, atol=1e-12)
     f.close()
     grew = [s for s in range(1, S) if recs[s] > recs[s - 1]]
-    assert grew, recs                                   # the record pool grew inside the run
+    assert len(grew) >= 2, recs                         # the record pool grew inside the run
     for s in grew:
         nb = [ms_each[k] for k in range(max(1, s - 3), min(S, s + 4)) if k != s and k not in grew]
         assert ms_each[s] - float(np.median(nb)) < 1.0, (s, ms_each[s], nb, ms_each)
