@@ -347,6 +347,7 @@ struct fs2_handle {
     bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
     bool refs_live = false;                // a resample has exchanged references (no local collection)
     uint64_t grows = 0;                    // collective pool growths
+    uint64_t vm_fallbacks = 0;             // growths that left the reserved range (allocate and copy)
     PeerMaps peers_host{};
     PeerMaps *peers_dev = nullptr;
     uint8_t *ep_dev = nullptr, *epochs_dev = nullptr;     // this rank's / every rank's collection epoch
@@ -658,15 +659,21 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         if (hipMemGetInfo(&fr, &tot) == hipSuccess)
             gm_init(h->pool_vm, h->cfg.device, std::min<size_t>((size_t)kIdMask * kPageBytes, tot));
     }
-    if (h->pool_vm.base && (size_t)pages * kPageBytes <= h->pool_vm.reserved) {
-        HIP_TRY(h, gm_grow(h->pool_vm, (size_t)pages * kPageBytes));
+    if (h->pool_vm.base && (size_t)pages * kPageBytes <= h->pool_vm.reserved &&
+        gm_grow(h->pool_vm, (size_t)pages * kPageBytes) == hipSuccess) {
         h->pool = h->pool_vm.base;
     } else {
-        if (h->pool_vm.base) return set_err(&h->err, FS2_ERR_OOM, "page pool beyond its reserved range");
+        // beyond the reservation, or the mapping failed: allocate and copy (the
+        // reserved range is left for good)
         char *pool = nullptr;
         HIP_TRY(h, hipMalloc(&pool, (size_t)pages * kPageBytes));
         if (h->pool) HIP_TRY(h, copy_sync(h, pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
-        hipFree(h->pool);
+        if (h->pool_vm.base) {
+            gm_free(h->pool_vm);
+            h->vm_fallbacks += 1;
+        } else {
+            hipFree(h->pool);
+        }
         h->pool = pool;
     }
     uint8_t *mark = nullptr;
@@ -713,15 +720,19 @@ static int grow_recs(fs2_handle *h, int64_t n) {
         if (hipMemGetInfo(&fr, &tot) == hipSuccess)
             gm_init(h->rpool_vm, h->cfg.device, std::min<size_t>((size_t)kRecIdLimit * kRecBytes, tot));
     }
-    if (h->rpool_vm.base && (size_t)n * kRecBytes <= h->rpool_vm.reserved) {
-        HIP_TRY(h, gm_grow(h->rpool_vm, (size_t)n * kRecBytes));
+    if (h->rpool_vm.base && (size_t)n * kRecBytes <= h->rpool_vm.reserved &&
+        gm_grow(h->rpool_vm, (size_t)n * kRecBytes) == hipSuccess) {
         h->rpool = h->rpool_vm.base;
     } else {
-        if (h->rpool_vm.base) return set_err(&h->err, FS2_ERR_OOM, "record pool beyond its reserved range");
         char *rp = nullptr;
         HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
         if (h->rpool) HIP_TRY(h, copy_sync(h, rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
-        hipFree(h->rpool);
+        if (h->rpool_vm.base) {
+            gm_free(h->rpool_vm);
+            h->vm_fallbacks += 1;
+        } else {
+            hipFree(h->rpool);
+        }
         h->rpool = rp;
     }
     uint8_t *mark = nullptr;
@@ -2195,6 +2206,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         stats->collections = h->collections;
         stats->pool_pages = (uint64_t)h->npool;
         stats->pool_records = (uint64_t)h->nrecs;
+        stats->pool_copies = h->vm_fallbacks;
         stats->pages_opened = st.opened;
         stats->reference_visits = st.ref_visits;
     }

@@ -84,6 +84,7 @@ class fs2_iter_stats(C.Structure):
         ("pages_opened", C.c_uint64),
         ("reference_visits", C.c_uint64),
         ("pool_records", C.c_uint64),
+        ("pool_copies", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -135,6 +135,8 @@ typedef struct fs2_iter_stats {
                                    j + 1 for a match at j, the map size for an append
                                    (landmark_utils.py:103-117; SURVEY §8d's V) */
     uint64_t pool_records;      /* records in the record pool (48 B each) */
+    uint64_t pool_copies;       /* pool growths that moved a pool (allocate and copy) instead of
+                                   mapping memory at the end of its reserved range (handle lifetime) */
 } fs2_iter_stats;
 
 typedef struct fs2_profile {

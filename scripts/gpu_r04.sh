@@ -5,6 +5,7 @@
 #   prof   rocprofv3 kernel stats of the config-3 bench
 #   host   scripts/host_turnaround.py (host share of a scan)
 #   pmc    HBM bytes by PMC: config 3 and its dense-map variant
+#   vmm    scripts/vmm_probe (growing a reserved range chunk by chunk)
 # Stops at the first failing step; each GPU step has its own time limit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -12,7 +13,11 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STAGES=${1:-all}
 TESTS=${TESTS:-tests}
-has() { [[ ",$STAGES," == *",$1,"* || ( $STAGES == all && $1 != host && $1 != pmc ) ]]; }
+has() { [[ ",$STAGES," == *",$1,"* || ( $STAGES == all && $1 != host && $1 != pmc && $1 != vmm ) ]]; }
+if has vmm; then
+  timeout -k 10 120 ./scripts/vmm_probe > gpurun_out/vmm_probe.txt 2>&1 || { echo vmm probe failed; tail -20 gpurun_out/vmm_probe.txt; exit 8; }
+  tail -1 gpurun_out/vmm_probe.txt
+fi
 if has tests; then
   timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v -rf --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
   rc=$?

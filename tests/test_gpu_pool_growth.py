@@ -62,6 +62,7 @@ def test_record_pool_grows_in_place():
     f.close()
     grew = [s for s in range(1, S) if recs[s] > recs[s - 1]]
     assert len(grew) >= 2, recs                         # the record pool grew inside the run
+    assert st.pool_copies == 0, st.pool_copies          # in place: nothing moved
     for s in grew:
         nb = [ms_each[k] for k in range(max(1, s - 3), min(S, s + 4)) if k != s and k not in grew]
         assert ms_each[s] - float(np.median(nb)) < 1.0, (s, ms_each[s], nb, ms_each)
