@@ -108,11 +108,16 @@ static hipMemAllocationProp gm_prop(int device) {
 static bool gm_init(GrowMem &g, int device, size_t max_bytes) {
     hipMemAllocationProp prop = gm_prop(device);
     size_t gran = 0;
-    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran)
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran) {
+        (void)hipGetLastError();
         return false;
+    }
     const size_t r = (max_bytes + gran - 1) / gran * gran;
     void *p = nullptr;
-    if (hipMemAddressReserve(&p, r, 0, nullptr, 0) != hipSuccess || !p) return false;
+    if (hipMemAddressReserve(&p, r, 0, nullptr, 0) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        return false;
+    }
     g.base = static_cast<char *>(p);
     g.reserved = r;
     g.gran = gran;
@@ -126,20 +131,29 @@ static hipError_t gm_grow(GrowMem &g, size_t bytes) {
     const size_t delta = want - g.mapped;
     hipMemAllocationProp prop = gm_prop(g.device);
     hipMemGenericAllocationHandle_t hd{};
+    // (a failure is reported once: the runtime's last error is cleared, so the
+    // caller's fallback launches do not inherit it)
     hipError_t e = hipMemCreate(&hd, delta, &prop, 0);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return e;
+    }
     e = hipMemMap(g.base + g.mapped, delta, 0, hd, 0);
     if (e != hipSuccess) {
         hipMemRelease(hd);
+        (void)hipGetLastError();
         return e;
     }
+    // access over everything mapped so far: setting it on the new chunk alone
+    // fails now and then on ROCm 7.2 (scripts/vmm_probe.hip, profiles/r04_vmm_probe.txt)
     hipMemAccessDesc ad{};
     ad.location = prop.location;
     ad.flags = hipMemAccessFlagsProtReadWrite;
-    e = hipMemSetAccess(g.base + g.mapped, delta, &ad, 1);
+    e = hipMemSetAccess(g.base, want, &ad, 1);
     if (e != hipSuccess) {
         hipMemUnmap(g.base + g.mapped, delta);
         hipMemRelease(hd);
+        (void)hipGetLastError();
         return e;
     }
     g.chunks.push_back({hd, delta});
