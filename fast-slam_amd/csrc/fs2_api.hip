@@ -362,6 +362,13 @@ struct fs2_handle {
     bool refs_live = false;                // a resample has exchanged references (no local collection)
     uint64_t grows = 0;                    // collective pool growths
     uint64_t vm_fallbacks = 0;             // growths that left the reserved range (allocate and copy)
+    // what a record collection could free at most: the free-list entries taken
+    // since the last one minus the records appended since (the rest were unused
+    // or replaced slots) -- a bound only while no particle was dropped (resample)
+    // and no map replaced (import) since
+    int64_t appends_since_rcollect = 0;
+    bool rcollect_exact = true;            // (a new handle's pools hold no record yet)
+    std::vector<uint8_t> imported;         // particles whose maps were imported before the first scan
     PeerMaps peers_host{};
     PeerMaps *peers_dev = nullptr;
     uint8_t *ep_dev = nullptr, *epochs_dev = nullptr;     // this rank's / every rank's collection epoch
@@ -489,7 +496,28 @@ static int refs_short(fs2_handle *h, const char *what) {
 // Collect the page pool: every page the current page table does not refer to
 // becomes free (fs2_pages.hip); the reservation cursor restarts.  With
 // `records`, the record pool is collected from the same marks as well.
+static int collect_body(fs2_handle *h, bool records);
+// (host wall time of collections and growths, fs2_profile)
+struct PoolTimer {
+    fs2_handle *h;
+    bool grow;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~PoolTimer() {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (grow) {
+            h->prof.pool_grows += 1;
+            h->prof.grow_ms += ms;
+        } else {
+            h->prof.pool_collections += 1;
+            h->prof.collect_ms += ms;
+        }
+    }
+};
 static int collect(fs2_handle *h, bool records) {
+    PoolTimer pt{h, false};
+    return collect_body(h, records);
+}
+static int collect_body(fs2_handle *h, bool records) {
     hipStream_t s = h->stream;
     if (h->epoch == 255) {
         HIP_TRY(h, hipMemsetAsync(h->mark, 0, (size_t)h->npool, s));
@@ -509,6 +537,8 @@ static int collect(fs2_handle *h, bool records) {
                                           h->rbcnt, h->rfreel, h->rnfree_dev, s));
         HIP_TRY(h, hipMemcpyAsync(&h->rnfree, h->rnfree_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         h->rcursor = 0;
+        h->appends_since_rcollect = 0;
+        h->rcollect_exact = true;
     }
     // page ids are recycled from here on: the transfer probe starts over
     if (h->sent_mask) HIP_TRY(h, hipMemsetAsync(h->sent_mask, 0, sizeof(uint32_t) * (size_t)h->npool, s));
@@ -661,6 +691,7 @@ static int regrow_collective(fs2_handle *h, bool pages, bool recs) {
 static int grow_pool(fs2_handle *h, int64_t pages) {
     if (pages <= h->npool) return FS2_OK;
     if (h->refs_shared) return refs_short(h, "page");
+    PoolTimer pt{h, true};
     if (h->refs && pages > (int64_t)kRefIdMask)
         return set_err(&h->err, FS2_ERR_CAPACITY, "page_refs mode: %lld pages exceed the %u local page ids",
                        (long long)pages, kRefIdMask);
@@ -724,6 +755,7 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
 static int grow_recs(fs2_handle *h, int64_t n) {
     if (n <= h->nrecs) return FS2_OK;
     if (h->refs_shared) return refs_short(h, "record");
+    PoolTimer pt{h, true};
     if (n > (int64_t)kRecIdLimit)
         return set_err(&h->err, FS2_ERR_OOM, "record pool of %lld records exceeds the 32-bit id space",
                        (long long)n);
@@ -794,10 +826,17 @@ static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
 static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
     if (h->rcursor + need > h->rnfree) {
         if (h->refs_live) return refs_short(h, "record");
-        int rc = collect(h, true);
-        if (rc) return rc;
-        if (need > h->rnfree) {
-            const int64_t live = h->nrecs - h->rnfree;
+        // a collection that cannot free enough is skipped: the pool grows at once
+        // (the free list keeps its taken entries, the new ids follow it)
+        const bool futile = h->rcollect_exact &&
+                            (h->rnfree - h->rcursor) + (h->rcursor - h->appends_since_rcollect) < need;
+        int rc = FS2_OK;
+        if (!futile) {
+            rc = collect(h, true);
+            if (rc) return rc;
+        }
+        if (h->rcursor + need > h->rnfree) {
+            const int64_t live = h->nrecs - (h->rnfree - h->rcursor);
             // grow by half, clamped to the id space (grow_recs fails beyond it)
             int64_t want = std::max(h->nrecs + h->nrecs / 2, live + 2 * need);
             if (want > (int64_t)kRecIdLimit) want = std::max<int64_t>(kRecIdLimit, live + need);
@@ -2184,6 +2223,8 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         }
     }
     if (st.resampled) h->cur = 1 - h->cur;
+    h->appends_since_rcollect += (int64_t)st.appends;
+    if (st.resampled) h->rcollect_exact = false;     // dropped particles' records: no bound
     h->cnt_upper = st.max_count;
     h->last_m = M;
     h->scan += 1;
@@ -2296,6 +2337,20 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         if (rc) return rc;
         const int32_t rows_each = std::max(1, (mx + kPageSlots - 1) / kPageSlots);
         h->cnt_upper = std::max(h->cnt_upper, mx);
+        // the collection bound (reserve_recs): the imported records are live; maps
+        // replaced (imported twice, or after a scan) leave records of unknown number
+        {
+            int64_t used = 0;
+            for (int32_t v : hc) used += v;
+            h->appends_since_rcollect += used;
+            if ((int64_t)h->imported.size() != h->n) h->imported.assign((size_t)h->n, 0);
+            bool replaced = h->scan > 0;
+            for (int64_t k = first; k < first + count; ++k) {
+                replaced |= h->imported[(size_t)k] != 0;
+                h->imported[(size_t)k] = 1;
+            }
+            if (replaced) h->rcollect_exact = false;
+        }
         // stage in chunks of <= 256 MiB
         const int64_t per = (int64_t)std::max(1, lm_cap) * 6 * 8;
         const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / per);

@@ -83,6 +83,7 @@ class Transport {
             }
             void *q = nullptr;
             if (hipIpcOpenMemHandle(&q, hs[p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();     // reported here, not by the next launch
                 if (err) *err = "hipIpcOpenMemHandle failed (page references across ranks)";
                 return FS2_ERR_COMM;
             }
@@ -131,7 +132,10 @@ class RcclTransport : public Transport {
     int share(void *base, void **peers, std::string *err) override {
         hipIpcMemHandle_t mine;
         const bool got = hipIpcGetMemHandle(&mine, base) == hipSuccess;
-        if (!got) std::memset(&mine, 0, sizeof mine);
+        if (!got) {
+            (void)hipGetLastError();
+            std::memset(&mine, 0, sizeof mine);
+        }
         std::vector<hipIpcMemHandle_t> hs(G);
         char *d = nullptr;
         hipStream_t s = nullptr;

@@ -125,6 +125,10 @@ class fs2_profile(C.Structure):
         ("model_box_bytes", C.c_uint64),
         ("localized_pages", C.c_uint64),
         ("page_refs", C.c_int64),
+        ("pool_collections", C.c_int64),
+        ("collect_ms", C.c_double),
+        ("pool_grows", C.c_int64),
+        ("grow_ms", C.c_double),
     ]
 
     def as_dict(self):

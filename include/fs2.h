@@ -188,6 +188,10 @@ typedef struct fs2_profile {
     int64_t page_refs;          /* page_refs mode: 1 in effect, 0 off, -1 turned off on every rank at
                                    the first scan because some rank could not map its peers' pools
                                    (no peer access between the devices; resamples then send pages) */
+    int64_t pool_collections;   /* pool collections run (host calls; each drains the stream) */
+    double collect_ms;          /* their host wall time */
+    int64_t pool_grows;         /* pool growths (in place, or allocate and copy: fs2_iter_stats.pool_copies) */
+    double grow_ms;             /* their host wall time */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */

@@ -38,6 +38,7 @@ def test_record_pool_grows_in_place():
     f = fast_slam_2.FastSLAM2(N, rng="device", seed=4, landmark_capacity=cap, verbose=False, reduce="exact",
                               record_assoc=True, record_pool=N * L + 12 * N)
     f.set_state(x, y, yaw, w, cnt, lm)
+    f.set_profiling(True)                   # (the collections' and growths' host time)
     o = orc.OracleFilter(N, cap)
     o.set_state(x, y, yaw, w, cnt, lm)
     rng = np.random.default_rng(12)
@@ -56,13 +57,15 @@ def test_record_pool_grows_in_place():
         assert np.array_equal(f.associations(), oassoc), s
         assert bool(st.resampled) == ors, s
         assert np.allclose(pose, opose, rtol=1e-9, atol=1e-12), s
+    prof = f.profile()
+    pool = {k: prof[k] for k in ("pool_collections", "collect_ms", "pool_grows", "grow_ms")}
     fx, fy, fyaw, fw, fc, flm = f.get_state(lm_cap=cap)
     assert np.array_equal(fc, o.cnt)
     assert np.allclose(flm, o.lm, rtol=1e-9, atol=1e-12)
     f.close()
     grew = [s for s in range(1, S) if recs[s] > recs[s - 1]]
-    assert len(grew) >= 2, recs                         # the record pool grew inside the run
+    assert len(grew) >= 2, (recs, pool)                 # the record pool grew inside the run
     assert st.pool_copies == 0, st.pool_copies          # in place: nothing moved
     for s in grew:
         nb = [ms_each[k] for k in range(max(1, s - 3), min(S, s + 4)) if k != s and k not in grew]
-        assert ms_each[s] - float(np.median(nb)) < 1.0, (s, ms_each[s], nb, ms_each)
+        assert ms_each[s] - float(np.median(nb)) < 1.0, (s, ms_each[s], nb, ms_each, pool)
