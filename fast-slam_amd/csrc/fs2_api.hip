@@ -202,6 +202,8 @@ struct fs2_handle {
     char *pool = nullptr;
     int64_t npool = 0;                     // pages in the pool
     GrowMem pool_vm, rpool_vm;             // in-place growth of the page / record pools (base null: hipMalloc)
+    GrowMem mark_vm, freel_vm, rmark_vm, rfreel_vm;   // their marks and free lists, alike
+    int64_t bcnt_cap = 0, rbcnt_cap = 0;   // sweep block counts allocated (collect_blocks)
     Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
     uint32_t *bbox[2] = {};                // [nblocks][kBBoxRows] workgroup row boxes of pt[0] / pt[1]
     Desc *rdesc = nullptr;                 // received particles' rows [n_recv][rows]
@@ -659,6 +661,45 @@ static int collect_collective(fs2_handle *h) {
     return FS2_OK;
 }
 
+// A pool's side array (marks, free list) grown to `bytes`, its first `keep` bytes
+// kept: in place in a reserved range when the pools grow in place (reserved at
+// the first growth, `reserve` bytes), else allocated anew and copied.  *moved
+// says which (a moved mark array restarts its epochs).
+static int grow_side(fs2_handle *h, GrowMem &vm, void **ptr, size_t reserve, size_t bytes, size_t keep,
+                     bool pools_in_place, bool *moved) {
+    *moved = false;
+    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, reserve);
+    if (vm.base && bytes <= vm.reserved && gm_grow(vm, bytes) == hipSuccess) {
+        *ptr = vm.base;
+        return FS2_OK;
+    }
+    void *np = nullptr;
+    HIP_TRY(h, hipMalloc(&np, bytes));
+    if (*ptr && keep) HIP_TRY(h, copy_sync(h, np, *ptr, keep, hipMemcpyDeviceToDevice));
+    if (vm.base) {
+        gm_free(vm);
+        h->vm_fallbacks += 1;
+    } else {
+        hipFree(*ptr);
+    }
+    *ptr = np;
+    *moved = true;
+    return FS2_OK;
+}
+
+// the sweep's per-block counts for `items` (capacity doubles: no free in a growth)
+static int ensure_bcnt(fs2_handle *h, int64_t **b, int64_t *cap, int64_t items) {
+    const int64_t need = collect_blocks(items);
+    if (need <= *cap) return FS2_OK;
+    hipFree(*b);
+    *b = nullptr;
+    *cap = 0;
+    const int64_t c = std::max<int64_t>(need, 2 * need);
+    HIP_TRY(h, hipMalloc(b, sizeof(int64_t) * (size_t)c));
+    *cap = c;
+    return FS2_OK;
+}
+
 // page_refs mode: every rank grows the pools some rank asked for (the flags are in
 // the all-gathered records), together -- pools shared by IPC cannot grow in place:
 // every rank unmaps the others' pools, a rendezvous, each reallocates its own
@@ -721,19 +762,22 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         }
         h->pool = pool;
     }
-    uint8_t *mark = nullptr;
-    HIP_TRY(h, hipMalloc(&mark, (size_t)pages));
-    HIP_TRY(h, hipMemset(mark, 0, (size_t)pages));
-    hipFree(h->mark);
-    h->mark = mark;
-    h->epoch = 0;
-    // the free list: the entries listed so far, then the new pages
-    uint32_t *fl = nullptr;
-    HIP_TRY(h, hipMalloc(&fl, sizeof(uint32_t) * (size_t)pages));
-    if (h->freel && h->nfree > 0)
-        HIP_TRY(h, copy_sync(h, fl, h->freel, sizeof(uint32_t) * (size_t)h->nfree, hipMemcpyDeviceToDevice));
-    hipFree(h->freel);
-    h->freel = fl;
+    // marks and free list: in place with the pool (new marks zero, new ids after
+    // the entries listed so far), else moved
+    const bool vm = h->pool == h->pool_vm.base && h->pool_vm.base != nullptr;
+    bool moved = false;
+    int rc = grow_side(h, h->mark_vm, (void **)&h->mark, (size_t)kIdMask, (size_t)pages, (size_t)h->npool, vm, &moved);
+    if (rc) return rc;
+    if (moved) {
+        HIP_TRY(h, hipMemsetAsync(h->mark, 0, (size_t)pages, s));
+        h->epoch = 0;
+    } else {
+        HIP_TRY(h, hipMemsetAsync(h->mark + h->npool, 0, (size_t)(pages - h->npool), s));
+    }
+    rc = grow_side(h, h->freel_vm, (void **)&h->freel, sizeof(uint32_t) * (size_t)kIdMask,
+                   sizeof(uint32_t) * (size_t)pages, sizeof(uint32_t) * (size_t)std::max<int64_t>(h->nfree, 0), vm,
+                   &moved);
+    if (rc) return rc;
     HIP_TRY(h, launch_iota_from(h->freel + h->nfree, (uint32_t)h->npool, pages - h->npool, s));
     h->nfree += pages - h->npool;
     if (h->cfg.world_size > 1) {
@@ -742,11 +786,9 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         HIP_TRY(h, hipMalloc(&h->sent_mask, sizeof(uint32_t) * (size_t)pages));
         HIP_TRY(h, hipMemsetAsync(h->sent_mask, 0, sizeof(uint32_t) * (size_t)pages, s));
     }
-    hipFree(h->bcnt);
-    h->bcnt = nullptr;
-    HIP_TRY(h, hipMalloc(&h->bcnt, sizeof(int64_t) * (size_t)collect_blocks(pages)));
+    rc = ensure_bcnt(h, &h->bcnt, &h->bcnt_cap, pages);
+    if (rc) return rc;
     h->npool = pages;
-    HIP_TRY(h, hipStreamSynchronize(s));
     return FS2_OK;
 }
 
@@ -781,25 +823,26 @@ static int grow_recs(fs2_handle *h, int64_t n) {
         }
         h->rpool = rp;
     }
-    uint8_t *mark = nullptr;
-    HIP_TRY(h, hipMalloc(&mark, (size_t)n));
-    HIP_TRY(h, hipMemset(mark, 0, (size_t)n));
-    hipFree(h->rmark);
-    h->rmark = mark;
-    h->repoch = 0;
-    uint32_t *fl = nullptr;
-    HIP_TRY(h, hipMalloc(&fl, sizeof(uint32_t) * (size_t)n));
-    if (h->rfreel && h->rnfree > 0)
-        HIP_TRY(h, copy_sync(h, fl, h->rfreel, sizeof(uint32_t) * (size_t)h->rnfree, hipMemcpyDeviceToDevice));
-    hipFree(h->rfreel);
-    h->rfreel = fl;
+    const bool vm = h->rpool == h->rpool_vm.base && h->rpool_vm.base != nullptr;
+    bool moved = false;
+    int rc = grow_side(h, h->rmark_vm, (void **)&h->rmark, (size_t)kRecIdLimit, (size_t)n, (size_t)h->nrecs, vm,
+                       &moved);
+    if (rc) return rc;
+    if (moved) {
+        HIP_TRY(h, hipMemsetAsync(h->rmark, 0, (size_t)n, s));
+        h->repoch = 0;
+    } else {
+        HIP_TRY(h, hipMemsetAsync(h->rmark + h->nrecs, 0, (size_t)(n - h->nrecs), s));
+    }
+    rc = grow_side(h, h->rfreel_vm, (void **)&h->rfreel, sizeof(uint32_t) * (size_t)kRecIdLimit,
+                   sizeof(uint32_t) * (size_t)n, sizeof(uint32_t) * (size_t)std::max<int64_t>(h->rnfree, 0), vm,
+                   &moved);
+    if (rc) return rc;
     HIP_TRY(h, launch_iota_from(h->rfreel + h->rnfree, (uint32_t)h->nrecs, n - h->nrecs, s));
     h->rnfree += n - h->nrecs;
-    hipFree(h->rbcnt);
-    h->rbcnt = nullptr;
-    HIP_TRY(h, hipMalloc(&h->rbcnt, sizeof(int64_t) * (size_t)collect_blocks(n)));
+    rc = ensure_bcnt(h, &h->rbcnt, &h->rbcnt_cap, n);
+    if (rc) return rc;
     h->nrecs = n;
-    HIP_TRY(h, hipStreamSynchronize(s));
     return FS2_OK;
 }
 
@@ -1323,8 +1366,12 @@ static void free_handle(fs2_handle *h) {
     else hipFree(h->pool);
     if (h->rpool_vm.base) gm_free(h->rpool_vm);
     else hipFree(h->rpool);
-    hipFree(h->freel); hipFree(h->mark); hipFree(h->bcnt); hipFree(h->nfree_dev);
-    hipFree(h->rfreel); hipFree(h->rmark); hipFree(h->rbcnt); hipFree(h->rnfree_dev);
+    if (h->freel_vm.base) gm_free(h->freel_vm); else hipFree(h->freel);
+    if (h->mark_vm.base) gm_free(h->mark_vm); else hipFree(h->mark);
+    if (h->rfreel_vm.base) gm_free(h->rfreel_vm); else hipFree(h->rfreel);
+    if (h->rmark_vm.base) gm_free(h->rmark_vm); else hipFree(h->rmark);
+    hipFree(h->bcnt); hipFree(h->nfree_dev);
+    hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->slb_pass); hipFree(h->ext_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
     hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
