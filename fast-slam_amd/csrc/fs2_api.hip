@@ -105,17 +105,27 @@ static hipMemAllocationProp gm_prop(int device) {
     prop.location.id = device;
     return prop;
 }
-static bool gm_init(GrowMem &g, int device, size_t max_bytes) {
+// (a failure is reported once: the runtime's last error is cleared, so the
+// caller's fallback launches do not inherit it)
+static hipError_t gm_fail(hipError_t e) {
+    (void)hipGetLastError();
+    return e;
+}
+// Reserves room for `bytes` with headroom (half again, at least 64 MiB): modest,
+// because the reservation is address space the process's other HIP runtimes
+// (PyTorch's) may need; a growth beyond it moves the mapping, not the data.
+static bool gm_init(GrowMem &g, int device, size_t bytes) {
     hipMemAllocationProp prop = gm_prop(device);
     size_t gran = 0;
     if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran) {
-        (void)hipGetLastError();
+        gm_fail(hipSuccess);
         return false;
     }
-    const size_t r = (max_bytes + gran - 1) / gran * gran;
+    const size_t want = bytes + std::max<size_t>(bytes / 2, size_t(64) << 20);
+    const size_t r = (want + gran - 1) / gran * gran;
     void *p = nullptr;
     if (hipMemAddressReserve(&p, r, 0, nullptr, 0) != hipSuccess || !p) {
-        (void)hipGetLastError();
+        gm_fail(hipSuccess);
         return false;
     }
     g.base = static_cast<char *>(p);
@@ -124,37 +134,72 @@ static bool gm_init(GrowMem &g, int device, size_t max_bytes) {
     g.device = device;
     return true;
 }
+static hipError_t gm_access(GrowMem &g, char *base, size_t bytes) {
+    // access over everything mapped: setting it on the new chunk alone fails now
+    // and then on ROCm 7.2 (scripts/vmm_probe.hip, profiles/r04_vmm_probe.txt)
+    hipMemAccessDesc ad{};
+    ad.location = gm_prop(g.device).location;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    return hipMemSetAccess(base, bytes, &ad, 1);
+}
+// A larger reservation with the same physical chunks mapped at the same offsets
+// (no data moves; the base changes: the caller drained the stream).
+static hipError_t gm_relocate(GrowMem &g, size_t need) {
+    const size_t want = std::max(need + need / 2, 2 * g.reserved);
+    const size_t r = (want + g.gran - 1) / g.gran * g.gran;
+    void *p = nullptr;
+    hipError_t e = hipMemAddressReserve(&p, r, 0, nullptr, 0);
+    if (e != hipSuccess || !p) return gm_fail(e != hipSuccess ? e : hipErrorOutOfMemory);
+    char *nb = static_cast<char *>(p);
+    size_t off = 0;
+    for (auto &c : g.chunks) {
+        e = hipMemMap(nb + off, c.second, 0, c.first, 0);
+        if (e != hipSuccess) break;
+        off += c.second;
+    }
+    if (e == hipSuccess && off > 0) e = gm_access(g, nb, off);
+    if (e != hipSuccess) {
+        size_t o = 0;
+        for (auto &c : g.chunks) {
+            if (o >= off) break;
+            hipMemUnmap(nb + o, c.second);
+            o += c.second;
+        }
+        hipMemAddressFree(nb, r);
+        return gm_fail(e);
+    }
+    off = 0;
+    for (auto &c : g.chunks) {
+        hipMemUnmap(g.base + off, c.second);
+        off += c.second;
+    }
+    hipMemAddressFree(g.base, g.reserved);
+    g.base = nb;
+    g.reserved = r;
+    return hipSuccess;
+}
 static hipError_t gm_grow(GrowMem &g, size_t bytes) {
     const size_t want = (bytes + g.gran - 1) / g.gran * g.gran;
     if (want <= g.mapped) return hipSuccess;
-    if (want > g.reserved) return hipErrorOutOfMemory;
+    if (want > g.reserved) {
+        const hipError_t e = gm_relocate(g, want);
+        if (e != hipSuccess) return e;
+    }
     const size_t delta = want - g.mapped;
     hipMemAllocationProp prop = gm_prop(g.device);
     hipMemGenericAllocationHandle_t hd{};
-    // (a failure is reported once: the runtime's last error is cleared, so the
-    // caller's fallback launches do not inherit it)
     hipError_t e = hipMemCreate(&hd, delta, &prop, 0);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return e;
-    }
+    if (e != hipSuccess) return gm_fail(e);
     e = hipMemMap(g.base + g.mapped, delta, 0, hd, 0);
     if (e != hipSuccess) {
         hipMemRelease(hd);
-        (void)hipGetLastError();
-        return e;
+        return gm_fail(e);
     }
-    // access over everything mapped so far: setting it on the new chunk alone
-    // fails now and then on ROCm 7.2 (scripts/vmm_probe.hip, profiles/r04_vmm_probe.txt)
-    hipMemAccessDesc ad{};
-    ad.location = prop.location;
-    ad.flags = hipMemAccessFlagsProtReadWrite;
-    e = hipMemSetAccess(g.base, want, &ad, 1);
+    e = gm_access(g, g.base, want);
     if (e != hipSuccess) {
         hipMemUnmap(g.base + g.mapped, delta);
         hipMemRelease(hd);
-        (void)hipGetLastError();
-        return e;
+        return gm_fail(e);
     }
     g.chunks.push_back({hd, delta});
     g.mapped = want;
@@ -663,13 +708,13 @@ static int collect_collective(fs2_handle *h) {
 
 // A pool's side array (marks, free list) grown to `bytes`, its first `keep` bytes
 // kept: in place in a reserved range when the pools grow in place (reserved at
-// the first growth, `reserve` bytes), else allocated anew and copied.  *moved
+// the first growth), else allocated anew and copied.  *moved
 // says which (a moved mark array restarts its epochs).
-static int grow_side(fs2_handle *h, GrowMem &vm, void **ptr, size_t reserve, size_t bytes, size_t keep,
-                     bool pools_in_place, bool *moved) {
+static int grow_side(fs2_handle *h, GrowMem &vm, void **ptr, size_t bytes, size_t keep, bool pools_in_place,
+                     bool *moved) {
     *moved = false;
-    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, reserve);
-    if (vm.base && bytes <= vm.reserved && gm_grow(vm, bytes) == hipSuccess) {
+    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, bytes);
+    if (vm.base && gm_grow(vm, bytes) == hipSuccess) {
         *ptr = vm.base;
         return FS2_OK;
     }
@@ -740,13 +785,8 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         return set_err(&h->err, FS2_ERR_OOM, "page pool of %lld pages exceeds the id space", (long long)pages);
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
-    if (!h->pool && !h->refs) {
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess)
-            gm_init(h->pool_vm, h->cfg.device, std::min<size_t>((size_t)kIdMask * kPageBytes, tot));
-    }
-    if (h->pool_vm.base && (size_t)pages * kPageBytes <= h->pool_vm.reserved &&
-        gm_grow(h->pool_vm, (size_t)pages * kPageBytes) == hipSuccess) {
+    if (!h->pool && !h->refs) gm_init(h->pool_vm, h->cfg.device, (size_t)pages * kPageBytes);
+    if (h->pool_vm.base && gm_grow(h->pool_vm, (size_t)pages * kPageBytes) == hipSuccess) {
         h->pool = h->pool_vm.base;
     } else {
         // beyond the reservation, or the mapping failed: allocate and copy (the
@@ -766,7 +806,7 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
     // the entries listed so far), else moved
     const bool vm = h->pool == h->pool_vm.base && h->pool_vm.base != nullptr;
     bool moved = false;
-    int rc = grow_side(h, h->mark_vm, (void **)&h->mark, (size_t)kIdMask, (size_t)pages, (size_t)h->npool, vm, &moved);
+    int rc = grow_side(h, h->mark_vm, (void **)&h->mark, (size_t)pages, (size_t)h->npool, vm, &moved);
     if (rc) return rc;
     if (moved) {
         HIP_TRY(h, hipMemsetAsync(h->mark, 0, (size_t)pages, s));
@@ -774,9 +814,8 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
     } else {
         HIP_TRY(h, hipMemsetAsync(h->mark + h->npool, 0, (size_t)(pages - h->npool), s));
     }
-    rc = grow_side(h, h->freel_vm, (void **)&h->freel, sizeof(uint32_t) * (size_t)kIdMask,
-                   sizeof(uint32_t) * (size_t)pages, sizeof(uint32_t) * (size_t)std::max<int64_t>(h->nfree, 0), vm,
-                   &moved);
+    rc = grow_side(h, h->freel_vm, (void **)&h->freel, sizeof(uint32_t) * (size_t)pages,
+                   sizeof(uint32_t) * (size_t)std::max<int64_t>(h->nfree, 0), vm, &moved);
     if (rc) return rc;
     HIP_TRY(h, launch_iota_from(h->freel + h->nfree, (uint32_t)h->npool, pages - h->npool, s));
     h->nfree += pages - h->npool;
@@ -803,13 +842,8 @@ static int grow_recs(fs2_handle *h, int64_t n) {
                        (long long)n);
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
-    if (!h->rpool && !h->refs) {
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess)
-            gm_init(h->rpool_vm, h->cfg.device, std::min<size_t>((size_t)kRecIdLimit * kRecBytes, tot));
-    }
-    if (h->rpool_vm.base && (size_t)n * kRecBytes <= h->rpool_vm.reserved &&
-        gm_grow(h->rpool_vm, (size_t)n * kRecBytes) == hipSuccess) {
+    if (!h->rpool && !h->refs) gm_init(h->rpool_vm, h->cfg.device, (size_t)n * kRecBytes);
+    if (h->rpool_vm.base && gm_grow(h->rpool_vm, (size_t)n * kRecBytes) == hipSuccess) {
         h->rpool = h->rpool_vm.base;
     } else {
         char *rp = nullptr;
@@ -825,8 +859,7 @@ static int grow_recs(fs2_handle *h, int64_t n) {
     }
     const bool vm = h->rpool == h->rpool_vm.base && h->rpool_vm.base != nullptr;
     bool moved = false;
-    int rc = grow_side(h, h->rmark_vm, (void **)&h->rmark, (size_t)kRecIdLimit, (size_t)n, (size_t)h->nrecs, vm,
-                       &moved);
+    int rc = grow_side(h, h->rmark_vm, (void **)&h->rmark, (size_t)n, (size_t)h->nrecs, vm, &moved);
     if (rc) return rc;
     if (moved) {
         HIP_TRY(h, hipMemsetAsync(h->rmark, 0, (size_t)n, s));
@@ -834,9 +867,8 @@ static int grow_recs(fs2_handle *h, int64_t n) {
     } else {
         HIP_TRY(h, hipMemsetAsync(h->rmark + h->nrecs, 0, (size_t)(n - h->nrecs), s));
     }
-    rc = grow_side(h, h->rfreel_vm, (void **)&h->rfreel, sizeof(uint32_t) * (size_t)kRecIdLimit,
-                   sizeof(uint32_t) * (size_t)n, sizeof(uint32_t) * (size_t)std::max<int64_t>(h->rnfree, 0), vm,
-                   &moved);
+    rc = grow_side(h, h->rfreel_vm, (void **)&h->rfreel, sizeof(uint32_t) * (size_t)n,
+                   sizeof(uint32_t) * (size_t)std::max<int64_t>(h->rnfree, 0), vm, &moved);
     if (rc) return rc;
     HIP_TRY(h, launch_iota_from(h->rfreel + h->rnfree, (uint32_t)h->nrecs, n - h->nrecs, s));
     h->rnfree += n - h->nrecs;
