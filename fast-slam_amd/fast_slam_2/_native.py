@@ -230,6 +230,33 @@ SIGNATURES = [
 _lib = None
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.  A PyTorch-ROCm wheel ships its own
+    libamdhip64.so (and HSA runtime), which its libraries name without the ".7"
+    (NEEDED libamdhip64.so, RPATH $ORIGIN); libfs2 names the system runtime's
+    soname, libamdhip64.so.7.  Loaded first, libfs2 brings in /opt/rocm's runtime,
+    and a later `import torch` loads the wheel's copy beside it -- two HSA runtimes,
+    and PyTorch then finds no GPU (tests/test_gpu_torch_coexist.py).  Loaded after
+    the wheel's copy, libfs2's soname matches it and both share it -- which is what
+    happens whenever torch is imported first.  So when a PyTorch wheel is
+    installed, its runtime is loaded here first (no torch import)."""
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except Exception:
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            try:
+                C.CDLL(p, mode=C.RTLD_GLOBAL)
+            except OSError:
+                pass
+            return
+
+
 def load():
     """Load libfs2.so (raises ImportError when it has not been built)."""
     global _lib
@@ -238,6 +265,7 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libfs2.so not found at {LIB_PATH}; build it with "
                           f"`python fast-slam_amd/build.py` (there is no CPU fallback)")
+    _share_torch_hip_runtime()
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)

@@ -1,10 +1,10 @@
-"""libfs2's pools grow in place inside reserved address ranges (hipMemAddressReserve,
-DESIGN.md §3).  The reservations are address space the process's other HIP
-runtime -- PyTorch's own -- needs when it initialises later: a first version that
-reserved the whole id space (~0.5 TB per handle) left PyTorch unable to start
-("No HIP GPUs are available") in a process that had created a handle first.  In a
-fresh process (the order matters, so not in this test process): a handle whose
-record pool grows, then PyTorch's first CUDA call and a tensor op."""
+"""One HIP runtime per process (fast_slam_2/_native.py _share_torch_hip_runtime).
+A PyTorch-ROCm wheel ships its own HIP and HSA runtimes; libfs2 links the system
+one.  Loaded first, libfs2 used to bring /opt/rocm's runtime in and a later
+`import torch` then loaded the wheel's copy beside it, after which PyTorch found
+no GPU ("No HIP GPUs are available").  In a fresh process (the order matters, so
+not in this test process): the shim, a handle whose record pool grows in place,
+then PyTorch's first CUDA call and a tensor op."""
 import os
 import subprocess
 import sys
@@ -16,8 +16,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SCRIPT = r"""
+import sys
 import numpy as np
 import fast_slam_2
+assert "torch" not in sys.modules
 N, L = 100000, 32
 f = fast_slam_2.FastSLAM2(N, rng="device", seed=1, landmark_capacity=L + 40, verbose=False,
                           record_pool=N * L + 2 * N)
