@@ -77,9 +77,6 @@ def test_sharded_matches_single(G, N, L):
         a, b = h.first_global, h.first_global + h.n_local
         h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
         h.set_profiling(True)
-    from fast_slam_2 import _native as nat
-    for g in refuse:
-        nat.check(shards[g]._lib.fs2_debug_refuse_peer_maps(shards[g]._h), shards[g]._h)
     resamples = 0
     moved = 0
     firsts = {g: {h.first_global} for g, h in enumerate(shards)}
