@@ -48,7 +48,12 @@ def test_config5_shape_eight_ranks_vs_oracle(tmp_path):
     cap = CAP(L, S)
     key = os.urandom(128).hex()
     env = dict(os.environ, FS2_SHM_TIMEOUT_S="300", OMP_NUM_THREADS="2")
-    logs = [open(tmp_path / f"rank{r}.log", "w") for r in range(G)]
+    # the ranks' logs under gpurun_out/ on the GPU box (they come back with the call)
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    logdir = os.path.join(root, "gpurun_out") if root and os.path.isdir(os.path.join(root, "gpurun_out")) \
+        else str(tmp_path)
+    logpaths = [os.path.join(logdir, f"cfg5_rank{r}.log") for r in range(G)]
+    logs = [open(q, "w") for q in logpaths]
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "cfg5_worker.py"), str(G), str(r), str(N),
                                str(L), str(S), key, str(tmp_path)], env=env, stdout=logs[r],
                               stderr=subprocess.STDOUT)
@@ -72,13 +77,22 @@ def test_config5_shape_eight_ranks_vs_oracle(tmp_path):
             _progress(f"oracle scan {s} resampled {rs} ({time.time() - t0:.0f} s)")
         checksum = np.concatenate([map_checksum(o.lm[a:a + 8192]) for a in range(0, N, 8192)])
         del o
+        # a rank whose log has not grown for 240 s is taken to be stuck: every rank
+        # is stopped and the test fails with their logs
+        last, sizes = time.time(), [0] * G
         for r, p in enumerate(procs):
             while True:
                 try:
                     p.wait(timeout=30)
                     break
                 except subprocess.TimeoutExpired:
+                    now = [os.path.getsize(q) for q in logpaths]
+                    if now != sizes:
+                        sizes, last = now, time.time()
                     _progress(f"waiting for rank {r}")
+                    if time.time() - last > 240:
+                        tails = "\n".join(f"rank {q}: " + open(logpaths[q]).read()[-600:] for q in range(G))
+                        pytest.fail("ranks stuck (no log line for 240 s):\n" + tails)
     finally:
         for p in procs:
             if p.poll() is None:
@@ -86,7 +100,7 @@ def test_config5_shape_eight_ranks_vs_oracle(tmp_path):
         for f in logs:
             f.close()
     for r, p in enumerate(procs):
-        assert p.returncode == 0, f"rank {r}:\n" + open(tmp_path / f"rank{r}.log").read()[-4000:]
+        assert p.returncode == 0, f"rank {r}:\n" + open(logpaths[r]).read()[-4000:]
     ranks = [np.load(tmp_path / f"rank{r}.npz") for r in range(G)]
     resamples = 0
     for s in range(S):
