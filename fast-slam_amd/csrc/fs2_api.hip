@@ -599,10 +599,20 @@ static int collect_body(fs2_handle *h, bool records) {
 // process are created one after the other, so creation cannot wait for them):
 // every rank's page pool, record pool and page marks, mapped here (IPC; the ranks
 // of one process share pointers).  From now on the pools never move.
+// FS2_TRACE=1: the sharing and collective steps of a rank on stderr (debugging)
+static void trace(const fs2_handle *h, const char *what, int k = -1) {
+    static const bool on = std::getenv("FS2_TRACE") != nullptr;
+    if (!on) return;
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "[fs2 rank %d %.3f] %s %d\n", h->cfg.rank, t, what, k);
+    std::fflush(stderr);
+}
+
 static int share_pools(fs2_handle *h, bool first) {
     const int G = h->cfg.world_size;
     hipStream_t s = h->stream;
     void *ptrs[kMaxRanks] = {};
+    trace(h, "share_pools start", first ? 1 : 0);
     HIP_TRY(h, hipStreamSynchronize(s));
     // Every rank takes part in the three exchanges and in the agreement after
     // them whatever its own mappings did: if some rank cannot map its peers' pools
@@ -614,7 +624,10 @@ static int share_pools(fs2_handle *h, bool first) {
         void *base = what == 0 ? (void *)h->pool : what == 1 ? (void *)h->rpool : (void *)h->mark;
         CommTimer ct(h);
         std::string e;
-        if (h->tp->share(base, ptrs, &e)) {
+        trace(h, "share", what);
+        const int src = h->tp->share(base, ptrs, &e);
+        trace(h, "shared", src);
+        if (src) {
             if (ok) why = e;
             ok = false;
             if (int rc = h->tp->status(&h->err)) return rc;     // the transport itself failed
@@ -631,6 +644,7 @@ static int share_pools(fs2_handle *h, bool first) {
         why = "peer mappings refused (fs2_debug_refuse_peer_maps)";
     }
     uint8_t all[kMaxRanks] = {};
+    trace(h, "agree", ok ? 1 : 0);
     HIP_TRY(h, hipMemsetAsync(h->ep_dev, ok ? 1 : 0, 1, s));
     {
         CommTimer ct(h);
@@ -642,6 +656,7 @@ static int share_pools(fs2_handle *h, bool first) {
     if (int rc = h->tp->status(&h->err)) return rc;
     bool every = true;
     for (int q = 0; q < G; ++q) every &= all[q] == 1;
+    trace(h, "agreed", every ? 1 : 0);
     if (!every && !first)             // references have crossed: the grown pools must map
         return set_err(&h->err, FS2_ERR_COMM, "page_refs: mapping the grown pools failed (%s)",
                        ok ? "on another rank" : why.c_str());
@@ -964,7 +979,9 @@ static int post_and_wait(fs2_handle *h, bool sizes) {
     const unsigned long long seq = ++h->post_seq;
     HIP_TRY(h, launch_post(h->stats_dev, sizes ? h->xmat : nullptr, sizes ? kXrowWords * G * G : 0, h->post, h->post_flag_dev,
                            seq, h->stream));
+    trace(h, "post wait", sizes ? 1 : 0);
     const int rc = wait_seq(h, h->post_flag, seq, "mid-scan statistics");
+    trace(h, "posted", rc);
     if (rc) return rc;
     // k_post runs after the collectives queued before it, so a stream-ordered
     // transport's status is final here: a failed exchange leaves stale staging
@@ -1866,6 +1883,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         h->collect_next = 0;
         collected = true;
     }
+    trace(h, "submit", (int)h->scan);
     rc = grow_rows(h, h->cnt_upper + M);
     if (rc) return rc;
     const int cur = h->cur;

@@ -82,6 +82,7 @@ class Transport {
                 continue;
             }
             void *q = nullptr;
+            if (std::getenv("FS2_TRACE")) std::fprintf(stderr, "[fs2 rank %d] open handle of rank %d\n", rank(), p);
             if (hipIpcOpenMemHandle(&q, hs[p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                 (void)hipGetLastError();     // reported here, not by the next launch
                 if (err) *err = "hipIpcOpenMemHandle failed (page references across ranks)";

@@ -47,7 +47,7 @@ def test_config5_shape_eight_ranks_vs_oracle(tmp_path):
     from oracle import oracle as orc
     cap = CAP(L, S)
     key = os.urandom(128).hex()
-    env = dict(os.environ, FS2_SHM_TIMEOUT_S="300", OMP_NUM_THREADS="2")
+    env = dict(os.environ, FS2_SHM_TIMEOUT_S="90", OMP_NUM_THREADS="2", FS2_TRACE="1")
     # the ranks' logs under gpurun_out/ on the GPU box (they come back with the call)
     root = os.environ.get("GRAFT_REPO_ROOT")
     logdir = os.path.join(root, "gpurun_out") if root and os.path.isdir(os.path.join(root, "gpurun_out")) \
