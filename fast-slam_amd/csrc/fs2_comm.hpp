@@ -74,24 +74,43 @@ class Transport {
     virtual bool in_process() const { return false; }
 
   protected:
+    // a host-side rendezvous of every rank (creation-time use only)
+    virtual bool host_barrier(std::string *err) = 0;
     std::vector<void *> opened_;     // IPC mappings to close
+    // The ranks open each other's handles one rank at a time (a rendezvous between
+    // turns): on ROCm 7.2 with dmabuf IPC, processes that all sat in
+    // hipIpcOpenMemHandle at once never returned (8 processes on one GPU,
+    // FS2_TRACE).  Every rank takes every turn's rendezvous, whatever its own
+    // opens did.
     int open_handles(const std::vector<hipIpcMemHandle_t> &hs, void *base, void **peers, std::string *err) {
-        for (int p = 0; p < (int)hs.size(); ++p) {
-            if (p == rank()) {
-                peers[p] = base;
-                continue;
+        const bool tr = std::getenv("FS2_TRACE") != nullptr;
+        int rc = FS2_OK;
+        for (int turn = 0; turn < (int)hs.size(); ++turn) {
+            if (turn == rank()) {
+                for (int p = 0; p < (int)hs.size() && rc == FS2_OK; ++p) {
+                    if (p == rank()) {
+                        peers[p] = base;
+                        continue;
+                    }
+                    void *q = nullptr;
+                    if (tr) std::fprintf(stderr, "[fs2 rank %d] open handle of rank %d\n", rank(), p);
+                    if (hipIpcOpenMemHandle(&q, hs[p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                        (void)hipGetLastError();     // reported here, not by the next launch
+                        if (err) *err = "hipIpcOpenMemHandle failed (page references across ranks)";
+                        rc = FS2_ERR_COMM;
+                        break;
+                    }
+                    opened_.push_back(q);
+                    peers[p] = q;
+                }
             }
-            void *q = nullptr;
-            if (std::getenv("FS2_TRACE")) std::fprintf(stderr, "[fs2 rank %d] open handle of rank %d\n", rank(), p);
-            if (hipIpcOpenMemHandle(&q, hs[p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-                (void)hipGetLastError();     // reported here, not by the next launch
-                if (err) *err = "hipIpcOpenMemHandle failed (page references across ranks)";
+            std::string berr;
+            if (!host_barrier(&berr)) {
+                if (err) *err = berr;
                 return FS2_ERR_COMM;
             }
-            opened_.push_back(q);
-            peers[p] = q;
         }
-        return FS2_OK;
+        return rc;
     }
     void close_handles() {
         for (void *q : opened_) hipIpcCloseMemHandle(q);
@@ -168,6 +187,23 @@ class RcclTransport : public Transport {
     }
     int world() const override { return G; }
     int rank() const override { return r; }
+  protected:
+    bool host_barrier(std::string *err) override {
+        char *d = nullptr;
+        hipStream_t s = nullptr;
+        bool ok = hipMalloc(&d, (size_t)G + 1) == hipSuccess &&
+                  hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+                  ncclAllGather(d, d + 1, 1, ncclUint8, comm, s) == ncclSuccess && hipStreamSynchronize(s) == hipSuccess;
+        if (s) hipStreamDestroy(s);
+        hipFree(d);
+        if (!ok) {
+            (void)hipGetLastError();
+            failed_ = true;
+            if (err) *err = "rccl transport: rendezvous failed";
+        }
+        return ok;
+    }
+  public:
     int allgather(const void *send, void *recv, size_t bytes, hipStream_t s,
                   std::string *err) override {
         ncclResult_t e = ncclAllGather(send, recv, bytes, ncclUint8, comm, s);
@@ -281,6 +317,15 @@ class LocalTransport : public Transport {
     }
 
     bool in_process() const override { return true; }
+
+  protected:
+    bool host_barrier(std::string *err) override {
+        if (grp->barrier()) return true;
+        if (err) *err = "local transport: rendezvous timed out";
+        return false;
+    }
+
+  public:
     // ranks are threads of this process: the bases themselves
     int share(void *base, void **peers, std::string *err) override {
         grp->send_ptr[r] = base;
@@ -442,6 +487,14 @@ class ShmTransport : public Transport {
         return FS2_ERR_COMM;
     }
 
+  protected:
+    bool host_barrier(std::string *err) override {
+        if (wait(hdr->bar)) return true;
+        fail(err, "rendezvous failed or timed out");
+        return false;
+    }
+
+  public:
     // the handles through the all-gather slots, host-side (creation: nothing in flight)
     int share(void *base, void **peers, std::string *err) override {
         if (int rc = status(err)) return rc;
