@@ -1665,7 +1665,13 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     // page_refs mode (fs2.h): 2..15 ranks, local page ids below 2^27 (the rank tag
     // above them); a default pool is clamped to the id space while it still holds
     // the initial maps 1.25 times over, else the mode stays off (auto) or fails (on)
-    if (G > 1 && cfg->page_refs >= 0) {
+    // auto: ranks that are threads of this process only.  Between processes the
+    // pools are mapped through IPC handles, and on ROCm 7.2 a process's
+    // hipIpcOpenMemHandle of another process's buffer on the same GPU never
+    // returned (profiles/r04_ipc_open_hang.txt); between GPUs it is unproven here,
+    // so multi-process groups send pages unless page_refs = 1 asks for references.
+    const bool refs_wanted = cfg->page_refs == 1 || (cfg->page_refs == 0 && cfg->comm_mode == FS2_COMM_LOCAL);
+    if (G > 1 && refs_wanted) {
         const int64_t lim = (int64_t)kRefIdMask - 1024;
         if (cfg->page_pool <= 0 && npages > lim && lim >= n * h->rows + n * h->rows / 4 + 8 * n) npages = lim;
         h->refs = G <= kRefMaxRanks && npages <= lim;

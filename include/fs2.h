@@ -97,7 +97,10 @@ typedef struct fs2_config {
                                        frees too little */
     int64_t record_pool;            /* initial slot-record pool (48 B each); 0 = 1.25x the
                                        initial capacity plus 64 per particle */
-    int32_t page_refs;              /* sharded resample: 0 = auto (on for 2..15 ranks), 1 = on,
+    int32_t page_refs;              /* sharded resample: 0 = auto (on for 2..15 ranks that are threads
+                                       of one process, comm_mode FS2_COMM_LOCAL: between processes the
+                                       IPC mapping is unproven -- it hung for processes on one GPU,
+                                       DESIGN.md §5), 1 = on,
                                        -1 = off.  On: a particle that changes ranks travels as its
                                        page-table row of references to pages on the rank that
                                        holds them (every rank maps the others' pools, IPC); the
