@@ -279,8 +279,10 @@ def test_page_refs_collective_collections():
                                           record_pool=n * rows * 8 * 2 + 64 * n)
     assert resamples >= 3
     cols = [st.collections for st in last]
-    # two at creation, then (after references cross ranks) collective ones, together
-    assert min(cols) >= 5 and len(set(cols)) == 1, cols
+    # (the imports' record shortfalls grow the fresh pools without collecting:
+    # nothing could be freed) then, after references cross ranks, collective
+    # collections, together
+    assert min(cols) >= 3 and len(set(cols)) == 1, cols
     assert sum(p["localized_pages"] for p in profs) > 0
 
 
