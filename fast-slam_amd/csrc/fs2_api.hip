@@ -728,8 +728,10 @@ static int collect_collective(fs2_handle *h) {
 static int grow_side(fs2_handle *h, GrowMem &vm, void **ptr, size_t bytes, size_t keep, bool pools_in_place,
                      bool *moved) {
     *moved = false;
-    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, bytes);
-    if (vm.base && gm_grow(vm, bytes) == hipSuccess) {
+    // (a side array is small next to its pool -- 1 or 4 B per 48 B record -- so it
+    // is mapped half again ahead and grows about every other pool growth)
+    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, 4 * bytes);
+    if (vm.base && (bytes <= vm.mapped || gm_grow(vm, std::max(bytes, vm.mapped + vm.mapped / 2)) == hipSuccess)) {
         *ptr = vm.base;
         return FS2_OK;
     }
@@ -903,7 +905,9 @@ static int reserve_pages(fs2_handle *h, int64_t need, PageAlloc *out) {
         if (rc) return rc;
         if (need > h->nfree) {
             const int64_t live = h->npool - h->nfree;
-            rc = grow_pool(h, std::max(h->npool + h->npool / 2, live + 2 * need));
+            // by a quarter when the pool grows in place (cheap, no copy), else by half
+            const int64_t step = h->pool_vm.base ? h->npool / 4 : h->npool / 2;
+            rc = grow_pool(h, std::max(h->npool + step, live + 2 * need));
             if (rc) return rc;
         }
     }
@@ -927,8 +931,10 @@ static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
         }
         if (h->rcursor + need > h->rnfree) {
             const int64_t live = h->nrecs - (h->rnfree - h->rcursor);
-            // grow by half, clamped to the id space (grow_recs fails beyond it)
-            int64_t want = std::max(h->nrecs + h->nrecs / 2, live + 2 * need);
+            // by a quarter in place, else by half; clamped to the id space (grow_recs
+            // fails beyond it)
+            const int64_t step = h->rpool_vm.base ? h->nrecs / 4 : h->nrecs / 2;
+            int64_t want = std::max(h->nrecs + step, live + 2 * need);
             if (want > (int64_t)kRecIdLimit) want = std::max<int64_t>(kRecIdLimit, live + need);
             rc = grow_recs(h, want);
             if (rc) return rc;
