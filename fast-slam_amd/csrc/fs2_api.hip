@@ -405,6 +405,7 @@ struct fs2_handle {
     bool refs = false;                     // the mode is on
     bool refs_off = false;                 // turned off at the first scan (a rank could not map its peers)
     bool refuse_maps = false;              // test hook: this rank reports its peer mappings as failed
+    bool room_check = false;               // page_refs: agree on pool room at the next scan (after a resample)
     bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
     bool refs_live = false;                // a resample has exchanged references (no local collection)
     uint64_t grows = 0;                    // collective pool growths
@@ -768,7 +769,7 @@ static int ensure_bcnt(fs2_handle *h, int64_t **b, int64_t *cap, int64_t items) 
 // (page and record ids keep their meaning), and the pools are shared anew.
 static int grow_pool(fs2_handle *h, int64_t pages);
 static int grow_recs(fs2_handle *h, int64_t n);
-static int regrow_collective(fs2_handle *h, bool pages, bool recs) {
+static int regrow_collective(fs2_handle *h, int64_t pages_to, int64_t recs_to) {
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
     h->tp->unshare();
@@ -780,8 +781,11 @@ static int regrow_collective(fs2_handle *h, bool pages, bool recs) {
     HIP_TRY(h, hipStreamSynchronize(s));
     h->refs_shared = false;
     int rc = FS2_OK;
-    if (pages) rc = grow_pool(h, std::min<int64_t>(h->npool + h->npool / 2, (int64_t)kRefIdMask - 1024));
-    if (!rc && recs) rc = grow_recs(h, std::min<int64_t>(h->nrecs + h->nrecs / 2, (int64_t)kRecIdLimit));
+    // (a target of 0: this rank's pool stays; it still takes part)
+    if (pages_to > 0)
+        rc = grow_pool(h, std::min<int64_t>(std::max(h->npool + h->npool / 2, pages_to), (int64_t)kRefIdMask - 1024));
+    if (!rc && recs_to > 0)
+        rc = grow_recs(h, std::min<int64_t>(std::max(h->nrecs + h->nrecs / 2, recs_to), (int64_t)kRecIdLimit));
     if (rc) return rc;
     h->grows += 1;
     return share_pools(h, false);
@@ -1887,13 +1891,59 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         // page_refs: some rank's pools ran short in the last scan (every rank read the
         // same records, so every rank collects -- and grows -- here, together)
         if (h->collect_next & 6) {
-            rc = regrow_collective(h, (h->collect_next & 2) != 0, (h->collect_next & 4) != 0);
+            rc = regrow_collective(h, (h->collect_next & 2) ? 1 : 0, (h->collect_next & 4) ? 1 : 0);
             if (rc) return rc;
         }
         rc = collect_collective(h);
         if (rc) return rc;
         h->collect_next = 0;
         collected = true;
+    }
+    if (h->refs_shared && h->room_check) {
+        // after a resample (every rank knows it resampled) the remote rows this scan
+        // may localise are new: the ranks agree, before any localisation, whether
+        // some rank lacks room for them and this scan's reservations -- then every
+        // rank collects, and grows what is still short, together
+        h->room_check = false;
+        const int64_t Mx = std::max<int64_t>(M, 1);
+        auto short_bits = [&]() -> uint8_t {
+            const int64_t pneed = Mx * h->n + h->remote_rows;
+            const int64_t rneed = Mx * h->n + (int64_t)kPageSlots * h->remote_rows;
+            return (uint8_t)((h->nfree - h->cursor < 2 * pneed ? 1 : 0) | (h->rnfree - h->rcursor < 2 * rneed ? 2 : 0));
+        };
+        auto any_short = [&](uint8_t mine, uint8_t *all_or) -> int {
+            uint8_t all[kMaxRanks] = {};
+            HIP_TRY(h, hipMemsetAsync(h->ep_dev, mine, 1, h->stream));
+            {
+                CommTimer ct(h);
+                const int rc2 = h->tp->allgather(h->ep_dev, h->epochs_dev, 1, h->stream, &h->err);
+                if (rc2) return rc2;
+            }
+            HIP_TRY(h, hipMemcpyAsync(all, h->epochs_dev, (size_t)h->cfg.world_size, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(h, hipStreamSynchronize(h->stream));
+            if (int rc2 = h->tp->status(&h->err)) return rc2;
+            *all_or = 0;
+            for (int q = 0; q < h->cfg.world_size; ++q) *all_or |= all[q];
+            return FS2_OK;
+        };
+        uint8_t any = 0;
+        rc = any_short(short_bits(), &any);
+        if (rc) return rc;
+        if (any && !collected) {
+            rc = collect_collective(h);
+            if (rc) return rc;
+            collected = true;
+            rc = any_short(short_bits(), &any);
+            if (rc) return rc;
+        }
+        if (any) {
+            const uint8_t mine = short_bits();
+            const int64_t pneed = Mx * h->n + h->remote_rows;
+            const int64_t rneed = Mx * h->n + (int64_t)kPageSlots * h->remote_rows;
+            rc = regrow_collective(h, (mine & 1) ? h->npool - (h->nfree - h->cursor) + 3 * pneed : 0,
+                                   (mine & 2) ? h->nrecs - (h->rnfree - h->rcursor) + 3 * rneed : 0);
+            if (rc) return rc;
+        }
     }
     trace(h, "submit", (int)h->scan);
     rc = grow_rows(h, h->cnt_upper + M);
@@ -2332,6 +2382,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         }
     }
     if (st.resampled) h->cur = 1 - h->cur;
+    if (st.resampled && h->refs_shared) h->room_check = true;   // new remote rows: agree on room next scan
     h->appends_since_rcollect += (int64_t)st.appends;
     if (st.resampled) h->rcollect_exact = false;     // dropped particles' records: no bound
     h->cnt_upper = st.max_count;
