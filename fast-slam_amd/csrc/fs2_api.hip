@@ -682,6 +682,7 @@ static int share_pools(fs2_handle *h, bool first) {
 // all-gather is the barrier before anyone sweeps.  Records as in collect(): the
 // remote-marked pages mark their records too.
 static int collect_collective(fs2_handle *h) {
+    trace(h, "collect_collective", (int)(h->nfree - h->cursor));
     hipStream_t s = h->stream;
     const int G = h->cfg.world_size;
     if (h->epoch == 255) {
@@ -770,6 +771,8 @@ static int ensure_bcnt(fs2_handle *h, int64_t **b, int64_t *cap, int64_t items) 
 static int grow_pool(fs2_handle *h, int64_t pages);
 static int grow_recs(fs2_handle *h, int64_t n);
 static int regrow_collective(fs2_handle *h, int64_t pages_to, int64_t recs_to) {
+    trace(h, "regrow pages_to (M)", (int)(pages_to >> 20));
+    trace(h, "regrow recs_to (M)", (int)(recs_to >> 20));
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
     h->tp->unshare();
@@ -1927,7 +1930,9 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
             return FS2_OK;
         };
         uint8_t any = 0;
+        trace(h, "room check remote_rows (K)", (int)(h->remote_rows >> 10));
         rc = any_short(short_bits(), &any);
+        trace(h, "room short", any);
         if (rc) return rc;
         if (any && !collected) {
             rc = collect_collective(h);
