@@ -363,7 +363,7 @@ def robustness(args, f, L, first_scan):
     out["no_gate_filter"]["note"] = "grid map, every slot's fp64 record read (no mirrors, no page boxes)"
     g.close()
     out["sharded_local_g2"] = sharded_local(args, L, n)
-    out["sharded_local_g8"] = sharded_local(args, L, n, G=8)
+    out["sharded_local_g8"] = sharded_local(args, L, n, G=8, page_refs="on")
     # the same with whole pages sent (round 3's transfer; A/B of the page references)
     out["sharded_local_g8_pages"] = sharded_local(args, L, n, G=8, page_refs="off")
     out["dropin_iterate"] = dropin(args, L, n)
@@ -371,7 +371,7 @@ def robustness(args, f, L, first_scan):
     return out
 
 
-def dropin(args, L, n, scans=16, warm=4, rng="numpy"):
+def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
     """What a reference caller gets: FastSLAM2.iterate(rotation, translation,
     list[Measurement]) (fast_slam_2.py:33, called at jde_robots_main.py:38) with
     numpy's global legacy RNG -- N normals per scan and the resample start,
@@ -391,8 +391,11 @@ def dropin(args, L, n, scans=16, warm=4, rng="numpy"):
         f.iterate(*syn.odometry(s), meas[s])
     t0 = time.perf_counter()
     res = 0
+    each = []
     for s in range(warm, scans):
+        t1 = time.perf_counter()
         f.iterate(*syn.odometry(s), meas[s])
+        each.append(time.perf_counter() - t1)
         res += f.last_stats.resampled
     dt = time.perf_counter() - t0
     f.close()
@@ -406,6 +409,8 @@ def dropin(args, L, n, scans=16, warm=4, rng="numpy"):
             + ("drawn on the GPU from np.random's state (MT19937 + polar method, fs2_mt_draw)" if rng == "numpy"
                else "drawn by numpy on one host core (host-RNG bound)"))
     return {"value": n * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k, "resamples": res,
+            "ms_per_scan_median": float(np.median(each)) * 1e3,
+            "window": f"scans {warm}..{scans - 1} (the headline's)",
             "host_rng_ms": rng_ms, "rng": rng, "numpy_state_sha1": state_digest, "note": note}
 
 

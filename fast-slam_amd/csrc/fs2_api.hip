@@ -665,9 +665,6 @@ static int share_pools(fs2_handle *h, bool first) {
         h->tp->unshare();
         h->refs = false;
         h->refs_off = true;
-        if (h->cfg.page_refs == 1)
-            return set_err(&h->err, FS2_ERR_COMM, "page_refs on, but %s",
-                           ok ? "another rank could not map its peers' pools" : why.c_str());
         return FS2_OK;
     }
     HIP_TRY(h, hipMemcpy(h->peers_dev, &h->peers_host, sizeof(PeerMaps), hipMemcpyHostToDevice));
@@ -1678,12 +1675,13 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     // page_refs mode (fs2.h): 2..15 ranks, local page ids below 2^27 (the rank tag
     // above them); a default pool is clamped to the id space while it still holds
     // the initial maps 1.25 times over, else the mode stays off (auto) or fails (on)
-    // auto: ranks that are threads of this process only.  Between processes the
-    // pools are mapped through IPC handles, and on ROCm 7.2 a process's
-    // hipIpcOpenMemHandle of another process's buffer on the same GPU never
-    // returned (profiles/r04_ipc_open_hang.txt); between GPUs it is unproven here,
-    // so multi-process groups send pages unless page_refs = 1 asks for references.
-    const bool refs_wanted = cfg->page_refs == 1 || (cfg->page_refs == 0 && cfg->comm_mode == FS2_COMM_LOCAL);
+    // on request only (page_refs = 1).  Measured in round 4: a
+    // resample sends ~10x fewer bytes, but the update passes then localise remote
+    // pages one particle-row at a time (siblings that share a remote page each copy
+    // it), which moved more bytes and took longer per scan than sending each
+    // distinct page once; and between processes the IPC mapping did not return
+    // for processes on one GPU (profiles/r04_ipc_open_hang.txt).
+    const bool refs_wanted = cfg->page_refs == 1;
     if (G > 1 && refs_wanted) {
         const int64_t lim = (int64_t)kRefIdMask - 1024;
         if (cfg->page_pool <= 0 && npages > lim && lim >= n * h->rows + n * h->rows / 4 + 8 * n) npages = lim;

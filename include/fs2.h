@@ -97,11 +97,11 @@ typedef struct fs2_config {
                                        frees too little */
     int64_t record_pool;            /* initial slot-record pool (48 B each); 0 = 1.25x the
                                        initial capacity plus 64 per particle */
-    int32_t page_refs;              /* sharded resample: 0 = auto (on for 2..15 ranks that are threads
-                                       of one process, comm_mode FS2_COMM_LOCAL: between processes the
-                                       IPC mapping is unproven -- it hung for processes on one GPU,
-                                       DESIGN.md §5), 1 = on,
-                                       -1 = off.  On: a particle that changes ranks travels as its
+    int32_t page_refs;              /* sharded resample: 0 = auto (off: measured slower than sending
+                                       pages, and the IPC mapping hung between processes on one GPU,
+                                       DESIGN.md §5), 1 = on (2..15 ranks; if a rank cannot map its
+                                       peers' pools every rank falls back to pages), -1 = off.
+                                       On: a particle that changes ranks travels as its
                                        page-table row of references to pages on the rank that
                                        holds them (every rank maps the others' pools, IPC); the
                                        receiver copies a page when the update pass first needs
@@ -387,8 +387,8 @@ int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, in
                      int32_t on_host);
 /* Test hook of page_refs' fallback: this rank reports, at its first scan, that it
  * could not map its peers' pools (as without peer access between devices); the
- * mode then turns off on every rank (fs2_profile.page_refs = -1; with page_refs
- * = 1 the first scan fails instead).  Before the first scan only. */
+ * mode then turns off on every rank (fs2_profile.page_refs = -1).  Before the
+ * first scan only. */
 int fs2_debug_refuse_peer_maps(fs2_handle *h);
 /* Test hook: the handle's motion-noise buffer (N_local values: the last scan's
  * injected draws, or fs2_mt_draw's) into out. */
