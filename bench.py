@@ -475,7 +475,7 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3, page_refs="auto"):
             "pages_sent_before_fraction": (sum(p["sent_pages_repeat"] for p in profs) /
                                            sum(p["sent_pages"] for p in profs)
                                            if sum(p["sent_pages"] for p in profs) else None),
-            "page_refs": page_refs != "off",
+            "page_refs": profs[0]["page_refs"] == 1,     # (in effect: fs2_profile.page_refs)
             # page_refs: remote pages the update passes copied (each with its 8 records)
             "localized_pages_per_scan": sum(p["localized_pages"] for p in profs) / k,
             "localized_bytes_per_scan": sum(p["localized_pages"] for p in profs) * (128 + 8 * 48) / k,

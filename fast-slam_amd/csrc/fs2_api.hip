@@ -806,7 +806,11 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         return set_err(&h->err, FS2_ERR_OOM, "page pool of %lld pages exceeds the id space", (long long)pages);
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
-    if (!h->pool && !h->refs) gm_init(h->pool_vm, h->cfg.device, (size_t)pages * kPageBytes);
+    // in place (VMM) unless the pool is shared through IPC handles (page_refs
+    // between processes: hipIpcGetMemHandle needs a hipMalloc allocation); ranks
+    // that are threads of one process share plain pointers, so theirs grow in place
+    const bool vm_ok = !h->refs || h->cfg.comm_mode == FS2_COMM_LOCAL;
+    if (!h->pool && vm_ok) gm_init(h->pool_vm, h->cfg.device, (size_t)pages * kPageBytes);
     if (h->pool_vm.base && gm_grow(h->pool_vm, (size_t)pages * kPageBytes) == hipSuccess) {
         h->pool = h->pool_vm.base;
     } else {
@@ -863,7 +867,8 @@ static int grow_recs(fs2_handle *h, int64_t n) {
                        (long long)n);
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
-    if (!h->rpool && !h->refs) gm_init(h->rpool_vm, h->cfg.device, (size_t)n * kRecBytes);
+    const bool vm_ok = !h->refs || h->cfg.comm_mode == FS2_COMM_LOCAL;   // (as grow_pool)
+    if (!h->rpool && vm_ok) gm_init(h->rpool_vm, h->cfg.device, (size_t)n * kRecBytes);
     if (h->rpool_vm.base && gm_grow(h->rpool_vm, (size_t)n * kRecBytes) == hipSuccess) {
         h->rpool = h->rpool_vm.base;
     } else {
