@@ -6,6 +6,7 @@
 #   host   scripts/host_turnaround.py (host share of a scan)
 #   pmc    HBM bytes by PMC: config 3 and its dense-map variant
 #   vmm    scripts/vmm_probe (growing a reserved range chunk by chunk)
+#   dltl   kernel timeline of the drop-in iterate() (scripts/dropin_probe.py under rocprofv3)
 # Stops at the first failing step; each GPU step has its own time limit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -13,7 +14,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STAGES=${1:-all}
 TESTS=${TESTS:-tests}
-has() { [[ ",$STAGES," == *",$1,"* || ( $STAGES == all && $1 != host && $1 != pmc && $1 != vmm ) ]]; }
+has() { [[ ",$STAGES," == *",$1,"* || ( $STAGES == all && $1 != host && $1 != pmc && $1 != vmm && $1 != dltl ) ]]; }
 if has vmm; then
   timeout -k 10 120 ./scripts/vmm_probe > gpurun_out/vmm_probe.txt 2>&1 || { echo vmm probe failed; tail -20 gpurun_out/vmm_probe.txt; exit 8; }
   tail -1 gpurun_out/vmm_probe.txt
@@ -37,6 +38,10 @@ fi
 if has prof; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python bench.py --no-cpu-baseline --no-extras > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof.log; exit 5; }
   python scripts/prof_summary.py /tmp/prof gpurun_out/prof_summary.txt "${PROF_TITLE:-}" > /dev/null && head -14 gpurun_out/prof_summary.txt
+fi
+if has dltl; then
+  timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/dl -o dl -- python3 scripts/dropin_probe.py > gpurun_out/dropin_probe.log 2>&1 || { echo dropin trace failed; tail -20 gpurun_out/dropin_probe.log; exit 9; }
+  python3 scripts/timeline.py "$(find /tmp/dl -name '*.db' | sort | tail -n 1)" 3 > gpurun_out/dropin_timeline.txt && grep -v "^W20\|^E20" gpurun_out/dropin_probe.log | tail -2
 fi
 if has pmc; then
   PMC_OUT=gpurun_out/pmc3 bash scripts/pmc_round.sh || { echo pmc failed; exit 7; }
