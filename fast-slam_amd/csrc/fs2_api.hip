@@ -326,7 +326,6 @@ struct fs2_handle {
         MtMeta *meta = nullptr, *meta_pin = nullptr;
         MtAmb *amb = nullptr, *amb_pin = nullptr;
         int64_t amb_cap = 0;
-        int64_t amb_last = 0;              // listed logs of the last draw
         uint32_t *words_pin = nullptr;     // [2 kMtN]: key in, state blocks out
         int64_t *pidx = nullptr, *pidx_pin = nullptr;
         double *pval = nullptr, *pval_pin = nullptr;
@@ -3275,7 +3274,6 @@ static int mt_end(fs2_handle *h, MtCtx &c, hipStream_t s) {
     }
     // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
     const int64_t na = meta.amb_n;
-    mt.amb_last = na;
     if (na > 0) {
         if (na > c.amb_pre) {
             HIP_TRY(h, hipMemcpyAsync(mt.amb_pin + c.amb_pre, mt.amb + c.amb_pre, sizeof(MtAmb) * (size_t)(na - c.amb_pre),
@@ -3417,16 +3415,7 @@ int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs
     if (rc) return rc;
     mt.armed = false;
     if (!mt.dstream) {
-        // the highest priority: the draw's small grids (one workgroup for the
-        // counts and states) are dispatched ahead of the candidate pass's waves
-        // instead of waiting behind them (a kernel trace showed k_mt_final's one
-        // workgroup waiting ~120 us for a slot)
-        int lo = 0, hi = 0;
-        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&mt.dstream, hipStreamNonBlocking, hi) != hipSuccess) {
-            (void)hipGetLastError();
-            HIP_TRY(h, hipStreamCreateWithFlags(&mt.dstream, hipStreamNonBlocking));
-        }
+        HIP_TRY(h, hipStreamCreateWithFlags(&mt.dstream, hipStreamNonBlocking));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_in, hipEventDisableTiming));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_noise, hipEventDisableTiming));
     }
@@ -3439,10 +3428,7 @@ int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs
     // the listed logs come back with the counts: about 5% of the pairs (a 0.05-ulp
     // window per log), so a prefix of P/12 holds them all but rarely
     c.amb_pre = 0;
-    // (the last draw's count and a fifth again: the copy is a blit on the draw's
-    // critical path, ~30 us per MB)
-    const int64_t guess = mt.amb_last > 0 ? mt.amb_last + mt.amb_last / 5 + 1024 : c.P / 12 + 2048;
-    const int64_t pre = std::min<int64_t>(guess, mt.amb_cap);
+    const int64_t pre = std::min<int64_t>(c.P / 12 + 2048, mt.amb_cap);
     if (pre > 0) {
         HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)pre, hipMemcpyDeviceToHost, mt.dstream));
         c.amb_pre = pre;
