@@ -230,7 +230,6 @@ struct MtCtx {
     fs2_mt_state in;
     double sigma = 0.0;
     int64_t N = 0, P = 0, A = 0, amb_cap = 0, pos0 = 0, have = 0, total = 0;
-    int64_t amb_pre = 0;                  // listed logs copied to the host with the counts
     int h0 = 0;
     fs2_mt_state *after = nullptr, *after_u0 = nullptr;
     double *u0_out = nullptr;
@@ -3159,9 +3158,22 @@ static int mt_attempt(fs2_handle *h, MtCtx &c, hipStream_t s) {
     uint32_t *raw = mt.raw[mt.cur];
     const int64_t nb = (c.A + 255) / 256;
     HIP_TRY(h, mt_grow((void **)&mt.boff, nullptr, 4, &mt.boff_cap, std::max<int64_t>(nb, 1)));
+    // the listed logs and the results go straight into (mapped) host memory: no
+    // result copy after the draw -- a copy is a blit kernel that would queue
+    // behind, or slow, the candidate pass beside it
     int64_t acap = mt.amb_cap;
-    HIP_TRY(h, mt_grow((void **)&mt.amb, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, c.amb_cap));
+    HIP_TRY(h, mt_grow(nullptr, (void **)&mt.amb_pin, sizeof(MtAmb), &acap, c.amb_cap));
     mt.amb_cap = acap;
+    MtAmb *amb_dev = mt.amb_pin;
+    MtMeta *meta_host_dev = mt.meta_pin;
+    if (hipHostGetDevicePointer((void **)&amb_dev, mt.amb_pin, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        amb_dev = mt.amb_pin;
+    }
+    if (hipHostGetDevicePointer((void **)&meta_host_dev, mt.meta_pin, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        meta_host_dev = mt.meta_pin;
+    }
     {
         int64_t made = 0;
         const int rcf = mt_fill(h, raw, c.have, c.total, s, &made);
@@ -3170,10 +3182,10 @@ static int mt_attempt(fs2_handle *h, MtCtx &c, hipStream_t s) {
     }
     HIP_TRY(h, hipMemsetAsync(mt.meta, 0, sizeof(MtMeta), s));
     HIP_TRY(h, launch_mt_draw(raw, c.pos0, (c.pos0 - c.in.pos) / kMtN, c.A, c.P, c.N, c.h0, c.in.gauss, c.sigma, h->first,
-                              h->n, h->noise_dev, mt.boff, mt.meta, mt.amb,
-                              (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX), mt.tab, mt.tab_ready ? 1 : 0, s));
+                              h->n, h->noise_dev, mt.boff, mt.meta, amb_dev,
+                              (int32_t)std::min<int64_t>(mt.amb_cap, INT32_MAX), mt.tab, mt.tab_ready ? 1 : 0,
+                              meta_host_dev, s));
     mt.tab_ready = true;
-    HIP_TRY(h, hipMemcpyAsync(mt.meta_pin, mt.meta, sizeof(MtMeta), hipMemcpyDeviceToHost, s));
     return FS2_OK;
 }
 
@@ -3268,18 +3280,12 @@ static int mt_end(fs2_handle *h, MtCtx &c, hipStream_t s) {
             break;
         }
         if (attempt == 6) return set_err(&h->err, FS2_ERR_STATE, "fs2_mt_draw: attempts did not converge");
-        c.amb_pre = 0;
         const int rca = mt_attempt(h, c, s);
         if (rca) return rca;
     }
     // the listed logs: libm's log on the host (what numpy's legacy_gauss calls)
     const int64_t na = meta.amb_n;
     if (na > 0) {
-        if (na > c.amb_pre) {
-            HIP_TRY(h, hipMemcpyAsync(mt.amb_pin + c.amb_pre, mt.amb + c.amb_pre, sizeof(MtAmb) * (size_t)(na - c.amb_pre),
-                                      hipMemcpyDeviceToHost, s));
-            HIP_TRY(h, hipStreamSynchronize(s));
-        }
         HIP_TRY(h, mt_grow((void **)&mt.pidx, (void **)&mt.pidx_pin, 8, &mt.patch_cap, 2 * na));
         HIP_TRY(h, mt_grow((void **)&mt.pval, (void **)&mt.pval_pin, 8, &mt.pval_cap, 2 * na));
         // entry k patches outputs 2k, 2k + 1 (index -1: not this rank's); split over
@@ -3425,14 +3431,6 @@ int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs
     MtCtx &c = mt.dc;
     rc = mt_begin(h, in, sigma, after, after_u0, u0_out, mt.dstream, c);
     if (rc) return rc;
-    // the listed logs come back with the counts: about 5% of the pairs (a 0.05-ulp
-    // window per log), so a prefix of P/12 holds them all but rarely
-    c.amb_pre = 0;
-    const int64_t pre = std::min<int64_t>(c.P / 12 + 2048, mt.amb_cap);
-    if (pre > 0) {
-        HIP_TRY(h, hipMemcpyAsync(mt.amb_pin, mt.amb, sizeof(MtAmb) * (size_t)pre, hipMemcpyDeviceToHost, mt.dstream));
-        c.amb_pre = pre;
-    }
     mt.deferred = true;
     return FS2_OK;
 }

@@ -717,7 +717,7 @@ hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t 
 hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t A, int64_t P, int64_t N, int32_t h0,
                           double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
                           int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, double *tab, int32_t tab_ready,
-                          hipStream_t s);   // tab: [2][97] log table, made here unless tab_ready
+                          MtMeta *meta_host, hipStream_t s);   // tab: [2][97] log table, made here unless tab_ready
 hipError_t launch_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n, hipStream_t s);
 // jump-ahead (fs2_mtrng.hip): G regions of J words made in parallel (J >= 2 x 20561,
 // G <= kMtMaxGen); g: the polynomials of mt_jump_polys(J, G) ([G - 1][mt_poly_words()]);

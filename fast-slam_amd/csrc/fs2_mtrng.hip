@@ -209,8 +209,11 @@ __global__ __launch_bounds__(256) void k_mt_normals(const MtParams p) {
 
 // numpy's state after the draw: the key block holding the last word consumed
 // (pos = words used of it, 624 before the next twist), and the u0 words
+// The draw's results, also into the host's copy (mapped, coherent host memory)
+// when given: no result copy follows the draw (a copy is a blit kernel that
+// competes with the candidate pass).
 __global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t P,
-                                                  MtMeta *meta) {
+                                                  MtMeta *meta, MtMeta *meta_host) {
     const int64_t E = P > 0 ? pos0 + 4 * (meta->last_attempt + 1) : pos0;
     const int64_t b1 = (E == pos0) ? b_in : (E - 1) / kMtN, b2 = (E + 1) / kMtN;
     for (int t = threadIdx.x; t < kMtN; t += 256) {
@@ -224,6 +227,12 @@ __global__ __launch_bounds__(256) void k_mt_final(const uint32_t *R, int64_t pos
         meta->w_u0[0] = R[E];
         meta->w_u0[1] = R[E + 1];
     }
+    if (!meta_host) return;
+    __syncthreads();
+    static_assert(sizeof(MtMeta) % 4 == 0, "MtMeta words");
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(meta);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(meta_host);
+    for (int k = threadIdx.x; k < (int)(sizeof(MtMeta) / 4); k += 256) dst[k] = src[k];
 }
 
 __global__ __launch_bounds__(256) void k_mt_patch(double *out, const int64_t *idx, const double *val, int64_t n) {
@@ -255,7 +264,7 @@ hipError_t launch_mt_words(uint32_t *R, int64_t begin, int64_t end, hipStream_t 
 hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t A, int64_t P, int64_t N, int32_t h0,
                           double gauss0, double sigma, int64_t first, int64_t n_local, double *out,
                           int32_t *boff, MtMeta *meta, MtAmb *amb, int32_t amb_cap, double *tab, int32_t tab_ready,
-                          hipStream_t s) {
+                          MtMeta *meta_host, hipStream_t s) {
     MtParams p{};
     p.tab = tab;
     if (!tab_ready) hipLaunchKernelGGL(k_mt_table, dim3(1), dim3(128), 0, s, tab);
@@ -282,7 +291,7 @@ hipError_t launch_mt_draw(const uint32_t *R, int64_t pos0, int64_t b_in, int64_t
         hipLaunchKernelGGL(k_mt_scan, dim3(1), dim3(1024), 0, s, p);
         hipLaunchKernelGGL(k_mt_normals, dim3(p.nb), dim3(256), 0, s, p);
     }
-    hipLaunchKernelGGL(k_mt_final, dim3(1), dim3(256), 0, s, R, pos0, b_in, P, meta);
+    hipLaunchKernelGGL(k_mt_final, dim3(1), dim3(256), 0, s, R, pos0, b_in, P, meta, meta_host);
     return hipGetLastError();
 }
 
