@@ -2,7 +2,7 @@
 1e6 particles in all, L = 500) with FS2_TRACE=1: each scan's wall time with its
 monotonic start on stdout, libfs2's per-rank trace (same clock) on stderr, so a
 multi-second scan can be placed in the sharing / collective / growth steps.
-Run on the GPU box:  FS2_TRACE=1 python3 scripts/g8_refs_probe.py [reps]"""
+Run on the GPU box:  FS2_TRACE=1 python3 scripts/g8_refs_probe.py [reps [pause_s]]"""
 import os
 import sys
 import threading
@@ -57,5 +57,10 @@ def one(rep):
         h.close()
 
 
+# optional pause (seconds) between one set of handles' close and the next set's creation
+PAUSE = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
 for r in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
+    if r and PAUSE:
+        torch.cuda.synchronize()
+        time.sleep(PAUSE)
     one(r)
