@@ -19,6 +19,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/fs2.h"
@@ -96,13 +97,15 @@ struct GrowMem {
     char *base = nullptr;
     size_t reserved = 0, mapped = 0, gran = 0;
     int device = 0;
+    bool shareable = false;        // chunks exportable as POSIX file descriptors (page_refs between processes)
     std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
 };
-static hipMemAllocationProp gm_prop(int device) {
+static hipMemAllocationProp gm_prop(int device, bool shareable = false) {
     hipMemAllocationProp prop{};
     prop.type = hipMemAllocationTypePinned;
     prop.location.type = hipMemLocationTypeDevice;
     prop.location.id = device;
+    if (shareable) prop.requestedHandleTypes = hipMemHandleTypePosixFileDescriptor;
     return prop;
 }
 // (a failure is reported once: the runtime's last error is cleared, so the
@@ -178,39 +181,166 @@ static hipError_t gm_relocate(GrowMem &g, size_t need) {
     g.reserved = r;
     return hipSuccess;
 }
+// Physical chunks of closed handles, kept for the next handles' growth (process-
+// wide).  A set of handles closed and a new set created in the same process: a
+// large hipMemCreate of the new set waited 4.3 s (the round-4 driver bench's
+// 2.9 s scan; profiles/r05_vmm_growth_trace.txt places it in hipMemCreate itself,
+// ~5 us otherwise) even with the device drained before the release -- the driver
+// is still reclaiming the tens of GB the closed handles released.  So pools grow
+// in chunks of power-of-two sizes (kChunkMax, or the remainder rounded up), kept
+// here on close and taken back by any later growth that needs a chunk of that size:
+// no new physical memory, nothing for the driver to reclaim.  FS2_VMM_CACHE_MB caps
+// what is kept (default 128 GiB, 0 keeps none); fs2_release_cached_memory() and an
+// allocation that runs out of device memory release it.
+constexpr size_t kChunkMax = size_t(256) << 20;
+static size_t chunk_size(size_t remaining, size_t gran) {
+    if (remaining >= kChunkMax) return kChunkMax;
+    size_t c = gran;
+    while (c < remaining) c <<= 1;
+    return c;
+}
+struct ChunkCache {
+    std::mutex mu;
+    struct Chunk {
+        int dev;
+        bool shareable;
+        size_t bytes;
+        hipMemGenericAllocationHandle_t hd;
+    };
+    std::vector<Chunk> chunks;
+    size_t bytes = 0;
+    size_t cap() const {
+        static const size_t c = [] {
+            const char *e = std::getenv("FS2_VMM_CACHE_MB");
+            return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)131072) << 20;
+        }();
+        return c;
+    }
+    bool put(const Chunk &c) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (bytes + c.bytes > cap()) return false;
+        chunks.push_back(c);
+        bytes += c.bytes;
+        return true;
+    }
+    bool take(int dev, bool shareable, size_t b, hipMemGenericAllocationHandle_t *hd) {
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t k = chunks.size(); k-- > 0;) {
+            const Chunk &c = chunks[k];
+            if (c.dev != dev || c.shareable != shareable || c.bytes != b) continue;
+            *hd = c.hd;
+            bytes -= b;
+            chunks.erase(chunks.begin() + (ptrdiff_t)k);
+            return true;
+        }
+        return false;
+    }
+    size_t release() {
+        std::lock_guard<std::mutex> lk(mu);
+        size_t n = 0;
+        for (auto &c : chunks) {
+            (void)hipMemRelease(c.hd);
+            n += c.bytes;
+        }
+        chunks.clear();
+        bytes = 0;
+        return n;
+    }
+};
+ChunkCache g_chunks;
+
+// Test hook (fs2_debug_vm_fail_after_relocate): the next growth that had to move
+// its mapping fails right after the move, as a failing hipMemCreate / hipMemMap /
+// hipMemSetAccess would; the callers then fall back to allocate and copy from the
+// moved mapping (g.base), never from the pointer they held before the growth.
+std::atomic<int> g_vm_fail_after_relocate{0};
+// FS2_TRACE: the host time of each step of a growth (where a slow growth waits)
+struct GmStep {
+    const char *what;
+    size_t bytes;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~GmStep() {
+        static const bool on = std::getenv("FS2_TRACE") != nullptr;
+        if (!on) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "[fs2 vmm] %s %zu MiB %.3f ms\n", what, bytes >> 20, ms);
+    }
+};
+// (a chunk that cannot be used after all goes back to the cache, or is released)
+static void gm_drop(const GrowMem &g, size_t b, hipMemGenericAllocationHandle_t hd) {
+    if (!g_chunks.put(ChunkCache::Chunk{g.device, g.shareable, b, hd})) (void)hipMemRelease(hd);
+}
 static hipError_t gm_grow(GrowMem &g, size_t bytes) {
-    const size_t want = (bytes + g.gran - 1) / g.gran * g.gran;
-    if (want <= g.mapped) return hipSuccess;
+    const size_t need = (bytes + g.gran - 1) / g.gran * g.gran;
+    if (need <= g.mapped) return hipSuccess;
+    // the chunks this growth maps, largest first (a last one rounded up to a power of two)
+    std::vector<size_t> plan;
+    size_t want = g.mapped;
+    while (want < need) {
+        plan.push_back(chunk_size(need - want, g.gran));
+        want += plan.back();
+    }
     if (want > g.reserved) {
+        GmStep st{"relocate", want};
         const hipError_t e = gm_relocate(g, want);
         if (e != hipSuccess) return e;
+        if (g_vm_fail_after_relocate.exchange(0)) return gm_fail(hipErrorOutOfMemory);
     }
-    const size_t delta = want - g.mapped;
-    hipMemAllocationProp prop = gm_prop(g.device);
-    hipMemGenericAllocationHandle_t hd{};
-    hipError_t e = hipMemCreate(&hd, delta, &prop, 0);
-    if (e != hipSuccess) return gm_fail(e);
-    e = hipMemMap(g.base + g.mapped, delta, 0, hd, 0);
-    if (e != hipSuccess) {
-        hipMemRelease(hd);
+    hipMemAllocationProp prop = gm_prop(g.device, g.shareable);
+    const size_t mapped0 = g.mapped, nchunks0 = g.chunks.size();
+    hipError_t e = hipSuccess;
+    int cached = 0;
+    {
+        GmStep st{"chunks", want - mapped0};
+        for (size_t b : plan) {
+            hipMemGenericAllocationHandle_t hd{};
+            if (g_chunks.take(g.device, g.shareable, b, &hd)) {
+                ++cached;
+            } else {
+                e = hipMemCreate(&hd, b, &prop, 0);
+                if (e == hipErrorOutOfMemory && g_chunks.release() > 0) {   // the kept chunks make room
+                    (void)hipGetLastError();
+                    e = hipMemCreate(&hd, b, &prop, 0);
+                }
+                if (e != hipSuccess) break;
+            }
+            e = hipMemMap(g.base + g.mapped, b, 0, hd, 0);
+            if (e != hipSuccess) {
+                gm_drop(g, b, hd);
+                break;
+            }
+            g.chunks.push_back({hd, b});
+            g.mapped += b;
+        }
+    }
+    if (e == hipSuccess) {
+        GmStep st{"access", want};
+        e = gm_access(g, g.base, want);
+    }
+    if (e != hipSuccess) {          // back to where it was: this growth's chunks unmapped, kept
+        while (g.chunks.size() > nchunks0) {
+            const auto c = g.chunks.back();
+            g.chunks.pop_back();
+            g.mapped -= c.second;
+            (void)hipMemUnmap(g.base + g.mapped, c.second);
+            gm_drop(g, c.second, c.first);
+        }
+        g.mapped = mapped0;
         return gm_fail(e);
     }
-    e = gm_access(g, g.base, want);
-    if (e != hipSuccess) {
-        hipMemUnmap(g.base + g.mapped, delta);
-        hipMemRelease(hd);
-        return gm_fail(e);
-    }
-    g.chunks.push_back({hd, delta});
-    g.mapped = want;
+    if (cached && std::getenv("FS2_TRACE")) std::fprintf(stderr, "[fs2 vmm] %d of %zu chunks from closed handles\n", cached, plan.size());
     return hipSuccess;
 }
+// (the caller drained the device: fs2_destroy.  A release the runtime must defer
+// because work is still in flight is what made the next handle's first growth wait
+// seconds -- profiles/r04_g8_refs_growth_probe.txt)
 static void gm_free(GrowMem &g) {
+    GmStep st{"free", g.mapped};
     size_t off = g.mapped;
     for (auto it = g.chunks.rbegin(); it != g.chunks.rend(); ++it) {
         off -= it->second;
         hipMemUnmap(g.base + off, it->second);
-        hipMemRelease(it->first);
+        gm_drop(g, it->second, it->first);      // kept for the next handle's growth
     }
     g.chunks.clear();
     if (g.base) hipMemAddressFree(g.base, g.reserved);
@@ -507,6 +637,40 @@ CommTimer::~CommTimer() {
 // reallocates both tables (~n * rows * 16 B), so row-by-row growth cost a
 // realloc every few scans of a long run.  Rows past a map's count are never
 // read (every kernel stops at ceil(cnt / 8)), so spare rows cost memory only.
+// The sharded resample's receive-side row buffers (received particles' rows, the
+// distinct received pages' descriptors), `bytes` each: every local output's whole
+// row fits (a rank receives at most n particles, at most n * rows distinct pages),
+// so a resample never allocates.  The stream is drained first.
+static int recv_bufs(fs2_handle *h, size_t bytes) {
+    if (bytes <= h->rdesc_cap && bytes <= h->udesc_cap) return FS2_OK;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    for (int k = 0; k < 2; ++k) {
+        Desc *&p = k ? h->udesc : h->rdesc;
+        size_t &cap = k ? h->udesc_cap : h->rdesc_cap;
+        if (bytes <= cap) continue;
+        hipFree(p);
+        p = nullptr;
+        cap = 0;
+        HIP_TRY(h, hipMalloc(&p, bytes));
+        cap = bytes;
+    }
+    return FS2_OK;
+}
+
+// The sharded resample's row-sized buffers for every row of the shard (a rank
+// sends at most its n particles' rows, receives at most n outputs' rows): the page
+// dedup table (twice the rows, a power of two) and the received rows / pages.
+// At creation and with every row growth, so a resample never allocates them (the
+// first resamples at G = 8 sent up to ~65 % of a rank's rows).
+static int reserve_xfer_table(fs2_handle *h, int64_t cap, int64_t nrows, bool in_scan);
+static int xfer_bufs(fs2_handle *h) {
+    const int64_t S = std::max<int64_t>(h->n, 1) * h->rows;
+    int lg = 10;
+    while ((int64_t(1) << lg) < 2 * S && lg < 31) ++lg;
+    const int rc = reserve_xfer_table(h, int64_t(1) << lg, S, false);
+    return rc ? rc : recv_bufs(h, sizeof(Desc) * (size_t)S);
+}
+
 static int grow_rows(fs2_handle *h, int need_slots) {
     if (need_slots <= h->cap) return FS2_OK;
     if (need_slots > h->max_cap)
@@ -530,6 +694,9 @@ static int grow_rows(fs2_handle *h, int need_slots) {
     }
     h->rows = rows;
     h->cap = rows * kPageSlots;
+    // (sharded: the resample's row buffers follow, here where the stream is drained
+    // anyway, not inside a later resample)
+    if (h->rdesc) return xfer_bufs(h);
     return FS2_OK;
 }
 
@@ -606,6 +773,12 @@ static void trace(const fs2_handle *h, const char *what, int k = -1) {
     const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     std::fprintf(stderr, "[fs2 rank %d %.3f] %s %d\n", h->cfg.rank, t, what, k);
     std::fflush(stderr);
+}
+
+// A buffer the sharded resample had to reallocate inside a scan (fs2_profile.scan_allocs)
+static void scan_alloc(fs2_handle *h, const char *what, size_t bytes) {
+    h->prof.scan_allocs += 1;
+    trace(h, what, (int)std::min<size_t>(bytes >> 20, INT32_MAX));
 }
 
 static int share_pools(fs2_handle *h, bool first) {
@@ -714,6 +887,10 @@ static int collect_collective(fs2_handle *h) {
     if (int rc = h->tp->status(&h->err)) return rc;
     h->cursor = 0;
     h->rcursor = 0;
+    if (h->nrecs > 0) {            // (as collect_body: the futile-collection bound starts over)
+        h->appends_since_rcollect = 0;
+        h->rcollect_exact = true;
+    }
     h->collections += 1;
     (void)G;
     return FS2_OK;
@@ -735,7 +912,8 @@ static int grow_side(fs2_handle *h, GrowMem &vm, void **ptr, size_t bytes, size_
     }
     void *np = nullptr;
     HIP_TRY(h, hipMalloc(&np, bytes));
-    if (*ptr && keep) HIP_TRY(h, copy_sync(h, np, *ptr, keep, hipMemcpyDeviceToDevice));
+    // (a growth that failed after moving its mapping left the data at vm.base only)
+    if (*ptr && keep) HIP_TRY(h, copy_sync(h, np, vm.base ? vm.base : *ptr, keep, hipMemcpyDeviceToDevice));
     if (vm.base) {
         gm_free(vm);
         h->vm_fallbacks += 1;
@@ -817,7 +995,10 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         // reserved range is left for good)
         char *pool = nullptr;
         HIP_TRY(h, hipMalloc(&pool, (size_t)pages * kPageBytes));
-        if (h->pool) HIP_TRY(h, copy_sync(h, pool, h->pool, (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
+        // (from the mapping itself: a growth that failed after moving it left the
+        // pages at pool_vm.base, not at the h->pool held before)
+        if (h->pool) HIP_TRY(h, copy_sync(h, pool, h->pool_vm.base ? h->pool_vm.base : h->pool,
+                                          (size_t)h->npool * kPageBytes, hipMemcpyDeviceToDevice));
         if (h->pool_vm.base) {
             gm_free(h->pool_vm);
             h->vm_fallbacks += 1;
@@ -873,7 +1054,8 @@ static int grow_recs(fs2_handle *h, int64_t n) {
     } else {
         char *rp = nullptr;
         HIP_TRY(h, hipMalloc(&rp, (size_t)n * kRecBytes));
-        if (h->rpool) HIP_TRY(h, copy_sync(h, rp, h->rpool, (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
+        if (h->rpool) HIP_TRY(h, copy_sync(h, rp, h->rpool_vm.base ? h->rpool_vm.base : h->rpool,
+                                           (size_t)h->nrecs * kRecBytes, hipMemcpyDeviceToDevice));
         if (h->rpool_vm.base) {
             gm_free(h->rpool_vm);
             h->vm_fallbacks += 1;
@@ -959,6 +1141,7 @@ static int reserve_recs(fs2_handle *h, int64_t need, PageAlloc *out) {
 // resamples, so a timed scan normally never allocates.
 static int ensure_arena(fs2_handle *h, char *&buf, size_t &cap, size_t bytes) {
     if (cap >= bytes) return FS2_OK;
+    if (h->tp) scan_alloc(h, "scan_alloc arena (MiB)", bytes);   // (creation sizes it without a transport)
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     hipFree(buf);
     buf = nullptr;
@@ -1008,8 +1191,9 @@ static const int64_t *posted_xmat(const fs2_handle *h) {
 }
 
 // The page-dedup table (XferTable) for `cap` slots and `nrows` row entries.
-static int reserve_xfer_table(fs2_handle *h, int64_t cap, int64_t nrows) {
+static int reserve_xfer_table(fs2_handle *h, int64_t cap, int64_t nrows, bool in_scan) {
     hipStream_t s = h->stream;
+    if (in_scan && (h->xt_cap < cap || h->xt_ecap < nrows)) scan_alloc(h, "scan_alloc dedup table (M rows)", (size_t)nrows);
     if (h->xt_cap < cap) {
         HIP_TRY(h, hipStreamSynchronize(s));
         hipFree(h->xt_key); hipFree(h->xt_ref); hipFree(h->xt_uidx); hipFree(h->xt_cmask); hipFree(h->xt_cbase);
@@ -1218,7 +1402,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         while ((int64_t(1) << lg) < 2 * nrows) ++lg;
         if (lg > 31) return set_err(&h->err, FS2_ERR_CAPACITY, "%lld page-table rows to send", (long long)nrows);
         const int64_t cap = int64_t(1) << lg;
-        rc = reserve_xfer_table(h, cap, nrows);
+        rc = reserve_xfer_table(h, cap, nrows, true);
         if (rc) return rc;
         T.key = h->xt_key;
         T.ref = h->xt_ref;
@@ -1405,6 +1589,14 @@ const char *fs2_last_error(const fs2_handle *h) {
 static void free_handle(fs2_handle *h) {
     if (!h) return;
     if (h->stream) hipStreamSynchronize(h->stream);
+    // In-place pools (VMM chunks): nothing of this process may still be in flight
+    // when they are unmapped and released, or the runtime defers the release and the
+    // next handle's first growth (hipMemCreate) waits for it -- 4 s in the round-4
+    // driver bench (profiles/r04_g8_refs_growth_probe.txt; a device synchronize
+    // between the sets of handles brought it back to milliseconds).
+    const bool vmm = h->pool_vm.base || h->rpool_vm.base || h->freel_vm.base || h->mark_vm.base ||
+                     h->rfreel_vm.base || h->rmark_vm.base;
+    if (vmm) hipDeviceSynchronize();
     if (h->refs_shared && h->tp && !h->tp->in_process()) {
         // page_refs: no rank frees its pools while another may still read them (an
         // export of maps naming remote pages): every rank arrives, unmaps the others'
@@ -1433,6 +1625,7 @@ static void free_handle(fs2_handle *h) {
     if (h->mark_vm.base) gm_free(h->mark_vm); else hipFree(h->mark);
     if (h->rfreel_vm.base) gm_free(h->rfreel_vm); else hipFree(h->rfreel);
     if (h->rmark_vm.base) gm_free(h->rmark_vm); else hipFree(h->rmark);
+    if (vmm) hipDeviceSynchronize();       // (the releases complete here, not at the next growth)
     hipFree(h->bcnt); hipFree(h->nfree_dev);
     hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->slb_pass); hipFree(h->ext_dev);
@@ -1528,7 +1721,14 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     const int64_t n = std::max<int64_t>(h->n, 1);
     const int64_t nb = (n + kBlock - 1) / kBlock;
     const int64_t nsb = (n + 1023) / 1024;
-    auto alloc = [&](void **p, size_t bytes) { return hipMalloc(p, bytes > 0 ? bytes : 16); };
+    auto alloc = [&](void **p, size_t bytes) {
+        hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 16);
+        if (e == hipErrorOutOfMemory && g_chunks.release() > 0) {   // closed handles' kept chunks
+            (void)hipGetLastError();
+            e = hipMalloc(p, bytes > 0 ? bytes : 16);
+        }
+        return e;
+    };
     bool ok = true;
     for (int s = 0; s < 2; ++s) {
         ok &= alloc((void **)&h->x[s], n * 8) == hipSuccess;
@@ -1709,16 +1909,10 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         // shared (the first resamples move up to ~40 % of a rank's particles, to up
         // to three ranks), and the received particles' rows and pages
         const int64_t K = n / 2 + 1, S = K * h->rows;
-        int lg = 10;
-        while ((int64_t(1) << lg) < 2 * S && lg < 31) ++lg;
-        rc = reserve_xfer_table(h, int64_t(1) << lg, S);
+        rc = xfer_bufs(h);
         const size_t bytes = (size_t)xfer_bytes(K, S, S, 0) + 256 * kMaxRanks;
         if (!rc) rc = ensure_arena(h, h->sarena, h->scap, bytes);
         if (!rc) rc = ensure_arena(h, h->rarena, h->rcap, bytes);
-        if (!rc && hipMalloc(&h->rdesc, sizeof(Desc) * (size_t)S) != hipSuccess) rc = FS2_ERR_OOM;
-        if (!rc) h->rdesc_cap = sizeof(Desc) * (size_t)S;
-        if (!rc && hipMalloc(&h->udesc, sizeof(Desc) * (size_t)S) != hipSuccess) rc = FS2_ERR_OOM;
-        if (!rc) h->udesc_cap = sizeof(Desc) * (size_t)S;
         if (rc) return fail(rc == FS2_ERR_OOM ? set_err(&h->err, rc, "sharded transfer buffers") : rc);
     }
     if (G > 1 || cfg->sharded_path) {
@@ -2306,6 +2500,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
             if (rc) return rc;
             // received maps can be longer than every local one: rows for the
             // largest map on any rank (k_global_finalize) before unpacking them
+            if (posted_stats(h).max_count > h->cap) scan_alloc(h, "scan_alloc rows (slots M)", (size_t)posted_stats(h).max_count << 20);
             rc = grow_rows(h, posted_stats(h).max_count);
             if (rc) return rc;
             rs.opt = h->pt[nxt];
@@ -2317,23 +2512,15 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
             rc = reserve_pages(h, h->u_recv, &rs.alloc);
             if (rc) return rc;
             rs.map = h->map();
+            // received rows and pages: sized for every local output's whole row at
+            // creation and with every row growth (recv_bufs), so these never fire
+            // unless n_recv * rows overflowed that (counted in scan_allocs)
             const size_t rbytes = sizeof(Desc) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
-            if (rbytes > h->rdesc_cap) {
-                HIP_TRY(h, hipStreamSynchronize(s));
-                hipFree(h->rdesc);
-                h->rdesc = nullptr;
-                h->rdesc_cap = 0;
-                HIP_TRY(h, hipMalloc(&h->rdesc, rbytes + rbytes / 4));
-                h->rdesc_cap = rbytes + rbytes / 4;
-            }
             const size_t ubytes = sizeof(Desc) * (size_t)std::max<int64_t>(h->u_recv, 1);
-            if (ubytes > h->udesc_cap) {
-                HIP_TRY(h, hipStreamSynchronize(s));
-                hipFree(h->udesc);
-                h->udesc = nullptr;
-                h->udesc_cap = 0;
-                HIP_TRY(h, hipMalloc(&h->udesc, ubytes + ubytes / 4));
-                h->udesc_cap = ubytes + ubytes / 4;
+            if (rbytes > h->rdesc_cap || ubytes > h->udesc_cap) {
+                scan_alloc(h, "scan_alloc recv rows (MiB)", std::max(rbytes, ubytes));
+                rc = recv_bufs(h, std::max(rbytes, ubytes));
+                if (rc) return rc;
             }
             rs.udesc = h->udesc;
             rs.rdesc = h->rdesc;
@@ -2434,6 +2621,10 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     }
     if (st.error_flags & 1)
         return set_err(&h->err, FS2_ERR_LINALG, "Singular matrix (landmark or observation covariance)");
+    if ((st.error_flags & 4) && h->cfg.reduce_mode == FS2_REDUCE_EXACT)
+        return set_err(&h->err, FS2_ERR_STATE,
+                       "sharded exact-order reduction incomplete (chain ops overflow or numpy chunk edges): "
+                       "the scan used the tree estimate, not the reference's summation order");
     if (st.error_flags & 8) return refs_short(h, "page or record");
     return FS2_OK;
 }
@@ -3438,6 +3629,13 @@ int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs
 int fs2_debug_mt_jump(const uint32_t key[624], uint64_t J, uint32_t out[624]) {
     if (!key || !out) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_mt_jump: null argument");
     if (!mt_jump_host(key, J, out)) return set_err(nullptr, FS2_ERR_STATE, "MT19937 characteristic polynomial not found");
+    return FS2_OK;
+}
+
+int64_t fs2_release_cached_memory(void) { return (int64_t)g_chunks.release(); }
+
+int fs2_debug_vm_fail_after_relocate(int32_t on) {
+    g_vm_fail_after_relocate.store(on ? 1 : 0);
     return FS2_OK;
 }
 

@@ -647,6 +647,7 @@ __global__ __launch_bounds__(64) void k_chain_fold(const ChainSummary *all, int3
     if (lane == 0) {
         if (over) {
             stats->reduce_amb += 1;          // the tree estimates stay: counted, never hidden
+            stats->error_flags |= 4;         // (fs2.h: EXACT fails the scan, AUTO reports it)
         } else {
             if (total) *total = s;
             if (entry) *entry = at;

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -129,6 +130,7 @@ class fs2_profile(C.Structure):
         ("collect_ms", C.c_double),
         ("pool_grows", C.c_int64),
         ("grow_ms", C.c_double),
+        ("scan_allocs", C.c_int64),
     ]
 
     def as_dict(self):
@@ -220,6 +222,8 @@ SIGNATURES = [
     ("fs2_debug_normals", C.c_int, [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, _vp]),
     ("fs2_debug_mt_log", C.c_int, [C.c_int32, _vp, C.c_int64, _vp, _vp, C.c_int32]),
     ("fs2_debug_refuse_peer_maps", C.c_int, [_H]),
+    ("fs2_debug_vm_fail_after_relocate", C.c_int, [C.c_int32]),
+    ("fs2_release_cached_memory", C.c_int64, []),
     ("fs2_debug_noise", C.c_int, [_H, _vp]),
     ("fs2_debug_mt_jump", C.c_int, [_vp, C.c_uint64, _vp]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
@@ -230,6 +234,29 @@ SIGNATURES = [
 _lib = None
 
 
+HIP_RUNTIME = None   # which HIP runtime libfs2 runs on: ("torch-wheel" | "system", path, version)
+
+
+def _wheel_hip_version(torch_dir):
+    """The HIP version a PyTorch wheel was built with, read from torch/version.py
+    as text (no torch import)."""
+    try:
+        for line in open(os.path.join(torch_dir, "version.py")):
+            if line.startswith("hip"):
+                v = line.split("=", 1)[1].strip().strip("'\"")
+                return None if v in ("None", "") else v
+    except OSError:
+        pass
+    return None
+
+
+def _system_hip_version():
+    try:
+        return open(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), ".info", "version")).read().strip()
+    except OSError:
+        return None
+
+
 def _share_torch_hip_runtime():
     """One HIP runtime per process.  A PyTorch-ROCm wheel ships its own
     libamdhip64.so (and HSA runtime), which its libraries name without the ".7"
@@ -238,23 +265,50 @@ def _share_torch_hip_runtime():
     and a later `import torch` loads the wheel's copy beside it -- two HSA runtimes,
     and PyTorch then finds no GPU (tests/test_gpu_torch_coexist.py).  Loaded after
     the wheel's copy, libfs2's soname matches it and both share it -- which is what
-    happens whenever torch is imported first.  So when a PyTorch wheel is
-    installed, its runtime is loaded here first (no torch import)."""
-    try:
-        import importlib.util
-        spec = importlib.util.find_spec("torch")
-    except Exception:
+    happens whenever torch is imported first.
+
+    FS2_HIP_RUNTIME chooses: "system" never loads the wheel's runtime (libfs2 and
+    /opt/rocm's RCCL on the runtime they were built against; a later `import
+    torch` in the same process then sees no GPU), "torch" always does.  Unset:
+    the wheel's runtime when torch is already imported (it is loaded anyway) or a
+    wheel is installed, so a later `import torch` works.  The choice and both
+    versions are recorded in HIP_RUNTIME; a version mismatch is reported once
+    (FS2_VERBOSE=1 prints the choice)."""
+    global HIP_RUNTIME
+    want = os.environ.get("FS2_HIP_RUNTIME", "").strip().lower()
+    sysv = _system_hip_version()
+    HIP_RUNTIME = ("system", None, sysv)
+    if want == "system":
         return
-    if spec is None or not spec.submodule_search_locations:
-        return
-    for d in spec.submodule_search_locations:
+    torch_dirs = []
+    if "torch" in sys.modules and getattr(sys.modules["torch"], "__file__", None):
+        torch_dirs = [os.path.dirname(sys.modules["torch"].__file__)]
+    else:
+        try:
+            import importlib.util
+            spec = importlib.util.find_spec("torch")
+        except Exception:
+            spec = None
+        if spec is not None and spec.submodule_search_locations:
+            torch_dirs = list(spec.submodule_search_locations)
+    for d in torch_dirs:
         p = os.path.join(d, "lib", "libamdhip64.so")
-        if os.path.exists(p):
-            try:
-                C.CDLL(p, mode=C.RTLD_GLOBAL)
-            except OSError:
-                pass
+        if not os.path.exists(p):
+            continue
+        try:
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+        except OSError:
             return
+        wv = _wheel_hip_version(d)
+        HIP_RUNTIME = ("torch-wheel", p, wv)
+        if wv and sysv and wv.split(".")[:2] != sysv.split(".")[:2]:
+            import warnings
+            warnings.warn(f"libfs2 runs on PyTorch's HIP runtime {wv} ({p}), not the system ROCm {sysv} it "
+                          f"was compiled against (one runtime per process; FS2_HIP_RUNTIME=system opts out)",
+                          RuntimeWarning, stacklevel=3)
+        break
+    if os.environ.get("FS2_VERBOSE"):
+        print(f"[fs2] HIP runtime: {HIP_RUNTIME}", file=sys.stderr)
 
 
 def load():

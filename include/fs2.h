@@ -123,7 +123,13 @@ typedef struct fs2_iter_stats {
     uint64_t slots_written;     /* landmark slots written (EKF updates + appends) */
     uint64_t ambiguous;         /* gate decisions within 1e-9 relative of the threshold */
     uint64_t resample_slots;    /* landmark slots the resampled maps refer to (shared, not copied) */
-    int32_t error_flags;        /* bit 0: singular covariance met; bit 1: non-finite weight */
+    int32_t error_flags;        /* bit 0: singular covariance met; bit 1: non-finite weight;
+                                   bit 2: a sharded exact-order reduction could not be completed
+                                   (a shard's chain ops overflowed, or numpy's chunk edges did not
+                                   fit) and the tree estimate stood in -- with reduce_mode EXACT
+                                   fs2_iterate_wait then fails with FS2_ERR_STATE, with AUTO the
+                                   scan completes and reduce_ambiguous counts it; bit 3: page_refs
+                                   localisation ran out of pool room (the scan fails) */
     int32_t reduce_ambiguous;   /* FS2_REDUCE_PARALLEL: resample boundaries (and the N_eff
                                    rule) within the rounding bound of the reference's
                                    summation order, i.e. decisions that may differ from it;
@@ -195,6 +201,11 @@ typedef struct fs2_profile {
     double collect_ms;          /* their host wall time */
     int64_t pool_grows;         /* pool growths (in place, or allocate and copy: fs2_iter_stats.pool_copies) */
     double grow_ms;             /* their host wall time */
+    int64_t scan_allocs;        /* buffers reallocated inside a scan's sharded resample (transfer
+                                   arenas, dedup table, received rows / pages, page-table rows for a
+                                   received map longer than every local one): each drains the stream
+                                   and allocates.  Counted whether or not profiling is on; 0 when the
+                                   creation-time sizes hold */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */
@@ -213,6 +224,14 @@ void fs2_config_default(fs2_config *cfg);
  * 1/N, empty maps.  Owns all device memory. */
 int fs2_create(const fs2_config *cfg, fs2_handle **out);
 void fs2_destroy(fs2_handle *h);
+
+/* Device memory of closed handles kept for reuse: fs2_destroy keeps the physical
+ * chunks of the pools that grow in place (up to FS2_VMM_CACHE_MB, default 128 GiB;
+ * 0 keeps none) and later handles of the process grow into them before they ask
+ * the driver for new memory -- a large allocation right after tens of GB were
+ * released waited seconds for the driver.  This releases every
+ * kept chunk; returns the bytes released. */
+int64_t fs2_release_cached_memory(void);
 
 /* Message for the last error on this handle (h may be NULL: last global error). */
 const char *fs2_last_error(const fs2_handle *h);
@@ -390,6 +409,11 @@ int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, in
  * mode then turns off on every rank (fs2_profile.page_refs = -1).  Before the
  * first scan only. */
 int fs2_debug_refuse_peer_maps(fs2_handle *h);
+/* Test hook of the in-place pools: on = 1 makes the next pool growth that must move
+ * its reserved range fail right after the move (as a failing hipMemCreate / hipMemMap
+ * would), so the allocate-and-copy fallback runs (fs2_iter_stats.pool_copies).
+ * Process-wide, one-shot. */
+int fs2_debug_vm_fail_after_relocate(int32_t on);
 /* Test hook: the handle's motion-noise buffer (N_local values: the last scan's
  * injected draws, or fs2_mt_draw's) into out. */
 int fs2_debug_noise(fs2_handle *h, double *out);

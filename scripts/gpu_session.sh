@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU session stages, comma-separated (default all = tests,bench,prof):
+# GPU session stages, comma-separated (default all = tests,bench,prof):
 #   tests  pytest -m gpu ($TESTS) + smoke
 #   bench  the default bench line (config 3, extra.configs cfg2 / cfg4)
 #   prof   rocprofv3 kernel stats of the config-3 bench

@@ -37,7 +37,8 @@ def main(argv):
     t0 = time.time()
     cap = CAP(L, scans)
     h = fast_slam_2.FastSLAM2(N, reduce="auto", record_assoc=True, seed=5, landmark_capacity=cap, rank=rank,
-                              world_size=G, comm_id=key, comm_mode="shm", verbose=False, rng="device")
+                              world_size=G, comm_id=key, comm_mode="shm", verbose=False, rng="device",
+                              page_refs=os.environ.get("FS2_CFG5_PAGE_REFS", "auto"))
     a, b = h.first_global, h.first_global + h.n_local
     x, y, yaw, w = initial_scalars(N)
     lm = syn.particle_maps(N, L, 0, a, b - a)
@@ -83,7 +84,7 @@ def main(argv):
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), first=rec["firsts"][-1], count=n_local,
              assoc=np.stack(assoc), scal=np.stack(scal), checksum=np.concatenate(cs),
              migrations=prof["migrations"], sent_particles=prof["sent_particles"],
-             sent_bytes=prof["sent_bytes"],
+             sent_bytes=prof["sent_bytes"], scan_allocs=prof["scan_allocs"],
              **{f"win{s}": wv for s, wv in enumerate(wins)}, **{k: np.array(v) for k, v in rec.items()})
     print(f"rank {rank} done in {time.time() - t0:.1f} s", flush=True)
     return 0

@@ -108,7 +108,8 @@ def main(argv):
     h.close()
     np.savez(out, first=a, count=b - a, assoc=np.stack(assoc), x=xs, y=ys, yaw=yaws, w=ws, cnt=cnts, lm=lms,
              sent_particles=prof["sent_particles"], sent_rows=prof["sent_rows"], sent_pages=prof["sent_pages"],
-             migrations=prof["migrations"], np_key=np.random.get_state()[1], np_pos=np.random.get_state()[2],
+             migrations=prof["migrations"], scan_allocs=prof["scan_allocs"],
+             np_key=np.random.get_state()[1], np_pos=np.random.get_state()[2],
              **{k: np.array(v) for k, v in rec.items()})
     return 0
 

@@ -103,6 +103,10 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     # siblings share pages once particles have resampled ancestors ("follow" moves
     # each particle's own initial map once: nothing shared yet)
     assert pages < rows if mode == "peaked" else pages <= rows
+    if mode != "follow":     #  no buffer was reallocated inside a scan
+        # ("follow" hands a whole shard over at once, beyond the half shard the
+        # transfer arenas are sized for at creation)
+        assert all(int(d["scan_allocs"]) == 0 for d in ranks), [int(d["scan_allocs"]) for d in ranks]
     if mode == "follow":     # rank 0 took the higher shard its sources fill most
         assert int(ranks[0]["firsts"][0]) > 0 and int(ranks[0]["first"]) > 0
 
