@@ -117,7 +117,7 @@ static hipError_t gm_fail(hipError_t e) {
 // Reserves room for `bytes` with headroom (half again, at least 64 MiB): modest,
 // because the reservation is address space the process's other HIP runtimes
 // (PyTorch's) may need; a growth beyond it moves the mapping, not the data.
-static bool gm_init(GrowMem &g, int device, size_t bytes) {
+static bool gm_init(GrowMem &g, int device, size_t bytes, bool shareable) {
     hipMemAllocationProp prop = gm_prop(device);
     size_t gran = 0;
     if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran) {
@@ -135,6 +135,7 @@ static bool gm_init(GrowMem &g, int device, size_t bytes) {
     g.reserved = r;
     g.gran = gran;
     g.device = device;
+    g.shareable = shareable;
     return true;
 }
 static hipError_t gm_access(GrowMem &g, char *base, size_t bytes) {
@@ -536,6 +537,7 @@ struct fs2_handle {
     bool refuse_maps = false;              // test hook: this rank reports its peer mappings as failed
     bool room_check = false;               // page_refs: agree on pool room at the next scan (after a resample)
     bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
+    bool vm_share = false;                 // page_refs between processes: pool chunks exportable (share_vm)
     bool refs_live = false;                // a resample has exchanged references (no local collection)
     uint64_t grows = 0;                    // collective pool growths
     uint64_t vm_fallbacks = 0;             // growths that left the reserved range (allocate and copy)
@@ -795,10 +797,22 @@ static int share_pools(fs2_handle *h, bool first) {
     std::string why;
     for (int what = 0; what < 3; ++what) {
         void *base = what == 0 ? (void *)h->pool : what == 1 ? (void *)h->rpool : (void *)h->mark;
+        const GrowMem &vm = what == 0 ? h->pool_vm : what == 1 ? h->rpool_vm : h->mark_vm;
         CommTimer ct(h);
         std::string e;
         trace(h, "share", what);
-        const int src = h->tp->share(base, ptrs, &e);
+        // pools grown in place go as their VMM chunks (every rank takes the same
+        // path: vm_share is the same on every rank, and a pool that left its
+        // reserved range fails the export, which the agreement below turns off)
+        int src;
+        if (h->vm_share) {
+            std::vector<fs2comm::VmChunk> ch;
+            if (vm.base == base)
+                for (const auto &c : vm.chunks) ch.push_back({c.first, c.second});
+            src = h->tp->share_vm(ch, base, h->cfg.device, ptrs, &e);
+        } else {
+            src = h->tp->share(base, ptrs, &e);
+        }
         trace(h, "shared", src);
         if (src) {
             if (ok) why = e;
@@ -905,7 +919,7 @@ static int grow_side(fs2_handle *h, GrowMem &vm, void **ptr, size_t bytes, size_
     *moved = false;
     // (a side array is small next to its pool -- 1 or 4 B per 48 B record -- so it
     // is mapped half again ahead and grows about every other pool growth)
-    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, 4 * bytes);
+    if (!vm.base && !*ptr && pools_in_place) gm_init(vm, h->cfg.device, 4 * bytes, h->vm_share);
     if (vm.base && (bytes <= vm.mapped || gm_grow(vm, std::max(bytes, vm.mapped + vm.mapped / 2)) == hipSuccess)) {
         *ptr = vm.base;
         return FS2_OK;
@@ -983,11 +997,9 @@ static int grow_pool(fs2_handle *h, int64_t pages) {
         return set_err(&h->err, FS2_ERR_OOM, "page pool of %lld pages exceeds the id space", (long long)pages);
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
-    // in place (VMM) unless the pool is shared through IPC handles (page_refs
-    // between processes: hipIpcGetMemHandle needs a hipMalloc allocation); ranks
-    // that are threads of one process share plain pointers, so theirs grow in place
-    const bool vm_ok = !h->refs || h->cfg.comm_mode == FS2_COMM_LOCAL;
-    if (!h->pool && vm_ok) gm_init(h->pool_vm, h->cfg.device, (size_t)pages * kPageBytes);
+    // in place (VMM); page_refs between processes: chunks exportable as POSIX
+    // descriptors (vm_share), mapped by the peers (Transport::share_vm)
+    if (!h->pool) gm_init(h->pool_vm, h->cfg.device, (size_t)pages * kPageBytes, h->vm_share);
     if (h->pool_vm.base && gm_grow(h->pool_vm, (size_t)pages * kPageBytes) == hipSuccess) {
         h->pool = h->pool_vm.base;
     } else {
@@ -1047,8 +1059,7 @@ static int grow_recs(fs2_handle *h, int64_t n) {
                        (long long)n);
     hipStream_t s = h->stream;
     HIP_TRY(h, hipStreamSynchronize(s));
-    const bool vm_ok = !h->refs || h->cfg.comm_mode == FS2_COMM_LOCAL;   // (as grow_pool)
-    if (!h->rpool && vm_ok) gm_init(h->rpool_vm, h->cfg.device, (size_t)n * kRecBytes);
+    if (!h->rpool) gm_init(h->rpool_vm, h->cfg.device, (size_t)n * kRecBytes, h->vm_share);   // (as grow_pool)
     if (h->rpool_vm.base && gm_grow(h->rpool_vm, (size_t)n * kRecBytes) == hipSuccess) {
         h->rpool = h->rpool_vm.base;
     } else {
@@ -1883,13 +1894,16 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     // resample sends ~10x fewer bytes, but the update passes then localise remote
     // pages one particle-row at a time (siblings that share a remote page each copy
     // it), which moved more bytes and took longer per scan than sending each
-    // distinct page once; and between processes the IPC mapping did not return
-    // for processes on one GPU (profiles/r04_ipc_open_hang.txt).
+    // distinct page once.  Between processes the pools are VMM chunks exported
+    // as file descriptors (vm_share, Transport::share_vm): the runtime's
+    // hipIpcOpenMemHandle did not return in a process that had exported an
+    // allocation itself (profiles/r05_ipc_probe.txt).
     const bool refs_wanted = cfg->page_refs == 1;
     if (G > 1 && refs_wanted) {
         const int64_t lim = (int64_t)kRefIdMask - 1024;
         if (cfg->page_pool <= 0 && npages > lim && lim >= n * h->rows + n * h->rows / 4 + 8 * n) npages = lim;
         h->refs = G <= kRefMaxRanks && npages <= lim;
+        h->vm_share = h->refs && cfg->comm_mode != FS2_COMM_LOCAL;
         // pools shared with the peers never grow: room for a few more scans of
         // reservations between the collective collections
         if (h->refs && cfg->page_pool <= 0) npages = std::min(lim, npages + 24 * n);

@@ -20,9 +20,12 @@
 
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <poll.h>
 #include <rccl/rccl.h>
 #include <sys/mman.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -52,6 +55,128 @@ struct Xfer {
     size_t bytes;
 };
 
+// One physical chunk of an allocation that grows in place (fs2_api.hip GrowMem):
+// the chunks are mapped back to back from the allocation's base.
+struct VmChunk {
+    hipMemGenericAllocationHandle_t hd;
+    size_t bytes;
+};
+
+// ---- file descriptors between the processes of one host (page_refs) ----
+//
+// A rank's pools are VMM chunks exported as POSIX file descriptors
+// (hipMemExportToShareableHandle) and handed to the other ranks over Unix
+// SOCK_SEQPACKET sockets in the abstract namespace (SCM_RIGHTS), named from the
+// group key and the rank.  hipIpcOpenMemHandle is not used between processes:
+// the runtime's own dmabuf IPC did not complete an open in a process that had
+// exported an allocation itself (profiles/r05_ipc_probe.txt), and every rank
+// exports its pools and opens the others'.
+namespace uds {
+inline bool name(const std::string &key, int rank, sockaddr_un *a, socklen_t *len) {
+    std::memset(a, 0, sizeof *a);
+    a->sun_family = AF_UNIX;
+    const int k = std::snprintf(a->sun_path + 1, sizeof a->sun_path - 1, "fs2vm.%s.%d", key.c_str(), rank);
+    if (k <= 0 || k >= (int)sizeof a->sun_path - 1) return false;
+    *len = (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + k);
+    return true;
+}
+inline int listen_on(const std::string &key, int rank) {
+    sockaddr_un a;
+    socklen_t len;
+    if (!name(key, rank, &a, &len)) return -1;
+    const int fd = socket(AF_UNIX, SOCK_SEQPACKET | SOCK_CLOEXEC, 0);
+    if (fd < 0) return -1;
+    if (bind(fd, (sockaddr *)&a, len) != 0 || listen(fd, 64) != 0) {
+        close(fd);
+        return -1;
+    }
+    return fd;
+}
+inline bool wait_fd(int fd, short ev, int ms) {
+    pollfd p{fd, ev, 0};
+    return poll(&p, 1, ms) == 1 && (p.revents & ev);
+}
+inline int accept_one(int lfd, int ms) {
+    if (!wait_fd(lfd, POLLIN, ms)) return -1;
+    return accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+}
+inline int connect_to(const std::string &key, int rank, int ms) {
+    sockaddr_un a;
+    socklen_t len;
+    if (!name(key, rank, &a, &len)) return -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const int fd = socket(AF_UNIX, SOCK_SEQPACKET | SOCK_CLOEXEC, 0);
+        if (fd < 0) return -1;
+        if (connect(fd, (sockaddr *)&a, len) == 0) return fd;
+        close(fd);
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms)) return -1;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+}
+// one message: `len` bytes and up to 250 descriptors
+inline bool send_msg(int fd, const void *buf, size_t len, const int *fds, int nfd) {
+    iovec io{const_cast<void *>(buf), len};
+    msghdr m{};
+    m.msg_iov = &io;
+    m.msg_iovlen = 1;
+    std::vector<char> ctl;
+    if (nfd > 0) {
+        ctl.assign(CMSG_SPACE(sizeof(int) * (size_t)nfd), 0);
+        m.msg_control = ctl.data();
+        m.msg_controllen = ctl.size();
+        cmsghdr *c = CMSG_FIRSTHDR(&m);
+        c->cmsg_level = SOL_SOCKET;
+        c->cmsg_type = SCM_RIGHTS;
+        c->cmsg_len = CMSG_LEN(sizeof(int) * (size_t)nfd);
+        std::memcpy(CMSG_DATA(c), fds, sizeof(int) * (size_t)nfd);
+    }
+    return sendmsg(fd, &m, MSG_NOSIGNAL) == (ssize_t)len;
+}
+inline ssize_t recv_msg(int fd, void *buf, size_t len, int *fds, int maxfd, int *nfd, int ms) {
+    *nfd = 0;
+    if (!wait_fd(fd, POLLIN, ms)) return -1;
+    iovec io{buf, len};
+    msghdr m{};
+    m.msg_iov = &io;
+    m.msg_iovlen = 1;
+    std::vector<char> ctl(CMSG_SPACE(sizeof(int) * (size_t)std::max(maxfd, 1)), 0);
+    m.msg_control = ctl.data();
+    m.msg_controllen = ctl.size();
+    const ssize_t n = recvmsg(fd, &m, MSG_CMSG_CLOEXEC);
+    if (n < 0) return n;
+    for (cmsghdr *c = CMSG_FIRSTHDR(&m); c; c = CMSG_NXTHDR(&m, c))
+        if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS) {
+            const int k = (int)((c->cmsg_len - CMSG_LEN(0)) / sizeof(int));
+            for (int i = 0; i < k; ++i) {
+                int f;
+                std::memcpy(&f, CMSG_DATA(c) + sizeof(int) * (size_t)i, sizeof f);
+                if (*nfd < maxfd) fds[(*nfd)++] = f;
+                else close(f);
+            }
+        }
+    return n;
+}
+}  // namespace uds
+
+// hipMemImportFromShareableHandle takes a pointer to the descriptor on the HIP 7.0
+// runtime PyTorch's wheel brings (the descriptor itself crashes it) and the
+// descriptor itself on ROCm 7.2 (a pointer is refused there): profiles/r05_ipc_probe.txt
+inline hipError_t import_fd(hipMemGenericAllocationHandle_t *hd, int fd) {
+    static const int ver = [] {
+        int v = 0;
+        return hipRuntimeGetVersion(&v) == hipSuccess ? v : 0;
+    }();
+    int f = fd;
+    if (ver > 0 && ver < 70100000) return hipMemImportFromShareableHandle(hd, &f, hipMemHandleTypePosixFileDescriptor);
+    hipError_t e = hipMemImportFromShareableHandle(hd, (void *)(intptr_t)fd, hipMemHandleTypePosixFileDescriptor);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        e = hipMemImportFromShareableHandle(hd, &f, hipMemHandleTypePosixFileDescriptor);
+    }
+    return e;
+}
+
 class Transport {
   public:
     virtual ~Transport() {}
@@ -69,7 +194,17 @@ class Transport {
     // device allocation (hipMalloc base), mapped into this process -- peers[r] for
     // rank r, this rank's own base at peers[rank()]; unmapped with the transport
     virtual int share(void *base, void **peers, std::string *err) = 0;
+    // page_refs mode, ranks that are processes: every rank's allocation made of VMM
+    // `chunks` (exportable as POSIX descriptors) from `base`, mapped into this
+    // process for `device` (peers[rank()] = base).  The descriptors go over Unix
+    // sockets one rank at a time (a rendezvous between turns); every rank takes
+    // every turn whatever its own imports did.
+    virtual int share_vm(const std::vector<VmChunk> &chunks, void *base, int device, void **peers,
+                         std::string *err) {
+        return share_vm_uds(chunks, base, device, peers, err);
+    }
     void unshare() { close_handles(); }
+    std::string group_key;          // hex of the group key / unique id: names the ranks' sockets
     // ranks are threads of one process (their handles are closed one after another)
     virtual bool in_process() const { return false; }
 
@@ -112,9 +247,163 @@ class Transport {
         }
         return rc;
     }
+    struct VmImport {
+        char *base;
+        size_t bytes;
+        std::vector<hipMemGenericAllocationHandle_t> hds;
+    };
+    std::vector<VmImport> vm_opened_;     // peers' chunks mapped here
+    int lfd_ = -1;                       // this rank's listening socket (share_vm_uds)
     void close_handles() {
-        for (void *q : opened_) hipIpcCloseMemHandle(q);
+        for (void *q : opened_) (void)hipIpcCloseMemHandle(q);
         opened_.clear();
+        for (auto &v : vm_opened_) {
+            if (v.base) {
+                (void)hipMemUnmap(v.base, v.bytes);
+                (void)hipMemAddressFree(v.base, v.bytes);
+            }
+            for (auto hd : v.hds) (void)hipMemRelease(hd);
+        }
+        vm_opened_.clear();
+    }
+    void close_listener() {
+        if (lfd_ >= 0) close(lfd_);
+        lfd_ = -1;
+    }
+    // the peer's chunks (descriptors, sizes) mapped back to back into a fresh range
+    int map_peer(const std::vector<int> &fds, const std::vector<uint64_t> &sizes, int device, void **out) {
+        VmImport v{nullptr, 0, {}};
+        for (uint64_t b : sizes) v.bytes += b;
+        bool ok = fds.size() == sizes.size() && v.bytes > 0;
+        for (size_t k = 0; ok && k < fds.size(); ++k) {
+            hipMemGenericAllocationHandle_t hd{};
+            ok = import_fd(&hd, fds[k]) == hipSuccess;
+            if (ok) v.hds.push_back(hd);
+        }
+        void *p = nullptr;
+        ok = ok && hipMemAddressReserve(&p, v.bytes, 0, nullptr, 0) == hipSuccess;
+        if (ok) v.base = (char *)p;
+        size_t off = 0, mapped = 0;
+        for (size_t k = 0; ok && k < v.hds.size(); ++k) {
+            ok = hipMemMap(v.base + off, sizes[k], 0, v.hds[k], 0) == hipSuccess;
+            if (ok) mapped = off + sizes[k];
+            off += sizes[k];
+        }
+        if (ok) {
+            hipMemAccessDesc ad{};
+            ad.location.type = hipMemLocationTypeDevice;
+            ad.location.id = device;
+            ad.flags = hipMemAccessFlagsProtReadWrite;
+            ok = hipMemSetAccess(v.base, v.bytes, &ad, 1) == hipSuccess;
+        }
+        for (int f : fds) close(f);
+        if (!ok) {
+            (void)hipGetLastError();
+            if (v.base) {
+                if (mapped) (void)hipMemUnmap(v.base, mapped);
+                (void)hipMemAddressFree(v.base, v.bytes);
+            }
+            for (auto hd : v.hds) (void)hipMemRelease(hd);
+            return FS2_ERR_COMM;
+        }
+        *out = v.base;
+        vm_opened_.push_back(std::move(v));
+        return FS2_OK;
+    }
+    int share_vm_uds(const std::vector<VmChunk> &chunks, void *base, int device, void **peers, std::string *err) {
+        const int G = world(), me = rank();
+        const int ms = 60000;
+        int rc = FS2_OK;
+        auto note = [&](const char *what) {
+            if (rc == FS2_OK && err) *err = std::string("page_refs (VMM descriptors): ") + what;
+            rc = FS2_ERR_COMM;
+        };
+        // this rank's chunks as descriptors (closed at the end: the peers hold their own)
+        std::vector<int> mine;
+        std::vector<uint64_t> sizes;
+        for (const VmChunk &c : chunks) {
+            int fd = -1;
+            if (hipMemExportToShareableHandle(&fd, c.hd, hipMemHandleTypePosixFileDescriptor, 0) != hipSuccess) {
+                (void)hipGetLastError();
+                note("hipMemExportToShareableHandle failed");
+                break;
+            }
+            mine.push_back(fd);
+            sizes.push_back(c.bytes);
+        }
+        if (lfd_ < 0) lfd_ = uds::listen_on(group_key, me);
+        if (lfd_ < 0) note("listening socket");
+        std::string berr;
+        if (!host_barrier(&berr)) {
+            for (int f : mine) close(f);
+            if (err) *err = berr;
+            return FS2_ERR_COMM;
+        }
+        const bool have = rc == FS2_OK;
+        for (int turn = 0; turn < G; ++turn) {
+            if (turn == me) {
+                peers[me] = base;
+                // serve every other rank: its rank, then the sizes, then the descriptors
+                // (an empty table when this rank has nothing to give: its peers fail)
+                for (int k = 0; k < G - 1; ++k) {
+                    const int c = lfd_ >= 0 ? uds::accept_one(lfd_, ms) : -1;
+                    if (c < 0) {
+                        note("accept");
+                        break;
+                    }
+                    int32_t who = -1;
+                    int nf = 0;
+                    if (uds::recv_msg(c, &who, sizeof who, nullptr, 0, &nf, ms) != (ssize_t)sizeof who) note("peer rank");
+                    std::vector<uint64_t> hdr(1 + sizes.size());
+                    hdr[0] = have ? sizes.size() : 0;
+                    for (size_t i = 0; have && i < sizes.size(); ++i) hdr[1 + i] = sizes[i];
+                    if (!uds::send_msg(c, hdr.data(), sizeof(uint64_t) * (have ? hdr.size() : 1), nullptr, 0))
+                        note("send sizes");
+                    for (size_t i = 0; have && i < mine.size(); i += 200) {
+                        const int n = (int)std::min<size_t>(200, mine.size() - i);
+                        const uint32_t cnt = (uint32_t)n;
+                        if (!uds::send_msg(c, &cnt, sizeof cnt, mine.data() + i, n)) note("send descriptors");
+                    }
+                    close(c);
+                }
+            } else {
+                const int c = uds::connect_to(group_key, turn, ms);
+                bool ok = c >= 0;
+                const int32_t who = me;
+                ok = ok && uds::send_msg(c, &who, sizeof who, nullptr, 0);
+                std::vector<uint64_t> hdr(1 + 65536);
+                int nf = 0;
+                const ssize_t hn = ok ? uds::recv_msg(c, hdr.data(), sizeof(uint64_t) * hdr.size(), nullptr, 0, &nf, ms) : -1;
+                ok = ok && hn >= (ssize_t)sizeof(uint64_t) && hdr[0] > 0 &&
+                     hn == (ssize_t)(sizeof(uint64_t) * (1 + hdr[0]));
+                std::vector<int> fds;
+                std::vector<uint64_t> psz;
+                if (ok) psz.assign(hdr.begin() + 1, hdr.begin() + 1 + (ptrdiff_t)hdr[0]);
+                while (ok && fds.size() < psz.size()) {
+                    uint32_t cnt = 0;
+                    int got[256];
+                    const ssize_t n = uds::recv_msg(c, &cnt, sizeof cnt, got, 256, &nf, ms);
+                    ok = n == (ssize_t)sizeof cnt && (int)cnt == nf;
+                    for (int i = 0; i < nf; ++i) fds.push_back(got[i]);
+                }
+                if (c >= 0) close(c);
+                void *q = nullptr;
+                if (ok && map_peer(fds, psz, device, &q) == FS2_OK) {
+                    peers[turn] = q;
+                } else {
+                    if (!ok)
+                        for (int f : fds) close(f);
+                    note("importing a peer's chunks");
+                }
+            }
+            if (!host_barrier(&berr)) {
+                for (int f : mine) close(f);
+                if (err) *err = berr;
+                return FS2_ERR_COMM;
+            }
+        }
+        for (int f : mine) close(f);
+        return rc;
     }
 };
 
@@ -123,6 +412,19 @@ class Transport {
 inline int nccl_fail(ncclResult_t r, std::string *err, const char *what) {
     if (err) *err = std::string(what) + ": " + ncclGetErrorString(r);
     return FS2_ERR_COMM;
+}
+
+// a digest of the whole group key / unique id in hex (names the ranks' sockets):
+// two FNV-1a passes with different offsets
+inline std::string key_hex(const uint8_t key[128]) {
+    uint64_t a = 0xcbf29ce484222325ull, b = 0x84222325cbf29ce4ull;
+    for (int i = 0; i < 128; ++i) {
+        a = (a ^ key[i]) * 0x100000001b3ull;
+        b = (b ^ key[127 - i]) * 0x100000001b3ull;
+    }
+    char s[40];
+    std::snprintf(s, sizeof s, "%016llx%016llx", (unsigned long long)a, (unsigned long long)b);
+    return std::string(s);
 }
 
 inline int unique_id(uint8_t out[128], std::string *err) {
@@ -145,6 +447,7 @@ class RcclTransport : public Transport {
     }
     ~RcclTransport() override {
         close_handles();
+        close_listener();
         if (comm) ncclCommDestroy(comm);
     }
     // (a rank whose handle or mappings fail still takes part in the exchange; it
@@ -233,6 +536,7 @@ inline int create_rccl(const uint8_t id_bytes[128], int world, int rank, Transpo
     auto *t = new RcclTransport();
     t->G = world;
     t->r = rank;
+    t->group_key = key_hex(id_bytes);
     ncclResult_t e = ncclCommInitRank(&t->comm, world, id, rank);
     if (e != ncclSuccess) {
         t->comm = nullptr;
@@ -326,6 +630,9 @@ class LocalTransport : public Transport {
     }
 
   public:
+    int share_vm(const std::vector<VmChunk> &, void *base, int, void **peers, std::string *err) override {
+        return share(base, peers, err);
+    }
     // ranks are threads of this process: the bases themselves
     int share(void *base, void **peers, std::string *err) override {
         grp->send_ptr[r] = base;
@@ -432,6 +739,7 @@ class ShmTransport : public Transport {
 
     ~ShmTransport() override {
         close_handles();
+        close_listener();
         if (ag_send) hipHostFree(ag_send);
         if (ag_recv) hipHostFree(ag_recv);
         for (char *p : xs) if (p) hipHostFree(p);
@@ -728,6 +1036,7 @@ inline int create_shm(const uint8_t key[128], int world, int rank, Transport **o
     auto *t = new ShmTransport();
     t->G = world;
     t->r = rank;
+    t->group_key = key_hex(key);
     t->seg = seg;
     t->seg_bytes = bytes;
     t->hdr = reinterpret_cast<ShmHeader *>(seg);

@@ -84,7 +84,8 @@ def main(argv):
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), first=rec["firsts"][-1], count=n_local,
              assoc=np.stack(assoc), scal=np.stack(scal), checksum=np.concatenate(cs),
              migrations=prof["migrations"], sent_particles=prof["sent_particles"],
-             sent_bytes=prof["sent_bytes"], scan_allocs=prof["scan_allocs"],
+             sent_bytes=prof["sent_bytes"], scan_allocs=prof["scan_allocs"], page_refs=prof["page_refs"],
+             localized_pages=prof["localized_pages"],
              **{f"win{s}": wv for s, wv in enumerate(wins)}, **{k: np.array(v) for k, v in rec.items()})
     print(f"rank {rank} done in {time.time() - t0:.1f} s", flush=True)
     return 0

@@ -19,7 +19,8 @@ import numpy as np  # noqa: E402
 
 def workload(N, L, seed, mode="peaked", G=1):
     """mode "peaked": peaked likelihoods, so resampling moves particles across
-    shards; "follow": only rank 0's particles carry weight (its first 100 ten
+    shards ("refs": the same with page references, the rank processes' pools
+    mapped into each other as VMM chunks); "follow": only rank 0's particles carry weight (its first 100 ten
     times more), so the first scan (no measurements) resamples and rank 0 keeps
     a higher shard (equal shards follow their sources); "numpy":
     "peaked" through iterate() with numpy's global stream drawn on the device
@@ -56,7 +57,8 @@ def main(argv):
     cap = L + 4 * scans + 8
     h = fast_slam_2.FastSLAM2(N, reduce="parallel", record_assoc=True, seed=5, landmark_capacity=cap, rank=rank,
                               world_size=G, comm_id=key, comm_mode="shm", verbose=False,
-                              rng="numpy" if mode == "numpy" else "device")
+                              rng="numpy" if mode == "numpy" else "device",
+                              page_refs="on" if mode == "refs" else "auto")
     np.random.seed(77)
     a, b = h.first_global, h.first_global + h.n_local
     h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
@@ -108,7 +110,8 @@ def main(argv):
     h.close()
     np.savez(out, first=a, count=b - a, assoc=np.stack(assoc), x=xs, y=ys, yaw=yaws, w=ws, cnt=cnts, lm=lms,
              sent_particles=prof["sent_particles"], sent_rows=prof["sent_rows"], sent_pages=prof["sent_pages"],
-             migrations=prof["migrations"], scan_allocs=prof["scan_allocs"],
+             migrations=prof["migrations"], scan_allocs=prof["scan_allocs"], page_refs=prof["page_refs"],
+             localized_pages=prof["localized_pages"],
              np_key=np.random.get_state()[1], np_pos=np.random.get_state()[2],
              **{k: np.array(v) for k, v in rec.items()})
     return 0

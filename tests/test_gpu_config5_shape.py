@@ -57,13 +57,19 @@ def _progress(msg):
 
 
 @pytest.mark.timeout(900)
-def test_config5_shape_eight_ranks_vs_oracle(tmp_path):
+@pytest.mark.parametrize("page_refs", ["auto", "on"])
+def test_config5_shape_eight_ranks_vs_oracle(tmp_path, page_refs):
+    """page_refs "on": a migrating particle travels as references to pages on the
+    rank that holds them; the rank processes map each other's pools (VMM chunks
+    exported as file descriptors over Unix sockets -- hipIpcOpenMemHandle did not
+    return here in round 4, profiles/r05_ipc_probe.txt) and grow them in place."""
     import fs2_synthetic as syn
     from cfg5_common import CAP, WINDOW, draws, initial_scalars, map_checksum, window_start
     from oracle import oracle as orc
     cap = CAP(L, S)
     key = os.urandom(128).hex()
-    env = dict(os.environ, FS2_SHM_TIMEOUT_S="90", OMP_NUM_THREADS="2", FS2_TRACE="1")
+    env = dict(os.environ, FS2_SHM_TIMEOUT_S="90", OMP_NUM_THREADS="2", FS2_TRACE="1",
+               FS2_CFG5_PAGE_REFS=os.environ.get("FS2_CFG5_PAGE_REFS", page_refs))
     # the ranks' logs under gpurun_out/ on the GPU box (they come back with the call)
     root = os.environ.get("GRAFT_REPO_ROOT")
     logdir = os.path.join(root, "gpurun_out") if root and os.path.isdir(os.path.join(root, "gpurun_out")) \
@@ -159,3 +165,6 @@ def test_config5_shape_eight_ranks_vs_oracle(tmp_path):
     # no buffer reallocated inside a scan (received rows / pages are
     # sized for a whole shard at creation, the transfer arenas for half of one)
     assert all(int(d["scan_allocs"]) == 0 for d in ranks), [int(d["scan_allocs"]) for d in ranks]
+    if env["FS2_CFG5_PAGE_REFS"] == "on":     # in effect on every rank, remote pages localised
+        assert all(int(d["page_refs"]) == 1 for d in ranks), [int(d["page_refs"]) for d in ranks]
+        assert sum(int(d["localized_pages"]) for d in ranks) > 0

@@ -15,7 +15,9 @@ the end every particle's state within 1e-9; reduce_ambiguous is 0 on every rank
 and scan (no decision the shard order could flip), at least two resamples move
 particles across shards.  The "numpy" case runs the drop-in iterate() with
 numpy's global stream drawn on the device (fs2_mt_draw) on every rank, shards
-that move included, and checks numpy's final state too.
+that move included, and checks numpy's final state too.  The "refs" case sends
+page references instead of pages: every rank maps the other processes' pools (VMM
+chunks exported as file descriptors over Unix sockets, fs2_comm.hpp share_vm).
 """
 import os
 import subprocess
@@ -30,7 +32,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.mark.parametrize("G,N,L,scans,mode", [(2, 6000, 40, 8, "peaked"), (3, 10007, 30, 8, "peaked"),
-                                               (2, 6000, 24, 4, "follow"), (2, 6000, 40, 8, "numpy")])
+                                               (2, 6000, 24, 4, "follow"), (2, 6000, 40, 8, "numpy"),
+                                               (3, 9000, 40, 8, "refs")])
 def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     import torch  # noqa: F401
     import fast_slam_2
@@ -103,6 +106,9 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     # siblings share pages once particles have resampled ancestors ("follow" moves
     # each particle's own initial map once: nothing shared yet)
     assert pages < rows if mode == "peaked" else pages <= rows
+    if mode == "refs":       # page references between processes (VMM chunks over Unix sockets)
+        assert all(int(d["page_refs"]) == 1 for d in ranks), [int(d["page_refs"]) for d in ranks]
+        assert sum(int(d["localized_pages"]) for d in ranks) > 0
     if mode != "follow":     #  no buffer was reallocated inside a scan
         # ("follow" hands a whole shard over at once, beyond the half shard the
         # transfer arenas are sized for at creation)
