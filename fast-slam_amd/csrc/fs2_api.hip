@@ -538,6 +538,7 @@ struct fs2_handle {
     bool room_check = false;               // page_refs: agree on pool room at the next scan (after a resample)
     bool refs_shared = false;              // pools mapped by the peers: they never move (no growth)
     bool vm_share = false;                 // page_refs between processes: pool chunks exportable (share_vm)
+    uint32_t loc_epoch = 0;                // k_localize passes so far (its table's key epoch)
     bool refs_live = false;                // a resample has exchanged references (no local collection)
     uint64_t grows = 0;                    // collective pool growths
     uint64_t vm_fallbacks = 0;             // growths that left the reserved range (allocate and copy)
@@ -2296,6 +2297,13 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
             lp.rfreel = h->rfreel;
             lp.rtail = h->rnfree;
             lp.stats = h->stats_dev;
+            // one copy per distinct remote page: the page-dedup table the page
+            // transfer would use (sized for every row of the shard, xfer_bufs), keys
+            // tagged with this pass's epoch so it is never cleared
+            lp.key = h->xt_key;
+            lp.val = h->xt_uidx;
+            lp.cap = h->xt_cap;
+            lp.epoch = ++h->loc_epoch;
             HIP_TRY(h, launch_localize(lp, s));
         }
         // a shard without particles launches nothing: its profiled intervals are
@@ -2583,7 +2591,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         h->nfree -= (int64_t)st.loc_pages;
         h->rnfree -= (int64_t)st.loc_recs;
         h->remote_rows = st.resampled ? (int64_t)st.remote_rows
-                                      : std::max<int64_t>(0, h->remote_rows - (int64_t)st.loc_pages);
+                                      : std::max<int64_t>(0, h->remote_rows - (int64_t)st.loc_rows);
         h->collect_next = st.collect_next;
         if (h->profiling) {
             h->prof.localized_pages += st.loc_pages;

@@ -102,6 +102,7 @@ struct DevStats {
     unsigned long long loc_pages;    // page_refs: remote pages localised (free-list tail consumed)
     unsigned long long loc_recs;     //            records taken for them
     unsigned long long remote_rows;  //            a resample's outputs: row entries naming remote pages
+    unsigned long long loc_rows;     //            row entries k_localize pointed at a local copy
 };
 
 // numpy's np.sum over 8192-element buffers (fs2_exact.hip).  The recursion over a
@@ -606,6 +607,13 @@ struct LocalizeParams {
     int64_t pcap, rcap;      // pages / records the tails may give (past them: error_flags bit 3, the
                              // pass's update kernels exit at once, the scan fails)
     DevStats *stats;
+    // one local copy per distinct remote page (round 5): open addressing over the
+    // tagged page id, keys epoch << 32 | tagged id (a slot of an older epoch is
+    // free, so the table is never cleared), the copy's page id alongside
+    unsigned long long *key;
+    uint32_t *val;
+    int64_t cap;             // power of two, >= twice the row entries a pass may localise
+    uint32_t epoch;          // this pass's (>= 1)
 };
 hipError_t launch_localize(const LocalizeParams &p, hipStream_t s);
 // estimate: also this rank's post-resample record (k_estimate); one GPU leaves

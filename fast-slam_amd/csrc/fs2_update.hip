@@ -830,12 +830,18 @@ hipError_t launch_update(const UpdateParams &p, hipStream_t s, hipEvent_t e0, hi
 // entry naming another rank's page that the pass could read -- its box inside
 // some measurement's band (the pages k_candidates opens and, a fortiori, those
 // k_update's overflow scan opens: page_reject never keeps a page the bands
-// reject) or the partly filled last row (an append writes there) -- is copied
-// into this rank's pools: the 8 mirrors, each live slot's record into a fresh
-// record (its mirror renamed), the page owned by the particle (its own copy).
+// reject) or the partly filled last row (an append writes there) -- is pointed at
+// a copy of that page in this rank's pools.  One copy per distinct remote page
+// and pass (round 5; round 4 copied it once per row entry, so siblings sharing a
+// remote page each copied it with its records: 1.3 GB per scan at G = 8):
+//   phase 0  every wanted entry inserts its tagged page id into the table; the
+//            lane that claims a key copies the page -- the 8 mirrors, each live
+//            slot's record into a fresh record (its mirror renamed) -- into pages
+//            and records from the free lists' tails (one atomic per workgroup);
+//   phase 1  every wanted entry looks its key up and names the copy, shared
+//            (not owned: the first write copies it, as after a resample).
 // Rows the workgroup row boxes reject are skipped like k_candidates skips them.
-// Pages and records come from the free lists' tails, one atomic per workgroup.
-template <int MAXM>
+template <int MAXM, int PHASE>
 __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
     __shared__ Band s_band[MAXM];
     __shared__ uint16_t s_rows[kBBoxRows];
@@ -879,25 +885,78 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
     }
     const int arow = (c % kPageSlots) ? c / kPageSlots : -1;     // an append may write this row
     auto row_at = [&](int q) -> int { return use_bb ? (int)s_rows[q] : q; };
-    // the row entries of this lane to localise: the open rows' remote pages, then
-    // the append row when it is remote and not among them
     auto wanted = [&](int r, const Desc &d) -> bool {
         return r * kPageSlots < c && ref_tag(d.x) != 0u && (box_open_mask<MAXM>(d.y, bc, P.m) != 0u || r == arow);
     };
-    int need = 0;
-    bool arow_seen = false;
-    if (live) {
+    // every wanted entry of this lane: the open rows' remote pages, then the append
+    // row when it is remote and not among them
+    auto for_wanted = [&](auto &&fn) {
+        if (!live) return;
+        bool arow_seen = false;
         for (int q = 0; q < nrows; ++q) {
             const int r = row_at(q);
             if (r * kPageSlots >= c) continue;
             const Desc d = *pt_entry(map, r, i);
             if (wanted(r, d)) {
-                ++need;
+                fn(r, d);
                 arow_seen |= r == arow;
             }
         }
-        if (arow >= 0 && !arow_seen && ref_tag(pt_entry(map, arow, i)->x) != 0u) ++need;
+        if (arow >= 0 && !arow_seen) {
+            const Desc d = *pt_entry(map, arow, i);
+            if (ref_tag(d.x) != 0u) fn(arow, d);
+        }
+    };
+    const unsigned long long ep = (unsigned long long)P.epoch << 32;
+    const uint64_t mask = (uint64_t)P.cap - 1u;
+    auto slot0 = [&](uint32_t x) -> uint64_t { return ((uint64_t)x * 0x9E3779B97F4A7C15ull >> 20) & mask; };
+    if (PHASE == 1) {
+        // every wanted entry names its page's copy (claimed and filled by phase 0)
+        unsigned long long rows = 0;
+        for_wanted([&](int r, const Desc &d) {
+            const unsigned long long want = ep | d.x;
+            uint64_t s = slot0(d.x);
+            for (int64_t probe = 0; probe < P.cap; ++probe, s = (s + 1) & mask)
+                if (P.key[s] == want) {
+                    const uint32_t id = P.val[s];
+                    if (!(id & 0x80000000u)) {        // (0xffffffff: the copy failed, left remote)
+                        *pt_entry(map, r, i) = make_uint2(id, d.y);
+                        ++rows;
+                    }
+                    break;
+                }
+        });
+        unsigned long long tot = rows;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if ((tid & 63) == 0 && tot) atomicAdd(&P.stats->loc_rows, tot);
+        return;
     }
+    // phase 0: claim the keys (the claimer's particle index, high bit set, in val:
+    // a lane claims a key at most once -- its rows name distinct pages), count them
+    const uint32_t marker = 0x80000000u | (uint32_t)i;
+    auto find = [&](uint32_t x, bool claim) -> int64_t {     // slot of key x (claim: insert it)
+        const unsigned long long want = ep | x;
+        uint64_t s = slot0(x);
+        for (int64_t probe = 0; probe < P.cap;) {
+            const unsigned long long cur = __atomic_load_n(&P.key[s], __ATOMIC_RELAXED);
+            if (cur == want) return (int64_t)s;
+            if (claim && (cur >> 32) != P.epoch) {             // a slot of an older pass: free
+                if (atomicCAS(&P.key[s], cur, want) == cur) {
+                    P.val[s] = marker;
+                    return -2 - (int64_t)s;                    // claimed by this lane
+                }
+                continue;                                      // taken meanwhile: look again
+            }
+            s = (s + 1) & mask;
+            ++probe;
+        }
+        return -1;
+    };
+    int need = 0;
+    for_wanted([&](int, const Desc &d) {
+        if (find(d.x, true) <= -2) ++need;
+    });
     // this workgroup's pages: one atomic, then each lane's run
     const int wid = tid >> 6, lane = tid & 63;
     int incl = need;
@@ -927,13 +986,22 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
         }
     }
     __syncthreads();
-    if (!need || s_base == ~0ull) return;
+    if (!need) return;
+    const bool failed = s_base == ~0ull;
     int64_t k = (int64_t)s_base + woff + incl - need;            // this lane's first localised page
-    auto localize = [&](int r, Desc d) {
-        const uint32_t t = ref_tag(d.x);
-        const float4 *src = reinterpret_cast<const float4 *>(map.peers->pool[t - 1] + (int64_t)ref_id(d.x) * kPageBytes);
-        const char *srecs = map.peers->recs[t - 1];
+    for_wanted([&](int r, const Desc &d) {
+        const int64_t slot = find(d.x, false);
+        if (slot < 0 || P.val[slot] != marker) return;          // another lane's copy
+        if (failed) {                                            // (phase 1 leaves the entry remote)
+            P.val[slot] = 0xffffffffu;
+            return;
+        }
+        const uint32_t tg = ref_tag(d.x);
+        const float4 *src = reinterpret_cast<const float4 *>(map.peers->pool[tg - 1] + (int64_t)ref_id(d.x) * kPageBytes);
+        const char *srecs = map.peers->recs[tg - 1];
         const uint32_t id = P.freel[P.ftail - 1 - k];
+        // every row naming a page holds the same slots of it (sharers of a page have
+        // the same map length up to its row: an append to a shared page copies it)
         const int valid = min(kPageSlots, c - r * kPageSlots);
         float4 mv[kPageSlots];
 #pragma unroll
@@ -956,24 +1024,15 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
             }
             dst[u] = mv[u];
         }
-        *pt_entry(map, r, i) = make_uint2(id | kOwned, d.y);
+        P.val[slot] = id;
         ++k;
-    };
-    for (int q = 0; q < nrows; ++q) {
-        const int r = row_at(q);
-        if (r * kPageSlots >= c) continue;
-        const Desc d = *pt_entry(map, r, i);
-        if (wanted(r, d)) localize(r, d);
-    }
-    if (arow >= 0 && !arow_seen) {
-        const Desc d = *pt_entry(map, arow, i);
-        if (ref_tag(d.x) != 0u) localize(arow, d);
-    }
+    });
 }
 
 hipError_t launch_localize(const LocalizeParams &p, hipStream_t s) {
     if (p.nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_localize<kMaxM>, dim3((unsigned)p.nblk), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((k_localize<kMaxM, 0>), dim3((unsigned)p.nblk), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((k_localize<kMaxM, 1>), dim3((unsigned)p.nblk), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 
