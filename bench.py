@@ -78,6 +78,10 @@ def parse(argv=None):
     ap.add_argument("--probe-side-kernels", type=int, default=0,
                     help="A/B (config 4 interference): launch this many tiny kernels on a second stream "
                          "before each scan, as the ICP hand-off does")
+    ap.add_argument("--sync", action="store_true",
+                    help="time the headline with step() (submit + wait per scan) instead of two scans in "
+                         "flight (step_submit / step_wait: the next scan's candidate pass beside this "
+                         "scan's tail, fs2.h fs2_iterate_submit)")
     ap.add_argument("--dropin", action="store_true",
                     help="time the drop-in FastSLAM2.iterate() (numpy RNG) beside the device-RNG step")
     return ap.parse_args(argv)
@@ -597,6 +601,7 @@ def main(argv=None):
                        "gate_filter": not args.no_gate_filter, "reduce": "exact" if N > 4096 and world == 1
                        else ("parallel" if world > 1 else "sequential"),
                        "parallelism": f"particle-shard{world}",
+                       "scans_in_flight": 2 if R["pipelined"] else 1,
                        "transport": args.comm if world > 1 else None,
                        "ranks_share_gpu": bool(args.share_gpu and world > 1)},
             "roofline": K["roofline"],
@@ -631,6 +636,20 @@ def main(argv=None):
         if extras and not cfg["icp"]:
             out["extra"]["robustness"] = robustness(args, f, L, args.warmup + args.steps)
         f.close()
+        if extras and R["pipelined"]:
+            # the same workload one scan at a time (step(): submit + wait), fresh handle
+            import copy
+            a2 = copy.copy(args)
+            a2.sync = True
+            R2 = run_config(a2, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, args.steps, args.warmup)
+            p2 = R2["prof"]
+            out["extra"]["sync_step"] = {
+                "value": N * args.steps / R2["dt"], "ms_per_step": R2["dt"] / args.steps * 1e3,
+                "reduce_and_resample_ms": p2["reduce_ms"] / max(p2["scans"], 1),
+                "resamples": R2["sums"]["resamples"],
+                "note": "step() per scan: the next scan is submitted after this one's statistics "
+                        "are back, so its candidate pass cannot run beside this scan's tail"}
+            R2["handle"].close()
         if extras and args.config == "3" and not (args.particles or args.landmarks):
             # the other single-GPU BASELINE configs, each on a fresh handle
             out["extra"]["configs"] = {k: config_line(args, k, world, rank, dev, barrier) for k in ("2", "4")}
@@ -729,12 +748,7 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
         f.set_profiling(True, every=args.profile_every)
     sums = dict(resamples=0, visited=0, copied_slots=0, cow=0, exact=0, opened=0, ref_visits=0, hits_appends=0)
     step_ms = []                 # (host ms, resampled) of each timed scan on this rank
-    barrier()
-    t0 = time.perf_counter()
-    for s in range(warmup, total_scans):
-        t1 = time.perf_counter()
-        _, st = one_scan(s)
-        step_ms.append(((time.perf_counter() - t1) * 1e3, st.resampled))
+    def account(st):
         sums["resamples"] += st.resampled
         sums["visited"] += st.slots_visited
         sums["copied_slots"] += st.resample_slots
@@ -743,6 +757,31 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
         sums["opened"] += st.pages_opened
         sums["ref_visits"] += st.reference_visits
         sums["hits_appends"] += st.hits + st.appends
+
+    # two scans in flight (one GPU, no ICP hand-off): scan s+1 is submitted before
+    # scan s is waited for, so its candidate pass runs beside scan s's tail
+    # (fs2_iterate_submit); the results are the same bits as step()'s
+    pipelined = scans_pts is None and world == 1 and not args.sync
+    barrier()
+    t0 = time.perf_counter()
+    if pipelined:
+        t1 = t0
+        for s in range(warmup, total_scans):
+            f.step_submit(*syn.odometry(s), meas[s])
+            if s > warmup:
+                _, st = f.step_wait()
+                step_ms.append(((time.perf_counter() - t1) * 1e3, st.resampled))
+                t1 = time.perf_counter()
+                account(st)
+        _, st = f.step_wait()
+        step_ms.append(((time.perf_counter() - t1) * 1e3, st.resampled))
+        account(st)
+    else:
+        for s in range(warmup, total_scans):
+            t1 = time.perf_counter()
+            _, st = one_scan(s)
+            step_ms.append(((time.perf_counter() - t1) * 1e3, st.resampled))
+            account(st)
     barrier()
     dt = time.perf_counter() - t0
     prof = f.profile()
@@ -761,7 +800,7 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
                      "step_submit and step_wait; before_scan: alignment work ahead of a scan's submission"}
             if scans_pts is not None else None)
     return {"handle": f, "dt": dt, "prof": prof, "st": st, "coll0": coll0, "sums": sums, "step_ms": step_ms,
-            "icp_us": icp_us, "icp_host": host}
+            "icp_us": icp_us, "icp_host": host, "pipelined": pipelined}
 
 
 # Algorithmic byte model of the two update kernels (include/fs2.h
@@ -844,7 +883,7 @@ def config_line(args, key, world, rank, dev, barrier, steps=20, warmup=3):
             "reduce_and_resample_ms": R["prof"]["reduce_ms"] / max(R["prof"]["scans"], 1),
             "resamples": sums["resamples"], "pages_opened_per_particle_scan": sums["opened"] / units,
             "cow_pages_per_particle_scan": sums["cow"] / units, "icp_us": R["icp_us"],
-            "icp_host_ms_per_scan": R["icp_host"]}
+            "icp_host_ms_per_scan": R["icp_host"], "scans_in_flight": 2 if R["pipelined"] else 1}
 
 if __name__ == "__main__":
     main()

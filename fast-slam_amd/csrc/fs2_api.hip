@@ -487,6 +487,39 @@ struct fs2_handle {
         int32_t m = 0;
         uint64_t fixed_bytes = 0;
     } pending;
+    // Pipelined submit (fs2.h fs2_iterate_submit): scan s+1 submitted while scan s is
+    // outstanding.  Its candidate pass runs beside s's tail on spec_stream (reading
+    // the buffer set current at that moment, BufSet / gen), a fix-up pass after the
+    // tail reruns the workgroups whose set changed (a resample), its exact update
+    // follows on the main stream; its own tail is enqueued when s is waited for
+    // (the host then knows s's decision, i.e. which set is current).
+    struct TailCtx {
+        int32_t M = 0;
+        int passes = 0;
+        uint64_t fixed_bytes = 0;
+        bool prof = false;
+        int evset = 0;
+        int32_t want_collect = 0;
+        bool has_u0 = false;
+        int par = 0;                       // parity of the scan's per-scan buffers (cpart, pins)
+    };
+    struct {
+        bool on = false;                   // a scan whose update pass is enqueued, its tail not yet
+        TailCtx t;
+    } next;
+    struct {                               // a scan completed early (a submit had to wait for it)
+        bool on = false;
+        int rc = FS2_OK;
+        double pose[3] = {};
+        fs2_iter_stats st{};
+    } stash;
+    hipStream_t spec_stream = nullptr;
+    hipEvent_t ev_upd = nullptr, ev_spec = nullptr;   // end of the last update pass / speculative pass
+    uint32_t *gen_dev = nullptr;           // the current set is (gen & 1) == cur (one GPU)
+    BufSet *sets_dev = nullptr;            // [2]
+    uint32_t *spec_gen = nullptr;          // [nblocks]
+    uint64_t submitted = 0;                // scans submitted (parity)
+    uint64_t overlapped = 0;               // scans whose candidate pass ran beside the previous tail
     int32_t cnt_upper = 0;
     double gate2 = 64.0;
     std::string err;
@@ -553,6 +586,10 @@ struct fs2_handle {
     PeerMaps *peers_dev = nullptr;
     uint8_t *ep_dev = nullptr, *epochs_dev = nullptr;     // this rank's / every rank's collection epoch
     int64_t remote_rows = 0;               // upper bound on row entries naming remote pages (localisations)
+    int64_t remote_pages = INT64_MAX;      // distinct remote pages the rows named after the last resample
+    // what the update passes may still localise per scan: at most one copy per
+    // distinct remote page and pass (k_localize), never more than the remote rows
+    int64_t remote_bound() const { return std::min(remote_rows, remote_pages); }
     int32_t collect_next = 0;              // before the next scan: bit 0 a collective collection, bits 1 / 2
                                            // every rank grows its page / record pool (published)
     ChainSummary *dch_send = nullptr, *dch_recv = nullptr;
@@ -674,6 +711,17 @@ static int xfer_bufs(fs2_handle *h) {
     return rc ? rc : recv_bufs(h, sizeof(Desc) * (size_t)S);
 }
 
+// The two buffer sets on the device (BufSet, pipelined submit): at creation and
+// whenever the page tables are reallocated (the stream is drained then).
+static int sync_sets(fs2_handle *h) {
+    if (!h->sets_dev) return FS2_OK;
+    BufSet b[2];
+    for (int k = 0; k < 2; ++k)
+        b[k] = BufSet{h->x[k], h->y[k], h->yaw[k], h->w[k], h->cnt[k], h->pt[k], h->row_boxes(k)};
+    HIP_TRY(h, copy_sync(h, h->sets_dev, b, sizeof b, hipMemcpyHostToDevice));
+    return FS2_OK;
+}
+
 static int grow_rows(fs2_handle *h, int need_slots) {
     if (need_slots <= h->cap) return FS2_OK;
     if (need_slots > h->max_cap)
@@ -697,6 +745,7 @@ static int grow_rows(fs2_handle *h, int need_slots) {
     }
     h->rows = rows;
     h->cap = rows * kPageSlots;
+    if (int rc = sync_sets(h)) return rc;
     // (sharded: the resample's row buffers follow, here where the stream is drained
     // anyway, not inside a later resample)
     if (h->rdesc) return xfer_bufs(h);
@@ -1601,6 +1650,7 @@ const char *fs2_last_error(const fs2_handle *h) {
 static void free_handle(fs2_handle *h) {
     if (!h) return;
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->spec_stream) hipStreamSynchronize(h->spec_stream);
     // In-place pools (VMM chunks): nothing of this process may still be in flight
     // when they are unmapped and released, or the runtime defers the release and the
     // next handle's first growth (hipMemCreate) waits for it -- 4 s in the round-4
@@ -1655,6 +1705,13 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->uop); hipFree(h->np_tail_g);
     hipFree(h->peers_dev); hipFree(h->ep_dev); hipFree(h->epochs_dev);
     hipFree(h->part_pose);
+    if (h->spec_stream) {
+        hipStreamSynchronize(h->spec_stream);
+        hipStreamDestroy(h->spec_stream);
+    }
+    if (h->ev_upd) hipEventDestroy(h->ev_upd);
+    if (h->ev_spec) hipEventDestroy(h->ev_spec);
+    hipFree(h->spec_gen); hipFree(h->gen_dev); hipFree(h->sets_dev);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -1730,6 +1787,16 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     if (hipSetDevice(cfg->device) != hipSuccess) return fail(set_err(&h->err, FS2_ERR_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
+    {
+        // the speculative candidate pass of a pipelined submit: its own stream at the
+        // lowest priority, so the previous scan's tail (latency chains) goes first
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (hipStreamCreateWithPriority(&h->spec_stream, hipStreamNonBlocking, least) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_upd, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_spec, hipEventDisableTiming) != hipSuccess)
+            return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
+    }
     const int64_t n = std::max<int64_t>(h->n, 1);
     const int64_t nb = (n + kBlock - 1) / kBlock;
     const int64_t nsb = (n + 1023) / 1024;
@@ -1769,7 +1836,10 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->cpart, nb * 8 * kNumCounters) == hipSuccess;
+    ok &= alloc((void **)&h->cpart, 2 * nb * 8 * kNumCounters) == hipSuccess;   // [2]: by scan parity
+    ok &= alloc((void **)&h->spec_gen, nb * 4) == hipSuccess;
+    ok &= alloc((void **)&h->gen_dev, 4) == hipSuccess;
+    ok &= alloc((void **)&h->sets_dev, 2 * sizeof(BufSet)) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_pose, nb * 24) == hipSuccess;
@@ -1826,10 +1896,12 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         if (ok)
             h->pub_flag_dev = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(h->pub_stats_dev) + off);
     }
-    ok &= hipHostMalloc((void **)&h->noise_pin, n * 8, 0) == hipSuccess;
-    ok &= hipHostMalloc((void **)&h->u0_pin, 8, 0) == hipSuccess;
+    ok &= hipHostMalloc((void **)&h->noise_pin, 2 * n * 8, 0) == hipSuccess;   // [2]: by scan parity
+    ok &= hipHostMalloc((void **)&h->u0_pin, 2 * 8, 0) == hipSuccess;
     if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
-    if (hipMemsetAsync(h->cpart, 0, nb * 8 * kNumCounters, h->stream) != hipSuccess ||
+    if (hipMemsetAsync(h->cpart, 0, 2 * nb * 8 * kNumCounters, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->gen_dev, 0, 4, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->spec_gen, 0xff, nb * 4, h->stream) != hipSuccess ||
         hipMemsetD32Async((hipDeviceptr_t)h->slb, 0x7f7fffff, 1, h->stream) != hipSuccess)   // FLT_MAX: no mirror yet
         return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     // Particle.__init__: (0, 0, 0), weight 1/NUM_PARTICLES, empty map (particle.py:11-20)
@@ -2070,262 +2142,22 @@ static int wait_flag(fs2_handle *h, unsigned long long seq) {
     return FS2_OK;
 }
 
-static int mt_finish(fs2_handle *h);
-
-int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
-                       const double *observed, int32_t M, const double *noise, const double *u0) {
-    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
-    if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan has not been waited for");
-    if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
-    // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise /
-    // u0; a draw is consumed by this call whatever happens below
-    const bool drawn = h->mt.armed || h->mt.deferred;
-    h->mt.armed = false;
-    HIP_TRY(h, hipSetDevice(h->cfg.device));
-    // a deferred draw ends between k_candidates and k_update below, or on the way out
-    // (its outputs are written whatever this call returns)
-    struct DrawEnd {
-        fs2_handle *h;
-        ~DrawEnd() {
-            if (h->mt.deferred) {
-                mt_finish(h);
-                h->mt.armed = false;
-            }
-        }
-    } draw_end{h};
-    if (drawn && (noise || u0))
-        return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
-    int rc;
-    if (h->refs && !h->refs_shared) {
-        rc = share_pools(h, true);
-        if (rc) return rc;
-    }
-    bool collected = false;
-    if (h->refs_shared && h->collect_next) {
-        // page_refs: some rank's pools ran short in the last scan (every rank read the
-        // same records, so every rank collects -- and grows -- here, together)
-        if (h->collect_next & 6) {
-            rc = regrow_collective(h, (h->collect_next & 2) ? 1 : 0, (h->collect_next & 4) ? 1 : 0);
-            if (rc) return rc;
-        }
-        rc = collect_collective(h);
-        if (rc) return rc;
-        h->collect_next = 0;
-        collected = true;
-    }
-    if (h->refs_shared && h->room_check) {
-        // after a resample (every rank knows it resampled) the remote rows this scan
-        // may localise are new: the ranks agree, before any localisation, whether
-        // some rank lacks room for them and this scan's reservations -- then every
-        // rank collects, and grows what is still short, together
-        h->room_check = false;
-        const int64_t Mx = std::max<int64_t>(M, 1);
-        auto short_bits = [&]() -> uint8_t {
-            const int64_t pneed = Mx * h->n + h->remote_rows;
-            const int64_t rneed = Mx * h->n + (int64_t)kPageSlots * h->remote_rows;
-            return (uint8_t)((h->nfree - h->cursor < 2 * pneed ? 1 : 0) | (h->rnfree - h->rcursor < 2 * rneed ? 2 : 0));
-        };
-        auto any_short = [&](uint8_t mine, uint8_t *all_or) -> int {
-            uint8_t all[kMaxRanks] = {};
-            HIP_TRY(h, hipMemsetAsync(h->ep_dev, mine, 1, h->stream));
-            {
-                CommTimer ct(h);
-                const int rc2 = h->tp->allgather(h->ep_dev, h->epochs_dev, 1, h->stream, &h->err);
-                if (rc2) return rc2;
-            }
-            HIP_TRY(h, hipMemcpyAsync(all, h->epochs_dev, (size_t)h->cfg.world_size, hipMemcpyDeviceToHost, h->stream));
-            HIP_TRY(h, hipStreamSynchronize(h->stream));
-            if (int rc2 = h->tp->status(&h->err)) return rc2;
-            *all_or = 0;
-            for (int q = 0; q < h->cfg.world_size; ++q) *all_or |= all[q];
-            return FS2_OK;
-        };
-        uint8_t any = 0;
-        trace(h, "room check remote_rows (K)", (int)(h->remote_rows >> 10));
-        rc = any_short(short_bits(), &any);
-        trace(h, "room short", any);
-        if (rc) return rc;
-        if (any && !collected) {
-            rc = collect_collective(h);
-            if (rc) return rc;
-            collected = true;
-            rc = any_short(short_bits(), &any);
-            if (rc) return rc;
-        }
-        if (any) {
-            const uint8_t mine = short_bits();
-            const int64_t pneed = Mx * h->n + h->remote_rows;
-            const int64_t rneed = Mx * h->n + (int64_t)kPageSlots * h->remote_rows;
-            rc = regrow_collective(h, (mine & 1) ? h->npool - (h->nfree - h->cursor) + 3 * pneed : 0,
-                                   (mine & 2) ? h->nrecs - (h->rnfree - h->rcursor) + 3 * rneed : 0);
-            if (rc) return rc;
-        }
-    }
-    trace(h, "submit", (int)h->scan);
-    rc = grow_rows(h, h->cnt_upper + M);
-    if (rc) return rc;
+// The tail of a scan whose update pass is enqueued: normalise, N_eff, estimate,
+// the resample when the rule fires, the publication (fast_slam_2.py:161-223).  In a
+// plain submit right after the update pass; for the second of two outstanding
+// scans when the first is waited for (h->cur is then the set its update used).
+static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
+    int rc = FS2_OK;
     const int cur = h->cur;
     hipStream_t s = h->stream;
     const int G = h->cfg.world_size;
-    const bool sh = h->tp != nullptr;             // sharded path (G > 1, or forced for testing)
+    const bool sh = h->tp != nullptr;
     const int red = h->reduce();
     const bool seq = red == FS2_REDUCE_SEQUENTIAL && !sh;
     const bool exact = red == FS2_REDUCE_EXACT;
-    // tree sums: |tree - reference| <= (2n + 64) 2^-53 of the value, for the
-    // total and hence for every normalised weight and prefix
     const double flip_margin = (red == FS2_REDUCE_PARALLEL) ? std::ldexp(2.0 * (double)h->n_global + 64.0, -53) : 0.0;
-    const bool prof = h->profiling && (h->prof_tick++ % (uint64_t)h->prof_period) == 0;
-
-    if (noise) {
-        std::memcpy(h->noise_pin, noise, sizeof(double) * h->n);
-        HIP_TRY(h, hipMemcpyAsync(h->noise_dev, h->noise_pin, sizeof(double) * h->n,
-                                  hipMemcpyHostToDevice, s));
-    }
-    if (u0) {
-        *h->u0_pin = *u0;
-        HIP_TRY(h, hipMemcpyAsync(h->u0_dev, h->u0_pin, 8, hipMemcpyHostToDevice, s));
-    }
-    if (h->cfg.record_assoc && (int64_t)M * h->n > h->assoc_cap) {
-        HIP_TRY(h, hipStreamSynchronize(s));
-        hipFree(h->assoc_dev);
-        h->assoc_dev = nullptr;
-        HIP_TRY(h, hipMalloc(&h->assoc_dev, sizeof(int32_t) * (size_t)M * h->n));
-        h->assoc_cap = (int64_t)M * h->n;
-    }
-    // the last scan's k_publish zeroed the stats; anything else (first scan, an
-    // error return) leaves them to be cleared here
-    if (!h->stats_clean) HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
-    h->stats_clean = false;
-    if (prof && h->ev.used == kProfSets) {   // pool used up: fold (the scans are long complete)
-        const int rc0 = fold_profile(h);
-        if (rc0) return rc0;
-    }
-    hipEvent_t *E = h->ev.e[h->ev.used];
-
-    // ---- fused update passes (move in the first) ----
-    UpdateParams up{};
-    up.n = h->n;
-    up.nblk = h->nblocks();
-    up.blk0 = 0;
-    up.blk1 = up.nblk;
-    up.gidx0 = h->first;
-    up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
-    up.map = h->map();
-    up.noise = (noise || drawn) ? h->noise_dev : nullptr;
-    up.seed = h->cfg.seed;
-    up.scan = h->scan;
-    up.sigma = (rotation != 0) ? h->cfg.rotation_noise : h->cfg.translation_noise;
-    up.rotation = rotation;
-    up.translation = translation;
-    up.gate2 = h->gate2;
-    // gate2 / (1 - 2^-18) rounded up: slack for the fp32 rounding in gate_reject_fast
-    up.gate2f = std::isinf(h->gate2) ? INFINITY
-                                     : std::nextafter((float)(h->gate2 / (1.0 - 0x1p-18)), INFINITY);
-    up.filter = h->cfg.gate_filter ? 1 : 0;
-    up.cand = h->cand;
-    up.ncand = h->ncand;
-    std::memcpy(up.R, h->cfg.measurement_noise, sizeof up.R);
-    std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
-    up.assoc = h->cfg.record_assoc ? h->assoc_dev : nullptr;
-    up.wpart = h->wpart;
-    up.cpart = h->cpart;
-    up.stats = h->stats_dev;
-    up.slb_pass = h->slb_pass;
-    // page_refs: this scan may ask for a collective collection before the next one
-    // (its pools' room after this scan's reservations and localisations, at most
-    // the remote row entries, below twice as much again)
-    int32_t want_collect = 0;
-    if (h->refs) {              // (also before references cross: this scan's resample may send them)
-        const int64_t pneed = (int64_t)std::max(M, 1) * h->n + h->remote_rows;
-        const int64_t rneed = (int64_t)std::max(M, 1) * h->n + (int64_t)kPageSlots * h->remote_rows;
-        const bool plow = h->nfree - h->cursor < 3 * pneed, rlow = h->rnfree - h->rcursor < 3 * rneed;
-        want_collect = (plow || rlow) ? 1 : 0;
-        // still short right after a collective collection: every rank grows next scan
-        if (collected && plow) want_collect |= 2;
-        if (collected && rlow) want_collect |= 4;
-    }
-    int passes = 0;
-    uint64_t fixed_bytes = 0;
-    for (int32_t k0 = 0; k0 < std::max(M, 1); k0 += kMaxM) {
-        const int32_t m = std::min(kMaxM, M - k0);
-        up.do_move = (k0 == 0);
-        up.k0 = k0;
-        up.m = std::max(m, 0);
-        up.last_pass = (k0 + kMaxM >= M);
-        for (int k = 0; k < kMaxM; ++k) {
-            if (k < up.m) {
-                const double d = meas[2 * (k0 + k)], b = meas[2 * (k0 + k) + 1];
-                up.meas.d[k] = d;
-                up.meas.b[k] = b;
-                up.meas.ox[k] = observed ? observed[2 * (k0 + k)] : d * std::cos(b);
-                up.meas.oy[k] = observed ? observed[2 * (k0 + k) + 1] : d * std::sin(b);
-            } else {
-                up.meas.d[k] = up.meas.b[k] = up.meas.ox[k] = up.meas.oy[k] = 0.0;
-            }
-            // fp32 observed point for the gate mirror and a bound on its rounding
-            const double ox = up.meas.ox[k], oy = up.meas.oy[k];
-            up.meas.fx[k] = (float)ox;
-            up.meas.fy[k] = (float)oy;
-            const double e = std::max(std::fabs(ox - (double)up.meas.fx[k]),
-                                      std::fabs(oy - (double)up.meas.fy[k]));
-            up.meas.fe[k] = std::isfinite(e) ? std::nextafter((float)e, INFINITY) : INFINITY;
-        }
-        rc = reserve_recs(h, (int64_t)up.m * h->n, &up.alloc);
-        if (rc) return rc;
-        rc = reserve_pages(h, (int64_t)up.m * h->n, &up.alloc);
-        if (rc) return rc;
-        up.map = h->map();
-        const bool first = k0 == 0, last = up.last_pass != 0;
-        const bool cand = up.filter && up.blk1 > up.blk0;
-        if (h->refs_shared && h->remote_rows > 0 && up.blk1 > up.blk0) {
-            // page_refs: the remote pages this pass could read, localised first (from
-            // the free lists' tails, clear of every reservation this scan makes; a
-            // tail too short fails the scan loudly, fs2.h error_flags bit 3)
-            const int64_t left = (int64_t)std::max(M - k0 - up.m, 0) * h->n;   // later passes' reservations
-            LocalizeParams lp{};
-            lp.pcap = h->nfree - h->cursor - left;
-            lp.rcap = h->rnfree - h->rcursor - left;
-            lp.map = up.map;
-            lp.cnt = up.cnt;
-            lp.n = h->n;
-            lp.nblk = up.nblk;
-            lp.m = up.m;
-            lp.gate2f = up.gate2f;
-            lp.meas = up.meas;
-            lp.freel = h->freel;
-            lp.ftail = h->nfree;
-            lp.rfreel = h->rfreel;
-            lp.rtail = h->rnfree;
-            lp.stats = h->stats_dev;
-            // one copy per distinct remote page: the page-dedup table the page
-            // transfer would use (sized for every row of the shard, xfer_bufs), keys
-            // tagged with this pass's epoch so it is never cleared
-            lp.key = h->xt_key;
-            lp.val = h->xt_uidx;
-            lp.cap = h->xt_cap;
-            lp.epoch = ++h->loc_epoch;
-            HIP_TRY(h, launch_localize(lp, s));
-        }
-        // a shard without particles launches nothing: its profiled intervals are
-        // recorded empty here (fold_one reads every event of the set)
-        if (prof && first && up.blk1 <= up.blk0)
-            for (int k : {0, 1, 4}) HIP_TRY(h, hipEventRecord(E[k], s));
-        HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
-        if (first && h->mt.deferred) {     // the draw's host half while k_candidates runs
-            rc = mt_finish(h);
-            if (rc) return rc;
-            h->mt.armed = false;
-        }
-        HIP_TRY(h, launch_update(up, s, (prof && first) ? (cand ? E[4] : E[0]) : nullptr,
-                                 (prof && last) ? E[2] : nullptr));
-        if (prof && last && up.blk1 <= up.blk0) HIP_TRY(h, hipEventRecord(E[2], s));
-        ++passes;
-        // pose/weight/count read + weight/count write; pose write on the move pass
-        fixed_bytes += (uint64_t)h->n * (32 + 4 + 8 + 4 + (up.do_move ? 24 : 0));
-        if (up.do_move && (noise || drawn)) fixed_bytes += (uint64_t)h->n * 8;
-        if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
-    }
-
+    const bool prof = t.prof;
+    hipEvent_t *E = h->ev.e[t.evset];
     // ---- normalise, N_eff, estimate ----
     ReduceParams rp{};
     rp.n = h->n;
@@ -2335,7 +2167,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rp.cnt = h->cnt[cur];
     rp.x = h->x[cur]; rp.y = h->y[cur]; rp.yaw = h->yaw[cur];
     rp.wpart = h->wpart;
-    rp.cpart = h->cpart;
+    rp.cpart = h->cpart + (size_t)t.par * kNumCounters * (size_t)h->nblocks();
     rp.nwpart = (int32_t)h->nblocks();
     rp.part_sq = h->part_sq;
     rp.part_best_w = h->part_best_w;
@@ -2356,7 +2188,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (rp.chunked) rp.nparts = normalize_chunk_parts(h->n);
     rp.part_pose = h->part_pose;
     rp.np_tail = exact ? h->np_tail : nullptr;
-    rp.u0_host = (u0 || drawn) ? h->u0_dev : nullptr;
+    rp.u0_host = t.has_u0 ? h->u0_dev : nullptr;
     rp.seed = h->cfg.seed;
     rp.scan = h->scan;
     rp.stats = h->stats_dev;
@@ -2367,7 +2199,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rp.rec = h->rec;
     rp.recs = sh ? h->recs : h->rec;
     rp.totals = h->totals;
-    rp.want_collect = want_collect;
+    rp.want_collect = t.want_collect;
 
     const int nxt = 1 - cur;
     ResampleParams rs{};
@@ -2402,7 +2234,13 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     rs.flip_margin = flip_margin;
     rs.use_chain = exact ? 1 : 0;
     rs.refs = h->refs ? 1 : 0;
+    if (h->refs && h->xt_key) {
+        rs.tkey = h->xt_key;
+        rs.tcap = h->xt_cap;
+        rs.tepoch = ++h->loc_epoch;
+    }
     rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout};
+    rs.gen = sh ? nullptr : h->gen_dev;      // (one GPU: k_tail_single bumps it on a resample)
 
     // weight total over all ranks (fast_slam_2.py:166).  Exact: Python's sum (in
     // particle order) from the update pass's block sums, the chain's units also
@@ -2411,7 +2249,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (prof && exact && !xsh && h->n <= 0) HIP_TRY(h, hipEventRecord(E[5], s));   // launch_chain records nothing
     if (exact && !xsh) {
         ChainParams cp = h->chain(h->w[cur], h->wpart, nullptr, &h->stats_dev->total, false);
-        cp.cpart = h->cpart;
+        cp.cpart = h->cpart + (size_t)t.par * kNumCounters * (size_t)h->nblocks();
         cp.ncpart = (int32_t)h->nblocks();
         cp.cstats = h->stats_dev;
         HIP_TRY(h, launch_chain(cp, s, prof ? E[5] : nullptr));
@@ -2569,15 +2407,334 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     h->pending.on = true;
     h->pending.seq = pseq;
     h->pending.prof = prof;
-    h->pending.passes = passes;
-    h->pending.m = M;
-    h->pending.fixed_bytes = fixed_bytes;
+    h->pending.passes = t.passes;
+    h->pending.m = t.M;
+    h->pending.fixed_bytes = t.fixed_bytes;
     return FS2_OK;
 }
 
-int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
+
+static int complete_oldest(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats);
+static int mt_finish(fs2_handle *h);
+
+int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
+                       const double *observed, int32_t M, const double *noise, const double *u0) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
-    if (!h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "no submitted scan to wait for");
+    if ((h->stash.on ? 1 : 0) + (h->pending.on ? 1 : 0) + (h->next.on ? 1 : 0) >= 2)
+        return set_err(&h->err, FS2_ERR_STATE, "two scans are outstanding: fs2_iterate_wait for the oldest first");
+    if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
+    // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise /
+    // u0; a draw is consumed by this call whatever happens below
+    const bool drawn = h->mt.armed || h->mt.deferred;
+    h->mt.armed = false;
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    // a deferred draw ends between k_candidates and k_update below, or on the way out
+    // (its outputs are written whatever this call returns)
+    struct DrawEnd {
+        fs2_handle *h;
+        ~DrawEnd() {
+            if (h->mt.deferred) {
+                mt_finish(h);
+                h->mt.armed = false;
+            }
+        }
+    } draw_end{h};
+    if (drawn && (noise || u0))
+        return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
+    int rc;
+    // A scan outstanding: this one's candidate pass runs beside its tail when nothing
+    // below needs the host to know its outcome first (one GPU, one pass, no draw, the
+    // reservations fit without a collection, no buffer to reallocate); else it is
+    // completed here and its results wait for fs2_iterate_wait.
+    bool overlap = false;
+    if (h->pending.on) {
+        const int64_t need = (int64_t)std::max(M, 1) * h->n;
+        overlap = !h->tp && !h->refs && !drawn && M <= kMaxM && h->cursor + need <= h->nfree &&
+                  h->rcursor + need <= h->rnfree && !(h->profiling && h->ev.used + 2 > kProfSets) &&
+                  !(h->cfg.record_assoc && (int64_t)M * h->n > h->assoc_cap) &&
+                  h->cnt_upper + h->pending.m + M <= h->cap;
+        if (!overlap) {
+            h->stash.rc = complete_oldest(h, h->stash.pose, &h->stash.st);
+            h->stash.on = true;
+            if (h->stash.rc)
+                return set_err(&h->err, FS2_ERR_STATE, "the outstanding scan failed (fs2_iterate_wait reports it)");
+        }
+    }
+    const int par = (int)(h->submitted & 1u);
+    const uint64_t scan_id = h->scan + (overlap ? 1u : 0u);      // (the outstanding scan is h->scan)
+    if (h->refs && !h->refs_shared) {
+        rc = share_pools(h, true);
+        if (rc) return rc;
+    }
+    bool collected = false;
+    if (h->refs_shared && h->collect_next) {
+        // page_refs: some rank's pools ran short in the last scan (every rank read the
+        // same records, so every rank collects -- and grows -- here, together)
+        if (h->collect_next & 6) {
+            rc = regrow_collective(h, (h->collect_next & 2) ? 1 : 0, (h->collect_next & 4) ? 1 : 0);
+            if (rc) return rc;
+        }
+        rc = collect_collective(h);
+        if (rc) return rc;
+        h->collect_next = 0;
+        collected = true;
+    }
+    if (h->refs_shared && h->room_check) {
+        // after a resample (every rank knows it resampled) the remote rows this scan
+        // may localise are new: the ranks agree, before any localisation, whether
+        // some rank lacks room for them and this scan's reservations -- then every
+        // rank collects, and grows what is still short, together
+        h->room_check = false;
+        const int64_t Mx = std::max<int64_t>(M, 1);
+        auto short_bits = [&]() -> uint8_t {
+            const int64_t pneed = Mx * h->n + h->remote_bound();
+            const int64_t rneed = Mx * h->n + (int64_t)kPageSlots * h->remote_bound();
+            return (uint8_t)((h->nfree - h->cursor < 2 * pneed ? 1 : 0) | (h->rnfree - h->rcursor < 2 * rneed ? 2 : 0));
+        };
+        auto any_short = [&](uint8_t mine, uint8_t *all_or) -> int {
+            uint8_t all[kMaxRanks] = {};
+            HIP_TRY(h, hipMemsetAsync(h->ep_dev, mine, 1, h->stream));
+            {
+                CommTimer ct(h);
+                const int rc2 = h->tp->allgather(h->ep_dev, h->epochs_dev, 1, h->stream, &h->err);
+                if (rc2) return rc2;
+            }
+            HIP_TRY(h, hipMemcpyAsync(all, h->epochs_dev, (size_t)h->cfg.world_size, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(h, hipStreamSynchronize(h->stream));
+            if (int rc2 = h->tp->status(&h->err)) return rc2;
+            *all_or = 0;
+            for (int q = 0; q < h->cfg.world_size; ++q) *all_or |= all[q];
+            return FS2_OK;
+        };
+        uint8_t any = 0;
+        trace(h, "room check remote pages (K)", (int)(h->remote_bound() >> 10));
+        rc = any_short(short_bits(), &any);
+        trace(h, "room short", any);
+        if (rc) return rc;
+        if (any && !collected) {
+            rc = collect_collective(h);
+            if (rc) return rc;
+            collected = true;
+            rc = any_short(short_bits(), &any);
+            if (rc) return rc;
+        }
+        if (any) {
+            const uint8_t mine = short_bits();
+            const int64_t pneed = Mx * h->n + h->remote_bound();
+            const int64_t rneed = Mx * h->n + (int64_t)kPageSlots * h->remote_bound();
+            rc = regrow_collective(h, (mine & 1) ? h->npool - (h->nfree - h->cursor) + 3 * pneed : 0,
+                                   (mine & 2) ? h->nrecs - (h->rnfree - h->rcursor) + 3 * rneed : 0);
+            if (rc) return rc;
+        }
+    }
+    trace(h, "submit", (int)scan_id);
+    if (!overlap) {             // (overlap: the rows already hold both scans' appends)
+        rc = grow_rows(h, h->cnt_upper + M);
+        if (rc) return rc;
+    }
+    // (overlap: h->cur may be stale -- one GPU takes its set on the device, up.gen)
+    const int cur = h->cur;
+    hipStream_t s = h->stream;
+    const bool sh = h->tp != nullptr;             // sharded path (G > 1, or forced for testing)
+    const bool prof = h->profiling && (h->prof_tick++ % (uint64_t)h->prof_period) == 0;
+
+    // (pinned staging by scan parity: the outstanding scan's copies may not have run)
+    if (noise) {
+        double *pin = h->noise_pin + (size_t)par * (size_t)h->n;
+        std::memcpy(pin, noise, sizeof(double) * h->n);
+        HIP_TRY(h, hipMemcpyAsync(h->noise_dev, pin, sizeof(double) * h->n, hipMemcpyHostToDevice, s));
+    }
+    if (u0) {
+        double *pin = h->u0_pin + par;
+        *pin = *u0;
+        HIP_TRY(h, hipMemcpyAsync(h->u0_dev, pin, 8, hipMemcpyHostToDevice, s));
+    }
+    if (h->cfg.record_assoc && (int64_t)M * h->n > h->assoc_cap) {
+        HIP_TRY(h, hipStreamSynchronize(s));
+        hipFree(h->assoc_dev);
+        h->assoc_dev = nullptr;
+        HIP_TRY(h, hipMalloc(&h->assoc_dev, sizeof(int32_t) * (size_t)M * h->n));
+        h->assoc_cap = (int64_t)M * h->n;
+    }
+    // the last scan's k_publish zeroed the stats; anything else (first scan, an
+    // error return) leaves them to be cleared here
+    if (!h->stats_clean) HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
+    h->stats_clean = false;
+    if (prof && !overlap && h->ev.used == kProfSets) {   // pool used up: fold (the scans are long complete)
+        const int rc0 = fold_profile(h);
+        if (rc0) return rc0;
+    }
+    // (event sets are taken by profiled scans only: the outstanding one's if it was)
+    const int evset = h->ev.used + ((overlap && h->pending.prof) ? 1 : 0);
+    hipEvent_t *E = h->ev.e[evset];
+
+    // ---- fused update passes (move in the first) ----
+    UpdateParams up{};
+    up.n = h->n;
+    up.nblk = h->nblocks();
+    up.blk0 = 0;
+    up.blk1 = up.nblk;
+    up.gidx0 = h->first;
+    up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
+    up.map = h->map();
+    up.noise = (noise || drawn) ? h->noise_dev : nullptr;
+    up.seed = h->cfg.seed;
+    up.scan = scan_id;
+    up.sigma = (rotation != 0) ? h->cfg.rotation_noise : h->cfg.translation_noise;
+    up.rotation = rotation;
+    up.translation = translation;
+    up.gate2 = h->gate2;
+    // gate2 / (1 - 2^-18) rounded up: slack for the fp32 rounding in gate_reject_fast
+    up.gate2f = std::isinf(h->gate2) ? INFINITY
+                                     : std::nextafter((float)(h->gate2 / (1.0 - 0x1p-18)), INFINITY);
+    up.filter = h->cfg.gate_filter ? 1 : 0;
+    up.cand = h->cand;
+    up.ncand = h->ncand;
+    std::memcpy(up.R, h->cfg.measurement_noise, sizeof up.R);
+    std::memcpy(up.init_cov, h->cfg.init_landmark_cov, sizeof up.init_cov);
+    up.assoc = h->cfg.record_assoc ? h->assoc_dev : nullptr;
+    up.wpart = h->wpart;
+    up.cpart = h->cpart + (size_t)par * kNumCounters * (size_t)h->nblocks();
+    up.stats = h->stats_dev;
+    up.slb_pass = h->slb_pass;
+    if (!sh) {                  // one GPU: the buffer set is taken on the device (BufSet)
+        up.gen = h->gen_dev;
+        up.sets = h->sets_dev;
+        up.spec_gen = h->spec_gen;
+    }
+    // page_refs: this scan may ask for a collective collection before the next one
+    // (its pools' room after this scan's reservations and localisations, at most
+    // the remote row entries, below twice as much again)
+    int32_t want_collect = 0;
+    if (h->refs) {              // (also before references cross: this scan's resample may send them)
+        const int64_t pneed = (int64_t)std::max(M, 1) * h->n + h->remote_bound();
+        const int64_t rneed = (int64_t)std::max(M, 1) * h->n + (int64_t)kPageSlots * h->remote_bound();
+        const bool plow = h->nfree - h->cursor < 3 * pneed, rlow = h->rnfree - h->rcursor < 3 * rneed;
+        want_collect = (plow || rlow) ? 1 : 0;
+        // still short right after a collective collection: every rank grows next scan
+        if (collected && plow) want_collect |= 2;
+        if (collected && rlow) want_collect |= 4;
+    }
+    int passes = 0;
+    uint64_t fixed_bytes = 0;
+    for (int32_t k0 = 0; k0 < std::max(M, 1); k0 += kMaxM) {
+        const int32_t m = std::min(kMaxM, M - k0);
+        up.do_move = (k0 == 0);
+        up.k0 = k0;
+        up.m = std::max(m, 0);
+        up.last_pass = (k0 + kMaxM >= M);
+        for (int k = 0; k < kMaxM; ++k) {
+            if (k < up.m) {
+                const double d = meas[2 * (k0 + k)], b = meas[2 * (k0 + k) + 1];
+                up.meas.d[k] = d;
+                up.meas.b[k] = b;
+                up.meas.ox[k] = observed ? observed[2 * (k0 + k)] : d * std::cos(b);
+                up.meas.oy[k] = observed ? observed[2 * (k0 + k) + 1] : d * std::sin(b);
+            } else {
+                up.meas.d[k] = up.meas.b[k] = up.meas.ox[k] = up.meas.oy[k] = 0.0;
+            }
+            // fp32 observed point for the gate mirror and a bound on its rounding
+            const double ox = up.meas.ox[k], oy = up.meas.oy[k];
+            up.meas.fx[k] = (float)ox;
+            up.meas.fy[k] = (float)oy;
+            const double e = std::max(std::fabs(ox - (double)up.meas.fx[k]),
+                                      std::fabs(oy - (double)up.meas.fy[k]));
+            up.meas.fe[k] = std::isfinite(e) ? std::nextafter((float)e, INFINITY) : INFINITY;
+        }
+        rc = reserve_recs(h, (int64_t)up.m * h->n, &up.alloc);
+        if (rc) return rc;
+        rc = reserve_pages(h, (int64_t)up.m * h->n, &up.alloc);
+        if (rc) return rc;
+        up.map = h->map();
+        const bool first = k0 == 0, last = up.last_pass != 0;
+        const bool cand = up.filter && up.blk1 > up.blk0;
+        if (h->refs_shared && h->remote_rows > 0 && up.blk1 > up.blk0) {
+            // page_refs: the remote pages this pass could read, localised first (from
+            // the free lists' tails, clear of every reservation this scan makes; a
+            // tail too short fails the scan loudly, fs2.h error_flags bit 3)
+            const int64_t left = (int64_t)std::max(M - k0 - up.m, 0) * h->n;   // later passes' reservations
+            LocalizeParams lp{};
+            lp.pcap = h->nfree - h->cursor - left;
+            lp.rcap = h->rnfree - h->rcursor - left;
+            lp.map = up.map;
+            lp.cnt = up.cnt;
+            lp.n = h->n;
+            lp.nblk = up.nblk;
+            lp.m = up.m;
+            lp.gate2f = up.gate2f;
+            lp.meas = up.meas;
+            lp.freel = h->freel;
+            lp.ftail = h->nfree;
+            lp.rfreel = h->rfreel;
+            lp.rtail = h->rnfree;
+            lp.stats = h->stats_dev;
+            // one copy per distinct remote page: the page-dedup table the page
+            // transfer would use (sized for every row of the shard, xfer_bufs), keys
+            // tagged with this pass's epoch so it is never cleared
+            lp.key = h->xt_key;
+            lp.val = h->xt_uidx;
+            lp.cap = h->xt_cap;
+            lp.epoch = ++h->loc_epoch;
+            HIP_TRY(h, launch_localize(lp, s));
+        }
+        // a shard without particles launches nothing: its profiled intervals are
+        // recorded empty here (fold_one reads every event of the set)
+        if (prof && first && up.blk1 <= up.blk0)
+            for (int k : {0, 1, 4}) HIP_TRY(h, hipEventRecord(E[k], s));
+        if (overlap && cand) {
+            // beside the outstanding scan's tail (after its update pass), then a
+            // fix-up behind the tail for the workgroups whose set a resample changed
+            HIP_TRY(h, hipStreamWaitEvent(h->spec_stream, h->ev_upd, 0));
+            UpdateParams us = up;
+            us.spec = 1;
+            HIP_TRY(h, launch_candidates(us, h->spec_stream, (prof && first) ? E[0] : nullptr,
+                                         (prof && first) ? E[1] : nullptr));
+            HIP_TRY(h, hipEventRecord(h->ev_spec, h->spec_stream));
+            HIP_TRY(h, hipStreamWaitEvent(s, h->ev_spec, 0));
+            us.spec = 2;
+            HIP_TRY(h, launch_candidates(us, s, nullptr, nullptr));
+        } else {
+            HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
+        }
+        if (first && h->mt.deferred) {     // the draw's host half while k_candidates runs
+            rc = mt_finish(h);
+            if (rc) return rc;
+            h->mt.armed = false;
+        }
+        HIP_TRY(h, launch_update(up, s, (prof && first) ? (cand ? E[4] : E[0]) : nullptr,
+                                 (prof && last) ? E[2] : nullptr));
+        if (prof && last && up.blk1 <= up.blk0) HIP_TRY(h, hipEventRecord(E[2], s));
+        ++passes;
+        // pose/weight/count read + weight/count write; pose write on the move pass
+        fixed_bytes += (uint64_t)h->n * (32 + 4 + 8 + 4 + (up.do_move ? 24 : 0));
+        if (up.do_move && (noise || drawn)) fixed_bytes += (uint64_t)h->n * 8;
+        if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
+    }
+    HIP_TRY(h, hipEventRecord(h->ev_upd, s));     // (a pipelined next scan's candidate pass starts here)
+    h->submitted += 1;
+
+    fs2_handle::TailCtx tc;
+    tc.M = M;
+    tc.passes = passes;
+    tc.fixed_bytes = fixed_bytes;
+    tc.prof = prof;
+    tc.evset = evset;
+    tc.want_collect = want_collect;
+    tc.has_u0 = (u0 || drawn);
+    tc.par = par;
+    if (overlap) {              // its tail when the outstanding scan is waited for
+        h->next.on = true;
+        h->next.t = tc;
+        h->stats_clean = false;
+        h->overlapped += 1;
+        return FS2_OK;
+    }
+    return enqueue_tail(h, tc);
+}
+
+// The oldest outstanding scan: its publication, the host's bookkeeping (which set
+// is current, reservations, profile), its pose and statistics.
+static int complete_oldest(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     h->pending.on = false;
     const int M = h->pending.m;
     int rc = wait_flag(h, h->pending.seq);
@@ -2592,6 +2749,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         h->rnfree -= (int64_t)st.loc_recs;
         h->remote_rows = st.resampled ? (int64_t)st.remote_rows
                                       : std::max<int64_t>(0, h->remote_rows - (int64_t)st.loc_rows);
+        if (st.resampled) h->remote_pages = (int64_t)st.remote_pages;
         h->collect_next = st.collect_next;
         if (h->profiling) {
             h->prof.localized_pages += st.loc_pages;
@@ -2651,9 +2809,29 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     return FS2_OK;
 }
 
+int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
+    if (h->stash.on) {                 // completed by a submit that had to wait for it
+        h->stash.on = false;
+        if (out_pose) std::memcpy(out_pose, h->stash.pose, sizeof h->stash.pose);
+        if (stats) *stats = h->stash.st;
+        return h->stash.rc;
+    }
+    if (!h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "no submitted scan to wait for");
+    int rc = complete_oldest(h, out_pose, stats);
+    if (h->next.on) {                  // the scan submitted behind it: its tail, now that the set is known
+        h->next.on = false;
+        const int rc2 = enqueue_tail(h, h->next.t);
+        if (rc == FS2_OK) rc = rc2;
+    }
+    return rc;
+}
+
 int fs2_iterate(fs2_handle *h, double rotation, double translation, const double *meas,
                 const double *observed, int32_t M, const double *noise, const double *u0,
                 double out_pose[3], fs2_iter_stats *stats) {
+    if (h && (h->pending.on || h->stash.on))
+        return set_err(&h->err, FS2_ERR_STATE, "submitted scans are outstanding (fs2_iterate_wait first)");
     const int rc = fs2_iterate_submit(h, rotation, translation, meas, observed, M, noise, u0);
     if (rc) return rc;
     return fs2_iterate_wait(h, out_pose, stats);

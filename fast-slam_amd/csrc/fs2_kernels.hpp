@@ -103,7 +103,34 @@ struct DevStats {
     unsigned long long loc_recs;     //            records taken for them
     unsigned long long remote_rows;  //            a resample's outputs: row entries naming remote pages
     unsigned long long loc_rows;     //            row entries k_localize pointed at a local copy
+    unsigned long long remote_pages; //            a resample's outputs: distinct remote pages their rows name
 };
+
+// Open-addressing set of tagged page ids (page_refs: k_localize's copies, the
+// gather's distinct remote pages): keys epoch << 32 | id, a slot of an older epoch
+// is free, so the table is never cleared.  Returns the slot and whether this call
+// inserted the key (a claim), or -1 when the table is full.
+__device__ inline int64_t ptable_insert(unsigned long long *key, int64_t cap, uint32_t epoch, uint32_t x,
+                                        bool *claimed) {
+    const unsigned long long want = ((unsigned long long)epoch << 32) | x;
+    const uint64_t mask = (uint64_t)cap - 1u;
+    uint64_t s = ((uint64_t)x * 0x9E3779B97F4A7C15ull >> 20) & mask;
+    *claimed = false;
+    for (int64_t probe = 0; probe < cap;) {
+        const unsigned long long cur = __atomic_load_n(&key[s], __ATOMIC_RELAXED);
+        if (cur == want) return (int64_t)s;
+        if ((cur >> 32) != epoch) {
+            if (atomicCAS(&key[s], cur, want) == cur) {
+                *claimed = true;
+                return (int64_t)s;
+            }
+            continue;                      // taken meanwhile: look again
+        }
+        s = (s + 1) & mask;
+        ++probe;
+    }
+    return -1;
+}
 
 // numpy's np.sum over 8192-element buffers (fs2_exact.hip).  The recursion over a
 // partial last chunk is fixed by the handle's particle count (np_tail_plan, host):
@@ -328,6 +355,17 @@ struct PageAlloc {
     int64_t rbase;
 };
 
+// The particle buffers of set b (A/B across resamples).  A scan enqueued before the
+// host knows whether the previous one resampled (pipelined submit, fs2_api.hip)
+// takes its buffers on the device: set (*gen & 1) is current, and k_tail_single
+// bumps *gen when a resample made the other set current.
+struct BufSet {
+    double *x, *y, *yaw, *w;
+    int32_t *cnt;
+    Desc *pt;
+    uint32_t *bbox;          // null when the maps outgrow the row boxes
+};
+
 struct UpdateParams {
     int64_t n;               // local particles
     int64_t blk0, blk1;      // workgroups [blk0, blk1) of kBlock particles in this launch
@@ -361,6 +399,13 @@ struct UpdateParams {
     // boxes with it (exact: its pages' mirrors predate the pass), so it opens no page
     // those bands rejected -- none that k_localize left remote (page_refs mode)
     float *slb_pass;
+    // pipelined submit: x .. cnt and map.pt / map.bbox come from sets[*gen & 1]
+    const uint32_t *gen;     // null: the pointers above
+    const BufSet *sets;
+    uint32_t *spec_gen;      // [nblk] the gen each workgroup of a speculative k_candidates read
+    int32_t spec;            // k_candidates: 0 plain; 1 speculative (beside the previous scan's
+                             // tail, records spec_gen); 2 fix-up (a workgroup whose speculative
+                             // run read the current set exits, the others run again)
 };
 
 struct ReduceParams {
@@ -436,6 +481,13 @@ struct ResampleParams {
     double *bsum;            // block sums (prefix)
     int32_t nblk;            // 1024-element blocks
     int32_t lazy;            // prefix kernels run only when the resample rule fired
+    uint32_t *gen;           // one GPU: bumped by k_tail_single when the scan resampled (BufSet)
+    // page_refs: the gather counts the distinct remote pages its outputs' rows name
+    // (ptable_insert over the handle's page table, epoch tepoch) -- the room bound
+    // of the localisations until the next resample
+    unsigned long long *tkey;
+    int64_t tcap;
+    uint32_t tepoch;
     double flip_margin;      // tree prefix: relative rounding bound counted in reduce_amb (0: off)
     int32_t use_chain;       // running sum from the exact chain's units (c: serial units only)
     ChainView chain;

@@ -1449,6 +1449,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     // over the wave's longest map so that every lane takes part in the row unions
     const int wrows = wave_max_i(rows);
     unsigned nremote = 0;            // page_refs: row entries naming another rank's page
+    unsigned npages = 0;             //            of them, first sightings of a page (distinct)
     for (int k0 = 0; k0 < wrows; k0 += 8) {
         Desc e[8];
 #pragma unroll
@@ -1457,7 +1458,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         for (int u = 0; u < 8; ++u) {
             if (k0 + u < rows) {
                 e[u].x &= keep;
-                if (P.refs && ref_tag(e[u].x)) ++nremote;
+                if (P.refs && ref_tag(e[u].x)) {
+                    ++nremote;
+                    bool claimed = false;
+                    if (P.tkey && ptable_insert(P.tkey, P.tcap, P.tepoch, e[u].x, &claimed) >= 0 && claimed)
+                        ++npages;
+                }
                 __builtin_nontemporal_store(((unsigned long long)e[u].y << 32) | e[u].x,
                                             reinterpret_cast<unsigned long long *>(P.opt + (int64_t)(k0 + u) * n + m));
             }
@@ -1493,6 +1499,9 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         const unsigned long long br = block_sum_u64<kBlock>(nremote, lds_u);
         if (threadIdx.x == 0 && br) atomicAdd(&P.stats->remote_rows, br);
         __syncthreads();             // lds_u is reused below
+        const unsigned long long bp = block_sum_u64<kBlock>(npages, lds_u);
+        if (threadIdx.x == 0 && bp) atomicAdd(&P.stats->remote_pages, bp);
+        __syncthreads();
     }
     // per-block partials (no same-address atomics), folded by estimate_body
     const unsigned long long bs = block_sum_u64<kBlock>(slots, lds_u);
@@ -1584,7 +1593,10 @@ __global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, co
     if (!R.stats->resampled) return;
     estimate_body(R, nparts);
     __syncthreads();
-    if (threadIdx.x == 0) global_best_body(P);
+    if (threadIdx.x == 0) {
+        global_best_body(P);
+        if (R.gen) *R.gen += 1u;        // the other set is current (BufSet; the next kernels read it)
+    }
     __syncthreads();
     publish_body(P.stats, host_stats, host_flag, seq);
 }

@@ -100,8 +100,18 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const int64_t blk = P.blk0 + blockIdx.x;   // this launch may cover a chunk of the blocks
     const int64_t i = blk * kBlock + tid;
     const bool live = i < n;
-    const int c = live ? P.cnt[i] : 0;
-    const MapRef map = P.map;
+    MapRef map = P.map;
+    const int32_t *cntp = P.cnt;
+    if (P.gen) {                               // pipelined: the current set, read on the device
+        const uint32_t g = __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)P.gen);
+        if (P.spec == 2 && P.spec_gen[blk] == g) return;   // the speculative run read this set
+        const BufSet &b = P.sets[g & 1u];
+        map.pt = b.pt;
+        map.bbox = b.bbox;
+        cntp = b.cnt;
+        if (P.spec == 1 && tid == 0) P.spec_gen[blk] = g;
+    }
+    const int c = live ? cntp[i] : 0;
     const Desc *ptrow = map.pt + (live ? i : 0);
     const float slb = *map.slb;
     if (blockIdx.x == 0 && tid == 0 && P.slb_pass) *P.slb_pass = slb;
@@ -287,19 +297,31 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     if (tid < MAXM) s_ms[tid] = Meas{P.meas.d[tid], P.meas.b[tid], P.meas.ox[tid], P.meas.oy[tid]};
 #pragma unroll
     for (int k = 0; k < MAXM; ++k) s_idx[k][tid] = (int16_t)-2;
-    if (P.map.bbox && tid < P.map.rows) lds_box_set(s_bb, tid, P.map.bbox[blk * kBBoxRows + tid]);
+    MapRef map = P.map;
+    double *xp = P.x, *yp = P.y, *yawp = P.yaw, *wp = P.w;
+    int32_t *cntp = P.cnt;
+    if (P.gen) {                               // pipelined: the current set, read on the device
+        const BufSet &b = P.sets[__builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)P.gen) & 1u];
+        xp = b.x;
+        yp = b.y;
+        yawp = b.yaw;
+        wp = b.w;
+        cntp = b.cnt;
+        map.pt = b.pt;
+        map.bbox = b.bbox;
+    }
+    if (map.bbox && tid < map.rows) lds_box_set(s_bb, tid, map.bbox[blk * kBBoxRows + tid]);
     __syncthreads();
 
     double px = 0.0, py = 0.0, pyaw = 0.0, w = 0.0;
     int c = 0;
     if (live) {
-        px = P.x[i];
-        py = P.y[i];
-        pyaw = P.yaw[i];
-        w = P.w[i];
-        c = P.cnt[i];
+        px = xp[i];
+        py = yp[i];
+        pyaw = yawp[i];
+        w = wp[i];
+        c = cntp[i];
     }
-    const MapRef map = P.map;
     const int64_t il = live ? i : 0;
     int nalloc = 0;                  // pages taken from this pass's reservation
     int nrec = 0;                    // records taken from this pass's reservation
@@ -786,12 +808,12 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     if (live) {
         if (P.do_move) {
-            P.x[i] = px;
-            P.y[i] = py;
-            P.yaw[i] = pyaw;
+            xp[i] = px;
+            yp[i] = py;
+            yawp[i] = pyaw;
         }
-        P.w[i] = w;
-        P.cnt[i] = c;
+        wp[i] = w;
+        cntp[i] = c;
     }
 
     FS2_PHASE(6);

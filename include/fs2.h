@@ -255,10 +255,19 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
 
 /* fs2_iterate in two halves: fs2_iterate_submit enqueues the scan (same
  * arguments; on a sharded handle it also performs the mid-scan exchanges) and
- * returns while the GPU works; fs2_iterate_wait completes it (pose, stats).  The
- * caller can do host work in between -- e.g. hand the next scan's ICP alignment
- * to the GPU (config 4) -- without delaying the scan.  One scan at a time:
- * submitting again, or reading / writing the state, before the wait fails with
+ * returns while the GPU works; fs2_iterate_wait completes the oldest submitted
+ * scan (pose, stats).  The caller can do host work in between -- e.g. hand the
+ * next scan's ICP alignment to the GPU (config 4) -- without delaying the scan.
+ *
+ * Up to two scans may be outstanding: submit(s + 1), then wait (returns s), then
+ * submit(s + 2), wait (returns s + 1), ...  On one GPU, with at most 4
+ * measurements and no fs2_mt_draw, the second scan's candidate pass runs beside the
+ * first one's tail (normalise, N_eff, resample) and the two overlap on the device;
+ * otherwise the submit completes the outstanding scan first and keeps its results
+ * for the next wait.  Results are identical to one scan at a time and come back
+ * in submission order; the second scan's tail is enqueued by the wait for the
+ * first, so call it promptly.  A third submit, fs2_iterate, and reading / writing
+ * the state (or the associations) while scans are outstanding fail with
  * FS2_ERR_STATE. */
 int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
                        const double *observed, int32_t M, const double *noise, const double *u0);
