@@ -172,7 +172,25 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
                     }
                 }
                 if (hit) {
-                    if (nc < kMaxCand) s_list[nc][tid] = cand_entry(mirror_slot(mv), j0 + u, mirror_rec(mv));
+                    // the kMaxCand smallest slots (an overflowing list still settles every
+                    // measurement that matches among them; k_update scans on past them)
+                    const uint64_t e = cand_entry(mirror_slot(mv), j0 + u, mirror_rec(mv));
+                    if (nc < kMaxCand) {
+                        s_list[nc][tid] = e;
+                    } else {
+                        // (rare: a rolled loop keeps k_candidates' registers at 8 waves)
+                        int mq = 0;
+                        uint64_t me = s_list[0][tid];
+#pragma unroll 1
+                        for (int q = 1; q < kMaxCand; ++q) {
+                            const uint64_t x = s_list[q][tid];
+                            if (x > me) {
+                                me = x;
+                                mq = q;
+                            }
+                        }
+                        if (e < me) s_list[mq][tid] = e;
+                    }
                     ++nc;
                 }
             }
@@ -227,18 +245,16 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     }
     if (live) {
         P.ncand[i] = nc;
-        if (nc <= kMaxCand) {
-            // pages may hold their slots in any order: the list goes out in slot
-            // (reference list) order; an overflowing list is not used (k_update
-            // runs the reference's own loop for that particle)
-            uint64_t e[kMaxCand];
+        // pages may hold their slots in any order: the list goes out in slot
+        // (reference list) order -- an overflowing list as its kMaxCand smallest
+        // slots, after which k_update runs the reference's loop for what is left
+        uint64_t e[kMaxCand];
 #pragma unroll
-            for (int q = 0; q < kMaxCand; ++q) e[q] = (q < nc) ? s_list[q][tid] : ~0ull;
-            sort8(e);
+        for (int q = 0; q < kMaxCand; ++q) e[q] = (q < nc) ? s_list[q][tid] : ~0ull;
+        sort8(e);
 #pragma unroll
-            for (int q = 0; q < kMaxCand; ++q)
-                if (q < nc) P.cand[(int64_t)q * n + i] = e[q];
-        }
+        for (int q = 0; q < kMaxCand; ++q)
+            if (q < nc) P.cand[(int64_t)q * n + i] = e[q];
     }
     // kCWords, kCGroups, kCVisited, kCOpened
     const unsigned cv[4] = {(unsigned)min(nc, kMaxCand), groups, visited, opened};
@@ -422,7 +438,12 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         }
     };
 
-    if (!overflow) {
+    // An overflowing list holds the kMaxCand smallest candidate slots: it settles
+    // the measurements that match among them, the overflow scan below only looks
+    // past its last slot (`lo`) for the rest.
+    int lo = -1;
+    int nmod_list = 0;
+    {
         // Listed candidates in slot order; the list names their records, so while
         // one is tested the next one's record and the entry after it are in flight
         // (every load is branch-free: a missing entry reads entry 0 and record 0,
@@ -449,7 +470,10 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 visit(mirror_slot(mv), j, load_rec(map.recs, mirror_rec(mv)));
             }
         }
-    } else {
+        if (overflow && ncl > 0) lo = cand_slot(P.cand[(int64_t)(ncl - 1) * n + il]);
+        nmod_list = nmod;
+    }
+    if (overflow && pend != 0u) {
         // An overflowing list: the reference's loop (landmark_utils.py:103-117),
         // each pending measurement in order taking the smallest slot index that
         // passes the exact gate with the states the earlier measurements left.
@@ -493,6 +517,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                     }
                     const float4 mv = load_mirror(pg, u);
                     const int slot = mirror_slot(mv);
+                    if (slot <= lo) continue;          // settled by the list (slot order)
                     const float cx = fabsf(mv.x) * 2.3841858e-7f, cy = fabsf(mv.y) * 2.3841858e-7f;
                     unsigned test = 0u;
 #pragma unroll
@@ -537,9 +562,10 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 scan(1u << k, true);
             }
             int bk = s_ws[tid >> 6].ov.best[k][tid & 63], pk = s_ws[tid >> 6].ov.bpos[k][tid & 63];
-            // the slots modified so far, with their new states
+            // the slots modified so far past the list, with their new states (the
+            // list's were tested in slot order with the states of their turn)
             int tk = -1;
-            for (int q = 0; q < nmod; ++q) {
+            for (int q = nmod_list; q < nmod; ++q) {
                 const int pos = (int)((mods >> (16 * q)) & 0xffffu);
                 const float4 mq = s_mv[q][tid];
                 const int slot = mirror_slot(mq);

@@ -2,9 +2,9 @@
 
 The split call runs exactly the scan fs2_iterate runs (reference
 fast_slam_2.py:33-67): same poses, stats, associations and state as a handle
-stepped with step(); while a scan is pending the handle refuses a second
-submission and any state access (FS2_ERR_STATE), and a wait without a
-submission fails the same way.
+stepped with step(); while a scan is pending the handle refuses any state
+access (FS2_ERR_STATE), and a wait without a submission fails the same way
+(two scans in flight: tests/test_gpu_pipelined.py).
 """
 import numpy as np
 import pytest
@@ -34,7 +34,7 @@ def test_submit_wait_equals_step():
         p0, s0 = hs[0].step(rot, tr, ms)
         hs[1].step_submit(rot, tr, ms)
         with pytest.raises(nat.FS2Error):
-            hs[1].step_submit(rot, tr, ms)            # one scan at a time
+            hs[1].associations()                      # (a second submit is allowed: test_gpu_pipelined.py)
         with pytest.raises(nat.FS2Error):
             hs[1].get_state(0, 4)                     # state is not readable mid-scan
         p1, s1 = hs[1].step_wait()
