@@ -1789,7 +1789,9 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
     {
         // the speculative candidate pass of a pipelined submit: its own stream at the
-        // lowest priority, so the previous scan's tail (latency chains) goes first
+        // lowest priority (a main stream at the greatest priority, a CU partition and
+        // more hardware queues were measured and changed nothing:
+        // profiles/r05_ab_pipelined.txt)
         int least = 0, greatest = 0;
         (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
         if (hipStreamCreateWithPriority(&h->spec_stream, hipStreamNonBlocking, least) != hipSuccess ||

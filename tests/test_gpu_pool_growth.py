@@ -100,8 +100,11 @@ def test_growth_after_close_is_fast():
     G, N, L, S = 8, 1_000_000, 500, 9
     for rep in range(2):
         key = b"grow" + bytes([rep]) * 124
+        # (a record pool just above the maps: the records the scans write make
+        # every set grow it -- the growth the stall was in)
         hs = [fast_slam_2.FastSLAM2(N, rng="device", seed=0, landmark_capacity=L + S + 8, rank=g, world_size=G,
-                                    comm_id=key, comm_mode="local", verbose=False, page_refs="on")
+                                    comm_id=key, comm_mode="local", verbose=False, page_refs="on",
+                                    record_pool=(N // G) * (L + 12))
               for g in range(G)]
         for g, h in enumerate(hs):
             bench.populate(h, h.n_local, L, 0, g)

@@ -277,8 +277,9 @@ def test_page_refs_collective_collections():
     cols = [st.collections for st in last]
     # (the imports' record shortfalls grow the fresh pools without collecting:
     # nothing could be freed) then, after references cross ranks, collective
-    # collections, together
-    assert min(cols) >= 3 and len(set(cols)) == 1, cols
+    # collections, together (since round 5 the room bound counts distinct remote
+    # pages, not remote row entries, so fewer collections are needed)
+    assert min(cols) >= 2 and len(set(cols)) == 1, cols
     assert sum(p["localized_pages"] for p in profs) > 0
 
 
