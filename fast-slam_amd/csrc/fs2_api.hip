@@ -488,11 +488,9 @@ struct fs2_handle {
         uint64_t fixed_bytes = 0;
     } pending;
     // Pipelined submit (fs2.h fs2_iterate_submit): scan s+1 submitted while scan s is
-    // outstanding.  Its candidate pass runs beside s's tail on spec_stream (reading
-    // the buffer set current at that moment, BufSet / gen), a fix-up pass after the
-    // tail reruns the workgroups whose set changed (a resample), its exact update
-    // follows on the main stream; its own tail is enqueued when s is waited for
-    // (the host then knows s's decision, i.e. which set is current).
+    // outstanding.  Its update pass is enqueued behind s's tail, taking its buffer set
+    // on the device (BufSet, gen: the host does not know yet whether s resampled);
+    // its own tail is enqueued when s is waited for (the host then knows the set).
     struct TailCtx {
         int32_t M = 0;
         int passes = 0;
@@ -513,11 +511,8 @@ struct fs2_handle {
         double pose[3] = {};
         fs2_iter_stats st{};
     } stash;
-    hipStream_t spec_stream = nullptr;
-    hipEvent_t ev_upd = nullptr, ev_spec = nullptr;   // end of the last update pass / speculative pass
     uint32_t *gen_dev = nullptr;           // the current set is (gen & 1) == cur (one GPU)
     BufSet *sets_dev = nullptr;            // [2]
-    uint32_t *spec_gen = nullptr;          // [nblocks]
     uint64_t submitted = 0;                // scans submitted (parity)
     uint64_t overlapped = 0;               // scans whose candidate pass ran beside the previous tail
     int32_t cnt_upper = 0;
@@ -1650,7 +1645,6 @@ const char *fs2_last_error(const fs2_handle *h) {
 static void free_handle(fs2_handle *h) {
     if (!h) return;
     if (h->stream) hipStreamSynchronize(h->stream);
-    if (h->spec_stream) hipStreamSynchronize(h->spec_stream);
     // In-place pools (VMM chunks): nothing of this process may still be in flight
     // when they are unmapped and released, or the runtime defers the release and the
     // next handle's first growth (hipMemCreate) waits for it -- 4 s in the round-4
@@ -1705,13 +1699,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->uop); hipFree(h->np_tail_g);
     hipFree(h->peers_dev); hipFree(h->ep_dev); hipFree(h->epochs_dev);
     hipFree(h->part_pose);
-    if (h->spec_stream) {
-        hipStreamSynchronize(h->spec_stream);
-        hipStreamDestroy(h->spec_stream);
-    }
-    if (h->ev_upd) hipEventDestroy(h->ev_upd);
-    if (h->ev_spec) hipEventDestroy(h->ev_spec);
-    hipFree(h->spec_gen); hipFree(h->gen_dev); hipFree(h->sets_dev);
+    hipFree(h->gen_dev); hipFree(h->sets_dev);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -1787,18 +1775,6 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     if (hipSetDevice(cfg->device) != hipSuccess) return fail(set_err(&h->err, FS2_ERR_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
-    {
-        // the speculative candidate pass of a pipelined submit: its own stream at the
-        // lowest priority (a main stream at the greatest priority, a CU partition and
-        // more hardware queues were measured and changed nothing:
-        // profiles/r05_ab_pipelined.txt)
-        int least = 0, greatest = 0;
-        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-        if (hipStreamCreateWithPriority(&h->spec_stream, hipStreamNonBlocking, least) != hipSuccess ||
-            hipEventCreateWithFlags(&h->ev_upd, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&h->ev_spec, hipEventDisableTiming) != hipSuccess)
-            return fail(set_err(&h->err, FS2_ERR_HIP, "hipStreamCreate failed"));
-    }
     const int64_t n = std::max<int64_t>(h->n, 1);
     const int64_t nb = (n + kBlock - 1) / kBlock;
     const int64_t nsb = (n + 1023) / 1024;
@@ -1839,7 +1815,6 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->cpart, 2 * nb * 8 * kNumCounters) == hipSuccess;   // [2]: by scan parity
-    ok &= alloc((void **)&h->spec_gen, nb * 4) == hipSuccess;
     ok &= alloc((void **)&h->gen_dev, 4) == hipSuccess;
     ok &= alloc((void **)&h->sets_dev, 2 * sizeof(BufSet)) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
@@ -1903,7 +1878,6 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
     if (hipMemsetAsync(h->cpart, 0, 2 * nb * 8 * kNumCounters, h->stream) != hipSuccess ||
         hipMemsetAsync(h->gen_dev, 0, 4, h->stream) != hipSuccess ||
-        hipMemsetAsync(h->spec_gen, 0xff, nb * 4, h->stream) != hipSuccess ||
         hipMemsetD32Async((hipDeviceptr_t)h->slb, 0x7f7fffff, 1, h->stream) != hipSuccess)   // FLT_MAX: no mirror yet
         return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     // Particle.__init__: (0, 0, 0), weight 1/NUM_PARTICLES, empty map (particle.py:11-20)
@@ -2602,7 +2576,6 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (!sh) {                  // one GPU: the buffer set is taken on the device (BufSet)
         up.gen = h->gen_dev;
         up.sets = h->sets_dev;
-        up.spec_gen = h->spec_gen;
     }
     // page_refs: this scan may ask for a collective collection before the next one
     // (its pools' room after this scan's reservations and localisations, at most
@@ -2683,21 +2656,7 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         // recorded empty here (fold_one reads every event of the set)
         if (prof && first && up.blk1 <= up.blk0)
             for (int k : {0, 1, 4}) HIP_TRY(h, hipEventRecord(E[k], s));
-        if (overlap && cand) {
-            // beside the outstanding scan's tail (after its update pass), then a
-            // fix-up behind the tail for the workgroups whose set a resample changed
-            HIP_TRY(h, hipStreamWaitEvent(h->spec_stream, h->ev_upd, 0));
-            UpdateParams us = up;
-            us.spec = 1;
-            HIP_TRY(h, launch_candidates(us, h->spec_stream, (prof && first) ? E[0] : nullptr,
-                                         (prof && first) ? E[1] : nullptr));
-            HIP_TRY(h, hipEventRecord(h->ev_spec, h->spec_stream));
-            HIP_TRY(h, hipStreamWaitEvent(s, h->ev_spec, 0));
-            us.spec = 2;
-            HIP_TRY(h, launch_candidates(us, s, nullptr, nullptr));
-        } else {
-            HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
-        }
+        HIP_TRY(h, launch_candidates(up, s, (prof && first) ? E[0] : nullptr, (prof && first) ? E[1] : nullptr));
         if (first && h->mt.deferred) {     // the draw's host half while k_candidates runs
             rc = mt_finish(h);
             if (rc) return rc;
@@ -2712,7 +2671,6 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         if (up.do_move && (noise || drawn)) fixed_bytes += (uint64_t)h->n * 8;
         if (up.assoc) fixed_bytes += (uint64_t)h->n * 4 * up.m;
     }
-    HIP_TRY(h, hipEventRecord(h->ev_upd, s));     // (a pipelined next scan's candidate pass starts here)
     h->submitted += 1;
 
     fs2_handle::TailCtx tc;

@@ -399,13 +399,10 @@ struct UpdateParams {
     // boxes with it (exact: its pages' mirrors predate the pass), so it opens no page
     // those bands rejected -- none that k_localize left remote (page_refs mode)
     float *slb_pass;
-    // pipelined submit: x .. cnt and map.pt / map.bbox come from sets[*gen & 1]
+    // one GPU: x .. cnt and map.pt / map.bbox come from sets[*gen & 1] (a scan may be
+    // enqueued before the host knows whether the previous one resampled)
     const uint32_t *gen;     // null: the pointers above
     const BufSet *sets;
-    uint32_t *spec_gen;      // [nblk] the gen each workgroup of a speculative k_candidates read
-    int32_t spec;            // k_candidates: 0 plain; 1 speculative (beside the previous scan's
-                             // tail, records spec_gen); 2 fix-up (a workgroup whose speculative
-                             // run read the current set exits, the others run again)
 };
 
 struct ReduceParams {

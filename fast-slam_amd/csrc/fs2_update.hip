@@ -102,14 +102,11 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const bool live = i < n;
     MapRef map = P.map;
     const int32_t *cntp = P.cnt;
-    if (P.gen) {                               // pipelined: the current set, read on the device
-        const uint32_t g = __builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)P.gen);
-        if (P.spec == 2 && P.spec_gen[blk] == g) return;   // the speculative run read this set
-        const BufSet &b = P.sets[g & 1u];
+    if (P.gen) {                               // the current set, read on the device
+        const BufSet &b = P.sets[__builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)P.gen) & 1u];
         map.pt = b.pt;
         map.bbox = b.bbox;
         cntp = b.cnt;
-        if (P.spec == 1 && tid == 0) P.spec_gen[blk] = g;
     }
     const int c = live ? cntp[i] : 0;
     const Desc *ptrow = map.pt + (live ? i : 0);
@@ -316,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     MapRef map = P.map;
     double *xp = P.x, *yp = P.y, *yawp = P.yaw, *wp = P.w;
     int32_t *cntp = P.cnt;
-    if (P.gen) {                               // pipelined: the current set, read on the device
+    if (P.gen) {                               // the current set, read on the device
         const BufSet &b = P.sets[__builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)P.gen) & 1u];
         xp = b.x;
         yp = b.y;

@@ -12,7 +12,7 @@ for rep in 1 2 3; do
   for v in $VARIANTS; do
     set -- ${v//:/ }
     lib=fast-slam_amd/lib/libfs2.so; [ "$1" != default ] && lib=fast-slam_amd/lib/libfs2_$1.so
-    extra=""; [ "$2" = sync ] && extra="--sync"
+    extra=""; [ "$2" = pipe ] && extra="--pipelined"
     FS2_LIB=$lib GPU_MAX_HW_QUEUES=${3:-4} timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras $extra > gpurun_out/ab_run.log 2>&1 || { echo "run $v failed"; tail -5 gpurun_out/ab_run.log; exit 3; }
     tail -1 gpurun_out/ab_run.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); e=d['extra']

@@ -1,14 +1,13 @@
 """Two scans in flight (fs2.h fs2_iterate_submit): scan s+1 is
-submitted before scan s is waited for.  Its candidate pass runs on a second stream
-beside scan s's tail, reading the buffer set current at that moment on the device
-(BufSet: a resample makes the other set current and bumps a generation); a fix-up
-pass behind the tail reruns every workgroup whose set changed; its exact update
-and its tail follow.  The results must be the bits of step() one scan at a time --
-reference semantics fast_slam_2.py:33-223 -- on a workload that resamples often
-(the fix-up path), with device Philox draws and with injected noise / u0 (the
-pinned staging is per scan parity), and when a scan cannot overlap (two update
-passes: M > 4) the library completes the outstanding scan first and hands its
-results back in order."""
+submitted before scan s is waited for.  Its update pass is enqueued behind scan
+s's tail and takes its buffer set on the device (BufSet: a resample makes the
+other set current and bumps a generation); its own tail is enqueued when scan s
+is waited for.  The results must be the bits of step() one scan at a time --
+reference semantics fast_slam_2.py:33-223 -- on a workload that resamples often,
+with device Philox draws and with injected noise / u0 (the pinned staging is per
+scan parity), and when a scan cannot be enqueued early (two update passes: M > 4)
+the library completes the outstanding scan first and hands its results back in
+order."""
 import numpy as np
 import pytest
 
