@@ -371,11 +371,13 @@ def robustness(args, f, L, first_scan):
     # the same with whole pages sent (round 3's transfer; A/B of the page references)
     out["sharded_local_g8_pages"] = sharded_local(args, L, n, G=8, page_refs="off")
     out["dropin_iterate"] = dropin(args, L, n)
+    # A/B: each scan's draw begun beside its own candidate pass (round 4's deferred draw)
+    out["dropin_iterate_no_speculation"] = dropin(args, L, n, spec=False)
     out["dropin_iterate_host_rng"] = dropin(args, L, n, rng="numpy-host")
     return out
 
 
-def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
+def dropin(args, L, n, scans=23, warm=3, rng="numpy", spec=True):
     """What a reference caller gets: FastSLAM2.iterate(rotation, translation,
     list[Measurement]) (fast_slam_2.py:33, called at jde_robots_main.py:38) with
     numpy's global legacy RNG -- N normals per scan and the resample start,
@@ -386,9 +388,14 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
     import fast_slam_2
     import fs2_synthetic as syn
     from fast_slam_2.models.measurement import Measurement
+    import ctypes
+    from fast_slam_2 import _native as nat
     np.random.seed(args.seed)
     f = fast_slam_2.FastSLAM2(n, rng=rng, seed=args.seed, landmark_capacity=L + scans + 8, verbose=False)
     populate(f, n, L, args.seed, 0)
+    lib = nat.load()
+    if not spec:
+        nat.check(lib.fs2_debug_mt_speculate(f._h, 0, None), f._h)
     meas = [[Measurement(float(d), float(b)) for d, b in syn.scan_measurements(L, s, args.seed)]
             for s in range(scans)]
     for s in range(warm):
@@ -402,6 +409,8 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
         each.append(time.perf_counter() - t1)
         res += f.last_stats.resampled
     dt = time.perf_counter() - t0
+    sc = (ctypes.c_uint64 * 2)()
+    nat.check(lib.fs2_debug_mt_speculate(f._h, -1, sc), f._h)
     f.close()
     state_digest = hashlib.sha1(np.random.get_state()[1].tobytes()).hexdigest()[:12]
     t1 = time.perf_counter()
@@ -412,9 +421,14 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
     note = ("FastSLAM2.iterate() with numpy's legacy RNG (the reference's draws, bit for bit); "
             + ("drawn on the GPU from np.random's state (MT19937 + polar method, fs2_mt_draw)" if rng == "numpy"
                else "drawn by numpy on one host core (host-RNG bound)"))
+    if rng == "numpy":
+        note += ("; each scan's draw begun when the scan before completed (speculative, fs2.h "
+                 "fs2_debug_mt_speculate)" if spec else "; speculation off: each draw begun by its own iterate()")
     return {"value": n * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k, "resamples": res,
             "ms_per_scan_median": float(np.median(each)) * 1e3,
+            "ms_each": [round(e * 1e3, 3) for e in each],
             "window": f"scans {warm}..{scans - 1} (the headline's)",
+            "speculative_draws": {"taken": int(sc[0]), "dropped": int(sc[1])},
             "host_rng_ms": rng_ms, "rng": rng, "numpy_state_sha1": state_digest, "note": note}
 
 

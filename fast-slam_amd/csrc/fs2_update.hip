@@ -351,7 +351,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     FS2_PHASE(0);
     // __move_particle (fast_slam_2.py:69-87)
     if (live && P.do_move) {
-        const double nz = P.noise ? P.noise[i]
+        // (a speculative numpy draw is made unscaled: numpy's loc + scale gauss here)
+        const double nz = P.noise ? (P.noise_unscaled ? 0.0 + __dmul_rn(P.noise_scale, P.noise[i]) : P.noise[i])
                                   : P.sigma * philox_normal(P.seed, P.scan, (uint64_t)(P.gidx0 + i));
         double ntr, nrot;
         if (P.rotation != 0.0) {
