@@ -38,6 +38,7 @@ fi
 if has prof; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run -- python bench.py --no-cpu-baseline --no-extras > gpurun_out/prof.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof.log; exit 5; }
   python scripts/prof_summary.py /tmp/prof gpurun_out/prof_summary.txt "${PROF_TITLE:-}" > /dev/null && head -14 gpurun_out/prof_summary.txt
+  python3 scripts/timeline.py "$(find /tmp/prof -name '*.db' | sort | tail -n 1)" 23 > gpurun_out/bench_timeline.txt || echo "(no timeline)"
 fi
 if has dltl; then
   timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/dl -o dl -- python3 scripts/dropin_probe.py > gpurun_out/dropin_probe.log 2>&1 || { echo dropin trace failed; tail -20 gpurun_out/dropin_probe.log; exit 9; }
