@@ -528,6 +528,7 @@ struct fs2_handle {
         fs2_iter_stats st{};
     } stash;
     uint32_t *gen_dev = nullptr;           // the current set is (gen & 1) == cur (one GPU)
+    unsigned long long *go_dev = nullptr;  // one GPU: publication sequence of the last resampling scan (the gather's marker)
     BufSet *sets_dev = nullptr;            // [2]
     uint64_t submitted = 0;                // scans submitted (parity)
     uint64_t overlapped = 0;               // scans whose candidate pass ran beside the previous tail
@@ -1716,7 +1717,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->uop); hipFree(h->np_tail_g);
     hipFree(h->peers_dev); hipFree(h->ep_dev); hipFree(h->epochs_dev);
     hipFree(h->part_pose);
-    hipFree(h->gen_dev); hipFree(h->sets_dev);
+    hipFree(h->gen_dev); hipFree(h->sets_dev); hipFree(h->go_dev);
     hipFree(h->wpart); hipFree(h->cpart); hipFree(h->part_sq); hipFree(h->part_best_w); hipFree(h->part_best_i); hipFree(h->part_slots);
     hipFree(h->part_maxcnt); hipFree(h->cbuf); hipFree(h->bsum);
     hipFree(h->stats_dev); hipFree(h->noise_dev); hipFree(h->u0_dev); hipFree(h->assoc_dev);
@@ -1834,6 +1835,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->cpart, 2 * nb * 8 * kNumCounters) == hipSuccess;   // [2]: by scan parity
     ok &= alloc((void **)&h->gen_dev, 4) == hipSuccess;
+    ok &= alloc((void **)&h->go_dev, 8) == hipSuccess;
     ok &= alloc((void **)&h->sets_dev, 2 * sizeof(BufSet)) == hipSuccess;
     ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
     ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
@@ -1896,6 +1898,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     if (!ok) return fail(set_err(&h->err, FS2_ERR_OOM, "device allocation failed for %lld particles", (long long)n));
     if (hipMemsetAsync(h->cpart, 0, 2 * nb * 8 * kNumCounters, h->stream) != hipSuccess ||
         hipMemsetAsync(h->gen_dev, 0, 4, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->go_dev, 0, 8, h->stream) != hipSuccess ||
         hipMemsetD32Async((hipDeviceptr_t)h->slb, 0x7f7fffff, 1, h->stream) != hipSuccess)   // FLT_MAX: no mirror yet
         return fail(set_err(&h->err, FS2_ERR_HIP, "state initialisation failed"));
     // Particle.__init__: (0, 0, 0), weight 1/NUM_PARTICLES, empty map (particle.py:11-20)
@@ -2346,9 +2349,19 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
             cp.s_entry = &h->stats_dev->offset;
             HIP_TRY(h, launch_chain_walk_from(cp, s));
         }
+        // one GPU: the post-resample estimate comes from the sources (k_ranges), so the
+        // scan is published before the gather -- the host returns and enqueues the
+        // next scan while the maps are copied, instead of after
+        if (!sh) {
+            rs.est_early = 1;
+            rs.go = h->go_dev;
+            rs.go_seq = pseq;
+        }
         // every local output is written below: the output ranges of the local
         // sources (k_ranges) and of the received ones (k_scatter_recv) partition them
         HIP_TRY(h, launch_resample_ranges(rs, s));
+        if (!sh)
+            HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s, nullptr));
         if (sh) {
             rc = exchange_particles(h, rs);
             if (rc) return rc;
@@ -2395,8 +2408,8 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
     // GPU: together with the post-resample estimate, in one launch)
     if (sh)
         HIP_TRY(h, launch_publish(h->stats_dev, h->pub_stats_dev, h->pub_flag_dev, pseq, s, prof ? E[3] : nullptr));
-    else
-        HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s, prof ? E[3] : nullptr));
+    else if (prof)
+        HIP_TRY(h, hipEventRecord(E[3], s));   // (the tail's end: after the gather, published before it)
     h->stats_clean = true;
     h->pending.on = true;
     h->pending.seq = pseq;

@@ -79,6 +79,11 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         fold_counters(P.cpart, P.ncpart, P.cstats, (int)(blockIdx.x - ngroups), s_c);
         return;
     }
+    // this thread's term, requested before the block-prefix loads below (one memory
+    // latency for both)
+    const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    const bool valid = i < P.n;
+    const double a = valid ? P.a[i] : 0.0;
     {
         // estimates of the chain at this workgroup's four 256-term block starts:
         // the block sums before them in any order (the margin bounds every order).
@@ -115,11 +120,8 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     }
     FS2_TS(0, 1);
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int64_t i = (int64_t)blockIdx.x * 1024 + t;
     const int64_t k = (int64_t)blockIdx.x * kChainGroup + wid;
     const int64_t nu = (P.n + kUnit - 1) / kUnit;
-    const bool valid = i < P.n;
-    const double a = valid ? P.a[i] : 0.0;
     const double incl = wave_incl_scan_f64(a);
     if (lane == 63) s_ws[wid] = incl;
     __syncthreads();

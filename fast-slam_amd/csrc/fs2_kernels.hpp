@@ -526,6 +526,13 @@ struct ResampleParams {
     // an output owns a page only when its source fills one output in all (a page sent
     // by reference must not be written in place on the sender)
     int32_t refs;
+    // one GPU: the post-resample estimate from the sources (k_ranges' partials), so
+    // k_tail_single publishes the scan before the gather; the gather then runs on
+    // a resample marker that outlives the publication's reset of the stats
+    // (*go == go_seq, written by k_tail_single)
+    int32_t est_early;
+    unsigned long long *go;
+    unsigned long long go_seq;
 };
 
 // A 64-term chain unit that is not one translation, as up to kChainSegs

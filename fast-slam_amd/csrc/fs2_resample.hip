@@ -288,6 +288,19 @@ __global__ __launch_bounds__(64) void k_finalize_chunked(const ReduceParams P) {
     double bv = -INFINITY, px = 0.0, py = 0.0, pyaw = 0.0;
     int64_t bi = INT64_MAX;
     int mc = 0;
+    // np.sum's full chunks (numpy's top node: half 2c + half 2c + 1), one per lane and
+    // register, loaded with the partials below and added in order from registers
+    // (readlane) by the whole wave: no LDS round trip per step of the serial sum
+    const int64_t nfull = P.n / kNpChunk;
+    const bool creg = nfull <= 128;
+    double cv[2] = {0.0, 0.0};
+    if (creg) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t c = lane + 64 * j;
+            if (c < nfull) cv[j] = P.np_part[2 * c] + P.np_part[2 * c + 1];
+        }
+    }
     for (int k0 = 0; k0 < P.nparts; k0 += 256) {
         double w4[4], x4[4], y4[4], a4[4], s4[4];
         int64_t i4[4];
@@ -334,6 +347,16 @@ __global__ __launch_bounds__(64) void k_finalize_chunked(const ReduceParams P) {
         }
     }
     mc = wave_max_i(mc);
+    // the full chunks' sums in order (wave-uniform: every lane adds the same values)
+    double sqr = 0.0;
+    if (creg) {
+        const int n0 = (int)min<int64_t>(nfull, 64);
+        for (int c = 0; c < n0; ++c) {
+            const double v = bcast(cv[0], c);
+            sqr = (c == 0) ? v : sqr + v;
+        }
+        for (int c = 64; c < (int)nfull; ++c) sqr = sqr + bcast(cv[1], c - 64);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -341,12 +364,13 @@ __global__ __launch_bounds__(64) void k_finalize_chunked(const ReduceParams P) {
     if (lane == 0) {
         // np.sum(weights ** 2): chunk c = half 2c + half 2c + 1 (numpy's top node),
         // a partial last chunk whole; the chunk sums in order
-        const int64_t nfull = P.n / kNpChunk;
         auto part = [&](int64_t k) -> double { return k < kNpStage ? s_np[k] : P.np_part[k]; };
-        double sq = 0.0;
-        for (int64_t c = 0; c < nfull; ++c) {
-            const double v = part(2 * c) + part(2 * c + 1);
-            sq = (c == 0) ? v : sq + v;
+        double sq = sqr;
+        if (!creg) {
+            for (int64_t c = 0; c < nfull; ++c) {
+                const double v = part(2 * c) + part(2 * c + 1);
+                sq = (c == 0) ? v : sq + v;
+            }
         }
         if (P.n % kNpChunk) sq = (nfull == 0) ? part(2 * nfull) : sq + part(2 * nfull);
         RankRecord r{};
@@ -758,6 +782,25 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     if (P.flip_margin > 0.0) {
         const unsigned long long ba = block_sum_u64<kBlock>(amb, lds_u);
         if (threadIdx.x == 0 && ba) atomicAdd(&P.stats->reduce_amb, ba);
+        __syncthreads();             // lds_u is reused below
+    }
+    if (P.est_early) {
+        // the outputs' first maximum (fast_slam_2.py:201-210 after :196): outputs are
+        // in source order and copy their source's weight, so it is the first output
+        // of the first heaviest source that has outputs; and the slots they refer to
+        __shared__ double lds_d[kBlock / 64];
+        __shared__ int64_t lds_l[kBlock / 64];
+        const bool has = i < P.n && llo <= lhi;
+        double bv = has ? P.w[i] : -INFINITY;
+        int64_t bi = has ? llo - P.ao : INT64_MAX;
+        const unsigned long long sl = has ? (unsigned long long)(lhi - llo + 1) * (unsigned long long)P.cnt[i] : 0ull;
+        const unsigned long long bs = block_sum_u64<kBlock>(sl, lds_u);
+        block_argmax<kBlock>(bv, bi, lds_d, lds_l);
+        if (threadIdx.x == 0) {
+            P.part_best_w[blockIdx.x] = bv;
+            P.part_best_i[blockIdx.x] = bi;
+            P.part_slots[blockIdx.x] = bs;
+        }
     }
 }
 
@@ -1391,7 +1434,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     __shared__ int s_src[kBlock];    // source workgroup of each local output (-1: none)
     __shared__ int s_sb[kBlock];     // the distinct ones, in order
     __shared__ int s_wc[kBlock / 64];
-    if (!P.stats->resampled) return;
+    if (P.go ? *(volatile const unsigned long long *)P.go != P.go_seq : !P.stats->resampled) return;
     const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     __shared__ unsigned long long lds_u[kBlock / 64];
     const bool bb = P.obbox != nullptr && P.map.bbox != nullptr;
@@ -1572,9 +1615,16 @@ __device__ void estimate_body(const ResampleParams &P, int32_t nparts) {
         r.best_w = bv;
         r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.ao + bi;
         if (bi != INT64_MAX) {
-            r.pose[0] = P.ox[bi];
-            r.pose[1] = P.oy[bi];
-            r.pose[2] = P.oyaw[bi];
+            if (P.est_early) {          // before the gather: the output's source (k_ranges)
+                const int32_t s = P.out_src[bi];
+                r.pose[0] = P.x[s];
+                r.pose[1] = P.y[s];
+                r.pose[2] = P.yaw[s];
+            } else {
+                r.pose[0] = P.ox[bi];
+                r.pose[1] = P.oy[bi];
+                r.pose[2] = P.oyaw[bi];
+            }
         }
         *P.rec = r;
     }
@@ -1596,6 +1646,7 @@ __global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, co
     if (threadIdx.x == 0) {
         global_best_body(P);
         if (R.gen) *R.gen += 1u;        // the other set is current (BufSet; the next kernels read it)
+        if (R.go) *R.go = R.go_seq;     // (published before the gather: it runs on this marker)
     }
     __syncthreads();
     publish_body(P.stats, host_stats, host_flag, seq);
