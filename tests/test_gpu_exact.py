@@ -46,7 +46,7 @@ def expected(w, u0):
     return seq_sum(w), wn, ne, rs, src
 
 
-def run_tail(fs, w, u0, reduce):
+def run_tail(fs, w, u0, reduce, with_pose=False):
     """One scan without measurements and without motion: only the tail
     (normalise, N_eff, resample, estimate) changes the state; x = particle index
     reveals each output's source."""
@@ -56,7 +56,16 @@ def run_tail(fs, w, u0, reduce):
     pose, st = f.step(0.0, 0.0, np.zeros((0, 2)), None, np.zeros(N), u0)
     x, _, _, wn, _, _ = f.get_state()
     f.close()
+    if with_pose:
+        return st, x.astype(np.int64), wn, pose
     return st, x.astype(np.int64), wn
+
+
+def expected_estimate(wn, src):
+    """fast_slam_2.py:201-210 after the resample: Python's max over the particles by
+    weight, the first of equal ones; x of output m is its source's index."""
+    ow = wn[src]
+    return float(src[int(np.argmax(ow))])
 
 
 def cases():
@@ -90,6 +99,16 @@ def cases():
         n = 2 * 8192 + tail
         out.append((f"tail_{tail}", rng.random(n) ** 2, 0.3 / n))
     out.append(("cfg3_size", rng.lognormal(0.0, 2.0, 1_000_000), 0.77e-6))
+    # the heaviest particle receives no output: the undivided weights below 1e-5 (Q6)
+    # sum past 1 before it, so the post-resample estimate is another particle's
+    n = 200_003
+    w = np.full(n, 9e-6)
+    w[150_000] = 0.01
+    out.append(("heavy_unsampled", w, 0.4 / n))
+    # equal heaviest weights far apart: the estimate is the first one's first output
+    w = rng.random(n) * 1e-7
+    w[70_001] = w[20_000] = 0.25
+    out.append(("estimate_tie", w, 0.3 / n))
     # a diverged filter: every likelihood underflowed (the total is 0, the
     # reference resets the weights to 1/N) -- the chain runs on zeros throughout
     out.append(("all_zero", np.zeros(1_000_000), 0.5e-6))
@@ -106,13 +125,36 @@ def cases():
 @pytest.mark.parametrize("name,w,u0", cases(), ids=[c[0] for c in cases()])
 def test_exact_tail_matches_reference_order(fs, name, w, u0):
     total, wn, ne, rs, src = expected(w, u0)
-    st, xs, wg = run_tail(fs, w, u0, "exact")
+    st, xs, wg, pose = run_tail(fs, w, u0, "exact", with_pose=True)
     assert st.total_weight == total, name
     assert np.array_equal(wg, wn[src]), name
     assert st.n_eff == ne, name
     assert bool(st.resampled) == rs, name
     assert np.array_equal(xs, src), name
     assert st.reduce_ambiguous == 0
+    # the estimate (published before the resample's gather on one GPU)
+    assert pose[0] == expected_estimate(wn, src), name
+
+
+@pytest.mark.parametrize("reduce,n", [("sequential", 3001), ("parallel", 150_000)])
+def test_post_resample_estimate_other_modes(fs, reduce, n):
+    """The same estimate rule in the sequential and the tree reduction modes: at
+    3001 particles two equal heaviest weights (the first one's first output); at
+    150 000 the heaviest particle left without an output (the undivided weights
+    below 1e-5 pass 1 before it)."""
+    w = np.full(n, 9e-6)
+    w[(3 * n) // 4] = 0.01
+    if n < 10_000:
+        w[n // 3] = 0.01
+    w[n // 8] = w[n // 5] = 3e-6    # below 1e-5, undivided (lighter than the rest)
+    u0 = 0.45 / n
+    total, wn, ne, rs, src = expected(w, u0)
+    assert rs
+    st, xs, _, pose = run_tail(fs, w, u0, reduce, with_pose=True)
+    # (tree sums: boundaries within the rounding bound may go the other way, and
+    # are counted; the estimate is checked on the resample that ran)
+    assert np.array_equal(xs, src) or (reduce == "parallel" and st.reduce_ambiguous > 0)
+    assert pose[0] == expected_estimate(wn, xs)
 
 
 def test_auto_is_exact_above_4096(fs):
