@@ -30,6 +30,10 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+# libfs2 keeps closed handles' VMM chunks for later growths only when asked (default
+# off); this process closes and re-creates handle sets of the headline's size, whose
+# first growth otherwise waits for the driver's deferred release
+os.environ.setdefault("FS2_VMM_CACHE_MB", "131072")
 sys.path.insert(0, os.path.join(REPO, "fast-slam_amd"))
 sys.path.insert(0, REPO)
 

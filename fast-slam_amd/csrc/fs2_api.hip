@@ -191,8 +191,11 @@ static hipError_t gm_relocate(GrowMem &g, size_t need) {
 // in chunks of power-of-two sizes (kChunkMax, or the remainder rounded up), kept
 // here on close and taken back by any later growth that needs a chunk of that size:
 // no new physical memory, nothing for the driver to reclaim.  FS2_VMM_CACHE_MB caps
-// what is kept (default 128 GiB, 0 keeps none); fs2_release_cached_memory() and an
-// allocation that runs out of device memory release it.
+// what is kept (read at every close; default 0: nothing is kept, a closed handle's
+// memory goes back to the device for PyTorch or any other allocator in the process
+// -- a caller that closes and re-creates large handles opts in, as bench.py does);
+// fs2_release_cached_memory() and an allocation that runs out of device memory
+// release it.
 constexpr size_t kChunkMax = size_t(256) << 20;
 static size_t chunk_size(size_t remaining, size_t gran) {
     if (remaining >= kChunkMax) return kChunkMax;
@@ -211,11 +214,8 @@ struct ChunkCache {
     std::vector<Chunk> chunks;
     size_t bytes = 0;
     size_t cap() const {
-        static const size_t c = [] {
-            const char *e = std::getenv("FS2_VMM_CACHE_MB");
-            return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)131072) << 20;
-        }();
-        return c;
+        const char *e = std::getenv("FS2_VMM_CACHE_MB");
+        return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)0) << 20;
     }
     bool put(const Chunk &c) {
         std::lock_guard<std::mutex> lk(mu);
@@ -1274,6 +1274,10 @@ static int reserve_xfer_table(fs2_handle *h, int64_t cap, int64_t nrows, bool in
         h->xt_ref = h->xt_uidx = h->xt_cmask = h->xt_cbase = nullptr;
         h->xt_cap = 0;
         HIP_TRY(h, hipMalloc((void **)&h->xt_key, (size_t)cap * 8));
+        // zeroed once here: page_refs' k_localize and the gather key it by epoch
+        // (epoch 0 is never used) and never clear it, so a table allocated over
+        // freed memory must not hold keys that look live
+        HIP_TRY(h, hipMemsetAsync(h->xt_key, 0, (size_t)cap * 8, s));
         HIP_TRY(h, hipMalloc((void **)&h->xt_ref, (size_t)cap * 4));
         HIP_TRY(h, hipMalloc((void **)&h->xt_uidx, (size_t)cap * 4));
         HIP_TRY(h, hipMalloc((void **)&h->xt_cmask, (size_t)cap * 4));
@@ -1661,6 +1665,12 @@ const char *fs2_last_error(const fs2_handle *h) {
 
 static void free_handle(fs2_handle *h) {
     if (!h) return;
+    // the handle's device is current while it is torn down (the device-wide
+    // synchronisations below must drain *its* device; ranks of one process may sit
+    // on several GPUs), and the caller's device is restored at the end
+    int prev_dev = -1;
+    if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
+    if (prev_dev != h->cfg.device) (void)hipSetDevice(h->cfg.device);
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->mt.dstream) hipStreamSynchronize(h->mt.dstream);   // (a speculative draw)
     // In-place pools (VMM chunks): nothing of this process may still be in flight
@@ -1749,7 +1759,9 @@ static void free_handle(fs2_handle *h) {
             for (auto &e : set) hipEventDestroy(e);
     delete h->tp;
     if (h->stream) hipStreamDestroy(h->stream);
+    const int dev = h->cfg.device;
     delete h;
+    if (prev_dev >= 0 && prev_dev != dev) (void)hipSetDevice(prev_dev);
 }
 
 int fs2_create(const fs2_config *cfg, fs2_handle **out) {
@@ -3959,6 +3971,15 @@ int fs2_debug_noise(fs2_handle *h, double *out) {
         std::memcpy(out, h->noise_pin, sizeof(double) * h->n);
     }
     return FS2_OK;
+}
+
+int64_t fs2_debug_out_src(fs2_handle *h, int32_t *out, int64_t capacity) {
+    if (!h || !out || capacity < h->n)
+        return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_debug_out_src: null argument or capacity < n");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    HIP_TRY(h, hipMemcpy(out, h->out_src, sizeof(int32_t) * (size_t)h->n, hipMemcpyDeviceToHost));
+    return h->n;
 }
 
 int fs2_debug_mt_log(int32_t device, const double *x, int64_t n, double *out, int32_t *amb, int32_t on_host) {

@@ -96,6 +96,12 @@ inline bool wait_fd(int fd, short ev, int ms) {
     pollfd p{fd, ev, 0};
     return poll(&p, 1, ms) == 1 && (p.revents & ev);
 }
+// the connected peer runs under this process's user (SO_PEERCRED)
+inline bool peer_is_us(int fd) {
+    ucred cr{};
+    socklen_t len = sizeof cr;
+    return getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &len) == 0 && len == sizeof cr && cr.uid == getuid();
+}
 inline int accept_one(int lfd, int ms) {
     if (!wait_fd(lfd, POLLIN, ms)) return -1;
     return accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
@@ -161,20 +167,30 @@ inline ssize_t recv_msg(int fd, void *buf, size_t len, int *fds, int maxfd, int 
 
 // hipMemImportFromShareableHandle takes a pointer to the descriptor on the HIP 7.0
 // runtime PyTorch's wheel brings (the descriptor itself crashes it) and the
-// descriptor itself on ROCm 7.2 (a pointer is refused there): profiles/r05_ipc_probe.txt
+// descriptor itself on ROCm 7.2 (a pointer is refused there): profiles/r05_ipc_probe.txt.
+// Only those two measured ABIs are used; any other runtime version fails the
+// import cleanly (page_refs then falls back to the page transfer on every rank)
+// rather than probing with a value the runtime might dereference.
+enum class FdAbi { pointer, value, unknown };
+inline FdAbi fd_abi(int ver) {
+    if (ver >= 70000000 && ver < 70100000) return FdAbi::pointer;     // 7.0.x (measured: 7.0.51831)
+    if (ver >= 70200000 && ver < 70300000) return FdAbi::value;       // 7.2.x (measured: 7.2.26015, ROCm 7.2.0)
+    return FdAbi::unknown;
+}
 inline hipError_t import_fd(hipMemGenericAllocationHandle_t *hd, int fd) {
     static const int ver = [] {
         int v = 0;
         return hipRuntimeGetVersion(&v) == hipSuccess ? v : 0;
     }();
     int f = fd;
-    if (ver > 0 && ver < 70100000) return hipMemImportFromShareableHandle(hd, &f, hipMemHandleTypePosixFileDescriptor);
-    hipError_t e = hipMemImportFromShareableHandle(hd, (void *)(intptr_t)fd, hipMemHandleTypePosixFileDescriptor);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        e = hipMemImportFromShareableHandle(hd, &f, hipMemHandleTypePosixFileDescriptor);
+    switch (fd_abi(ver)) {
+    case FdAbi::pointer:
+        return hipMemImportFromShareableHandle(hd, &f, hipMemHandleTypePosixFileDescriptor);
+    case FdAbi::value:
+        return hipMemImportFromShareableHandle(hd, (void *)(intptr_t)fd, hipMemHandleTypePosixFileDescriptor);
+    default:
+        return hipErrorNotSupported;
     }
-    return e;
 }
 
 class Transport {
@@ -344,16 +360,31 @@ class Transport {
             if (turn == me) {
                 peers[me] = base;
                 // serve every other rank: its rank, then the sizes, then the descriptors
-                // (an empty table when this rank has nothing to give: its peers fail)
-                for (int k = 0; k < G - 1; ++k) {
-                    const int c = lfd_ >= 0 ? uds::accept_one(lfd_, ms) : -1;
+                // (an empty table when this rank has nothing to give: its peers fail).
+                // Only a process of this user that names a rank of the group not yet
+                // served gets anything: any other connection is closed unanswered and
+                // does not take a peer's place (the socket name is visible in
+                // /proc/net/unix).
+                std::vector<uint8_t> served((size_t)G, 0);
+                const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+                for (int k = 0; k < G - 1;) {
+                    const int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                                         deadline - std::chrono::steady_clock::now()).count();
+                    const int c = (lfd_ >= 0 && left > 0) ? uds::accept_one(lfd_, left) : -1;
                     if (c < 0) {
                         note("accept");
                         break;
                     }
                     int32_t who = -1;
                     int nf = 0;
-                    if (uds::recv_msg(c, &who, sizeof who, nullptr, 0, &nf, ms) != (ssize_t)sizeof who) note("peer rank");
+                    const bool got = uds::recv_msg(c, &who, sizeof who, nullptr, 0, &nf, std::max(left, 1)) ==
+                                     (ssize_t)sizeof who;
+                    if (!got || !uds::peer_is_us(c) || who < 0 || who >= G || who == me || served[(size_t)who]) {
+                        close(c);
+                        continue;
+                    }
+                    served[(size_t)who] = 1;
+                    ++k;
                     std::vector<uint64_t> hdr(1 + sizes.size());
                     hdr[0] = have ? sizes.size() : 0;
                     for (size_t i = 0; have && i < sizes.size(); ++i) hdr[1 + i] = sizes[i];

@@ -28,6 +28,14 @@ from .utils.serializer import Serializer
 _OUT_OF_SCOPE = {"EvaluationUtils"}
 
 
+def release_cached_memory() -> int:
+    """Release the device memory libfs2 keeps from closed handles for later pool
+    growth (kept only when FS2_VMM_CACHE_MB opts in; fs2.h
+    fs2_release_cached_memory).  Returns the bytes released."""
+    from . import _native
+    return int(_native.load().fs2_release_cached_memory())
+
+
 def __getattr__(name):
     if name in _OUT_OF_SCOPE:
         raise ImportError(f"fast_slam_2.{name} drives the JdeRobot simulator (HAL), which this "
@@ -36,4 +44,5 @@ def __getattr__(name):
 
 
 __all__ = ["FastSLAM2", "HoughTransformation", "ICP", "LineFilter", "DirectedPoint", "EvaluationResults", "Landmark",
-           "Measurement", "Particle", "Point", "Robot", "GeometryUtils", "LandmarkUtils", "Serializer"]
+           "Measurement", "Particle", "Point", "Robot", "GeometryUtils", "LandmarkUtils", "Serializer",
+           "release_cached_memory"]

@@ -226,8 +226,8 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out);
 void fs2_destroy(fs2_handle *h);
 
 /* Device memory of closed handles kept for reuse: fs2_destroy keeps the physical
- * chunks of the pools that grow in place (up to FS2_VMM_CACHE_MB, default 128 GiB;
- * 0 keeps none) and later handles of the process grow into them before they ask
+ * chunks of the pools that grow in place (up to FS2_VMM_CACHE_MB MiB, read at every close;
+ * default 0: nothing is kept, opt in when closing and re-creating large handles) and later handles of the process grow into them before they ask
  * the driver for new memory -- a large allocation right after tens of GB were
  * released waited seconds for the driver.  This releases every
  * kept chunk; returns the bytes released. */
@@ -435,6 +435,10 @@ int fs2_debug_vm_fail_after_relocate(int32_t on);
 /* Test hook: the handle's motion-noise buffer (N_local values: the last scan's
  * injected draws, or fs2_mt_draw's) into out. */
 int fs2_debug_noise(fs2_handle *h, double *out);
+/* The source of each local output of the last resample (out[n_local]: >= 0 a
+ * local source index, < 0 -(k+1) the k-th received particle); returns n_local
+ * or a negative error.  For the drift study (scripts/drift_study.py). */
+int64_t fs2_debug_out_src(fs2_handle *h, int32_t *out, int64_t capacity);
 /* Test hook of fs2_mt_draw's jump-ahead: the stream words x[J + 1 .. J + 624]
  * after the key x[0 .. 624) (J >= 1), as the GF(2) combination of x[1 .. 20561)
  * given by x^J mod the characteristic polynomial (host arithmetic). */

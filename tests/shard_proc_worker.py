@@ -48,8 +48,12 @@ def main(argv):
     key = bytes.fromhex(argv[6])
     out = argv[7]
     mode = argv[8] if len(argv) > 8 else "peaked"
-    import torch  # noqa: F401  -- one HIP runtime in the process
+    if os.environ.get("FS2_HIP_RUNTIME", "").lower() != "system":
+        import torch  # noqa: F401  -- one HIP runtime in the process
+    # (FS2_HIP_RUNTIME=system: this process never imports torch; libfs2 and RCCL run
+    # on the system ROCm runtime they were built against)
     import fast_slam_2
+    from fast_slam_2 import _native as nat
     import fs2_synthetic as syn
     from gpu_util import configure
     configure()
@@ -111,7 +115,8 @@ def main(argv):
     np.savez(out, first=a, count=b - a, assoc=np.stack(assoc), x=xs, y=ys, yaw=yaws, w=ws, cnt=cnts, lm=lms,
              sent_particles=prof["sent_particles"], sent_rows=prof["sent_rows"], sent_pages=prof["sent_pages"],
              migrations=prof["migrations"], scan_allocs=prof["scan_allocs"], page_refs=prof["page_refs"],
-             localized_pages=prof["localized_pages"],
+             localized_pages=prof["localized_pages"], hip_runtime=str(nat.HIP_RUNTIME[0]),
+             torch_imported=("torch" in sys.modules),
              np_key=np.random.get_state()[1], np_pos=np.random.get_state()[2],
              **{k: np.array(v) for k, v in rec.items()})
     return 0

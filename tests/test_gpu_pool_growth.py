@@ -12,6 +12,7 @@ grow by 4 N per scan and the pool must grow several times.  Every scan is
 compared with the C oracle, and no scan takes more than 1 ms longer than the
 median of its neighbours.
 """
+import os
 import time
 
 import numpy as np
@@ -98,6 +99,22 @@ def test_growth_after_close_is_fast():
     import fast_slam_2
     import fs2_synthetic as syn
     G, N, L, S = 8, 1_000_000, 500, 9
+    # the chunk cache is opt-in (by default a closed handle's memory
+    # goes back to the device); this process closes and re-creates large handles
+    old = os.environ.get("FS2_VMM_CACHE_MB")
+    os.environ["FS2_VMM_CACHE_MB"] = "131072"
+    try:
+        _two_sets(G, N, L, S, bench, fast_slam_2, syn, threading)
+    finally:
+        if old is None:
+            os.environ.pop("FS2_VMM_CACHE_MB", None)
+        else:
+            os.environ["FS2_VMM_CACHE_MB"] = old
+        released = fast_slam_2.release_cached_memory()
+        print(f"released {released >> 20} MiB of cached chunks")
+
+
+def _two_sets(G, N, L, S, bench, fast_slam_2, syn, threading):
     for rep in range(2):
         key = b"grow" + bytes([rep]) * 124
         # (a record pool just above the maps: the records the scans write make

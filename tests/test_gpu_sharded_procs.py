@@ -18,6 +18,9 @@ numpy's global stream drawn on the device (fs2_mt_draw) on every rank, shards
 that move included, and checks numpy's final state too.  The "refs" case sends
 page references instead of pages: every rank maps the other processes' pools (VMM
 chunks exported as file descriptors over Unix sockets, fs2_comm.hpp share_vm).
+"refs_system" is the same on the system ROCm 7.2 runtime (FS2_HIP_RUNTIME=system,
+rank processes that never import torch): the import branch that passes the
+descriptor by value (fs2_comm.hpp import_fd), which the wheel's HIP 7.0 never takes.
 """
 import os
 import subprocess
@@ -33,7 +36,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 @pytest.mark.parametrize("G,N,L,scans,mode", [(2, 6000, 40, 8, "peaked"), (3, 10007, 30, 8, "peaked"),
                                                (2, 6000, 24, 4, "follow"), (2, 6000, 40, 8, "numpy"),
-                                               (3, 9000, 40, 8, "refs")])
+                                               (3, 9000, 40, 8, "refs"), (3, 9000, 40, 8, "refs_system")])
 def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     import torch  # noqa: F401
     import fast_slam_2
@@ -43,9 +46,16 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     configure()
     key = os.urandom(128).hex()
     env = dict(os.environ, FS2_SHM_CHUNK=str(64 << 10), FS2_SHM_TIMEOUT_S="40")   # small mailboxes: rounds
+    wmode = mode
+    if mode == "refs_system":
+        env["FS2_HIP_RUNTIME"] = "system"
+        wmode = mode = "refs"
+        system_rt = True
+    else:
+        system_rt = False
     outs = [str(tmp_path / f"rank{r}.npz") for r in range(G)]
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "shard_proc_worker.py"), str(G), str(r),
-                               str(N), str(L), "21", str(scans), key, outs[r], mode],
+                               str(N), str(L), "21", str(scans), key, outs[r], wmode],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for r in range(G)]
     logs = []
@@ -59,6 +69,11 @@ def test_sharded_processes_match_single(G, N, L, scans, mode, tmp_path):
     for r, p in enumerate(procs):
         assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-4000:]}"
     ranks = [np.load(o) for o in outs]
+    for d in ranks:
+        if system_rt:
+            assert str(d["hip_runtime"]) == "system" and not bool(d["torch_imported"])
+        else:
+            assert bool(d["torch_imported"])
 
     wl, x, y, yaw, w, cnt, lm = workload(N, L, 21, mode, G)
     cap = L + 4 * scans + 8
