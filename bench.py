@@ -370,6 +370,7 @@ def robustness(args, f, L, first_scan):
     out["no_gate_filter"] = timed_scans(g, scans, gm.__getitem__, syn.odometry, 3)
     out["no_gate_filter"]["note"] = "grid map, every slot's fp64 record read (no mirrors, no page boxes)"
     g.close()
+    out["appended_maps"] = appended_maps(args, L, n)
     out["sharded_local_g2"] = sharded_local(args, L, n)
     out["sharded_local_g8"] = sharded_local(args, L, n, G=8, page_refs="on")
     # the same with whole pages sent (round 3's transfer; A/B of the page references)
@@ -379,6 +380,40 @@ def robustness(args, f, L, first_scan):
     out["dropin_iterate_no_speculation"] = dropin(args, L, n, spec=False)
     out["dropin_iterate_host_rng"] = dropin(args, L, n, rng="numpy-host")
     return out
+
+
+def appended_maps(args, L, n, per_scan=8):
+    """The reference's own operating mode: maps grown by appends
+    from fs2_create's empty maps (fast_slam_2.py:20-31 -- every particle at the
+    origin, no landmark) through the misses of a robot discovering the L grid
+    landmarks in observation order (a lawnmower sweep, fs2_synthetic.
+    buildup_measurements: 8 new landmarks and 2 re-observations per scan, standing
+    still), so pages hold landmarks in the order they were seen and no import
+    layout is involved; then the headline's 3 warm-up + 20 timed scans of
+    measurements on those maps."""
+    import fast_slam_2
+    import fs2_synthetic as syn
+    import torch
+    nb = syn.buildup_scans(L, per_scan)
+    cap = L + 40
+    g = fast_slam_2.FastSLAM2(n, rng="device", seed=args.seed, landmark_capacity=cap, verbose=False)
+    t0 = time.perf_counter()
+    res_b = 0
+    for s in range(nb):
+        _, st = g.step(0.0, 0.0, np.ascontiguousarray(syn.buildup_measurements(L, s, args.seed, per_scan)))
+        res_b += st.resampled
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    cnt = g.get_state(lm_cap=0)[4] if n <= 2_000_000 else None
+    meas = {s: np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64) for s in range(23)}
+    r = timed_scans(g, list(range(23)), meas.__getitem__, syn.odometry, 3)
+    g.close()
+    r.update(buildup_scans=nb, buildup_s=t_build, buildup_resamples=res_b,
+             map_size_after_buildup=(None if cnt is None else [int(cnt.min()), int(cnt.max())]),
+             note=f"maps grown from empty by appends in observation order ({nb} scans of {per_scan} new "
+                  f"landmarks + 2 re-observations, lawnmower discovery order), then the headline's "
+                  f"measurement stream; compare pages_opened_per_particle_scan with the imported layout's")
+    return r
 
 
 def dropin(args, L, n, scans=23, warm=3, rng="numpy", spec=True):

@@ -197,6 +197,8 @@ static hipError_t gm_relocate(GrowMem &g, size_t need) {
 // fs2_release_cached_memory() and an allocation that runs out of device memory
 // release it.
 constexpr size_t kChunkMax = size_t(256) << 20;
+constexpr size_t kGuardBytes = size_t(64) << 10;     // FS2_GUARD: pattern after each buffer
+constexpr int kGuardByte = 0xa5;
 static size_t chunk_size(size_t remaining, size_t gran) {
     if (remaining >= kChunkMax) return kChunkMax;
     size_t c = gran;
@@ -609,6 +611,12 @@ struct fs2_handle {
     double *est_base = nullptr;
     int32_t *uop = nullptr;
     NpTailPlan *np_tail_g = nullptr;
+    // FS2_GUARD: the pattern after each buffer fs2_create made (fs2_debug_check_guards)
+    struct Guard {
+        char *at;
+        const char *name;
+    };
+    std::vector<Guard> guards;
 
     MapRef map() const {
         return MapRef{pool, pt[cur], std::max<int64_t>(n, 1), rows, rpool, frame, slb, row_boxes(cur),
@@ -1809,77 +1817,95 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     const int64_t n = std::max<int64_t>(h->n, 1);
     const int64_t nb = (n + kBlock - 1) / kBlock;
     const int64_t nsb = (n + 1023) / 1024;
-    auto alloc = [&](void **p, size_t bytes) {
-        hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 16);
+    // FS2_GUARD=1 (tests): every buffer below is followed by kGuardBytes of a known
+    // pattern that fs2_debug_check_guards verifies -- a kernel writing past the end
+    // of one of them is found by name instead of by a fault (or by nothing)
+    const bool guard = [] {
+        const char *e = std::getenv("FS2_GUARD");
+        return e && *e && std::strcmp(e, "0") != 0;
+    }();
+    auto alloc = [&](void **p, size_t bytes, const char *name) {
+        const size_t b = bytes > 0 ? bytes : 16, tot = guard ? b + kGuardBytes : b;
+        hipError_t e = hipMalloc(p, tot);
         if (e == hipErrorOutOfMemory && g_chunks.release() > 0) {   // closed handles' kept chunks
             (void)hipGetLastError();
-            e = hipMalloc(p, bytes > 0 ? bytes : 16);
+            e = hipMalloc(p, tot);
+        }
+        if (e == hipSuccess && guard) {
+            e = hipMemset(static_cast<char *>(*p) + b, kGuardByte, kGuardBytes);
+            h->guards.push_back(fs2_handle::Guard{static_cast<char *>(*p) + b, name});
         }
         return e;
     };
+#define FS2_ALLOC(ptr, bytes) alloc((void **)&(ptr), (size_t)(bytes), #ptr)
     bool ok = true;
     for (int s = 0; s < 2; ++s) {
-        ok &= alloc((void **)&h->x[s], n * 8) == hipSuccess;
-        ok &= alloc((void **)&h->y[s], n * 8) == hipSuccess;
-        ok &= alloc((void **)&h->yaw[s], n * 8) == hipSuccess;
-        ok &= alloc((void **)&h->w[s], n * 8) == hipSuccess;
-        ok &= alloc((void **)&h->cnt[s], n * 4) == hipSuccess;
-        ok &= alloc((void **)&h->bbox[s], nb * kBBoxRows * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->x[s], n * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->y[s], n * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->yaw[s], n * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->w[s], n * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->cnt[s], n * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->bbox[s], nb * kBBoxRows * 4) == hipSuccess;
     }
-    ok &= alloc((void **)&h->nfree_dev, sizeof(int64_t)) == hipSuccess;
-    ok &= alloc((void **)&h->rnfree_dev, sizeof(int64_t)) == hipSuccess;
-    ok &= alloc((void **)&h->slb, sizeof(float)) == hipSuccess;
-    ok &= alloc((void **)&h->slb_pass, sizeof(float)) == hipSuccess;
-    ok &= alloc((void **)&h->ext_dev, sizeof(uint32_t)) == hipSuccess;
-    ok &= alloc((void **)&h->mlo, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->mhi, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->out_src, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->cand, n * 8 * kMaxCand) == hipSuccess;
-    ok &= alloc((void **)&h->ncand, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->rec, sizeof(RankRecord)) == hipSuccess;
-    ok &= alloc((void **)&h->recs, sizeof(RankRecord) * G) == hipSuccess;
-    ok &= alloc((void **)&h->totals, sizeof(double) * G) == hipSuccess;
-    ok &= alloc((void **)&h->xrow, sizeof(int64_t) * kXrowWords * G) == hipSuccess;
-    ok &= alloc((void **)&h->xmat, sizeof(int64_t) * kXrowWords * G * G) == hipSuccess;
-    ok &= alloc((void **)&h->rank_d, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->rank_e, n * 4) == hipSuccess;
-    ok &= alloc((void **)&h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
-    ok &= alloc((void **)&h->wpart, nb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->cpart, 2 * nb * 8 * kNumCounters) == hipSuccess;   // [2]: by scan parity
-    ok &= alloc((void **)&h->gen_dev, 4) == hipSuccess;
-    ok &= alloc((void **)&h->go_dev, 8) == hipSuccess;
-    ok &= alloc((void **)&h->sets_dev, 2 * sizeof(BufSet)) == hipSuccess;
-    ok &= alloc((void **)&h->part_sq, nb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->part_best_w, nb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->part_pose, nb * 24) == hipSuccess;
-    ok &= alloc((void **)&h->part_best_i, nb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->part_slots, nb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->part_maxcnt, nb * 4) == hipSuccess;
-    ok &= alloc((void **)&h->cbuf, n * 8) == hipSuccess;
-    ok &= alloc((void **)&h->bsum, nsb * 8) == hipSuccess;
-    ok &= alloc((void **)&h->stats_dev, sizeof(DevStats)) == hipSuccess;
+    ok &= FS2_ALLOC(h->nfree_dev, sizeof(int64_t)) == hipSuccess;
+    ok &= FS2_ALLOC(h->rnfree_dev, sizeof(int64_t)) == hipSuccess;
+    ok &= FS2_ALLOC(h->slb, sizeof(float)) == hipSuccess;
+    ok &= FS2_ALLOC(h->slb_pass, sizeof(float)) == hipSuccess;
+    ok &= FS2_ALLOC(h->ext_dev, sizeof(uint32_t)) == hipSuccess;
+    ok &= FS2_ALLOC(h->mlo, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->mhi, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->out_src, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->cand, n * 8 * kMaxCand) == hipSuccess;
+    ok &= FS2_ALLOC(h->ncand, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->rec, sizeof(RankRecord)) == hipSuccess;
+    ok &= FS2_ALLOC(h->recs, sizeof(RankRecord) * G) == hipSuccess;
+    ok &= FS2_ALLOC(h->totals, sizeof(double) * G) == hipSuccess;
+    ok &= FS2_ALLOC(h->xrow, sizeof(int64_t) * kXrowWords * G) == hipSuccess;
+    ok &= FS2_ALLOC(h->xmat, sizeof(int64_t) * kXrowWords * G * G) == hipSuccess;
+    ok &= FS2_ALLOC(h->rank_d, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->rank_e, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->iblk, (2 * nsb + 2) * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->wpart, nb * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->cpart, 2 * nb * 8 * kNumCounters) == hipSuccess;   // [2]: by scan parity
+    ok &= FS2_ALLOC(h->gen_dev, 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->go_dev, 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->sets_dev, 2 * sizeof(BufSet)) == hipSuccess;
+    ok &= FS2_ALLOC(h->part_sq, nb * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->part_best_w, nb * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->part_pose, nb * 24) == hipSuccess;
+    ok &= FS2_ALLOC(h->part_best_i, nb * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->part_slots, nb * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->part_maxcnt, nb * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->cbuf, n * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->bsum, nsb * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->stats_dev, sizeof(DevStats)) == hipSuccess;
     {
         const int64_t nu = (n + 63) / 64;
-        ok &= alloc((void **)&h->uinfo, nu * 4) == hipSuccess;
-        ok &= alloc((void **)&h->uol, nu * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->uinfo, nu * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->uol, nu * 4) == hipSuccess;
         const int64_t ng = (nu + kChainGroup - 1) / kChainGroup;
-        ok &= alloc((void **)&h->bD, ng * 8) == hipSuccess;
-        ok &= alloc((void **)&h->bC, ng * 4) == hipSuccess;
-        ok &= alloc((void **)&h->bM, ng * 4) == hipSuccess;
-        ok &= alloc((void **)&h->bpd, ng * 8) == hipSuccess;
-        ok &= alloc((void **)&h->bpc, ng * 4) == hipSuccess;
-        ok &= alloc((void **)&h->seql, nu * 4) == hipSuccess;
-        ok &= alloc((void **)&h->udelta, nu * 8) == hipSuccess;
-        ok &= alloc((void **)&h->ugl, nu * 8) == hipSuccess;
-        ok &= alloc((void **)&h->sout, nu * 8) == hipSuccess;
-        ok &= alloc((void **)&h->sentry, nu * 8) == hipSuccess;
-        ok &= alloc((void **)&h->urec, nu * sizeof(UnitRec)) == hipSuccess;
-        ok &= alloc((void **)&h->np_leaf, (np_sumsq_chunks(n) * 64 + 64) * 8) == hipSuccess;
-        ok &= alloc((void **)&h->part_w, nb * 8) == hipSuccess;
-        ok &= alloc((void **)&h->np_part, np_sumsq_chunks(n) * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->bD, ng * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->bC, ng * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->bM, ng * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->bpd, ng * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->bpc, ng * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->seql, nu * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->udelta, nu * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->ugl, nu * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->sout, nu * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->sentry, nu * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->urec, nu * sizeof(UnitRec)) == hipSuccess;
+        ok &= FS2_ALLOC(h->np_leaf, (np_sumsq_chunks(n) * 64 + 64) * 8) == hipSuccess;
+        ok &= FS2_ALLOC(h->part_w, nb * 8) == hipSuccess;
+        // (one sum per numpy chunk in the tree modes, one per half chunk in the
+        // chunked exact mode: k_normalize_chunks writes normalize_chunk_parts(n) --
+        // sized by chunks alone, the N = 8e6 drift study's first scan wrote past it
+        // and faulted; at N = 1e6 the overrun stayed inside the allocation's granule)
+        ok &= FS2_ALLOC(h->np_part,
+                    std::max<int64_t>(np_sumsq_chunks(n), normalize_chunk_parts(n)) * 8) == hipSuccess;
     }
-    ok &= alloc((void **)&h->noise_dev, n * 8) == hipSuccess;
-    ok &= alloc((void **)&h->u0_dev, 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->noise_dev, n * 8) == hipSuccess;
+    ok &= FS2_ALLOC(h->u0_dev, 8) == hipSuccess;
     {
         // post block: DevStats, xmat (kXrowWords G x G words), then the flag on its own line
         const size_t body = sizeof(DevStats) + sizeof(int64_t) * kXrowWords * kMaxRanks * kMaxRanks;
@@ -1893,7 +1919,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
             if (ok) h->post_flag_dev = reinterpret_cast<unsigned long long *>(h->post + off);
         }
     }
-    ok &= alloc((void **)&h->plan, sizeof(PackPlan) * kMaxRanks) == hipSuccess;
+    ok &= FS2_ALLOC(h->plan, sizeof(PackPlan) * kMaxRanks) == hipSuccess;
     // one coherent block: the published stats, then the flag on its own 64-byte line
     ok &= hipHostMalloc((void **)&h->pub_stats, sizeof(DevStats) + 128, hipHostMallocCoherent | hipHostMallocMapped) ==
           hipSuccess;
@@ -3971,6 +3997,23 @@ int fs2_debug_noise(fs2_handle *h, double *out) {
         std::memcpy(out, h->noise_pin, sizeof(double) * h->n);
     }
     return FS2_OK;
+}
+
+int64_t fs2_debug_check_guards(fs2_handle *h, char *first_bad, int64_t len) {
+    if (!h) return set_err(nullptr, FS2_ERR_ARG, "fs2_debug_check_guards: null handle");
+    if (first_bad && len > 0) first_bad[0] = 0;
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    std::vector<unsigned char> buf(kGuardBytes);
+    int64_t bad = 0;
+    for (const auto &g : h->guards) {
+        HIP_TRY(h, hipMemcpy(buf.data(), g.at, kGuardBytes, hipMemcpyDeviceToHost));
+        int64_t k = 0;
+        for (unsigned char c : buf) k += c != (unsigned char)kGuardByte;
+        if (k && first_bad && len > 0 && !first_bad[0]) std::snprintf(first_bad, (size_t)len, "%s", g.name);
+        bad += k;
+    }
+    return bad;
 }
 
 int64_t fs2_debug_out_src(fs2_handle *h, int32_t *out, int64_t capacity) {

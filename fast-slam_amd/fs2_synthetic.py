@@ -131,6 +131,53 @@ def scan_measurements(L: int, scan: int, seed: int = 0, n_hits: int = 3,
     return np.array(rows, dtype=np.float64).reshape(-1, 2)
 
 
+def discovery_order(L: int) -> np.ndarray:
+    """The order in which a robot sweeping the landmark grid row by row, turning at
+    each row's end (a lawnmower path), first sees the L landmarks of
+    common_landmarks: the order its map grows in by appends (fast_slam_2.py:108-111)."""
+    rows, cols = grid_shape(L)
+    order = []
+    for r in range(rows):
+        for c in (range(cols) if r % 2 == 0 else range(cols - 1, -1, -1)):
+            if r * cols + c < L:
+                order.append(r * cols + c)
+    return np.array(order, dtype=np.int64)
+
+
+def buildup_scans(L: int, per_scan: int = 8) -> int:
+    """Scans of the map build-up (buildup_measurements) that discover all L landmarks."""
+    return (L + per_scan - 1) // per_scan
+
+
+def buildup_measurements(L: int, scan: int, seed: int = 0, per_scan: int = 8, rehits: int = 2,
+                         recent: int = 24) -> np.ndarray:
+    """Scan `scan` of the reference's own operating mode, maps grown by appends from
+    empty (fast_slam_2.py:20-31, :108-111): the next `per_scan` landmarks in
+    discovery order (each a miss for every particle, so each is appended, in
+    observation order), then `rehits` observations of landmarks discovered in the
+    scans before (within `recent` landmarks of the front: what the robot still
+    sees), which associate, update the maps and move the weights.  Points within
+    HIT_RADIUS of the true landmark, encoded like scan_measurements."""
+    base = common_landmarks(L, seed)
+    order = discovery_order(L)
+    rng = substream(seed, 300000 + scan)
+    lo = scan * per_scan
+    rows = []
+    for j in order[lo:lo + per_scan]:
+        r = HIT_RADIUS * math.sqrt(rng.uniform())
+        a = rng.uniform(-math.pi, math.pi)
+        p = base[j] + np.array([r * math.cos(a), r * math.sin(a)])
+        rows.append(encode(float(p[0]), float(p[1])))
+    if lo > 0:
+        for _ in range(rehits):
+            j = order[int(rng.integers(max(0, lo - recent), min(lo, L)))]
+            r = HIT_RADIUS * math.sqrt(rng.uniform())
+            a = rng.uniform(-math.pi, math.pi)
+            p = base[j] + np.array([r * math.cos(a), r * math.sin(a)])
+            rows.append(encode(float(p[0]), float(p[1])))
+    return np.array(rows, dtype=np.float64).reshape(-1, 2)
+
+
 def beam_angles(P: int) -> np.ndarray:
     if P == 180:
         return np.radians(np.arange(180) - 90.0)

@@ -439,6 +439,11 @@ int fs2_debug_noise(fs2_handle *h, double *out);
  * local source index, < 0 -(k+1) the k-th received particle); returns n_local
  * or a negative error.  For the drift study (scripts/drift_study.py). */
 int64_t fs2_debug_out_src(fs2_handle *h, int32_t *out, int64_t capacity);
+/* Handles created with FS2_GUARD=1 in the environment follow every buffer
+ * fs2_create allocates with a known pattern: the number of pattern bytes that
+ * changed (a kernel wrote past a buffer's end), the first such buffer's name in
+ * first_bad; 0 when clean or without FS2_GUARD.  Drains the handle's stream. */
+int64_t fs2_debug_check_guards(fs2_handle *h, char *first_bad, int64_t len);
 /* Test hook of fs2_mt_draw's jump-ahead: the stream words x[J + 1 .. J + 624]
  * after the key x[0 .. 624) (J >= 1), as the GF(2) combination of x[1 .. 20561)
  * given by x^J mod the characteristic polynomial (host arithmetic). */

@@ -47,7 +47,10 @@ def dump(args):
     from fast_slam_2 import _native as nat
     torch.cuda.set_device(0)
     N, L = args.particles, args.landmarks
+    if args.guard:
+        os.environ["FS2_GUARD"] = "1"       # buffers followed by a checked pattern (fs2_debug_check_guards)
     f = fast_slam_2.FastSLAM2(N, rng="device", seed=args.seed, landmark_capacity=L + args.scans + 8, verbose=False)
+    os.environ.pop("FS2_GUARD", None)
     t0 = time.time()
     bench.populate(f, N, L, args.seed, 0)
     print(f"populated N={N} L={L} in {time.time() - t0:.1f} s", flush=True)
@@ -65,6 +68,11 @@ def dump(args):
             diffs.append(np.diff(buf, prepend=0).astype(np.int32))
             scans.append(s)
             sums.append(float(st.n_eff))
+        if args.guard:
+            name = C.create_string_buffer(128)
+            bad = lib.fs2_debug_check_guards(f._h, name, 128)
+            if bad:
+                raise RuntimeError(f"scan {s}: {bad} guard bytes overwritten after {name.value.decode()}")
         print(f"scan {s}: resampled {int(st.resampled)} n_eff {st.n_eff:.1f}", flush=True)
     f.close()
     np.savez_compressed(args.out, N=N, L=L, seed=args.seed, scans=np.array(scans),
@@ -250,6 +258,7 @@ def main():
     a.add_argument("--scans", type=int, default=30)
     a.add_argument("--seed", type=int, default=0)
     a.add_argument("--out", required=True)
+    a.add_argument("--guard", action="store_true", help="FS2_GUARD: check every buffer's end after each scan")
     b = sub.add_parser("sim")
     b.add_argument("npz")
     b.add_argument("--ranks", type=int, default=8)
