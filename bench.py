@@ -532,6 +532,8 @@ def sharded_local(args, L, n_total, G=2, scans=9, warm=3, page_refs="auto"):
             "pages_sent_before_fraction": (sum(p["sent_pages_repeat"] for p in profs) /
                                            sum(p["sent_pages"] for p in profs)
                                            if sum(p["sent_pages"] for p in profs) else None),
+            "recv_bytes_per_rank_scan_max": max(p["recv_bytes"] for p in profs) / k,
+            "exchange_ms_per_scan_rank_max": max(p["exchange_ms"] for p in profs) / k,
             "page_refs": profs[0]["page_refs"] == 1,     # (in effect: fs2_profile.page_refs)
             # page_refs: remote pages the update passes copied (each with its 8 records)
             "localized_pages_per_scan": sum(p["localized_pages"] for p in profs) / k,
@@ -598,10 +600,14 @@ def main(argv=None):
     migration = None
     if world > 1:
         # the sharded resample's transfers, summed over the ranks
-        keys = ("migrations", "sent_particles", "sent_rows", "sent_pages", "sent_bytes", "migrate_ms", "comm_ms")
+        keys = ("migrations", "sent_particles", "sent_rows", "sent_pages", "sent_bytes", "migrate_ms", "comm_ms",
+                "recv_bytes", "exchange_ms")
         mt = torch.tensor([float(prof[k]) for k in keys], dtype=torch.float64, device=tdev)
+        mx = mt.clone()
         dist.all_reduce(mt, op=dist.ReduceOp.SUM)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = dict(zip(keys, mt.tolist()))
+        top = dict(zip(keys, mx.tolist()))
         resamples = R["sums"]["resamples"]
         per = max(resamples, 1)
         rs_ms = sorted(m for m, r in R["step_ms"] if r)
@@ -615,6 +621,13 @@ def main(argv=None):
             "page_dedup_ratio": tot["sent_rows"] / tot["sent_pages"] if tot["sent_pages"] else None,
             "host_ms_per_resample_rank_mean": tot["migrate_ms"] / world / per,
             "comm_ms_per_scan_rank_mean": tot["comm_ms"] / world / args.steps,
+            # what must arrive before a rank's next update pass, and the device time the
+            # exchanges hold the scan's stream (nothing overlaps them): per rank and scan,
+            # the largest rank's
+            "recv_bytes_per_rank_scan_max": top["recv_bytes"] / args.steps,
+            "recv_bytes_per_rank_resample_max": top["recv_bytes"] / per,
+            "exchange_ms_per_scan_rank_max": top["exchange_ms"] / args.steps,
+            "exchange_ms_per_resample_rank_max": top["exchange_ms"] / per,
             "scan_ms_resample_median_rank0": rs_ms[len(rs_ms) // 2] if rs_ms else None,
             "scan_ms_other_median_rank0": ot_ms[len(ot_ms) // 2] if ot_ms else None,
             "note": "every resample moves the particles whose outputs land on another rank's shard, "

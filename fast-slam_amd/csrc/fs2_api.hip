@@ -611,6 +611,11 @@ struct fs2_handle {
     double *est_base = nullptr;
     int32_t *uop = nullptr;
     NpTailPlan *np_tail_g = nullptr;
+    // profiling, sharded: a start / end event pair around each resample's exchange
+    // (its device time: nothing else runs on the stream meanwhile), folded into
+    // prof.exchange_ms by fs2_get_profile
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> xev;
+    size_t xev_used = 0;
     // FS2_GUARD: the pattern after each buffer fs2_create made (fs2_debug_check_guards)
     struct Guard {
         char *at;
@@ -1344,6 +1349,30 @@ static void keep_shards(const fs2_handle *h, int G, At at, int keep_of[]) {
     for (uint32_t m = full; m; m &= ~(1u << pick[m])) keep_of[__builtin_popcount(m) - 1] = pick[m];
 }
 
+// One resample's exchange, timed on the device when profiling (fs2_profile
+// exchange_ms, recv_bytes: what must arrive before the next update pass).
+static int timed_exchange(fs2_handle *h, const std::vector<fs2comm::Xfer> &sends,
+                          const std::vector<fs2comm::Xfer> &recvs, hipStream_t s) {
+    std::pair<hipEvent_t, hipEvent_t> *ev = nullptr;
+    if (h->profiling) {
+        if (h->xev_used == h->xev.size() && h->xev.size() < 256) {
+            std::pair<hipEvent_t, hipEvent_t> e{nullptr, nullptr};
+            if (hipEventCreate(&e.first) == hipSuccess && hipEventCreate(&e.second) == hipSuccess) h->xev.push_back(e);
+            else (void)hipGetLastError();
+        }
+        if (h->xev_used < h->xev.size()) ev = &h->xev[h->xev_used++];
+        for (const auto &x : recvs) h->prof.recv_bytes += x.bytes;
+    }
+    if (ev) HIP_TRY(h, hipEventRecord(ev->first, s));
+    int rc;
+    {
+        CommTimer ct(h);
+        rc = h->tp->exchange(sends, recvs, s, &h->err);
+    }
+    if (ev) HIP_TRY(h, hipEventRecord(ev->second, s));
+    return rc;
+}
+
 // page_refs mode, after the sizes: each particle sent is its header and its rows
 // as tagged descriptors (no page dedup, no page content, no second size round).
 static int exchange_refs(fs2_handle *h, ResampleParams &rs, const std::vector<int64_t> &mat, int keep,
@@ -1394,10 +1423,7 @@ static int exchange_refs(fs2_handle *h, ResampleParams &rs, const std::vector<in
         pp.kbase = kbase;
         kbase += (int32_t)K;
     }
-    {
-        CommTimer ct(h);
-        rc = h->tp->exchange(sends, recvs, s, &h->err);
-    }
+    rc = timed_exchange(h, sends, recvs, s);
     if (rc) return rc;
     h->n_recv = kbase;
     h->u_recv = 0;
@@ -1561,10 +1587,7 @@ static int exchange_particles(fs2_handle *h, ResampleParams &rs) {
         kbase += (int32_t)K;
         ubase += U;
     }
-    {
-        CommTimer ct(h);
-        rc = h->tp->exchange(sends, recvs, s, &h->err);
-    }
+    rc = timed_exchange(h, sends, recvs, s);
     if (rc) return rc;
     h->n_recv = kbase;
     h->u_recv = ubase;
@@ -1765,6 +1788,10 @@ static void free_handle(fs2_handle *h) {
     if (h->ev.ok)
         for (auto &set : h->ev.e)
             for (auto &e : set) hipEventDestroy(e);
+    for (auto &e : h->xev) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+    }
     delete h->tp;
     if (h->stream) hipStreamDestroy(h->stream);
     const int dev = h->cfg.device;
@@ -1901,8 +1928,12 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         // chunked exact mode: k_normalize_chunks writes normalize_chunk_parts(n) --
         // sized by chunks alone, the N = 8e6 drift study's first scan wrote past it
         // and faulted; at N = 1e6 the overrun stayed inside the allocation's granule)
+#ifdef FS2_AB_OLD_NP_PART            // (the round-5 size: validates FS2_GUARD against the real overrun)
+        ok &= FS2_ALLOC(h->np_part, np_sumsq_chunks(n) * 8) == hipSuccess;
+#else
         ok &= FS2_ALLOC(h->np_part,
                     std::max<int64_t>(np_sumsq_chunks(n), normalize_chunk_parts(n)) * 8) == hipSuccess;
+#endif
     }
     ok &= FS2_ALLOC(h->noise_dev, n * 8) == hipSuccess;
     ok &= FS2_ALLOC(h->u0_dev, 8) == hipSuccess;
@@ -2078,6 +2109,7 @@ int fs2_set_profiling(fs2_handle *h, int32_t enable) {
         h->ev.ok = true;
     }
     h->ev.used = 0;
+    h->xev_used = 0;
     h->profiling = enable > 0;
     h->prof_period = enable > 0 ? enable : 1;
     h->prof_tick = 0;
@@ -2093,6 +2125,13 @@ int fs2_get_profile(const fs2_handle *hc, fs2_profile *out) {
     if (h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "a submitted scan is pending (fs2_iterate_wait first)");
     const int rc = fold_profile(h);
     if (rc) return rc;
+    for (size_t k = 0; k < h->xev_used; ++k) {
+        float ms = 0.0f;
+        HIP_TRY(h, hipEventSynchronize(h->xev[k].second));
+        HIP_TRY(h, hipEventElapsedTime(&ms, h->xev[k].first, h->xev[k].second));
+        h->prof.exchange_ms += ms;
+    }
+    h->xev_used = 0;
     *out = h->prof;
     out->page_refs = h->refs_off ? -1 : (h->refs ? 1 : 0);
     return FS2_OK;

@@ -350,7 +350,11 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
     FS2_PHASE(0);
     // __move_particle (fast_slam_2.py:69-87)
+#ifdef FS2_AB_NO_MOVE
+    if (false) {                     // A/B timing only (wrong results): the motion sample's share of k_update
+#else
     if (live && P.do_move) {
+#endif
         // (a speculative numpy draw is made unscaled: numpy's loc + scale gauss here)
         const double nz = P.noise ? (P.noise_unscaled ? 0.0 + __dmul_rn(P.noise_scale, P.noise[i]) : P.noise[i])
                                   : P.sigma * philox_normal(P.seed, P.scan, (uint64_t)(P.gidx0 + i));

@@ -131,6 +131,8 @@ class fs2_profile(C.Structure):
         ("pool_grows", C.c_int64),
         ("grow_ms", C.c_double),
         ("scan_allocs", C.c_int64),
+        ("recv_bytes", C.c_uint64),
+        ("exchange_ms", C.c_double),
     ]
 
     def as_dict(self):

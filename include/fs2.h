@@ -206,6 +206,11 @@ typedef struct fs2_profile {
                                    received map longer than every local one): each drains the stream
                                    and allocates.  Counted whether or not profiling is on; 0 when the
                                    creation-time sizes hold */
+    uint64_t recv_bytes;        /* sharded: transfer bytes this rank received at resamples (what must
+                                   arrive before its next update pass can run) */
+    double exchange_ms;         /* sharded: device time of the resamples' exchanges (HIP events around
+                                   the transport's grouped send / receive on the scan's stream; nothing
+                                   overlaps them: the exposed exchange time) */
 } fs2_profile;
 
 /* ---------------------------------------------------------------- core ---- */

@@ -213,6 +213,17 @@ def sim(args):
     G = args.ranks
     out = {"N": N, "L": int(d["L"]), "G": G, "cap": args.cap, "resamples": int(len(src_all)),
            "scans": d["scans"].tolist(), "policies": {}}
+    # the least any balanced placement must move: rank r's sources have c_r outputs,
+    # at most cap * N / G of them can stay (contiguous shards or not)
+    starts, order = equal_starts(N, G), list(range(G))
+    forced = []
+    for src in src_all:
+        lo, hi = natural(src, starts, order)
+        forced.append(int(np.maximum(0, (hi - lo) - int(args.cap * N / G)).sum()))
+        starts, order = movable(src, starts, order, N, G, args.cap)
+    out["forced_outputs_frac_mean"] = float(np.mean(forced)) / N if forced else 0.0
+    print(f"lower bound (movable placements, cap {args.cap}): {out['forced_outputs_frac_mean'] * 100:.2f} % of N "
+          f"per resample must change ranks", flush=True)
     for pol in ("pinned", "follow", "movable"):
         starts = equal_starts(N, G)
         order = list(range(G))
