@@ -376,8 +376,6 @@ def robustness(args, f, L, first_scan):
     # the same with whole pages sent (round 3's transfer; A/B of the page references)
     out["sharded_local_g8_pages"] = sharded_local(args, L, n, G=8, page_refs="off")
     out["dropin_iterate"] = dropin(args, L, n)
-    # A/B: each scan's draw begun beside its own candidate pass (round 4's deferred draw)
-    out["dropin_iterate_no_speculation"] = dropin(args, L, n, spec=False)
     out["dropin_iterate_host_rng"] = dropin(args, L, n, rng="numpy-host")
     return out
 
@@ -416,7 +414,7 @@ def appended_maps(args, L, n, per_scan=8):
     return r
 
 
-def dropin(args, L, n, scans=23, warm=3, rng="numpy", spec=True):
+def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
     """What a reference caller gets: FastSLAM2.iterate(rotation, translation,
     list[Measurement]) (fast_slam_2.py:33, called at jde_robots_main.py:38) with
     numpy's global legacy RNG -- N normals per scan and the resample start,
@@ -432,24 +430,20 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy", spec=True):
     np.random.seed(args.seed)
     f = fast_slam_2.FastSLAM2(n, rng=rng, seed=args.seed, landmark_capacity=L + scans + 8, verbose=False)
     populate(f, n, L, args.seed, 0)
-    lib = nat.load()
-    if not spec:
-        nat.check(lib.fs2_debug_mt_speculate(f._h, 0, None), f._h)
     meas = [[Measurement(float(d), float(b)) for d, b in syn.scan_measurements(L, s, args.seed)]
             for s in range(scans)]
     for s in range(warm):
         f.iterate(*syn.odometry(s), meas[s])
     t0 = time.perf_counter()
     res = 0
-    each = []
+    each, rs_each = [], []
     for s in range(warm, scans):
         t1 = time.perf_counter()
         f.iterate(*syn.odometry(s), meas[s])
         each.append(time.perf_counter() - t1)
         res += f.last_stats.resampled
+        rs_each.append(int(f.last_stats.resampled))
     dt = time.perf_counter() - t0
-    sc = (ctypes.c_uint64 * 2)()
-    nat.check(lib.fs2_debug_mt_speculate(f._h, -1, sc), f._h)
     f.close()
     state_digest = hashlib.sha1(np.random.get_state()[1].tobytes()).hexdigest()[:12]
     t1 = time.perf_counter()
@@ -460,14 +454,16 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy", spec=True):
     note = ("FastSLAM2.iterate() with numpy's legacy RNG (the reference's draws, bit for bit); "
             + ("drawn on the GPU from np.random's state (MT19937 + polar method, fs2_mt_draw)" if rng == "numpy"
                else "drawn by numpy on one host core (host-RNG bound)"))
-    if rng == "numpy":
-        note += ("; each scan's draw begun when the scan before completed (speculative, fs2.h "
-                 "fs2_debug_mt_speculate)" if spec else "; speculation off: each draw begun by its own iterate()")
+    ms_rs = [e * 1e3 for e, r in zip(each, rs_each) if r]
+    ms_ot = [e * 1e3 for e, r in zip(each, rs_each) if not r]
     return {"value": n * k / dt, "ms_per_scan": dt / k * 1e3, "scans": k, "resamples": res,
             "ms_per_scan_median": float(np.median(each)) * 1e3,
             "ms_each": [round(e * 1e3, 3) for e in each],
+            "resampled_each": rs_each,
+            # scan by scan against the headline (extra.scan_ms_by_kind): the same kinds of scan
+            "ms_resampling_scan_mean": float(np.mean(ms_rs)) if ms_rs else None,
+            "ms_other_scan_mean": float(np.mean(ms_ot)) if ms_ot else None,
             "window": f"scans {warm}..{scans - 1} (the headline's)",
-            "speculative_draws": {"taken": int(sc[0]), "dropped": int(sc[1])},
             "host_rng_ms": rng_ms, "rng": rng, "numpy_state_sha1": state_digest, "note": note}
 
 
@@ -685,6 +681,12 @@ def main(argv=None):
                       "update_pass_bytes": prof["update_bytes"] / max(prof["update_launches"], 1),
                       "reduce_and_resample_ms": prof["reduce_ms"] / max(prof["scans"], 1),
                       "resamples": sums["resamples"],
+                      # host wall time per scan by kind (the drop-in line reports the same split)
+                      "scan_ms_by_kind": {
+                          "resampling_mean": (float(np.mean([m for m, r in R["step_ms"] if r]))
+                                              if any(r for _, r in R["step_ms"]) else None),
+                          "other_mean": (float(np.mean([m for m, r in R["step_ms"] if not r]))
+                                         if any(not r for _, r in R["step_ms"]) else None)},
                       "resample_shared_slots": sums["copied_slots"],
                       "cow_pages_per_particle_scan": sums["cow"] / units,
                       "pool_collections": st.collections,

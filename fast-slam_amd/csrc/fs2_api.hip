@@ -475,22 +475,9 @@ struct fs2_handle {
         hipEvent_t ev_in = nullptr, ev_noise = nullptr;
         bool deferred = false;
         MtCtx dc;
-        // speculation (one GPU): when a scan that used a deferred draw completes, the
-        // next scan's draw is begun at once from the state that draw left numpy in
-        // (after the normals, or after u0 when the scan resampled) -- on the draw
-        // stream while the host returns to the caller, instead of beside the next
-        // candidate pass -- and made unscaled (sigma 1; the update pass applies numpy's
-        // loc + scale g).  The next fs2_mt_draw_deferred takes it when it starts from
-        // that state; any other draw, or a scan with other noise, drops it.
-        bool spec_enabled = true;
-        bool last_valid = false;           // last_after: the states the last deferred draw produced
-        fs2_mt_state last_after[2];
-        bool spec_on = false;              // dc holds a speculative draw begun from spec_in
-        fs2_mt_state spec_in, spec_after, spec_after_u0;
-        hipEvent_t ev_spec = nullptr;
-        bool unscaled = false;             // the armed / deferred draw is N(0, 1), scaled by usigma
-        double usigma = 0.0;
-        uint64_t spec_taken = 0, spec_dropped = 0;
+        // (round 5 began the next scan's draw speculatively when a scan completed;
+        // measured neutral twice on the drop-in -- profiles/r05_dropin_ab.json -- and
+        // removed in round 6: each draw is begun by its own fs2_mt_draw_deferred)
     } mt;
     int32_t *assoc_dev = nullptr;
     int64_t assoc_cap = 0;
@@ -1703,7 +1690,7 @@ static void free_handle(fs2_handle *h) {
     if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
     if (prev_dev != h->cfg.device) (void)hipSetDevice(h->cfg.device);
     if (h->stream) hipStreamSynchronize(h->stream);
-    if (h->mt.dstream) hipStreamSynchronize(h->mt.dstream);   // (a speculative draw)
+    if (h->mt.dstream) hipStreamSynchronize(h->mt.dstream);   // (a deferred draw)
     // In-place pools (VMM chunks): nothing of this process may still be in flight
     // when they are unmapped and released, or the runtime defers the release and the
     // next handle's first growth (hipMemCreate) waits for it -- 4 s in the round-4
@@ -1773,7 +1760,6 @@ static void free_handle(fs2_handle *h) {
         hipStreamDestroy(h->mt.dstream);
         hipEventDestroy(h->mt.ev_in);
         hipEventDestroy(h->mt.ev_noise);
-        if (h->mt.ev_spec) hipEventDestroy(h->mt.ev_spec);
     }
     hipFree(h->mt.raw[0]); hipFree(h->mt.raw[1]); hipFree(h->mt.boff);
     if (h->mt.ev_words) hipEventDestroy(h->mt.ev_words);
@@ -2500,8 +2486,6 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
 
 static int complete_oldest(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats);
 static int mt_finish(fs2_handle *h);
-static void mt_speculate(fs2_handle *h, bool resampled);
-static void mt_drop_spec(fs2_handle *h);
 
 int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
                        const double *observed, int32_t M, const double *noise, const double *u0) {
@@ -2512,15 +2496,8 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise /
     // u0; a draw is consumed by this call whatever happens below
     const bool drawn = h->mt.armed || h->mt.deferred;
-    const bool unscaled = drawn && h->mt.unscaled;     // a speculative draw taken: N(0, 1)
-    const double usigma = h->mt.usigma;
     h->mt.armed = false;
-    h->mt.unscaled = false;
     HIP_TRY(h, hipSetDevice(h->cfg.device));
-    if (!drawn) {
-        mt_drop_spec(h);               // this scan's noise is not a draw: the buffer is ours again
-        h->mt.last_valid = false;
-    }
     // a deferred draw ends between k_candidates and k_update below, or on the way out
     // (its outputs are written whatever this call returns)
     struct DrawEnd {
@@ -2671,8 +2648,6 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     up.x = h->x[cur]; up.y = h->y[cur]; up.yaw = h->yaw[cur]; up.w = h->w[cur]; up.cnt = h->cnt[cur];
     up.map = h->map();
     up.noise = (noise || drawn) ? h->noise_dev : nullptr;
-    up.noise_unscaled = unscaled ? 1 : 0;
-    up.noise_scale = unscaled ? usigma : 0.0;
     up.seed = h->cfg.seed;
     up.scan = scan_id;
     up.sigma = (rotation != 0) ? h->cfg.rotation_noise : h->cfg.translation_noise;
@@ -2905,9 +2880,6 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
         const int rc2 = enqueue_tail(h, h->next.t);
         if (rc == FS2_OK) rc = rc2;
     }
-    // nothing outstanding: the next scan's draw, begun now (MtWork speculation)
-    if (rc == FS2_OK && !h->pending.on && !h->next.on && !h->stash.on) mt_speculate(h, sp->resampled != 0);
-    h->mt.last_valid = false;
     return rc;
 }
 
@@ -3866,77 +3838,8 @@ static int mt_finish(fs2_handle *h) {
     const int rc = mt_end(h, mt.dc, mt.dstream);
     HIP_TRY(h, hipEventRecord(mt.ev_noise, mt.dstream));
     HIP_TRY(h, hipStreamWaitEvent(h->stream, mt.ev_noise, 0));
-    if (rc) {
-        mt.unscaled = false;
-        return rc;
-    }
+    if (rc) return rc;
     mt.armed = true;
-    // where this draw leaves numpy: the next draw starts from one of these
-    mt.last_after[0] = *mt.dc.after;
-    mt.last_after[1] = *mt.dc.after_u0;
-    mt.last_valid = true;
-    return FS2_OK;
-}
-
-// A speculative draw not taken: the handle's stream waits for it (it writes the
-// noise buffer and the draw's results), and the words it used are not reused.
-static void mt_drop_spec(fs2_handle *h) {
-    auto &mt = h->mt;
-    if (!mt.spec_on) return;
-    mt.spec_on = false;
-    ++mt.spec_dropped;
-    if (hipEventRecord(mt.ev_spec, mt.dstream) != hipSuccess ||
-        hipStreamWaitEvent(h->stream, mt.ev_spec, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        hipStreamSynchronize(mt.dstream);
-    }
-}
-
-// The next scan's draw, begun when a scan that used a deferred draw completes (one
-// GPU, nothing outstanding): from numpy's state after that scan -- past its
-// normals, and past its u0 when it resampled (fast_slam_2.py:79,81,183) -- on the
-// draw stream, after this scan's work (its update pass read the noise buffer).
-// Made with sigma 1: the scale is the next call's.  A failure here only means no
-// speculation (the error is not the caller's: h->err is restored).
-static void mt_speculate(fs2_handle *h, bool resampled) {
-    auto &mt = h->mt;
-    if (!mt.spec_enabled || !mt.last_valid || mt.deferred || mt.armed || mt.spec_on || h->tp || !mt.dstream) return;
-    mt.last_valid = false;
-    if (!mt.ev_spec && hipEventCreateWithFlags(&mt.ev_spec, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        mt.ev_spec = nullptr;
-        return;
-    }
-    const std::string saved = h->err;
-    mt.spec_in = mt.last_after[resampled ? 1 : 0];
-    bool ok = hipEventRecord(mt.ev_in, h->stream) == hipSuccess &&
-              hipStreamWaitEvent(mt.dstream, mt.ev_in, 0) == hipSuccess;
-    if (ok) ok = mt_begin(h, &mt.spec_in, 1.0, &mt.spec_after, &mt.spec_after_u0, nullptr, mt.dstream, mt.dc) == FS2_OK;
-    if (!ok) {
-        (void)hipGetLastError();
-        h->err = saved;
-        hipStreamSynchronize(mt.dstream);
-        return;
-    }
-    mt.spec_on = true;
-}
-
-static bool mt_same_state(const fs2_mt_state &a, const fs2_mt_state &b) {
-    return a.pos == b.pos && a.has_gauss == b.has_gauss &&
-           (!a.has_gauss || std::memcmp(&a.gauss, &b.gauss, sizeof a.gauss) == 0) &&
-           std::memcmp(a.key, b.key, sizeof a.key) == 0;
-}
-
-int fs2_debug_mt_speculate(fs2_handle *h, int32_t on, uint64_t counts[2]) {
-    if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
-    if (on >= 0) {
-        h->mt.spec_enabled = on != 0;
-        if (!h->mt.spec_enabled) mt_drop_spec(h);
-    }
-    if (counts) {
-        counts[0] = h->mt.spec_taken;
-        counts[1] = h->mt.spec_dropped;
-    }
     return FS2_OK;
 }
 
@@ -3946,10 +3849,7 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
     HIP_TRY(h, hipSetDevice(h->cfg.device));
     int rc = mt_finish(h);                     // a deferred draw first (its outputs are written)
     if (rc) return rc;
-    mt_drop_spec(h);
     h->mt.armed = false;
-    h->mt.unscaled = false;
-    h->mt.last_valid = false;
     MtCtx c;
     rc = mt_begin(h, in, sigma, after, after_u0, u0_out, h->stream, c);
     if (rc) return rc;
@@ -3967,22 +3867,6 @@ int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs
     int rc = mt_finish(h);
     if (rc) return rc;
     mt.armed = false;
-    mt.unscaled = false;
-    mt.last_valid = false;
-    if (mt.spec_on && in && after && after_u0 && sigma >= 0.0 && !h->pending.on && mt_same_state(*in, mt.spec_in)) {
-        // the speculative draw started from this very state: it is this draw (its
-        // host half, as for any deferred draw, in the next submit; the scan scales)
-        mt.spec_on = false;
-        ++mt.spec_taken;
-        mt.dc.after = after;
-        mt.dc.after_u0 = after_u0;
-        mt.dc.u0_out = u0_out;
-        mt.unscaled = true;
-        mt.usigma = sigma;
-        mt.deferred = true;
-        return FS2_OK;
-    }
-    mt_drop_spec(h);                           // numpy moved on otherwise (or bad arguments, refused below)
     if (!mt.dstream) {
         HIP_TRY(h, hipStreamCreateWithFlags(&mt.dstream, hipStreamNonBlocking));
         HIP_TRY(h, hipEventCreateWithFlags(&mt.ev_in, hipEventDisableTiming));
@@ -4026,15 +3910,9 @@ int fs2_debug_noise(fs2_handle *h, double *out) {
         const int rcm = mt_finish(h);
         if (rcm) return rcm;
     }
-    mt_drop_spec(h);
     HIP_TRY(h, hipMemcpyAsync(h->noise_pin, h->noise_dev, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
-    if (h->mt.armed && h->mt.unscaled) {       // a speculative draw taken: N(0, 1), scaled as the scan will
-        const double s = h->mt.usigma;
-        for (int64_t i = 0; i < h->n; ++i) out[i] = 0.0 + s * h->noise_pin[i];
-    } else {
-        std::memcpy(out, h->noise_pin, sizeof(double) * h->n);
-    }
+    std::memcpy(out, h->noise_pin, sizeof(double) * h->n);
     return FS2_OK;
 }
 

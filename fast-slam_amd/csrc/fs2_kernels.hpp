@@ -378,8 +378,6 @@ struct UpdateParams {
     uint64_t seed, scan;
     double sigma;            // std of the selected motion noise
     double rotation, translation;
-    double noise_scale;      // noise_unscaled: the draws are N(0, 1), each used as 0 + scale g
-    int32_t noise_unscaled;
     int32_t do_move;
     int32_t m;               // measurements in this pass
     int32_t k0;              // first measurement index of this pass

@@ -355,8 +355,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #else
     if (live && P.do_move) {
 #endif
-        // (a speculative numpy draw is made unscaled: numpy's loc + scale gauss here)
-        const double nz = P.noise ? (P.noise_unscaled ? 0.0 + __dmul_rn(P.noise_scale, P.noise[i]) : P.noise[i])
+        const double nz = P.noise ? P.noise[i]
                                   : P.sigma * philox_normal(P.seed, P.scan, (uint64_t)(P.gidx0 + i));
         double ntr, nrot;
         if (P.rotation != 0.0) {

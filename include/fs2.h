@@ -309,15 +309,6 @@ int fs2_mt_draw(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_stat
  * and fs2_debug_noise end a pending deferred draw first. */
 int fs2_mt_draw_deferred(fs2_handle *h, const fs2_mt_state *in, double sigma, fs2_mt_state *after,
                          fs2_mt_state *after_u0, double *u0);
-/* On one GPU a scan that used a deferred draw also begins the next scan's draw
- * when fs2_iterate_wait completes it (nothing else outstanding): from numpy's state
- * after that scan, on the draw stream, while the caller is away.  The next
- * fs2_mt_draw_deferred takes it if its *in is that state (any sigma: it is made
- * unscaled and the scan applies 0 + sigma g, numpy's loc + scale g); another state,
- * another draw or a scan with other noise drops it.  Results are identical either
- * way.  Test / A-B hook: on = 1 / 0 enables / disables (-1 leaves it); counts (may
- * be NULL) = {taken, dropped}. */
-int fs2_debug_mt_speculate(fs2_handle *h, int32_t on, uint64_t counts[2]);
 
 /* Particle state in the reference's object layout (Particle.x/.y/.yaw/.weight,
  * Particle.landmarks[j] = Landmark(x, y, cov) -- models/particle.py:11-20,

@@ -15,4 +15,9 @@ timeout -k 10 900 python -u scripts/ab_lib.py --rounds 3 base=fast-slam_amd/lib/
 rc=$?
 cat gpurun_out/ab_nomove.log | grep '^{'
 grep -E "guard bytes|passed|failed" gpurun_out/guard_validate.log | tail -3
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_mtrng.py \
+    tests/test_gpu_dropin.py tests/test_gpu_pipelined.py > gpurun_out/tests_c.log 2>&1
+rc=$?
+tail -n 3 gpurun_out/tests_c.log
 exit $rc

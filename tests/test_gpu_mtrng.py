@@ -68,25 +68,14 @@ def test_mt_draw_matches_numpy(fs, N, pre, words):
     f.close()
 
 
-def spec_counts(f):
-    from fast_slam_2 import _native as nat
-    c = (C.c_uint64 * 2)()
-    nat.check(nat.load().fs2_debug_mt_speculate(f._h, -1, c), f._h)
-    return int(c[0]), int(c[1])
-
-
-def run_scans(fs, rng, N, L, scans, interfere=(), spec=True, reseed_at=()):
+def run_scans(fs, rng, N, L, scans, interfere=(), reseed_at=()):
     """The bench's synthetic state, `scans` iterate() calls from seed 17; on the scans
     in `interfere` the caller draws from numpy first, on those in `reseed_at` it
-    reseeds (a speculative draw must then be dropped).  Returns the per-scan
-    outputs, numpy's final state and the speculation counts."""
+    reseeds.  Returns the per-scan outputs and numpy's final state."""
     import bench
     import fs2_synthetic as syn
-    from fast_slam_2 import _native as nat
     f = fs.FastSLAM2(N, rng=rng, verbose=False, landmark_capacity=L + scans + 8)
     bench.populate(f, N, L, 3, 0)              # the bench's synthetic state (seeded, identical)
-    if not spec:
-        nat.check(nat.load().fs2_debug_mt_speculate(f._h, 0, None), f._h)
     np.random.seed(17)
     out = []
     for s in range(scans):
@@ -99,9 +88,8 @@ def run_scans(fs, rng, N, L, scans, interfere=(), spec=True, reseed_at=()):
         pose = f.iterate(rot, tr, ms)
         st = f.last_stats
         out.append((pose, st.resampled, st.n_eff, f.get_state(lm_cap=L + scans + 8)))
-    counts = spec_counts(f) if rng == "numpy" else (0, 0)
     f.close()
-    return out, np.random.get_state(), counts
+    return out, np.random.get_state()
 
 
 def assert_same_runs(a, b):
@@ -116,35 +104,27 @@ def assert_same_runs(a, b):
 def test_iterate_device_draws_equal_host_draws(fs):
     """Two handles from the same state, one drawing numpy's stream on the GPU, one
     with numpy on the host: every scan's pose, decision, state and numpy's state
-    afterwards agree bit for bit (resampling scans included).  The device handle
-    draws every scan after the first speculatively (begun when the scan before
-    completed, from the state it left numpy in, unscaled; the odometry alternates
-    the two noise scales)."""
+    afterwards agree bit for bit (resampling scans included; the odometry
+    alternates the two noise scales)."""
     from gpu_util import configure
     configure()
     N, L, scans = 20000, 40, 8
     a = run_scans(fs, "numpy", N, L, scans)
     b = run_scans(fs, "numpy-host", N, L, scans)
     assert_same_runs(a, b)
-    assert a[2] == (scans - 1, 0), a[2]
 
 
-def test_speculative_draw_dropped_when_numpy_moves(fs):
+def test_draw_follows_numpy_when_the_caller_moves_it(fs):
     """The caller draws from numpy (scans 2, 5) or reseeds it (scan 4) between
-    iterate() calls: the speculative draw begun for that scan is dropped and the
-    draw starts from numpy's actual state -- still bit for bit the host draws; with
-    speculation off, the same results."""
+    iterate() calls: every draw starts from numpy's actual state -- bit for bit the
+    host draws."""
     from gpu_util import configure
     configure()
     N, L, scans = 20000, 40, 7
     kw = dict(interfere=(2, 5), reseed_at=(4,))
     a = run_scans(fs, "numpy", N, L, scans, **kw)
     b = run_scans(fs, "numpy-host", N, L, scans, **kw)
-    c = run_scans(fs, "numpy", N, L, scans, spec=False, **kw)
     assert_same_runs(a, b)
-    assert_same_runs(c, b)
-    assert a[2] == (scans - 1 - 3, 3), a[2]
-    assert c[2] == (0, 0), c[2]
 
 
 def test_mt_draw_rejects_negative_scale(fs):
