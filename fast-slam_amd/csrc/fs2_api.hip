@@ -2689,6 +2689,13 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     for (int32_t k0 = 0; k0 < std::max(M, 1); k0 += kMaxM) {
         const int32_t m = std::min(kMaxM, M - k0);
         up.do_move = (k0 == 0);
+        // the motion sample in the candidate pass unless a deferred numpy draw ends
+        // only after it (mt_finish below) or no candidate pass runs (no gate filter)
+#ifdef FS2_AB_MOVE_IN_UPDATE
+        up.move_cand = 0;
+#else
+        up.move_cand = (up.do_move && up.filter && !h->mt.deferred) ? 1 : 0;
+#endif
         up.k0 = k0;
         up.m = std::max(m, 0);
         up.last_pass = (k0 + kMaxM >= M);

@@ -379,6 +379,7 @@ struct UpdateParams {
     double sigma;            // std of the selected motion noise
     double rotation, translation;
     int32_t do_move;
+    int32_t move_cand;       // do_move in k_candidates (the noise is final before it); k_update reads the moved pose
     int32_t m;               // measurements in this pass
     int32_t k0;              // first measurement index of this pass
     int32_t last_pass;

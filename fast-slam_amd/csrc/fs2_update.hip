@@ -88,6 +88,25 @@ __device__ __forceinline__ void sort8(uint64_t (&e)[8]) {
     cmpx(e[1], e[2]); cmpx(e[3], e[4]); cmpx(e[5], e[6]);
 }
 
+// __move_particle (fast_slam_2.py:69-87) of local particle i: noisy odometry from
+// the injected / numpy draw or Philox(seed, scan, global index), yaw wrapped by
+// Python's floor-mod, then the translation along the new yaw.
+__device__ __forceinline__ void move_particle(const UpdateParams &P, int64_t i, double &px, double &py,
+                                              double &pyaw) {
+    const double nz = P.noise ? P.noise[i] : P.sigma * philox_normal(P.seed, P.scan, (uint64_t)(P.gidx0 + i));
+    double ntr, nrot;
+    if (P.rotation != 0.0) {
+        ntr = 0.0;
+        nrot = P.rotation + nz;
+    } else {
+        ntr = P.translation + nz;
+        nrot = 0.0;
+    }
+    pyaw = pymod(pyaw + nrot + kPi, kTwoPi) - kPi;
+    px += ntr * cos(pyaw);
+    py += ntr * sin(pyaw);
+}
+
 template <int MAXM>
 __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     if (P.stats->error_flags & 8) return;     // page_refs: localisation failed, the scan fails
@@ -102,13 +121,29 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const bool live = i < n;
     MapRef map = P.map;
     const int32_t *cntp = P.cnt;
+    double *xp = P.x, *yp = P.y, *yawp = P.yaw;
     if (P.gen) {                               // the current set, read on the device
         const BufSet &b = P.sets[__builtin_amdgcn_readfirstlane(*(volatile const uint32_t *)P.gen) & 1u];
         map.pt = b.pt;
         map.bbox = b.bbox;
         cntp = b.cnt;
+        xp = b.x;
+        yp = b.y;
+        yawp = b.yaw;
     }
     const int c = live ? cntp[i] : 0;
+    // The motion sample runs here when its noise is final before this pass
+    // (move_cand): association does not read the pose (Q2, the robot-frame point
+    // against world landmarks), so the fp64 sample's arithmetic overlaps this
+    // kernel's page-line latency instead of k_update's memory stream, which then
+    // reads the moved pose.
+    if (P.move_cand && live) {
+        double px = xp[i], py = yp[i], pyaw = yawp[i];
+        move_particle(P, i, px, py, pyaw);
+        xp[i] = px;
+        yp[i] = py;
+        yawp[i] = pyaw;
+    }
     const Desc *ptrow = map.pt + (live ? i : 0);
     const float slb = *map.slb;
     if (blockIdx.x == 0 && tid == 0 && P.slb_pass) *P.slb_pass = slb;
@@ -349,25 +384,13 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         frec[t] = (live && t < P.m) ? P.alloc.rfreel[P.alloc.rbase + (int64_t)t * n + i] : 0u;
     }
     FS2_PHASE(0);
-    // __move_particle (fast_slam_2.py:69-87)
+    // __move_particle (fast_slam_2.py:69-87), unless k_candidates moved it
 #ifdef FS2_AB_NO_MOVE
     if (false) {                     // A/B timing only (wrong results): the motion sample's share of k_update
 #else
-    if (live && P.do_move) {
+    if (live && P.do_move && !P.move_cand) {
 #endif
-        const double nz = P.noise ? P.noise[i]
-                                  : P.sigma * philox_normal(P.seed, P.scan, (uint64_t)(P.gidx0 + i));
-        double ntr, nrot;
-        if (P.rotation != 0.0) {
-            ntr = 0.0;
-            nrot = P.rotation + nz;
-        } else {
-            ntr = P.translation + nz;
-            nrot = 0.0;
-        }
-        pyaw = pymod(pyaw + nrot + kPi, kTwoPi) - kPi;
-        px += ntr * cos(pyaw);
-        py += ntr * sin(pyaw);
+        move_particle(P, i, px, py, pyaw);
     }
 
     const M2 R{P.R[0], P.R[1], P.R[2], P.R[3]};
@@ -834,7 +857,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     }
 
     if (live) {
-        if (P.do_move) {
+        if (P.do_move && !P.move_cand) {
             xp[i] = px;
             yp[i] = py;
             yawp[i] = pyaw;

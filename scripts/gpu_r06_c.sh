@@ -10,14 +10,16 @@ FS2_LIB=$PWD/fast-slam_amd/lib/libfs2_oldnp.so timeout -k 10 300 python -u -m py
 rc=$?
 echo "guard validation rc=$rc (1 expected: the overrun is found)"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 900 python -u scripts/ab_lib.py --rounds 3 base=fast-slam_amd/lib/libfs2.so \
-    nomove=fast-slam_amd/lib/libfs2_nomove.so --out gpurun_out/ab_nomove.json > gpurun_out/ab_nomove.log 2>&1
+timeout -k 10 900 python -u scripts/ab_lib.py --rounds 3 movecand=fast-slam_amd/lib/libfs2.so \
+    moveupd=fast-slam_amd/lib/libfs2_moveupd.so nomove=fast-slam_amd/lib/libfs2_nomove.so \
+    --out gpurun_out/ab_nomove.json > gpurun_out/ab_nomove.log 2>&1
 rc=$?
 cat gpurun_out/ab_nomove.log | grep '^{'
 grep -E "guard bytes|passed|failed" gpurun_out/guard_validate.log | tail -3
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_mtrng.py \
-    tests/test_gpu_dropin.py tests/test_gpu_pipelined.py > gpurun_out/tests_c.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_mtrng.py \
+    tests/test_gpu_dropin.py tests/test_gpu_pipelined.py tests/test_gpu_fullsize.py tests/test_gpu_parity.py \
+    tests/test_gpu_exact.py > gpurun_out/tests_c.log 2>&1
 rc=$?
 tail -n 3 gpurun_out/tests_c.log
 exit $rc
