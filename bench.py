@@ -83,9 +83,9 @@ def parse(argv=None):
                     help="A/B (config 4 interference): launch this many tiny kernels on a second stream "
                          "before each scan, as the ICP hand-off does")
     ap.add_argument("--pipelined", action="store_true",
-                    help="time the headline with two scans in flight (step_submit / step_wait: the next "
-                         "scan's candidate pass beside this scan's tail, fs2.h fs2_iterate_submit) instead "
-                         "of step() one scan at a time (measured no faster: profiles/r05_ab_pipelined.txt)")
+                    help="time the headline through step_submit / step_wait with two submits outstanding "
+                         "(fs2.h fs2_iterate_submit: the second completes the first; round 5's overlapped "
+                         "variant measured no faster, profiles/r05_ab_pipelined.txt, and was removed)")
     ap.add_argument("--dropin", action="store_true",
                     help="time the drop-in FastSLAM2.iterate() (numpy RNG) beside the device-RNG step")
     return ap.parse_args(argv)
@@ -704,22 +704,6 @@ def main(argv=None):
         if extras and not cfg["icp"]:
             out["extra"]["robustness"] = robustness(args, f, L, args.warmup + args.steps)
         f.close()
-        if extras and not cfg["icp"] and not R["pipelined"]:
-            # the same workload with two scans in flight (fs2_iterate_submit twice, then
-            # wait for the oldest), fresh handle: the next scan's candidate pass beside
-            # this scan's tail (DESIGN.md §4 "Pipelined submit")
-            import copy
-            a2 = copy.copy(args)
-            a2.pipelined = True
-            R2 = run_config(a2, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, args.steps, args.warmup)
-            p2 = R2["prof"]
-            out["extra"]["pipelined_step"] = {
-                "value": N * args.steps / R2["dt"], "ms_per_step": R2["dt"] / args.steps * 1e3,
-                "reduce_and_resample_ms": p2["reduce_ms"] / max(p2["scans"], 1),
-                "resamples": R2["sums"]["resamples"],
-                "note": "two scans in flight; the tail stretches beside the candidate pass "
-                        "(profiles/r05_ab_pipelined.txt), so the headline is one scan at a time"}
-            R2["handle"].close()
         if extras and args.config == "3" and not (args.particles or args.landmarks):
             # the other single-GPU BASELINE configs, each on a fresh handle
             out["extra"]["configs"] = {k: config_line(args, k, world, rank, dev, barrier) for k in ("2", "4")}

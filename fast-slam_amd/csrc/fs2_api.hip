@@ -506,10 +506,6 @@ struct fs2_handle {
         bool has_u0 = false;
         int par = 0;                       // parity of the scan's per-scan buffers (cpart, pins)
     };
-    struct {
-        bool on = false;                   // a scan whose update pass is enqueued, its tail not yet
-        TailCtx t;
-    } next;
     struct {                               // a scan completed early (a submit had to wait for it)
         bool on = false;
         int rc = FS2_OK;
@@ -520,7 +516,6 @@ struct fs2_handle {
     unsigned long long *go_dev = nullptr;  // one GPU: publication sequence of the last resampling scan (the gather's marker)
     BufSet *sets_dev = nullptr;            // [2]
     uint64_t submitted = 0;                // scans submitted (parity)
-    uint64_t overlapped = 0;               // scans whose candidate pass ran beside the previous tail
     int32_t cnt_upper = 0;
     double gate2 = 64.0;
     std::string err;
@@ -2490,7 +2485,7 @@ static int mt_finish(fs2_handle *h);
 int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
                        const double *observed, int32_t M, const double *noise, const double *u0) {
     if (!h) return set_err(nullptr, FS2_ERR_ARG, "null handle");
-    if ((h->stash.on ? 1 : 0) + (h->pending.on ? 1 : 0) + (h->next.on ? 1 : 0) >= 2)
+    if ((h->stash.on ? 1 : 0) + (h->pending.on ? 1 : 0) >= 2)
         return set_err(&h->err, FS2_ERR_STATE, "two scans are outstanding: fs2_iterate_wait for the oldest first");
     if (M < 0 || (M > 0 && !meas)) return set_err(&h->err, FS2_ERR_ARG, "bad measurements (M=%d)", M);
     // draws of fs2_mt_draw (numpy's stream, made on the device) stand in for noise /
@@ -2512,26 +2507,19 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     if (drawn && (noise || u0))
         return set_err(&h->err, FS2_ERR_ARG, "fs2_iterate: noise / u0 given after fs2_mt_draw");
     int rc;
-    // A scan outstanding: this one's candidate pass runs beside its tail when nothing
-    // below needs the host to know its outcome first (one GPU, one pass, no draw, the
-    // reservations fit without a collection, no buffer to reallocate); else it is
-    // completed here and its results wait for fs2_iterate_wait.
-    bool overlap = false;
+    // A scan outstanding: it is completed here and its results wait for
+    // fs2_iterate_wait.  (Round 5 enqueued this scan's update pass behind the
+    // outstanding one's tail when nothing needed its outcome first, the two scans in
+    // flight reading their buffer set on the device; measured no faster in order --
+    // profiles/r05_ab_pipelined.txt -- and removed in round 6.)
     if (h->pending.on) {
-        const int64_t need = (int64_t)std::max(M, 1) * h->n;
-        overlap = !h->tp && !h->refs && !drawn && M <= kMaxM && h->cursor + need <= h->nfree &&
-                  h->rcursor + need <= h->rnfree && !(h->profiling && h->ev.used + 2 > kProfSets) &&
-                  !(h->cfg.record_assoc && (int64_t)M * h->n > h->assoc_cap) &&
-                  h->cnt_upper + h->pending.m + M <= h->cap;
-        if (!overlap) {
-            h->stash.rc = complete_oldest(h, h->stash.pose, &h->stash.st);
-            h->stash.on = true;
-            if (h->stash.rc)
-                return set_err(&h->err, FS2_ERR_STATE, "the outstanding scan failed (fs2_iterate_wait reports it)");
-        }
+        h->stash.rc = complete_oldest(h, h->stash.pose, &h->stash.st);
+        h->stash.on = true;
+        if (h->stash.rc)
+            return set_err(&h->err, FS2_ERR_STATE, "the outstanding scan failed (fs2_iterate_wait reports it)");
     }
     const int par = (int)(h->submitted & 1u);
-    const uint64_t scan_id = h->scan + (overlap ? 1u : 0u);      // (the outstanding scan is h->scan)
+    const uint64_t scan_id = h->scan;
     if (h->refs && !h->refs_shared) {
         rc = share_pools(h, true);
         if (rc) return rc;
@@ -2598,11 +2586,8 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
         }
     }
     trace(h, "submit", (int)scan_id);
-    if (!overlap) {             // (overlap: the rows already hold both scans' appends)
-        rc = grow_rows(h, h->cnt_upper + M);
-        if (rc) return rc;
-    }
-    // (overlap: h->cur may be stale -- one GPU takes its set on the device, up.gen)
+    rc = grow_rows(h, h->cnt_upper + M);
+    if (rc) return rc;
     const int cur = h->cur;
     hipStream_t s = h->stream;
     const bool sh = h->tp != nullptr;             // sharded path (G > 1, or forced for testing)
@@ -2630,12 +2615,12 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     // error return) leaves them to be cleared here
     if (!h->stats_clean) HIP_TRY(h, hipMemsetAsync(h->stats_dev, 0, sizeof(DevStats), s));
     h->stats_clean = false;
-    if (prof && !overlap && h->ev.used == kProfSets) {   // pool used up: fold (the scans are long complete)
+    if (prof && h->ev.used == kProfSets) {   // pool used up: fold (the scans are long complete)
         const int rc0 = fold_profile(h);
         if (rc0) return rc0;
     }
     // (event sets are taken by profiled scans only: the outstanding one's if it was)
-    const int evset = h->ev.used + ((overlap && h->pending.prof) ? 1 : 0);
+    const int evset = h->ev.used;
     hipEvent_t *E = h->ev.e[evset];
 
     // ---- fused update passes (move in the first) ----
@@ -2783,13 +2768,6 @@ int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const
     tc.want_collect = want_collect;
     tc.has_u0 = (u0 || drawn);
     tc.par = par;
-    if (overlap) {              // its tail when the outstanding scan is waited for
-        h->next.on = true;
-        h->next.t = tc;
-        h->stats_clean = false;
-        h->overlapped += 1;
-        return FS2_OK;
-    }
     return enqueue_tail(h, tc);
 }
 
@@ -2880,14 +2858,7 @@ int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats) {
     }
     if (!h->pending.on) return set_err(&h->err, FS2_ERR_STATE, "no submitted scan to wait for");
     fs2_iter_stats st_local{};
-    fs2_iter_stats *sp = stats ? stats : &st_local;
-    int rc = complete_oldest(h, out_pose, sp);
-    if (h->next.on) {                  // the scan submitted behind it: its tail, now that the set is known
-        h->next.on = false;
-        const int rc2 = enqueue_tail(h, h->next.t);
-        if (rc == FS2_OK) rc = rc2;
-    }
-    return rc;
+    return complete_oldest(h, out_pose, stats ? stats : &st_local);
 }
 
 int fs2_iterate(fs2_handle *h, double rotation, double translation, const double *meas,
