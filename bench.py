@@ -434,6 +434,7 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
             for s in range(scans)]
     for s in range(warm):
         f.iterate(*syn.odometry(s), meas[s])
+    f.set_profiling(True)          # every scan's device time (events), to split host from device
     t0 = time.perf_counter()
     res = 0
     each, rs_each = [], []
@@ -444,6 +445,7 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
         res += f.last_stats.resampled
         rs_each.append(int(f.last_stats.resampled))
     dt = time.perf_counter() - t0
+    pr = f.profile()
     f.close()
     state_digest = hashlib.sha1(np.random.get_state()[1].tobytes()).hexdigest()[:12]
     t1 = time.perf_counter()
@@ -463,6 +465,11 @@ def dropin(args, L, n, scans=23, warm=3, rng="numpy"):
             # scan by scan against the headline (extra.scan_ms_by_kind): the same kinds of scan
             "ms_resampling_scan_mean": float(np.mean(ms_rs)) if ms_rs else None,
             "ms_other_scan_mean": float(np.mean(ms_ot)) if ms_ot else None,
+            # the scans' device time (first kernel to publication) against the wall time per
+            # iterate(): the rest is the host's share (measurement objects, numpy's state
+            # read and written, the draw's host half: counts, listed logs)
+            "scan_device_ms_mean": pr["scan_ms"] / max(pr["scans"], 1),
+            "host_share_ms_per_scan": dt / k * 1e3 - pr["scan_ms"] / max(pr["scans"], 1),
             "window": f"scans {warm}..{scans - 1} (the headline's)",
             "host_rng_ms": rng_ms, "rng": rng, "numpy_state_sha1": state_digest, "note": note}
 
