@@ -404,8 +404,13 @@ def appended_maps(args, L, n, per_scan=8):
     t_build = time.perf_counter() - t0
     cnt = g.get_state(lm_cap=0)[4] if n <= 2_000_000 else None
     meas = {s: np.ascontiguousarray(syn.scan_measurements(L, s, args.seed), dtype=np.float64) for s in range(23)}
+    g.set_profiling(True, every=PROFILE_EVERY)
     r = timed_scans(g, list(range(23)), meas.__getitem__, syn.odometry, 3)
+    pr = g.profile()
     g.close()
+    r["kernel_ms"] = {"k_candidates": pr["filter_ms"] / max(pr["filter_launches"], 1),
+                      "k_update": pr["exact_ms"] / max(pr["exact_launches"], 1),
+                      "reduce_and_resample": pr["reduce_ms"] / max(pr["scans"], 1)}
     r.update(buildup_scans=nb, buildup_s=t_build, buildup_resamples=res_b,
              map_size_after_buildup=(None if cnt is None else [int(cnt.min()), int(cnt.max())]),
              note=f"maps grown from empty by appends in observation order ({nb} scans of {per_scan} new "
