@@ -265,15 +265,11 @@ int fs2_iterate(fs2_handle *h, double rotation, double translation, const double
  * next scan's ICP alignment to the GPU (config 4) -- without delaying the scan.
  *
  * Up to two scans may be outstanding: submit(s + 1), then wait (returns s), then
- * submit(s + 2), wait (returns s + 1), ...  On one GPU, with at most 4
- * measurements and no fs2_mt_draw, the second scan's candidate pass runs beside the
- * first one's tail (normalise, N_eff, resample) and the two overlap on the device;
- * otherwise the submit completes the outstanding scan first and keeps its results
- * for the next wait.  Results are identical to one scan at a time and come back
- * in submission order; the second scan's tail is enqueued by the wait for the
- * first, so call it promptly.  A third submit, fs2_iterate, and reading / writing
- * the state (or the associations) while scans are outstanding fail with
- * FS2_ERR_STATE. */
+ * submit(s + 2), wait (returns s + 1), ...  The second submit completes the
+ * outstanding scan first and keeps its results for the next wait, so results are
+ * identical to one scan at a time and come back in submission order.  A third
+ * submit, fs2_iterate, and reading / writing the state (or the associations)
+ * while scans are outstanding fail with FS2_ERR_STATE. */
 int fs2_iterate_submit(fs2_handle *h, double rotation, double translation, const double *meas,
                        const double *observed, int32_t M, const double *noise, const double *u0);
 int fs2_iterate_wait(fs2_handle *h, double out_pose[3], fs2_iter_stats *stats);
