@@ -2993,8 +2993,17 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         float ext = 0.0f;
         std::memcpy(&ext, &eb, sizeof ext);
         h->ext_seen = std::max(h->ext_seen, ext);
-        float cell = 1.0f / 64.0f;
+        // cell: the smallest multiple of 1/64 m whose 127 cells each side cover 1.25x
+        // the extent (round 5 rounded it up to a power of two: up to 2x coarser boxes,
+        // e.g. 1 m instead of 0.66 m at config 3, so a measurement between landmarks
+        // 3 m away opened their pages through the quantisation slack alone)
+#ifdef FS2_AB_POW2_CELL
+        float cell = 1.0f / 64.0f;                       // (round 5, A/B)
         while (127.0f * cell < 1.25f * h->ext_seen && cell < 65536.0f) cell *= 2.0f;
+#else
+        float cell = (float)std::max(1.0, std::ceil(1.25 * (double)h->ext_seen / 127.0 * 64.0)) / 64.0f;
+        if (!(cell < 65536.0f)) cell = 65536.0f;
+#endif
         if (cell != h->frame.cell) {
             h->frame = SumFrame{-127.0f * cell, cell, 1.0f / cell};
             HIP_TRY(h, launch_describe(h->map(), h->cnt[c], 0, h->n, s));

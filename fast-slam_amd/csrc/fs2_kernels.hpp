@@ -46,7 +46,7 @@ typedef uint2 Desc;
 // and org a multiple of it, so every bound is exact in fp32.
 struct SumFrame {
     float org, cell;
-    float icell;             // 1 / cell (exact: cell is a power of two)
+    float icell;             // 1 / cell, rounded (informational: codes are computed against the exact bounds)
 };
 constexpr uint32_t kSumOpen = 0xff00ff00u;   // unbounded box: never rejected
 

@@ -393,22 +393,35 @@ __device__ __forceinline__ float4 store_slot(const MapRef &m, char *page, int po
 
 // ---- page summaries (fs2_kernels.hpp) ----
 
+// Grid bound k: org + k cell, exact in fp64 (org and cell are fp32, |k| < 2^8, so
+// the product and the sum need < 50 bits).  The cell need not be a power of two
+// (round 6: a cell fitted to the maps' extent, not rounded up to one, halves the
+// boxes' quantisation slack); every code is checked against these exact bounds.
+__device__ __forceinline__ double sum_grid(const SumFrame &f, double k) { return (double)f.org + k * (double)f.cell; }
 // Code of the largest grid bound <= v (0: unbounded) / of the smallest >= v (255).
 __device__ __forceinline__ uint32_t sum_lo(const SumFrame &f, float v) {
-    const double k = floor(((double)v - (double)f.org) * (double)f.icell);   // = / cell, exactly
-    if (!(k >= 0.0)) return 0u;
-    return (uint32_t)fmin(k, 254.0) + 1u;
+    // (v - org) / cell through the rounded reciprocal: off by < 2^-16 cells, so k is
+    // at most one code off -- a step too low is merely conservative, a step too
+    // high is undone against the exact bound below (at most once)
+    double k = floor(((double)v - (double)f.org) * (double)f.icell);
+    if (!(k >= 0.0)) return 0u;          // (also NaN)
+    k = fmin(k, 254.0);
+    while (k >= 0.0 && sum_grid(f, k) > (double)v) k -= 1.0;
+    return k >= 0.0 ? (uint32_t)k + 1u : 0u;
 }
 __device__ __forceinline__ uint32_t sum_hi(const SumFrame &f, float v) {
-    const double k = ceil(((double)v - (double)f.org) * (double)f.icell);
-    if (!(k <= 254.0)) return 255u;
-    return (uint32_t)fmax(k, 0.0);
+    double k = ceil(((double)v - (double)f.org) * (double)f.icell);
+    if (!(k <= 254.0)) return 255u;      // (also NaN)
+    k = fmax(k, 0.0);
+    while (k <= 254.0 && sum_grid(f, k) < (double)v) k += 1.0;
+    return k <= 254.0 ? (uint32_t)k : 255u;
 }
+// the bounds as fp32, rounded outwards (the fp32 page test stays conservative)
 __device__ __forceinline__ float sum_lo_val(const SumFrame &f, uint32_t c) {
-    return c == 0u ? -INFINITY : fmaf((float)(c - 1u), f.cell, f.org);
+    return c == 0u ? -INFINITY : __double2float_rd(sum_grid(f, (double)(c - 1u)));
 }
 __device__ __forceinline__ float sum_hi_val(const SumFrame &f, uint32_t c) {
-    return c == 255u ? INFINITY : fmaf((float)c, f.cell, f.org);
+    return c == 255u ? INFINITY : __double2float_ru(sum_grid(f, (double)c));
 }
 
 // Summary of the first nvalid mirrors of a page: their box on the grid, or the
