@@ -411,6 +411,10 @@ def appended_maps(args, L, n, per_scan=8):
     r["kernel_ms"] = {"k_candidates": pr["filter_ms"] / max(pr["filter_launches"], 1),
                       "k_update": pr["exact_ms"] / max(pr["exact_launches"], 1),
                       "reduce_and_resample": pr["reduce_ms"] / max(pr["scans"], 1)}
+    # pool upkeep inside the 23 scans (the maps grew to L by appends: the pools hold
+    # what the build-up wrote, so collections / growths come sooner than after an import)
+    r["pool"] = {"collections": pr["pool_collections"], "collect_ms": pr["collect_ms"],
+                 "grows": pr["pool_grows"], "grow_ms": pr["grow_ms"]}
     r.update(buildup_scans=nb, buildup_s=t_build, buildup_resamples=res_b,
              map_size_after_buildup=(None if cnt is None else [int(cnt.min()), int(cnt.max())]),
              note=f"maps grown from empty by appends in observation order ({nb} scans of {per_scan} new "

@@ -530,6 +530,7 @@ struct fs2_handle {
     double *totals = nullptr;                       // all ranks' weight totals
     int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (particles, rows, pages, covariances) per peer
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr;
+    int4 *runs = nullptr;                           // k_ranges' long output runs (k_fill_runs)
     uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
     // the sharded resample's transfers: one send and one receive arena, each
@@ -1727,7 +1728,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->slb_pass); hipFree(h->ext_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
-    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src);
+    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src); hipFree(h->runs);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
     hipFree(h->sarena);
     hipFree(h->rarena);
@@ -1863,6 +1864,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= FS2_ALLOC(h->mlo, n * 4) == hipSuccess;
     ok &= FS2_ALLOC(h->mhi, n * 4) == hipSuccess;
     ok &= FS2_ALLOC(h->out_src, n * 4) == hipSuccess;
+    ok &= FS2_ALLOC(h->runs, sizeof(int4) * kMaxLongRuns) == hipSuccess;
     ok &= FS2_ALLOC(h->cand, n * 8 * kMaxCand) == hipSuccess;
     ok &= FS2_ALLOC(h->ncand, n * 4) == hipSuccess;
     ok &= FS2_ALLOC(h->rec, sizeof(RankRecord)) == hipSuccess;
@@ -2273,6 +2275,7 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
     rs.mlo = h->mlo;
     rs.mhi = h->mhi;
     rs.out_src = h->out_src;
+    rs.runs = h->runs;
     rs.x = h->x[cur]; rs.y = h->y[cur]; rs.yaw = h->yaw[cur]; rs.cnt = h->cnt[cur];
     rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
     rs.map = h->map();
@@ -3918,6 +3921,14 @@ int64_t fs2_debug_check_guards(fs2_handle *h, char *first_bad, int64_t len) {
         bad += k;
     }
     return bad;
+}
+
+int fs2_debug_weights(fs2_handle *h, int32_t other, double *out) {
+    if (!h || !out) return set_err(h ? &h->err : nullptr, FS2_ERR_ARG, "fs2_debug_weights: null argument");
+    HIP_TRY(h, hipSetDevice(h->cfg.device));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    HIP_TRY(h, hipMemcpy(out, h->w[other ? 1 - h->cur : h->cur], sizeof(double) * (size_t)h->n, hipMemcpyDeviceToHost));
+    return FS2_OK;
 }
 
 int64_t fs2_debug_out_src(fs2_handle *h, int32_t *out, int64_t capacity) {

@@ -69,6 +69,13 @@ enum : int {
 };
 
 // Device statistics of one scan (zeroed before every scan).
+// A source whose local outputs exceed kLongRun is filled by all of k_fill_runs'
+// workgroups instead of by its wave 64 outputs at a time (Q10: when the normalised
+// weights sum below 1 the last particle takes every output past their total --
+// a third of 10^6 outputs in the appended-maps workload, 1.5 ms for one wave).
+constexpr int64_t kLongRun = 2048;
+constexpr int kMaxLongRuns = 1024;
+
 struct DevStats {
     double total;            // normalise total (sum of w after update)
     double sumsq;            // sum of normalised w^2
@@ -80,7 +87,8 @@ struct DevStats {
     int32_t resampled;
     int32_t max_count;
     int32_t error_flags;
-    int32_t pad1;
+    uint32_t long_runs;      // k_ranges: sources whose outputs form a run longer than kLongRun (listed
+                             // in ResampleParams.runs, filled by k_fill_runs)
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
     unsigned long long words;    // candidate list entries (8 B: slot, record) written by k_candidates
     unsigned long long cow_pages;    // pages copied before their first write (shared)
@@ -491,6 +499,8 @@ struct ResampleParams {
     ChainView chain;
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
+    int4 *runs;              // [kMaxLongRuns] (first, last local output, source): out_src runs too long
+                             // for one wave, filled by k_fill_runs (count: stats->long_runs)
     const double *x, *y, *yaw;
     const int32_t *cnt;
     double *ox, *oy, *oyaw, *ow;

@@ -228,6 +228,7 @@ SIGNATURES = [
     ("fs2_release_cached_memory", C.c_int64, []),
     ("fs2_debug_noise", C.c_int, [_H, _vp]),
     ("fs2_debug_out_src", C.c_int64, [_H, _vp, C.c_int64]),
+    ("fs2_debug_weights", C.c_int, [_H, C.c_int32, _vp]),
     ("fs2_debug_check_guards", C.c_int64, [_H, C.c_char_p, C.c_int64]),
     ("fs2_debug_mt_jump", C.c_int, [_vp, C.c_uint64, _vp]),
     ("fs2_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),

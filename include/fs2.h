@@ -431,6 +431,10 @@ int fs2_debug_noise(fs2_handle *h, double *out);
  * local source index, < 0 -(k+1) the k-th received particle); returns n_local
  * or a negative error.  For the drift study (scripts/drift_study.py). */
 int64_t fs2_debug_out_src(fs2_handle *h, int32_t *out, int64_t capacity);
+/* The weights of the current particle buffer set (other = 0) or of the other one
+ * (other = 1: after a resampling scan, the sources' normalised weights the
+ * resample read), n_local values.  For diagnosing the exact-order reductions. */
+int fs2_debug_weights(fs2_handle *h, int32_t other, double *out);
 /* Handles created with FS2_GUARD=1 in the environment follow every buffer
  * fs2_create allocates with a known pattern: the number of pattern bytes that
  * changed (a kernel wrote past a buffer's end), the first such buffer's name in
