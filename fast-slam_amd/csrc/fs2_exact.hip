@@ -138,15 +138,26 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         // grid of step 2^-1074 (binade -1022 below): every add there is exact, so a
         // run of zero or subnormal weights (a diverged filter's underflowed
         // likelihoods) is a translation too, not a unit walked term by term
-        bool ok = valid && !(i == 0 && P.chain_first) && a >= 0.0 && a < INFINITY && lo >= 0.0 && hi < 0x1p1020;
-        const int E = ok ? chain_binade(lo) : -4096;
-        ok = ok && chain_binade(hi) == E;
+        const bool base = valid && !(i == 0 && P.chain_first) && a >= 0.0 && a < INFINITY && lo >= 0.0 &&
+                          hi < 0x1p1020;
+        const int E = base ? chain_binade(lo) : -4096;
+        bool ok = base && chain_binade(hi) == E;
+        // A term below half the step of binade E leaves the chain where it is in E and
+        // in every binade above (round to nearest, no tie): an exact identity wherever
+        // in [lo, hi] the chain is, even when that estimate straddles a binade
+        // boundary.  Without this a long run of tiny weights after a chain that ends
+        // within the estimate's margin of a power of two (a resample whose normalised
+        // weights sum to 1 - 6e-11: 2600 units, 2.5 ms in k_chain_walk) was walked
+        // term by term; now such a unit is listed as one segment adding 0.
+        const bool ident = base && !ok && scaled(a, E) < 0.5;
         long long r = 0;
         if (ok) {
             const double q = scaled(a, E);          // < 2^53: exact
             ok = q - floor(q) != 0.5;               // a tie: the rounding depends on s
             r = ok ? (long long)rint(q) : 0;
         }
+        const bool okt = ok;                        // a translation term proper (in binade E)
+        ok = ok || ident;                           // segments may also hold identities (r = 0)
         const unsigned long long vmask = __ballot(valid);
         const int E0 = __builtin_amdgcn_readfirstlane(E);
         if (k == 0 && P.chain_first) {
@@ -169,7 +180,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
                 P.udelta[k] = 0;
                 P.urec[k] = rec;
             }
-        } else if (!(k == 0 && P.force_list0) && __ballot(ok && E == E0) == vmask) {     // one translation
+        } else if (!(k == 0 && P.force_list0) && __ballot(okt && E == E0) == vmask) {    // one translation
             // (a sharded rank lists its unit 0: the walk and the ranges need a listed
             // unit before every translation, and the chain enters there from another rank)
             D = (unsigned long long)wave_sum_i64(r);

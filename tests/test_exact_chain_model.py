@@ -25,20 +25,23 @@ def model_chain(a):
         e_in = bpre[b] + sum(a[b * 256 + q * UNIT:b * 256 + (q + 1) * UNIT].sum() for q in range(k % 4))
         incl = e_in + np.cumsum(seg)
         lo, hi = (incl - seg) * (1 - margin), incl * (1 + margin)
-        ok, E, r = [], [], []
+        ok, okt, E, r = [], [], [], []
         for j, v in enumerate(seg):
-            o = k * UNIT + j != 0 and 0 <= v < np.inf and lo[j] >= 2.0 ** -1020 and hi[j] < 2.0 ** 1020
-            e = math.frexp(lo[j])[1] - 1 if o else -4096
-            o = o and math.frexp(hi[j])[1] - 1 == e
+            base = k * UNIT + j != 0 and 0 <= v < np.inf and lo[j] >= 2.0 ** -1020 and hi[j] < 2.0 ** 1020
+            e = math.frexp(lo[j])[1] - 1 if base else -4096
+            o = base and math.frexp(hi[j])[1] - 1 == e
+            # (round 6) below half the step of binade e: an identity in e and above
+            ident = base and not o and math.ldexp(v, 52 - e) < 0.5
             rr = 0
             if o:
                 q = math.ldexp(v, 52 - e)
                 o = q - math.floor(q) != 0.5
                 rr = int(np.rint(q)) if o else 0
-            ok.append(o)
+            okt.append(o)
+            ok.append(o or ident)
             E.append(e)
             r.append(rr)
-        if all(ok) and len(set(E)) == 1:
+        if all(okt) and len(set(E)) == 1:
             units.append(("t", E[0], sum(r)))
             continue
         segs = []
@@ -101,6 +104,15 @@ def test_chain_model_matches_running_sum():
     w = rng.random(N)
     w[:1000] = 0.0
     cases.append(w)
+    # (round 6) a chain that reaches 1 - 6e-11 early, then only tiny terms: the
+    # estimate's margin straddles 2^0 for every later term (identities, one segment
+    # per unit instead of a term-by-term walk); also heavy terms after such a stretch
+    w = 10.0 ** rng.uniform(-23, -8, N)
+    w[100] = 1.0 - 6.5e-11 - w[:100].sum()
+    cases.append(w)
+    w2 = w.copy()
+    w2[15000] = 0.25
+    cases.append(w2)
     for a in cases:
         c = model_chain(a)
         assert np.array_equal(c, np.cumsum(a))

@@ -119,6 +119,13 @@ def cases():
     w[120_000:] = rng.random(80_003) * 1e-300
     w[190_000:] = rng.random(10_003) * 1e-3
     out.append(("subnormal_grid", w, 0.45 / 200_003))
+    # (round 6) the normalised chain reaches 1 - ~1e-10 after two heavy weights, then
+    # a million tiny ones: the prefix estimate's margin straddles 2^0 for every later
+    # term (identities, listed as one segment per unit; the appended-maps workload's
+    # 2.5 ms walk), and both heavy sources take >100 K outputs (k_fill_runs)
+    w = 10.0 ** rng.uniform(-24, -15, 1_000_000)
+    w[10], w[20] = 0.3, 0.2
+    out.append(("straddle_one", w, 0.3e-6))
     return out
 
 
