@@ -573,6 +573,9 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     if (!P.c) return;
     __syncthreads();                             // sentry of the last batch
     // (3) prefix mode: the values inside the segmented units, one unit per wave
+#ifdef FS2_AB_NO_PHASE3
+    if (true) return;                 // (timing probe only)
+#endif
     for (int o = wid; o < nseq; o += 16) {
         const int64_t q = P.seql[o];
         const int32_t info = P.uinfo[q];

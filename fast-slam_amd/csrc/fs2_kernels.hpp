@@ -69,12 +69,15 @@ enum : int {
 };
 
 // Device statistics of one scan (zeroed before every scan).
-// A source whose local outputs exceed kLongRun is filled by all of k_fill_runs'
-// workgroups instead of by its wave 64 outputs at a time (Q10: when the normalised
-// weights sum below 1 the last particle takes every output past their total --
-// a third of 10^6 outputs in the appended-maps workload, 1.5 ms for one wave).
-constexpr int64_t kLongRun = 2048;
-constexpr int kMaxLongRuns = 1024;
+// A wave of k_ranges whose sources have more than kWaveFill outputs in all lists
+// them for k_fill_runs in pieces of kFillChunk instead of filling them 64 per step
+// (Q10: when the normalised weights sum below 1 the last particle takes every
+// output past their total -- a third of 10^6 outputs in the appended-maps workload,
+// 1.5 ms for one wave; a collapsed filter's heavy siblings sit side by side, 64
+// sources of ~2000 outputs in one wave, 0.7 ms).
+constexpr int64_t kWaveFill = 4096;
+constexpr int64_t kFillChunk = 4096;
+constexpr int kMaxLongRuns = 65536;
 
 struct DevStats {
     double total;            // normalise total (sum of w after update)
@@ -87,8 +90,7 @@ struct DevStats {
     int32_t resampled;
     int32_t max_count;
     int32_t error_flags;
-    uint32_t long_runs;      // k_ranges: sources whose outputs form a run longer than kLongRun (listed
-                             // in ResampleParams.runs, filled by k_fill_runs)
+    uint32_t long_runs;      // k_ranges: output pieces listed for k_fill_runs (ResampleParams.runs)
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
     unsigned long long words;    // candidate list entries (8 B: slot, record) written by k_candidates
     unsigned long long cow_pages;    // pages copied before their first write (shared)
@@ -499,8 +501,8 @@ struct ResampleParams {
     ChainView chain;
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
-    int4 *runs;              // [kMaxLongRuns] (first, last local output, source): out_src runs too long
-                             // for one wave, filled by k_fill_runs (count: stats->long_runs)
+    int4 *runs;              // [kMaxLongRuns] (first, last local output, source): out_src pieces of the
+                             // waves with more than kWaveFill outputs, filled by k_fill_runs
     const double *x, *y, *yaw;
     const int32_t *cnt;
     double *ox, *oy, *oyaw, *ow;

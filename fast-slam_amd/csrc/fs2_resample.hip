@@ -742,15 +742,6 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         lhi = min(hi, P.ao + P.n - 1);
     }
     if (!(P.ranges_mode & 2)) llo = INT64_MAX;     // ranges only: no output filled here
-    // a run too long for the wave goes to k_fill_runs (listed; a full list leaves it here)
-    bool lng = false;
-    if (llo <= lhi && lhi - llo + 1 > kLongRun && P.runs) {
-        const uint32_t slot = atomicAdd(&P.stats->long_runs, 1u);
-        if (slot < (uint32_t)kMaxLongRuns) {
-            P.runs[slot] = make_int4((int)(llo - P.ao), (int)(lhi - P.ao), (int)i, 0);
-            lng = true;
-        }
-    }
     // out_src of the local outputs.  The wave's sources are consecutive and their
     // local output ranges partition one contiguous range in order, so the wave
     // fills that range together, 64 outputs per step (one lane per source would
@@ -777,30 +768,38 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int64_t *wk = s_key + (threadIdx.x - lane);
-        // the wave's outputs between its long runs (listed above, in lane order, so
-        // in output order): each stretch 64 outputs per step
+        // A wave with more than kWaveFill outputs (heavy sources: the siblings of a
+        // good ancestor sit side by side, so one wave can hold 64 sources of ~2000
+        // outputs each -- 700 us for that wave alone in a collapsed resample) lists its
+        // runs, cut into kFillChunk pieces, for k_fill_runs, where every workgroup
+        // takes pieces; a full list leaves the rest of the wave's runs to the wave.
+        bool listed = false;
+        if (wlo <= whi && whi - wlo + 1 > kWaveFill && P.runs) {
+            const bool mine = llo <= lhi;
+            const int64_t pieces = mine ? (lhi - llo + kFillChunk) / kFillChunk : 0;
+            const uint32_t base = pieces ? atomicAdd(&P.stats->long_runs, (uint32_t)pieces) : 0u;
+            const bool fits = !mine || base + (uint64_t)pieces <= (uint64_t)kMaxLongRuns;
+            // every slot below the list's end that this lane took is written (k_fill_runs
+            // reads all of them), a lane that did not fit whole included
+            for (int64_t q = 0; q < pieces && base + (uint64_t)q < (uint64_t)kMaxLongRuns; ++q) {
+                const int64_t a = llo + q * kFillChunk, b = min(lhi, a + kFillChunk - 1);
+                P.runs[base + q] = make_int4((int)(a - P.ao), (int)(b - P.ao), (int)i, 0);
+            }
+            listed = __ballot(!fits) == 0ull;
+        }
+#ifdef FS2_AB_NO_FILL
+        listed = true;                // (timing probe only: out_src left unfilled)
+#endif
+        // otherwise the wave fills its outputs 64 per step
         // (a wave without local outputs has wlo = INT64_MAX: no step)
-        unsigned long long lm = __ballot(lng);
-        int64_t seg_lo = wlo;
-        for (;;) {
-            int64_t seg_hi = whi;
-            int j = -1;
-            if (lm) {
-                j = (int)__builtin_ctzll(lm);
-                seg_hi = bcast_i64(llo, j) - 1;
+        for (int64_t o = (!listed && wlo <= whi) ? wlo + lane : INT64_MAX; o <= whi; o += 64) {
+            int l = 0, h = 63;
+            while (l < h) {
+                const int mid = (l + h + 1) >> 1;
+                if (wk[mid] <= o) l = mid;
+                else h = mid - 1;
             }
-            for (int64_t o = (seg_lo <= seg_hi) ? seg_lo + lane : INT64_MAX; o <= seg_hi; o += 64) {
-                int l = 0, h = 63;
-                while (l < h) {
-                    const int mid = (l + h + 1) >> 1;
-                    if (wk[mid] <= o) l = mid;
-                    else h = mid - 1;
-                }
-                P.out_src[o - P.ao] = (int32_t)(i - lane + l);
-            }
-            if (j < 0) break;
-            seg_lo = bcast_i64(lhi, j) + 1;
-            lm &= lm - 1;
+            P.out_src[o - P.ao] = (int32_t)(i - lane + l);
         }
     }
     if (P.flip_margin > 0.0) {
@@ -828,14 +827,14 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     }
 }
 
-// The long runs k_ranges listed: every workgroup strides over every run (a run's
-// outputs all name its source).  Lazy like k_ranges: nothing listed, nothing done.
+// The pieces k_ranges listed (at most kFillChunk outputs each, all naming one
+// source): one workgroup per piece at a time.  Lazy like k_ranges: nothing listed,
+// nothing done.
 __global__ __launch_bounds__(kBlock) void k_fill_runs(const ResampleParams P) {
     const uint32_t nr = min(P.stats->long_runs, (uint32_t)kMaxLongRuns);
-    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x, stride = (int64_t)gridDim.x * kBlock;
-    for (uint32_t r = 0; r < nr; ++r) {
+    for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
         const int4 run = P.runs[r];
-        for (int64_t o = run.x + t0; o <= run.y; o += stride) P.out_src[o] = run.z;
+        for (int64_t o = run.x + (int64_t)threadIdx.x; o <= run.y; o += kBlock) P.out_src[o] = run.z;
     }
 }
 
@@ -844,7 +843,7 @@ hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s) {
     if (g == 0) return hipSuccess;
     hipLaunchKernelGGL(k_ranges, dim3(g), dim3(kBlock), 0, s, p);
     if ((p.ranges_mode & 2) && p.runs)
-        hipLaunchKernelGGL(k_fill_runs, dim3(std::min<unsigned>(g, 512u)), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL(k_fill_runs, dim3(std::min<unsigned>(g, 256u)), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 
