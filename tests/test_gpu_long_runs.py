@@ -1,13 +1,13 @@
-"""Resamples whose sources take thousands of outputs each (fast_slam_2.py:177-199):
-k_ranges hands a source with more than kLongRun outputs to k_fill_runs (all
-workgroups fill its run) instead of its wave filling 64 outputs per step.  Two
-shapes, each one scan without measurements (the weights are the imported ones)
-against the C oracle on the same draws: heavy particles -- two of them adjacent
-in one wave, one further on -- and normalised weights that sum below 1 (total <
-1, Q6), where the reference's `min(particle_index + 1, N - 1)` hands every output
-past the total to the last particle (Q10); and a family of 128 heavy siblings side
-by side (a wave of sources with ~156 outputs each, listed in pieces).  Every particle's state after the
-resample must be the oracle's."""
+"""Resamples whose sources take thousands of outputs (fast_slam_2.py:177-199):
+a wave of k_ranges with more than kWaveFill outputs lists its sources' runs in
+pieces for k_fill_runs (every workgroup takes pieces) instead of filling 64
+outputs per step.  Three shapes, each one scan without measurements (the weights
+are the imported ones) against the C oracle on the same draws: heavy particles --
+two of them adjacent in one wave, one further on; a family of 128 heavy siblings
+side by side (two waves of sources with ~156 outputs each); and normalised weights
+that sum below 1 (total < 1, Q6), where the reference's
+`min(particle_index + 1, N - 1)` hands every output past the total to the last
+particle (Q10).  Every particle's state after the resample must be the oracle's."""
 import numpy as np
 import pytest
 
