@@ -550,6 +550,7 @@ struct fs2_handle {
     // exact-order reductions (fs2_exact.hip)
     int32_t *uinfo = nullptr, *uol = nullptr, *seql = nullptr, *bC = nullptr, *bpc = nullptr;
     uint32_t *bM = nullptr;
+    int32_t *uel = nullptr, *bE = nullptr, *bpe = nullptr;
     long long *udelta = nullptr;
     unsigned long long *ugl = nullptr, *bD = nullptr, *bpd = nullptr;
     double *sout = nullptr, *part_w = nullptr, *np_part = nullptr, *np_leaf = nullptr, *sentry = nullptr;
@@ -639,6 +640,9 @@ struct fs2_handle {
         p.bM = bM;
         p.bpd = bpd;
         p.bpc = bpc;
+        p.uel = uel;
+        p.bE = bE;
+        p.bpe = bpe;
         p.seql = seql;
         p.sout = sout;
         p.urec = urec;
@@ -1735,6 +1739,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->cand); hipFree(h->ncand);
     hipFree(h->uinfo); hipFree(h->uol); hipFree(h->seql); hipFree(h->udelta); hipFree(h->ugl);
     hipFree(h->bD); hipFree(h->bC); hipFree(h->bM); hipFree(h->bpd); hipFree(h->bpc);
+    hipFree(h->uel); hipFree(h->bE); hipFree(h->bpe);
     hipFree(h->sout); hipFree(h->np_leaf); hipFree(h->part_w); hipFree(h->np_part); hipFree(h->np_tail);
     hipFree(h->urec); hipFree(h->sentry);
     hipFree(h->dch_send); hipFree(h->dch_recv); hipFree(h->recx); hipFree(h->recxs); hipFree(h->est_base);
@@ -1899,6 +1904,9 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
         ok &= FS2_ALLOC(h->bM, ng * 4) == hipSuccess;
         ok &= FS2_ALLOC(h->bpd, ng * 8) == hipSuccess;
         ok &= FS2_ALLOC(h->bpc, ng * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->uel, nu * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->bE, ng * 4) == hipSuccess;
+        ok &= FS2_ALLOC(h->bpe, ng * 4) == hipSuccess;
         ok &= FS2_ALLOC(h->seql, nu * 4) == hipSuccess;
         ok &= FS2_ALLOC(h->udelta, nu * 8) == hipSuccess;
         ok &= FS2_ALLOC(h->ugl, nu * 8) == hipSuccess;
@@ -2297,7 +2305,7 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
         rs.tcap = h->xt_cap;
         rs.tepoch = ++h->loc_epoch;
     }
-    rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout};
+    rs.chain = ChainView{h->uinfo, h->ugl, h->uol, h->bpd, h->bpc, h->seql, h->sout, h->uel, h->bpe};
     rs.gen = sh ? nullptr : h->gen_dev;      // (one GPU: k_tail_single bumps it on a resample)
 
     // weight total over all ranks (fast_slam_2.py:166).  Exact: Python's sum (in

@@ -124,7 +124,19 @@ __device__ inline double chain_unit(double a, int cnt, double &s, bool first) {
     return mine;
 }
 
-// Chain value before unit k's first term, for a translation unit.
+// The binade of the chain at the last translation unit proper (not an identity
+// unit) at or before unit k -- the binade of every translation run that ends
+// after it, up to the next listed unit: the chain's binade is constant along a run
+// of translation and identity units, and a run of identity units alone adds 0
+// (then any binade will do: 0 when there is none).
+__device__ __forceinline__ int chain_elast(const int32_t *uel, const int32_t *bpe, int64_t k) {
+    int e = uel[k];
+    if (e == 0) e = bpe[k / kChainGroup];
+    return e ? e - 4096 : 0;
+}
+
+// Chain value before unit k's first term, for a translation unit; E: the binade
+// of the translation run before k (chain_elast(k - 1)).
 __device__ __forceinline__ double chain_unit_entry(const ChainView &V, int64_t k, int E) {
     const int64_t g = k / kChainGroup;
     const int o = V.bpc[g] + V.uol[k] - 1;            // the last listed unit before k (unit 0 is listed)

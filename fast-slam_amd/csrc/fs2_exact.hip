@@ -68,7 +68,7 @@ __device__ __forceinline__ bool lazy_skip(const ChainParams &P) {
 __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     __shared__ double s_ws[16];
     __shared__ unsigned long long s_D[16];
-    __shared__ int s_f[16];
+    __shared__ int s_f[16], s_e[16];
     __shared__ double s_red[16], s_bp[4];
     __shared__ unsigned long long s_c[16][kNumCounters];
     if (P.lazy && lazy_skip(P)) return;
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     if (lane == 63) s_ws[wid] = incl;
     __syncthreads();
     unsigned long long D = 0;
-    int listed = 0;
+    int listed = 0, etr = 0;                         // etr: binade + 4096 of a translation proper
     if (k < nu) {
         // estimate of the chain before this unit: the 256-term block prefix, then
         // the units of that block ahead of this one
@@ -148,7 +148,8 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
         // boundary.  Without this a long run of tiny weights after a chain that ends
         // within the estimate's margin of a power of two (a resample whose normalised
         // weights sum to 1 - 6e-11: 2600 units, 2.5 ms in k_chain_walk) was walked
-        // term by term; now such a unit is listed as one segment adding 0.
+        // term by term; a unit of identities alone is a translation by 0 whose binade
+        // is inherited (chain_elast), one that mixes them with other terms is listed.
         const bool ident = base && !ok && scaled(a, E) < 0.5;
         long long r = 0;
         if (ok) {
@@ -184,9 +185,15 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
             // (a sharded rank lists its unit 0: the walk and the ranges need a listed
             // unit before every translation, and the chain enters there from another rank)
             D = (unsigned long long)wave_sum_i64(r);
+            etr = E0 + 4096;
             if (lane == 0) {
                 P.uinfo[k] = (E0 + 4096) << 2;
                 P.udelta[k] = (long long)D;
+            }
+        } else if (!(k == 0 && P.force_list0) && __ballot(ok && r == 0) == vmask) {   // identities only
+            if (lane == 0) {
+                P.uinfo[k] = ((E0 + 4096) << 2) | 2;
+                P.udelta[k] = 0;
             }
         } else {
             listed = 1;
@@ -235,27 +242,31 @@ __global__ __launch_bounds__(1024) void k_chain_units(const ChainParams P) {
     if (lane == 0) {
         s_D[wid] = D;
         s_f[wid] = listed;
+        s_e[wid] = etr;
     }
     __syncthreads();
     if (t < kChainGroup) {
         // the group's scan (16 values, lanes 0..15 of wave 0)
         unsigned long long dx = 0;
-        int cx = 0;
+        int cx = 0, ex = 0;
         unsigned mask = 0;
         for (int q = 0; q < kChainGroup; ++q) {
             if (q < t) dx += s_D[q];
             if (q <= t) cx += s_f[q];
+            if (q <= t && s_e[q]) ex = s_e[q];
             mask |= (unsigned)s_f[q] << q;
         }
         const int64_t kk = (int64_t)blockIdx.x * kChainGroup + t;
         if (kk < nu) {
             P.ugl[kk] = dx;
             P.uol[kk] = cx;
+            P.uel[kk] = ex;
         }
         if (t == kChainGroup - 1) {
             P.bD[blockIdx.x] = dx + s_D[t];
             P.bC[blockIdx.x] = cx;
             P.bM[blockIdx.x] = mask;
+            P.bE[blockIdx.x] = ex;
         }
     }
     FS2_TS(0, 3);
@@ -305,24 +316,21 @@ __device__ void chain_export(const ChainParams &P, int nseq, int64_t nu, unsigne
     ChainSummary *S = P.ops_out;
     int base = 0;
     unsigned long long gprev = 0;
-    int Eprev = 0;
     for (int o0 = 0; o0 < nseq; o0 += 64) {
         const int ol = o0 + lane;
         const bool in = ol < nseq;
         int64_t q = 0;
         int32_t info = 0;
         unsigned long long g = 0;
-        int En = 0;
+        int Eb = 0;                                   // the binade of the run before q
         if (in) {
             q = P.seql[ol];
             info = P.uinfo[q];
             g = P.bpd[q / kChainGroup] + P.ugl[q];
-            En = (q + 1 < nu) ? unit_binade(P.uinfo[q + 1]) : 0;
+            if (q > 0) Eb = chain_elast(P.uel, P.bpe, q - 1);
         }
         const unsigned long long gp = __shfl_up(g, 1, 64);
-        const int Ep = __shfl_up(En, 1, 64);
         const unsigned long long gb = (lane == 0) ? gprev : gp;
-        const int Eb = (lane == 0) ? Eprev : Ep;
         const double run = (in && ol > 0) ? (double)(long long)(g - gb) * unit_ulp(Eb) : 0.0;
         const int cnt = in ? (int)min<int64_t>(kUnit, P.n - q * kUnit) : 0;
         const bool terms = in && ((info & 2) || (q == 0 && P.chain_first));
@@ -355,11 +363,10 @@ __device__ void chain_export(const ChainParams &P, int nseq, int64_t nu, unsigne
         const int nb = min(64, nseq - o0);
         base += (int)bcast_i64(incl, 63);
         gprev = bcast_i64((long long)g, nb - 1);
-        Eprev = __builtin_amdgcn_readlane(En, nb - 1);
     }
     if (lane == 0) {
         int k = base;
-        const double run = (double)(long long)(dtot - gprev) * unit_ulp(Eprev);
+        const double run = (double)(long long)(dtot - gprev) * unit_ulp(chain_elast(P.uel, P.bpe, nu - 1));
         if (run != 0.0) {
             if (k < kChainOpsCap) S->ops[k] = run;
             ++k;
@@ -370,7 +377,7 @@ __device__ void chain_export(const ChainParams &P, int nseq, int64_t nu, unsigne
 
 __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     __shared__ unsigned long long s_d[2][16];
-    __shared__ int s_c[2][16];
+    __shared__ int s_c[2][16], s_e[2][16];
     __shared__ int s_nseq;
     __shared__ unsigned long long s_dtot;
     __shared__ double s_terms[kWalkStage][kUnit];     // term-by-term units of a batch: terms, then values
@@ -388,44 +395,53 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     // (1) the scan over groups of kChainGroup units (one group per thread and step)
     const int64_t ng = (nu + kChainGroup - 1) / kChainGroup;
     unsigned long long carry = 0;
-    int ccount = 0;
+    int ccount = 0, ecarry = 0;
     for (int64_t j0 = 0; j0 < ng; j0 += 1024) {
         const int64_t gi = j0 + t;
         const bool in = gi < ng;
         const unsigned long long d = in ? P.bD[gi] : 0ull;
         const int f = in ? P.bC[gi] : 0;
         const unsigned m = in ? P.bM[gi] : 0u;
+        const int e = in ? P.bE[gi] : 0;
         const int b = (int)((j0 >> 10) & 1);
         unsigned long long di = d;
-        int ci = f;
+        int ci = f, ei = e;                       // ei: the last nonzero binade up to this group
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const unsigned long long v = __shfl_up(di, o, 64);
             const int c = __shfl_up(ci, o, 64);
+            const int x = __shfl_up(ei, o, 64);
             if (lane >= o) {
                 di += v;
                 ci += c;
+                if (!ei) ei = x;
             }
         }
+        const int eb = __shfl_up(ei, 1, 64);     // up to the group before (lane > 0)
         if (lane == 63) {
             s_d[b][wid] = di;
             s_c[b][wid] = ci;
+            s_e[b][wid] = ei;
         }
         __syncthreads();                          // s_d[b] is rewritten two steps later
         unsigned long long dx = carry + di - d, tot = 0;
-        int cx = ccount + ci - f, ctot = 0;
+        int cx = ccount + ci - f, ctot = 0, ex = ecarry;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             if (q < wid) {
                 dx += s_d[b][q];
                 cx += s_c[b][q];
+                if (s_e[b][q]) ex = s_e[b][q];
             }
             tot += s_d[b][q];
             ctot += s_c[b][q];
+            if (s_e[b][q]) ecarry = s_e[b][q];
         }
+        if (lane > 0 && eb) ex = eb;
         if (in) {
             P.bpd[gi] = dx;
             P.bpc[gi] = cx;
+            P.bpe[gi] = ex;
             for (unsigned mm = m; mm; mm &= mm - 1) P.seql[cx++] = (int32_t)(gi * kChainGroup + __builtin_ctz(mm));
         }
         carry += tot;
@@ -453,18 +469,17 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     // waves; wave 0 walks; then the staged values are written out
     double s = P.s_entry ? *P.s_entry : 0.0;       // the running value (wave 0)
     unsigned long long gprev = 0;
-    int Eprev = 0;
     for (int o0 = 0; o0 < nseq; o0 += 64) {
         const int ol = o0 + lane;
         int64_t q = 0;
         unsigned long long g = 0;
-        int32_t info = 0, En = 0;
+        int32_t info = 0, Eb = 0;                    // Eb: the binade of the run before q
         if (ol < nseq) {
             q = P.seql[ol];
             info = P.uinfo[q];
             if (wid == 0) {
                 g = P.bpd[q / kChainGroup] + P.ugl[q];
-                En = (q + 1 < nu) ? unit_binade(P.uinfo[q + 1]) : 0;
+                if (q > 0) Eb = chain_elast(P.uel, P.bpe, q - 1);
             }
         }
         const unsigned long long wsm = __ballot(ol < nseq && (info & 2));   // term by term
@@ -497,12 +512,9 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
                 for (int u = 0; u < kChainSegs; ++u) rv[u] = rr.val[u];
             }
             const unsigned long long gp = __shfl_up(g, 1, 64);
-            const int Ep = __shfl_up(En, 1, 64);
             const unsigned long long gb = (lane == 0) ? gprev : gp;
-            const int Eb = (lane == 0) ? Eprev : Ep;
             const double run = (ol > 0 && ol < nseq) ? (double)(long long)(g - gb) * unit_ulp(Eb) : 0.0;
             gprev = bcast_i64((long long)g, nb - 1);
-            Eprev = __builtin_amdgcn_readlane(En, nb - 1);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -568,7 +580,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     FS2_CHAIN_STAMP(3);
     if (wid == 0 && lane == 0 && P.total) {
         // the chain ends in the translation run after the last listed unit (if any)
-        *P.total = s + (double)(long long)(s_dtot - gprev) * unit_ulp(Eprev);
+        *P.total = s + (double)(long long)(s_dtot - gprev) * unit_ulp(chain_elast(P.uel, P.bpe, nu - 1));
     }
     if (!P.c) return;
     __syncthreads();                             // sentry of the last batch

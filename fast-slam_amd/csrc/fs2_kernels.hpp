@@ -467,13 +467,15 @@ struct ReduceParams {
 // The unit table of an evaluated chain (fs2_exact.hip k_chain_walk), as the
 // resample's range kernel reads it to evaluate the running sum in place.
 struct ChainView {
-    const int32_t *uinfo;             // [nu] bit 0: listed (values in c), else binade
+    const int32_t *uinfo;             // [nu] bit 0: listed (values in c), else binade (bit 1: identity)
     const unsigned long long *ugl;    // [nu] exclusive translation sum inside the unit's group
     const int32_t *uol;               // [nu] listed units of the group up to and including k
     const unsigned long long *bpd;    // [ng] exclusive translation sum before each group
     const int32_t *bpc;               // [ng] listed units before each group
     const int32_t *seql;              // listed units in order
     const double *sout;               // chain value after each listed unit
+    const int32_t *uel;               // [nu] binade + 4096 of the last translation proper in the group up to k
+    const int32_t *bpe;               // [ng] ... before each group (0: none)
 };
 
 // Resample of a shard of n particles / n outputs starting at global index a.
@@ -569,9 +571,10 @@ struct ChainParams {
     const unsigned long long *cpart;   // non-null: fold these update counters [kNumCounters][ncpart]
     int32_t ncpart;
     DevStats *cstats;        // into these statistics (k_wsum's other job; total mode)
-    int32_t *uinfo;          // [nu] per 64-term unit: (binade + 4096) << 2 for a translation; bit 0:
-                             // listed: segments (UnitRec, count in bits 3-6), or bit 1: evaluated
-                             // term by term (chain_unit)
+    int32_t *uinfo;          // [nu] per 64-term unit: (binade + 4096) << 2 for a translation (bit 1:
+                             // identity, every term adds 0 wherever the chain is -- its binade is
+                             // inherited, chain_elast); bit 0: listed: segments (UnitRec, count in
+                             // bits 3-6), or bit 1: evaluated term by term (chain_unit)
     UnitRec *urec;           // [nu] segments of the units with uinfo bit 0
     double *sentry;          // [nu] chain value before each non-translation unit (by ordinal)
     long long *udelta;       // [nu] translation in ulps of the unit's binade
@@ -580,6 +583,10 @@ struct ChainParams {
     unsigned long long *bD;  // [ng] per group: translation sum
     int32_t *bC;             // [ng]            listed units
     uint32_t *bM;            // [ng]            listed-unit mask
+    int32_t *uel;            // [nu] binade + 4096 of the last translation proper (not identity) in
+                             // the group up to and including k (0: none)
+    int32_t *bE;             // [ng] ... of the group; bpe: before each group (k_chain_walk)
+    int32_t *bpe;
     unsigned long long *bpd; // [ng] exclusive scans of bD / bC (k_chain_walk)
     int32_t *bpc;
     int32_t *seql;           // [nu] serial units in order

@@ -708,10 +708,12 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
             // (a sharded rank's first element: the chain value before it, k_chain_fold)
             cprev = (i > 0 && i - 1 < P.n) ? P.c[i - 1] : (i == 0 && P.a > 0 ? P.stats->offset : 0.0);
         } else {
+            // (an identity unit adds 0 and inherits the run's binade)
+            const bool idu = (info & 2) != 0;
             const int E = unit_binade(info);
             const double u = unit_ulp(E);
-            const double s_in = chain_unit_entry(P.chain, k, E);
-            const long long r = (i < P.n) ? (long long)rint(scaled(P.w[i], E)) : 0;
+            const double s_in = chain_unit_entry(P.chain, k, (idu && k > 0) ? chain_elast(P.chain.uel, P.chain.bpe, k - 1) : E);
+            const long long r = (i < P.n && !idu) ? (long long)rint(scaled(P.w[i], E)) : 0;
             const long long pre = wave_incl_scan_i64(r);
             cv = s_in + (double)pre * u;
             cprev = s_in + (double)(pre - r) * u;

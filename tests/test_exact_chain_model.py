@@ -9,7 +9,7 @@ import numpy as np
 UNIT = 64
 
 
-def model_chain(a):
+def model_chain(a, return_units=False):
     """fs2_exact.hip: k_chain_units (per-term binade estimates -> one translation,
     up to 4 segments, or term by term), k_chain_walk and its prefix post-pass."""
     n = len(a)
@@ -44,6 +44,11 @@ def model_chain(a):
         if all(okt) and len(set(E)) == 1:
             units.append(("t", E[0], sum(r)))
             continue
+        if all(o and rr == 0 for o, rr in zip(ok, r)):
+            # (round 6) every term an identity: a translation by 0 whose binade is
+            # inherited (the estimate may straddle a boundary the chain never crosses)
+            units.append(("i", E[0], 0))
+            continue
         segs = []
         for j in range(len(seg)):
             if j == 0 or not ok[j] or not ok[j - 1] or E[j] != E[j - 1]:
@@ -60,17 +65,32 @@ def model_chain(a):
             else:
                 desc.append(("s", None, seg[st], st, en))
         units.append(("g", desc, None))
+    # Elast(k): the binade of the last translation unit proper at or before k (identity
+    # units inherit it; None: no such unit, so every run before k adds 0)
+    elast, e = [], None
+    for kind, x, y in units:
+        if kind == "t":
+            e = x
+        elast.append(e)
     c = np.empty(n)
-    s = 0.0
+    s_out, dsum = 0.0, 0               # value after the last listed unit, D since it
     for k, (kind, x, y) in enumerate(units):
         lo_i = k * UNIT
         vals = a[lo_i:lo_i + UNIT]
-        if kind == "t":
-            u = math.ldexp(1.0, x - 52)
-            pre = np.cumsum(np.rint(np.ldexp(vals, 52 - x)).astype(np.int64))
-            c[lo_i:lo_i + len(vals)] = s + pre.astype(np.float64) * u
-            s = s + float(y) * u
-        elif kind == "w":
+        er = elast[k - 1] if k > 0 else None
+        assert dsum == 0 or er is not None
+        s_in = s_out + float(dsum) * (math.ldexp(1.0, er - 52) if er is not None else 0.0)
+        if kind in "ti":
+            if kind == "i":
+                c[lo_i:lo_i + len(vals)] = s_in
+            else:
+                u = math.ldexp(1.0, x - 52)
+                pre = np.cumsum(np.rint(np.ldexp(vals, 52 - x)).astype(np.int64))
+                c[lo_i:lo_i + len(vals)] = s_in + pre.astype(np.float64) * u
+            dsum += y
+            continue
+        s = s_in
+        if kind == "w":
             out, s = chain_unit_ref(vals, s, k == 0)
             c[lo_i:lo_i + len(vals)] = out
         else:
@@ -83,7 +103,8 @@ def model_chain(a):
                     pre = np.cumsum(np.rint(np.ldexp(vals[st:en], 52 - e)).astype(np.int64))
                     c[lo_i + st:lo_i + en] = s + pre.astype(np.float64) * u
                     s = s + float(d) * u
-    return c
+        s_out, dsum = s, 0
+    return (c, units, elast) if return_units else c
 
 
 def chain_unit_ref(vals, s, first):
@@ -116,6 +137,26 @@ def test_chain_model_matches_running_sum():
     for a in cases:
         c = model_chain(a)
         assert np.array_equal(c, np.cumsum(a))
+
+
+def test_chain_model_identity_units_inherit_binade():
+    """(round 6) chain_cases.straddle_runs: units of identities alone whose estimate
+    straddles 2^0 are translations by 0 in the binade of the run they sit in --
+    below 1 before the crossing, above it after, where the estimate's lower bound
+    still names [0.5, 1)."""
+    from chain_cases import straddle_runs
+    a = straddle_runs(20011, np.random.default_rng(3), normalised=True)
+    c, units, elast = model_chain(a, return_units=True)
+    assert np.array_equal(c, np.cumsum(a))
+    kinds = [u[0] for u in units]
+    idx = [k for k, kd in enumerate(kinds) if kd == "i"]
+    assert len(idx) > 50
+    # identities after the crossing (chain in [1, 2)) still name [0.5, 1) ...
+    cross = 20011 // 5 // 64
+    after = [k for k in idx if k > cross and c[k * 64] >= 1.0]
+    assert after and all(units[k][1] == -1 for k in after)
+    # ... and translations with D != 0 follow in [1, 2)
+    assert any(kd == "t" and units[k][1] == 0 and units[k][2] > 0 for k, kd in enumerate(kinds))
 
 
 def model_chain_unit(a, s, first):

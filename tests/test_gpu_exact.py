@@ -126,6 +126,10 @@ def cases():
     w = 10.0 ** rng.uniform(-24, -15, 1_000_000)
     w[10], w[20] = 0.3, 0.2
     out.append(("straddle_one", w, 0.3e-6))
+    # (round 6) identity units on both sides of a crossing inside the margin zone
+    # (translations by 0 whose binade is inherited, tests/chain_cases.py)
+    from chain_cases import straddle_runs
+    out.append(("straddle_runs", straddle_runs(1_000_000, rng), 0.7e-6))
     return out
 
 

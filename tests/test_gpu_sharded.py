@@ -175,6 +175,52 @@ def test_sharded_exact_is_bitwise(G, N, L):
         h.close()
 
 
+@pytest.mark.parametrize("G", [2, 4])
+def test_sharded_exact_straddle(G):
+    """(round 6) The exact chain across shards on tests/chain_cases.straddle_runs:
+    long runs of identity units whose estimate straddles 2^0, on both sides of the
+    crossing (translations by 0 in an inherited binade, chain_export's runs), a
+    crossing inside one shard and heavy sources feeding every rank.  One scan
+    without measurements (the tail alone) equals the single exact handle bit for
+    bit."""
+    import torch  # noqa: F401
+    import fast_slam_2
+    from chain_cases import straddle_runs
+    from gpu_util import configure
+    configure()
+    N, L = 200_003, 4
+    rng = np.random.default_rng(9)
+    w = straddle_runs(N, rng)
+    x, y, yaw = rng.normal(0, 1, N), rng.normal(0, 1, N), rng.normal(0, 0.1, N)
+    lm = np.zeros((N, L, 6))
+    lm[:, :, 0] = rng.normal(0, 5, (N, L))
+    lm[:, :, 1] = rng.normal(0, 5, (N, L))
+    lm[:, :, 2] = lm[:, :, 5] = 0.01
+    cnt = np.full(N, L, np.int32)
+    single = fast_slam_2.FastSLAM2(N, reduce="exact", seed=5, landmark_capacity=L, verbose=False)
+    single.set_state(x, y, yaw, w, cnt, lm)
+    key = os.urandom(128)
+    shards = [fast_slam_2.FastSLAM2(N, reduce="auto", seed=5, landmark_capacity=L, rank=g, world_size=G,
+                                    comm_id=key, comm_mode="local", verbose=False) for g in range(G)]
+    for h in shards:
+        a, b = h.first_global, h.first_global + h.n_local
+        h.set_state(x[a:b], y[a:b], yaw[a:b], w[a:b], cnt[a:b], lm[a:b])
+    ms = np.zeros((0, 2))
+    pose1, st1 = single.step(0.0, 0.0, ms)
+    assert st1.resampled
+    for pose, st in _step_all(shards, 0.0, 0.0, ms):
+        assert st.reduce_ambiguous == 0 and st.error_flags == 0
+        assert st.total_weight == st1.total_weight and st.n_eff == st1.n_eff
+        assert st.best_index == st1.best_index
+        assert np.array_equal(pose, pose1)
+    s1 = single.get_state(lm_cap=L)
+    sg = _gather(shards, L)
+    for k in range(6):
+        assert np.array_equal(s1[k], sg[k]), k
+    for h in shards + [single]:
+        h.close()
+
+
 def _run_sharded(G, N, L, scans, page_refs, seed=21, page_pool=0, record_pool=0, refuse=()):
     """G local ranks over the peaked workload, each scan checked against a single
     handle (decisions, estimates, associations; states within 1e-9); returns the
