@@ -25,7 +25,12 @@
 // term, or the chain's first element are evaluated in order from their exact
 // entry value (chain_unit, fs2_chain.hpp).  Only those (~20-40 per chain: one
 // per binade crossed) are walked serially; the translations between them are an
-// integer scan.
+// integer scan.  A term below half the step of its estimate's lower binade adds
+// 0 wherever the chain is; a unit of such terms alone is a translation by 0 even
+// when the estimate straddles a binade boundary, its binade inherited from the
+// last translation unit before it (chain_elast: a run's binade is constant, and a
+// run of identities alone adds nothing) -- a collapsed resample's million tiny
+// weights after a chain ending within the margin of 2^0 are one scan, not a walk.
 //
 //   k_chain_units  per unit: translation (binade E, D) or serial (each workgroup
 //                  estimates the chain at its block starts from the block sums
