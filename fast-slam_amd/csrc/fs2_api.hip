@@ -530,6 +530,7 @@ struct fs2_handle {
     double *totals = nullptr;                       // all ranks' weight totals
     int64_t *xrow = nullptr, *xmat = nullptr;       // transfer sizes (particles, rows, pages, covariances) per peer
     int32_t *mlo = nullptr, *mhi = nullptr, *out_src = nullptr;
+    uint32_t *runs_n = nullptr;
     int4 *runs = nullptr;                           // k_ranges' long output runs (k_fill_runs)
     uint64_t *cand = nullptr;                       // [kMaxCand/4][n] candidate slots
     int32_t *ncand = nullptr;
@@ -1732,7 +1733,7 @@ static void free_handle(fs2_handle *h) {
     hipFree(h->rbcnt); hipFree(h->rnfree_dev);
     hipFree(h->slb); hipFree(h->slb_pass); hipFree(h->ext_dev);
     hipFree(h->rank_d); hipFree(h->rank_e); hipFree(h->iblk);
-    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src); hipFree(h->runs);
+    hipFree(h->mlo); hipFree(h->mhi); hipFree(h->out_src); hipFree(h->runs); hipFree(h->runs_n);
     hipFree(h->rec); hipFree(h->recs); hipFree(h->totals); hipFree(h->xrow); hipFree(h->xmat);
     hipFree(h->sarena);
     hipFree(h->rarena);
@@ -1870,6 +1871,7 @@ int fs2_create(const fs2_config *cfg, fs2_handle **out) {
     ok &= FS2_ALLOC(h->mhi, n * 4) == hipSuccess;
     ok &= FS2_ALLOC(h->out_src, n * 4) == hipSuccess;
     ok &= FS2_ALLOC(h->runs, sizeof(int4) * kMaxLongRuns) == hipSuccess;
+    ok &= FS2_ALLOC(h->runs_n, 4) == hipSuccess && hipMemset(h->runs_n, 0, 4) == hipSuccess;
     ok &= FS2_ALLOC(h->cand, n * 8 * kMaxCand) == hipSuccess;
     ok &= FS2_ALLOC(h->ncand, n * 4) == hipSuccess;
     ok &= FS2_ALLOC(h->rec, sizeof(RankRecord)) == hipSuccess;
@@ -2284,6 +2286,7 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
     rs.mhi = h->mhi;
     rs.out_src = h->out_src;
     rs.runs = h->runs;
+    rs.runs_n = h->runs_n;
     rs.x = h->x[cur]; rs.y = h->y[cur]; rs.yaw = h->yaw[cur]; rs.cnt = h->cnt[cur];
     rs.ox = h->x[nxt]; rs.oy = h->y[nxt]; rs.oyaw = h->yaw[nxt]; rs.ow = h->w[nxt]; rs.ocnt = h->cnt[nxt];
     rs.map = h->map();
@@ -2428,7 +2431,7 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
         }
         // every local output is written below: the output ranges of the local
         // sources (k_ranges) and of the received ones (k_scatter_recv) partition them
-        HIP_TRY(h, launch_resample_ranges(rs, s));
+        HIP_TRY(h, launch_resample_ranges(rs, s, sh));     // (one GPU: k_tail_single fills the runs)
         if (!sh)
             HIP_TRY(h, launch_tail_single(rs, rp, h->pub_stats_dev, h->pub_flag_dev, pseq, s, nullptr));
         if (sh) {

@@ -130,8 +130,8 @@ __device__ inline double chain_unit(double a, int cnt, double &s, bool first) {
 // of translation and identity units, and a run of identity units alone adds 0
 // (then any binade will do: 0 when there is none).
 __device__ __forceinline__ int chain_elast(const int32_t *uel, const int32_t *bpe, int64_t k) {
-    int e = uel[k];
-    if (e == 0) e = bpe[k / kChainGroup];
+    const int u = uel[k], b = bpe[k / kChainGroup];     // both requested at once
+    const int e = u ? u : b;
     return e ? e - 4096 : 0;
 }
 

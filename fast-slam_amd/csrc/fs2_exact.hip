@@ -473,6 +473,8 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     // per lane); the term-by-term ones have their terms staged in LDS by all
     // waves; wave 0 walks; then the staged values are written out
     double s = P.s_entry ? *P.s_entry : 0.0;       // the running value (wave 0)
+    // the binade of the run after the last listed unit, requested now (read at the end)
+    const int e_end = (t == 0 && P.total) ? chain_elast(P.uel, P.bpe, nu - 1) : 0;
     unsigned long long gprev = 0;
     for (int o0 = 0; o0 < nseq; o0 += 64) {
         const int ol = o0 + lane;
@@ -585,7 +587,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainParams P) {
     FS2_CHAIN_STAMP(3);
     if (wid == 0 && lane == 0 && P.total) {
         // the chain ends in the translation run after the last listed unit (if any)
-        *P.total = s + (double)(long long)(s_dtot - gprev) * unit_ulp(chain_elast(P.uel, P.bpe, nu - 1));
+        *P.total = s + (double)(long long)(s_dtot - gprev) * unit_ulp(e_end);
     }
     if (!P.c) return;
     __syncthreads();                             // sentry of the last batch

@@ -78,6 +78,7 @@ enum : int {
 constexpr int64_t kWaveFill = 4096;
 constexpr int64_t kFillChunk = 4096;
 constexpr int kMaxLongRuns = 65536;
+constexpr unsigned kTailFill = 64;         // k_tail_single workgroups filling listed runs
 
 struct DevStats {
     double total;            // normalise total (sum of w after update)
@@ -90,7 +91,7 @@ struct DevStats {
     int32_t resampled;
     int32_t max_count;
     int32_t error_flags;
-    uint32_t long_runs;      // k_ranges: output pieces listed for k_fill_runs (ResampleParams.runs)
+    uint32_t pad1;
     unsigned long long visited, candidates, hits, appends, written, ambiguous, resample_slots;
     unsigned long long words;    // candidate list entries (8 B: slot, record) written by k_candidates
     unsigned long long cow_pages;    // pages copied before their first write (shared)
@@ -504,7 +505,9 @@ struct ResampleParams {
     int32_t *mlo, *mhi;      // [n] global output range served by each local particle
     int32_t *out_src;        // [n] source of each local output: >= 0 local, < 0 -(k+1) received
     int4 *runs;              // [kMaxLongRuns] (first, last local output, source): out_src pieces of the
-                             // waves with more than kWaveFill outputs, filled by k_fill_runs
+                             // waves with more than kWaveFill outputs, filled by k_fill_runs (one
+                             // GPU: by k_tail_single's other workgroups)
+    uint32_t *runs_n;        // pieces listed (k_ranges); zeroed by the gather that follows
     const double *x, *y, *yaw;
     const int32_t *cnt;
     double *ox, *oy, *oyaw, *ow;
@@ -655,7 +658,7 @@ hipError_t launch_prefix(const ResampleParams &p, int sequential, hipStream_t s)
 hipError_t launch_finalize(const ReduceParams &p, hipStream_t s);
 hipError_t launch_global_finalize(const ReduceParams &p, hipStream_t s);
 // resample, split where the sharded path needs the host (sizes of transfers)
-hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s);
+hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s, bool fill_runs = true);
 hipError_t launch_pack_count(const ResampleParams &p, hipStream_t s);
 // the distinct pages of every destination's rows (xt sized for sum S, key and
 // ref zeroed by the caller), counted into xrow[6 p + 2], their covariances

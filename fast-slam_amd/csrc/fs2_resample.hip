@@ -779,7 +779,7 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
         if (wlo <= whi && whi - wlo + 1 > kWaveFill && P.runs) {
             const bool mine = llo <= lhi;
             const int64_t pieces = mine ? (lhi - llo + kFillChunk) / kFillChunk : 0;
-            const uint32_t base = pieces ? atomicAdd(&P.stats->long_runs, (uint32_t)pieces) : 0u;
+            const uint32_t base = pieces ? atomicAdd(P.runs_n, (uint32_t)pieces) : 0u;
             const bool fits = !mine || base + (uint64_t)pieces <= (uint64_t)kMaxLongRuns;
             // every slot below the list's end that this lane took is written (k_fill_runs
             // reads all of them), a lane that did not fit whole included
@@ -812,12 +812,14 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
     if (P.est_early) {
         // the outputs' first maximum (fast_slam_2.py:201-210 after :196): outputs are
         // in source order and copy their source's weight, so it is the first output
-        // of the first heaviest source that has outputs; and the slots they refer to
+        // of the first heaviest source that has outputs; and the slots they refer to.
+        // The key carries the source (output << 32 | source): its outputs may sit in
+        // a listed run that k_tail_single's other workgroups fill meanwhile
         __shared__ double lds_d[kBlock / 64];
         __shared__ int64_t lds_l[kBlock / 64];
         const bool has = i < P.n && llo <= lhi;
         double bv = has ? P.w[i] : -INFINITY;
-        int64_t bi = has ? llo - P.ao : INT64_MAX;
+        int64_t bi = has ? ((llo - P.ao) << 32) | i : INT64_MAX;
         const unsigned long long sl = has ? (unsigned long long)(lhi - llo + 1) * (unsigned long long)P.cnt[i] : 0ull;
         const unsigned long long bs = block_sum_u64<kBlock>(sl, lds_u);
         block_argmax<kBlock>(bv, bi, lds_d, lds_l);
@@ -832,19 +834,23 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const ResampleParams P) {
 // The pieces k_ranges listed (at most kFillChunk outputs each, all naming one
 // source): one workgroup per piece at a time.  Lazy like k_ranges: nothing listed,
 // nothing done.
-__global__ __launch_bounds__(kBlock) void k_fill_runs(const ResampleParams P) {
-    const uint32_t nr = min(P.stats->long_runs, (uint32_t)kMaxLongRuns);
-    for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+__device__ __forceinline__ void fill_runs_body(const ResampleParams &P, uint32_t b, uint32_t nb) {
+    const uint32_t nr = min(*P.runs_n, (uint32_t)kMaxLongRuns);
+    for (uint32_t r = b; r < nr; r += nb) {
         const int4 run = P.runs[r];
-        for (int64_t o = run.x + (int64_t)threadIdx.x; o <= run.y; o += kBlock) P.out_src[o] = run.z;
+        for (int64_t o = run.x + (int64_t)threadIdx.x; o <= run.y; o += blockDim.x) P.out_src[o] = run.z;
     }
 }
 
-hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s) {
+__global__ __launch_bounds__(kBlock) void k_fill_runs(const ResampleParams P) {
+    fill_runs_body(P, blockIdx.x, gridDim.x);
+}
+
+hipError_t launch_resample_ranges(const ResampleParams &p, hipStream_t s, bool fill_runs) {
     const unsigned g = (unsigned)((p.n + kBlock - 1) / kBlock);
     if (g == 0) return hipSuccess;
     hipLaunchKernelGGL(k_ranges, dim3(g), dim3(kBlock), 0, s, p);
-    if ((p.ranges_mode & 2) && p.runs)
+    if (fill_runs && (p.ranges_mode & 2) && p.runs)
         hipLaunchKernelGGL(k_fill_runs, dim3(std::min<unsigned>(g, 256u)), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
@@ -1474,6 +1480,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     __shared__ int s_wc[kBlock / 64];
     if (P.go ? *(volatile const unsigned long long *)P.go != P.go_seq : !P.stats->resampled) return;
     const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m == 0 && P.runs_n) *P.runs_n = 0u;      // the runs were filled before this kernel
     __shared__ unsigned long long lds_u[kBlock / 64];
     const bool bb = P.obbox != nullptr && P.map.bbox != nullptr;
     if (bb) lds_box_set(s_bb, threadIdx.x, kBoxEmpty);      // kBBoxRows == kBlock
@@ -1651,17 +1658,19 @@ __device__ void estimate_body(const ResampleParams &P, int32_t nparts) {
         P.stats->resample_slots = sl;
         RankRecord r = *P.rec;
         r.best_w = bv;
-        r.best_gidx = (bi == INT64_MAX) ? INT64_MAX : P.ao + bi;
-        if (bi != INT64_MAX) {
+        // (before the gather the key is k_ranges': output << 32 | its source)
+        const int64_t bo = (P.est_early && bi != INT64_MAX) ? (bi >> 32) : bi;
+        r.best_gidx = (bo == INT64_MAX) ? INT64_MAX : P.ao + bo;
+        if (bo != INT64_MAX) {
             if (P.est_early) {          // before the gather: the output's source (k_ranges)
-                const int32_t s = P.out_src[bi];
+                const int32_t s = (int32_t)(bi & 0xffffffffll);
                 r.pose[0] = P.x[s];
                 r.pose[1] = P.y[s];
                 r.pose[2] = P.yaw[s];
             } else {
-                r.pose[0] = P.ox[bi];
-                r.pose[1] = P.oy[bi];
-                r.pose[2] = P.oyaw[bi];
+                r.pose[0] = P.ox[bo];
+                r.pose[1] = P.oy[bo];
+                r.pose[2] = P.oyaw[bo];
             }
         }
         *P.rec = r;
@@ -1679,6 +1688,10 @@ __global__ __launch_bounds__(1024) void k_tail_single(const ResampleParams R, co
                                                      DevStats *host_stats, unsigned long long *host_flag,
                                                      unsigned long long seq) {
     if (!R.stats->resampled) return;
+    if (blockIdx.x > 0) {                  // the other workgroups: k_ranges' listed runs
+        fill_runs_body(R, blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
     estimate_body(R, nparts);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1694,7 +1707,10 @@ hipError_t launch_tail_single(const ResampleParams &r, const ReduceParams &p, De
                               unsigned long long *host_flag, unsigned long long seq, hipStream_t s,
                               hipEvent_t e1) {
     const int32_t nparts = (int32_t)((r.n + kBlock - 1) / kBlock);
-    FS2_LAUNCH_EV(k_tail_single, dim3(1), dim3(1024), s, nullptr, e1, r, p, nparts, host_stats, host_flag, seq);
+    // one workgroup for the tail, kTailFill more for the runs k_ranges listed (none
+    // listed: they return at once -- cheaper than a kernel of their own every scan)
+    const unsigned fill = ((r.ranges_mode & 2) && r.runs) ? kTailFill : 0u;
+    FS2_LAUNCH_EV(k_tail_single, dim3(1 + fill), dim3(1024), s, nullptr, e1, r, p, nparts, host_stats, host_flag, seq);
     return hipGetLastError();
 }
 
