@@ -796,6 +796,62 @@ def test_maps_beyond_row_boxes(fs):
         f.close()
 
 
+@pytest.mark.parametrize("order,wild", [((3, 0, 2, 1), False), ((0, 3, 1, 2), False), ((2, 0, 1, 3), True)])
+def test_overflow_scan_only_where_candidates_remain(fs, order, wild):
+    """Round 6: the overflow path in every measurement order.  Two crowds of 30
+    (interleaved indices, tight to loose covariances) and a grid hit, with the far
+    miss (no candidate: it is appended, then re-observed on the slot it appended)
+    first, second or last; `wild`: an ill-conditioned slot (s = 0 mirror: a
+    candidate of every measurement, never rejected) placed past the listed slots.
+    Every scan equals the filter-off handle and the oracle (landmark_utils.py:92-117's
+    first match with the map left by the earlier measurements)."""
+    import fs2_synthetic as syn
+    from oracle import oracle as orc
+    N, L, seed = 2048, 120, 5
+    wl = syn.Workload(N, L, seed=seed)
+    x, y, yaw = wl.poses()
+    lm = wl.maps()
+    rng = np.random.default_rng(seed + 200)
+    base = wl.measurements(0)
+    ms4 = np.concatenate([base[:3], [[40.0, 2.0]]])
+    idx = rng.permutation(L)[:60]
+    for k, crowd in enumerate((idx[:30], idx[30:])):
+        ox, oy = ms4[k, 0] * np.cos(ms4[k, 1]), ms4[k, 0] * np.sin(ms4[k, 1])
+        lm[:, crowd, 0] = ox + rng.normal(0, 0.6, (N, 30))
+        lm[:, crowd, 1] = oy + rng.normal(0, 0.6, (N, 30))
+        v = np.exp(rng.uniform(np.log(0.005), np.log(0.5), (N, 30)))
+        lm[:, crowd, 2] = lm[:, crowd, 5] = v
+        lm[:, crowd, 3] = lm[:, crowd, 4] = 0.0
+    if wild:
+        j = L - 3                    # past every crowd's smallest slots
+        lm[:, j, 2], lm[:, j, 5] = 1e-5, 1e4
+        lm[:, j, 3] = lm[:, j, 4] = 0.0
+    ms = ms4[list(order)]
+    fl = [fs.FastSLAM2(N, reduce="parallel", record_assoc=True, gate_filter=g, verbose=False,
+                       landmark_capacity=L + 16) for g in (True, False)]
+    for f in fl:
+        f.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L, np.int32), lm)
+    o = orc.OracleFilter(N, L + 16)
+    o.set_state(x, y, yaw, np.full(N, 1.0 / N), np.full(N, L), lm)
+    for sc in range(4):
+        rot, tr = syn.odometry(sc)
+        nz = rng.normal(0, 0.001 if rot else 0.0055, N)
+        u0 = 0.3 / N
+        out = [f.step(rot, tr, ms, None, nz, u0) for f in fl]
+        opose, oassoc, ors, one = o.iterate(rot, tr, ms, nz, u0)
+        assert np.array_equal(fl[0].associations(), oassoc), sc
+        assert np.array_equal(fl[1].associations(), oassoc), sc
+        assert np.array_equal(out[0][0], out[1][0]), sc
+        assert np.allclose(out[0][0], opose, rtol=RTOL, atol=1e-12), sc
+    s0, s1 = fl[0].get_state(lm_cap=L + 16), fl[1].get_state(lm_cap=L + 16)
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(s0[4], o.cnt)
+    assert np.allclose(s0[5], o.lm, rtol=RTOL, atol=1e-12)
+    for f in fl:
+        f.close()
+
+
 @pytest.mark.parametrize("seed", [3, 11])
 def test_overflow_list_then_scan(fs, seed):
     """Round 5: an overflowing candidate list keeps its kMaxCand smallest slots, the
