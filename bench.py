@@ -876,11 +876,11 @@ def run_config(args, cfg, n_per_gpu, L, world, rank, dev, comm_id, barrier, step
 # Algorithmic byte model of the two update kernels (include/fs2.h
 # fs2_profile): bytes per unit the counters count
 BYTE_MODEL = {
-    "k_candidates": {"descriptor_streamed": 8, "page_opened": 128, "list_entry": 8,
+    "k_candidates": {"descriptor_streamed": 4, "page_opened": 128, "list_entry": 8,
                      "particle_pass (cnt read, count write)": 8, "row_box_read": 4},
     "k_update": {"fixed (scalars, free-list ids, counts; per particle, summed)": 1, "list_entry": 8,
-                 "candidate_record": 48, "slot_written (record 48, mirror 16, descriptor r+w 16)": 80,
-                 "page_copied (128 read + 128 write)": 256, "row_box_read_and_written": 8},
+                 "candidate_record": 48, "slot_written (record 48, mirror 16, descriptor read 4)": 68,
+                 "page_copied (128 read + 128 write, descriptor write 4)": 260, "row_box_read_and_written": 8},
 }
 
 
@@ -905,8 +905,8 @@ def kernel_summary(prof, cfg, n_per_gpu, L):
                                                   "fixed_bytes", "box_bytes")}
         model = {"units": BYTE_MODEL, "counts_per_launch": c,
                  "k_candidates_bytes": kern["k_candidates"][1], "k_update_bytes": kern["k_update"][1],
-                 "note": "k_candidates = 8 groups + 128 opened + 8 words + 8 n + 4/12 box_bytes; "
-                         "k_update = fixed_bytes + 8 words + 48 candidates + 80 written + 256 cow + 8/12 box_bytes; "
+                 "note": "k_candidates = 4 groups + 128 opened + 8 words + 8 n + 4/12 box_bytes; "
+                         "k_update = fixed_bytes + 8 words + 48 candidates + 68 written + 260 cow + 8/12 box_bytes; "
                          "reuse = model bytes / PMC HBM bytes (> 1: L2 / MALL hits, e.g. siblings' shared pages)"}
         for k in ("k_candidates", "k_update"):
             t = pmc_traffic(pmc, k)

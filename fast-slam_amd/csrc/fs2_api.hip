@@ -383,8 +383,8 @@ struct fs2_handle {
     int64_t bcnt_cap = 0, rbcnt_cap = 0;   // sweep block counts allocated (collect_blocks)
     Desc *pt[2] = {};                      // [rows][n] page descriptors (A/B across resamples)
     uint32_t *bbox[2] = {};                // [nblocks][kBBoxRows] workgroup row boxes of pt[0] / pt[1]
-    Desc *rdesc = nullptr;                 // received particles' rows [n_recv][rows]
-    Desc *udesc = nullptr;                 // received distinct pages [u_recv]
+    XDesc *rdesc = nullptr;                // received particles' rows [n_recv][rows] (with boxes)
+    XDesc *udesc = nullptr;                // received distinct pages [u_recv] (with boxes)
     size_t udesc_cap = 0;
     // page dedup of the outgoing transfers (XferTable)
     unsigned long long *xt_key = nullptr;
@@ -698,7 +698,7 @@ static int recv_bufs(fs2_handle *h, size_t bytes) {
     if (bytes <= h->rdesc_cap && bytes <= h->udesc_cap) return FS2_OK;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     for (int k = 0; k < 2; ++k) {
-        Desc *&p = k ? h->udesc : h->rdesc;
+        XDesc *&p = k ? h->udesc : h->rdesc;
         size_t &cap = k ? h->udesc_cap : h->rdesc_cap;
         if (bytes <= cap) continue;
         hipFree(p);
@@ -721,7 +721,7 @@ static int xfer_bufs(fs2_handle *h) {
     int lg = 10;
     while ((int64_t(1) << lg) < 2 * S && lg < 31) ++lg;
     const int rc = reserve_xfer_table(h, int64_t(1) << lg, S, false);
-    return rc ? rc : recv_bufs(h, sizeof(Desc) * (size_t)S);
+    return rc ? rc : recv_bufs(h, sizeof(XDesc) * (size_t)S);
 }
 
 // The two buffer sets on the device (BufSet, pipelined submit): at creation and
@@ -1406,7 +1406,7 @@ static int exchange_refs(fs2_handle *h, ResampleParams &rs, const std::vector<in
         pp = RecvPeer{};
         pp.pre = reinterpret_cast<const RefPreamble *>(rb);
         pp.hdr = reinterpret_cast<const PackHeader *>(rb + 64);
-        pp.refs = reinterpret_cast<const Desc *>(rb + 64 + 64 * K);
+        pp.refs = reinterpret_cast<const XDesc *>(rb + 64 + 64 * K);
         pp.K = (int32_t)K;
         pp.kbase = kbase;
         kbase += (int32_t)K;
@@ -2156,12 +2156,13 @@ static int fold_one(fs2_handle *h, int set) {
     const uint64_t n = (uint64_t)h->n, nblk = (uint64_t)h->nblocks();
     const uint64_t box_rows = h->row_boxes(h->cur) ? (uint64_t)h->rows : 0ull;
     const bool filt = h->cfg.gate_filter != 0;
-    const uint64_t cand_bytes = filt ? 8ull * st.groups + 128ull * st.opened + 8ull * st.words +
+    const uint64_t cand_bytes = filt ? sizeof(Desc) * st.groups + 128ull * st.opened + 8ull * st.words +
                                            8ull * n * p.passes + 4ull * box_rows * nblk
                                      : 0ull;
     const uint64_t upd_fixed = p.fixed_bytes + (filt ? 4ull * n * p.passes : 0ull) + 8ull * n * (uint64_t)p.m;
     const uint64_t exact_bytes = upd_fixed + (filt ? 8ull * st.words : 0ull) + 48ull * st.candidates +
-                                 80ull * st.written + 2ull * kPageBytes * st.cow_pages + 8ull * box_rows * nblk;
+                                 (64ull + sizeof(Desc)) * st.written + (2ull * kPageBytes + sizeof(Desc)) * st.cow_pages +
+                                 8ull * box_rows * nblk;
     if (filt && p.m <= kMaxM) {
         // k_candidates and, one pass, k_update alone
         HIP_TRY(h, hipEventElapsedTime(&f, E[0], E[1]));
@@ -2454,8 +2455,8 @@ static int enqueue_tail(fs2_handle *h, const fs2_handle::TailCtx &t) {
             // received rows and pages: sized for every local output's whole row at
             // creation and with every row growth (recv_bufs), so these never fire
             // unless n_recv * rows overflowed that (counted in scan_allocs)
-            const size_t rbytes = sizeof(Desc) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
-            const size_t ubytes = sizeof(Desc) * (size_t)std::max<int64_t>(h->u_recv, 1);
+            const size_t rbytes = sizeof(XDesc) * (size_t)std::max<int64_t>((int64_t)h->n_recv * h->rows, 1);
+            const size_t ubytes = sizeof(XDesc) * (size_t)std::max<int64_t>(h->u_recv, 1);
             if (rbytes > h->rdesc_cap || ubytes > h->udesc_cap) {
                 scan_alloc(h, "scan_alloc recv rows (MiB)", std::max(rbytes, ubytes));
                 rc = recv_bufs(h, std::max(rbytes, ubytes));
@@ -2992,7 +2993,6 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
             if (e == hipSuccess)
                 e = launch_import(stage, cstage, first + o, k, lm_cap, h->map(), pa, rows_each, h->cnt[c], h->ext_dev,
                                   perm_len > 0 ? perm_dev : nullptr, perm_len, s);
-            if (e == hipSuccess) e = launch_describe(h->map(), h->cnt[c], first + o, k, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc2 = set_err(&h->err, FS2_ERR_HIP, "state import failed: %s", hipGetErrorString(e));
         }
@@ -3018,11 +3018,8 @@ int fs2_set_state(fs2_handle *h, int64_t first, int64_t count, const double *x, 
         float cell = (float)std::max(1.0, std::ceil(1.25 * (double)h->ext_seen / 127.0 * 64.0)) / 64.0f;
         if (!(cell < 65536.0f)) cell = 65536.0f;
 #endif
-        if (cell != h->frame.cell) {
-            h->frame = SumFrame{-127.0f * cell, cell, 1.0f / cell};
-            HIP_TRY(h, launch_describe(h->map(), h->cnt[c], 0, h->n, s));
-        }
-        // the workgroup row boxes, rebuilt from the descriptors
+        if (cell != h->frame.cell) h->frame = SumFrame{-127.0f * cell, cell, 1.0f / cell};
+        // the workgroup row boxes, rebuilt from the pages on this grid
         HIP_TRY(h, launch_bbox_build(h->map(), h->cnt[c], s));
     }
     HIP_TRY(h, hipStreamSynchronize(s));

@@ -588,7 +588,7 @@ __global__ __launch_bounds__(kBlock) void k_cl_gather_maps(MapRef map, const int
     const int c = cnt[i];
     const int j0 = row * kPageSlots;
     if (j0 >= c) return;
-    const uint32_t e = pt_entry(map, row, i)->x;
+    const uint32_t e = *pt_entry(map, row, i);
     const char *pg = page_ptr_any(map, e), *recs = recs_of(map, e);    // (a remote page: its rank's pools)
     double2 *o = out + off[i];
     for (int j = j0; j < min(c, j0 + kPageSlots); ++j) {      // position j holds slot mirror_slot

@@ -23,23 +23,28 @@ constexpr int kMaxCand = 8;          // candidate slots listed per particle and 
 // record (x, y, P00, P01, P10, P11; 48 B) in the record pool.  Records are
 // immutable and shared like pages: a slot write stores a new record and points
 // the (private) page's mirror at it, so copy-on-write moves 128 B, not the slots.
-// Pages live in one pool (page id p at pool + 128 p).  A map is a row of 8-byte
-// page descriptors in the page table pt[row][particle] (Desc = uint2):
-//   .x  page id; bit 31 says the map owns the page (no other entry refers to
-//       it) and may write it in place, otherwise the first write copies the page
-//       (copy-on-write).  Resampling shares pages instead of copying maps.
-//   .y  the page's bounding box on the handle's summary grid, rounded outward:
-//       four 8-bit cell codes (x lo, x hi, y lo, y hi; SumFrame).
-// With the handle-wide lower bound slb on every nonzero mirror s, the summary
-// lets the candidate stream reject a whole page with one test that is never
-// less conservative than the slot tests it replaces (page_reject); a page with
-// an s = 0 slot gets an unbounded box (never rejected).
+// Pages live in one pool (page id p at pool + 128 p).  A map is a row of 4-byte
+// page descriptors in the page table pt[row][particle] (Desc = uint32): the page
+// id; bit 31 says the map owns the page (no other entry refers to it) and may
+// write it in place, otherwise the first write copies the page (copy-on-write).
+// Resampling shares pages instead of copying maps, and copies 4 bytes per row.
+// Boxes (bounding boxes on the handle's summary grid, rounded outward: four 8-bit
+// cell codes x lo, x hi, y lo, y hi; SumFrame) live per workgroup row (bbox
+// below), not per page (round 6: a per-page box in an 8-byte descriptor rejected
+// ~1 % of the rows the row boxes stream, for twice the resample's row copy).
+// With the handle-wide lower bound slb on every nonzero mirror s, a box lets the
+// candidate stream reject a whole row with one test that is never less
+// conservative than the slot tests it replaces (page_reject); an s = 0 slot
+// makes its row's box unbounded (never rejected).
 constexpr int kPageBytes = 128;
 constexpr int kRecBytes = 48;   // 64-byte records measured slower (profiles/r03_ab_rec64.txt)
 constexpr uint32_t kOwned = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7fffffffu;
 constexpr uint32_t kRecIdLimit = 0xffffffffu;   // record ids are uint32 (mirror .w, free lists)
-typedef uint2 Desc;
+typedef uint32_t Desc;
+// A descriptor with a box, as the sharded transfers carry it (.x entry, .y box:
+// the page's own box, or its source workgroup's row box)
+typedef uint2 XDesc;
 
 // Summary grid: box bound codes c in [0, 255]; lo(c) = org + (c - 1) cell (c = 0:
 // unbounded), hi(c) = org + c cell (c = 255: unbounded).  cell is a power of two
@@ -50,12 +55,14 @@ struct SumFrame {
 };
 constexpr uint32_t kSumOpen = 0xff00ff00u;   // unbounded box: never rejected
 
-// Workgroup row boxes: bbox[b * kBBoxRows + r] is a box (same codes) holding the
-// box of row r of every particle of workgroup b (particles [256 b, 256 b + 256)).
-// k_candidates tests it against the measurement bands once per workgroup and
-// streams only the rows it cannot reject, so most descriptors are never read.
-// Boxes only grow between rebuilds (k_update merges what it writes; resampling
-// and imports recompute them); maps of more than kBBoxRows rows run without.
+// Workgroup row boxes: bbox[b * kBBoxRows + r] is a box (same codes) holding
+// every live slot mirror of row r's pages of every particle of workgroup b
+// (particles [256 b, 256 b + 256)).  k_candidates tests it against the
+// measurement bands once per workgroup and streams only the rows it cannot
+// reject, so most descriptors are never read.  Boxes only grow between rebuilds
+// (k_update merges each mirror it writes; a resample unions its sources'
+// workgroups' boxes; imports rebuild them from the pages); maps of more than
+// kBBoxRows rows run without (every page of every row is opened).
 constexpr int kBBoxRows = 256;
 constexpr uint32_t kBoxEmpty = 0x00ff00ffu;  // x lo = y lo = 255, x hi = y hi = 0: holds nothing
 
@@ -284,7 +291,7 @@ struct RecvPeer {
     const uint32_t *idx;     // row entries
     const XferPage *pages;   // U distinct pages
     const double2 *covs;     // their covariances that differ from the initial one (2 per)
-    const Desc *refs;        // page_refs mode: the rows' descriptors (tagged)
+    const XDesc *refs;       // page_refs mode: the rows' descriptors (tagged), with boxes
     const RefPreamble *pre;  // page_refs mode: the sender's preamble
     int32_t K;               // particles from this peer
     int32_t kbase;           // index of its first particle among all received
@@ -515,8 +522,8 @@ struct ResampleParams {
     MapRef map;              // current page table
     Desc *opt;               // next page table [rows][n]
     uint32_t *obbox;         // its workgroup row boxes (null: none)
-    Desc *rdesc;             // [nrecv][rows] descriptors of received particles' rows
-    Desc *udesc;             // [sum U] descriptors of the received distinct pages
+    XDesc *rdesc;            // [nrecv][rows] descriptors (with boxes) of received particles' rows
+    XDesc *udesc;            // [sum U] descriptors (with boxes) of the received distinct pages
     PageAlloc alloc;         // received page u -> page freel[base + u], its slot j ->
                              // record rfreel[rbase + 8 u + j]
     int32_t *rank_d;         // [n] non-empty ranges before i in its 1024-block
@@ -733,10 +740,7 @@ hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t 
                          int64_t count, int32_t lm_cap, MapRef map, PageAlloc alloc,
                          int32_t rows_each, int32_t *cnt, uint32_t *ext, const int32_t *perm,
                          int32_t perm_len, hipStream_t s);
-// page summaries of rows [0, ceil(cnt/8)) of particles first .. first+count-1
-hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count,
-                           hipStream_t s);
-// workgroup row boxes of every particle's map, from the descriptors (no-op without bbox)
+// workgroup row boxes of every particle's map, from its pages' mirrors (no-op without bbox)
 hipError_t launch_bbox_build(MapRef map, const int32_t *cnt, hipStream_t s);
 hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm_cap,
                          MapRef map, const int32_t *cnt, hipStream_t s);

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kBlock) void k_mark(const MapRef map, const int32_t
     for (int r0 = 0; r0 < rows; r0 += 8) {
         uint32_t e[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) e[u] = pt_entry(map, min(r0 + u, rows - 1), i)->x;
+        for (int u = 0; u < 8; ++u) e[u] = *pt_entry(map, min(r0 + u, rows - 1), i);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if (r0 + u >= rows) continue;

@@ -296,7 +296,7 @@ __device__ __forceinline__ Desc *pt_entry(const MapRef &m, int row, int64_t i) {
 
 // Page of slot j of particle i (read access).
 __device__ __forceinline__ char *page_of(const MapRef &m, int j, int64_t i) {
-    return page_ptr(m.pool, pt_entry(m, j / kPageSlots, i)->x);
+    return page_ptr(m.pool, *pt_entry(m, j / kPageSlots, i));
 }
 
 // Cold readers in page_refs mode (fs2_kernels.hpp PeerMaps): the page a
@@ -357,7 +357,7 @@ __device__ __forceinline__ uint32_t take_rec(const PageAlloc &a, int64_t n, int6
 __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t i,
                                                const PageAlloc &a, int &t, unsigned &cow) {
     Desc *pe = pt_entry(m, row, i);
-    const uint32_t e = pe->x;
+    const uint32_t e = *pe;
     if (e & kOwned) return page_ptr(m.pool, e);
     const uint32_t id = take_page(a, m.n, i, t);
     const v4i *src = reinterpret_cast<const v4i *>(page_ptr(m.pool, e));
@@ -367,7 +367,7 @@ __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t
     for (int u = 0; u < kPageBytes / 16; ++u) v[u] = src[u];
 #pragma unroll
     for (int u = 0; u < kPageBytes / 16; ++u) dst[u] = v[u];
-    pe->x = id | kOwned;       // same content: the summary stays valid
+    *pe = id | kOwned;         // same content: the row box stays valid
     ++cow;
     return reinterpret_cast<char *>(dst);
 }
@@ -376,7 +376,7 @@ __device__ __forceinline__ char *writable_page(const MapRef &m, int row, int64_t
 __device__ __forceinline__ char *fresh_page(const MapRef &m, int row, int64_t i, const PageAlloc &a,
                                             int &t) {
     const uint32_t id = take_page(a, m.n, i, t);
-    pt_entry(m, row, i)->x = id | kOwned;      // summary refreshed by the caller
+    *pt_entry(m, row, i) = id | kOwned;        // (the caller grows the row box)
     return page_ptr(m.pool, id);
 }
 
@@ -424,9 +424,9 @@ __device__ __forceinline__ float sum_hi_val(const SumFrame &f, uint32_t c) {
     return c == 255u ? INFINITY : __double2float_ru(sum_grid(f, (double)c));
 }
 
-// Summary of the first nvalid mirrors of a page: their box on the grid, or the
-// unbounded box when a mirror is not finite or has s = 0 (never reject).
-__device__ __forceinline__ Desc describe_page(uint32_t entry, const float4 *mir, int nvalid, const SumFrame &f) {
+// Box of the first nvalid mirrors of a page on the grid, or the unbounded box
+// when a mirror is not finite or has s = 0 (never reject).
+__device__ __forceinline__ uint32_t page_box(const float4 *mir, int nvalid, const SumFrame &f) {
     float xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY, smin = INFINITY;
     bool finite = nvalid > 0;
     for (int u = 0; u < nvalid; ++u) {
@@ -438,22 +438,16 @@ __device__ __forceinline__ Desc describe_page(uint32_t entry, const float4 *mir,
         ymax = fmaxf(ymax, m.y);
         smin = fminf(smin, mirror_s(m));
     }
-    if (!finite || !(smin > 0.0f)) return make_uint2(entry, kSumOpen);
-    return make_uint2(entry, sum_lo(f, xmin) | (sum_hi(f, xmax) << 8) | (sum_lo(f, ymin) << 16) |
-                                 (sum_hi(f, ymax) << 24));
+    if (!finite || !(smin > 0.0f)) return kSumOpen;
+    return sum_lo(f, xmin) | (sum_hi(f, xmax) << 8) | (sum_lo(f, ymin) << 16) | (sum_hi(f, ymax) << 24);
 }
 
-// Summary after a slot (mirror mv) was written: the box grows to include mv (it
-// may also cover values since replaced: still conservative).
-__device__ __forceinline__ Desc merge_summary(Desc d, const float4 &mv, const SumFrame &f) {
-    if (!(isfinite(mv.x) && isfinite(mv.y)) || !(mirror_s(mv) > 0.0f)) {
-        d.y = kSumOpen;
-        return d;
-    }
-    const uint32_t xl = min(d.y & 0xffu, sum_lo(f, mv.x)), xh = max((d.y >> 8) & 0xffu, sum_hi(f, mv.x));
-    const uint32_t yl = min((d.y >> 16) & 0xffu, sum_lo(f, mv.y)), yh = max(d.y >> 24, sum_hi(f, mv.y));
-    d.y = xl | (xh << 8) | (yl << 16) | (yh << 24);
-    return d;
+// Box of one written mirror mv (a box a row's box grows by: it may also cover
+// values since replaced, still conservative); unbounded when mv is not finite or
+// has s = 0.
+__device__ __forceinline__ uint32_t point_box(const float4 &mv, const SumFrame &f) {
+    if (!(isfinite(mv.x) && isfinite(mv.y)) || !(mirror_s(mv) > 0.0f)) return kSumOpen;
+    return sum_lo(f, mv.x) | (sum_hi(f, mv.x) << 8) | (sum_lo(f, mv.y) << 16) | (sum_hi(f, mv.y) << 24);
 }
 
 // ---- workgroup row boxes (fs2_kernels.hpp, MapRef::bbox) ----
@@ -598,22 +592,6 @@ __device__ inline Band gate_band(float fx, float fy, float fe, float slb, float 
     return b;
 }
 
-// the page's summary after slot j (mirror mv) was written; returns the new descriptor
-__device__ __forceinline__ Desc note_write(const MapRef &m, int j, int64_t i, const float4 &mv, bool fresh) {
-    Desc *pe = pt_entry(m, j / kPageSlots, i);
-    const Desc d = *pe;
-    const Desc nd = fresh ? describe_page(d.x, &mv, 1, m.frame) : merge_summary(d, mv, m.frame);
-    *pe = nd;
-    return nd;
-}
-
-// Recompute the summary of page `row` of particle i from its mirrors (map size c).
-__device__ __forceinline__ void refresh_summary(const MapRef &m, int row, int64_t i, int c) {
-    Desc *pe = pt_entry(m, row, i);
-    const uint32_t e = pe->x;
-    const float4 *mir = reinterpret_cast<const float4 *>(page_ptr_any(m, e));   // (page_refs: maybe remote)
-    *pe = describe_page(e, mir, min(kPageSlots, c - row * kPageSlots), m.frame);
-}
 
 // slb lowered to the smallest positive s the wave's lanes pass (+inf: none); at
 // most one atomic per wave, and only when it lowers the bound.  Call with the

@@ -1027,7 +1027,7 @@ __device__ __forceinline__ DedupRow dedup_row(const ResampleParams &P, int p, in
     if (k * kPageSlots >= c) return r;
     const int64_t lo = P.mlo[i], hi = P.mhi[i];
     if (lo > hi) return r;
-    const uint32_t page = pt_entry(P.map, k, i)->x & kIdMask;
+    const uint32_t page = *pt_entry(P.map, k, i) & kIdMask;
     const unsigned long long fill = (unsigned long long)min(kPageSlots, c - k * kPageSlots);
     r.key = (fill << 40) | ((unsigned long long)(p + 1) << 32) | page;
     r.single = max(lo, pl.pa) == min(hi, pl.pb - 1);
@@ -1303,14 +1303,17 @@ __global__ __launch_bounds__(kBlock) void k_pack_refs(const ResampleParams P) {
     if (i >= P.xt.i_hi || i >= P.n) return;
     const int c = P.cnt[i];
     if (k * kPageSlots >= c || P.mlo[i] > P.mhi[i]) return;
-    Desc d = *pt_entry(P.map, k, i);
-    const uint32_t t = ref_tag(d.x);
-    d.x = ((t ? t : (uint32_t)P.rank + 1u) << kRefShift) | ref_id(d.x);
+    const Desc e = *pt_entry(P.map, k, i);
+    const uint32_t t = ref_tag(e);
+    XDesc d;
+    d.x = ((t ? t : (uint32_t)P.rank + 1u) << kRefShift) | ref_id(e);
+    // (pages carry no box: the source's workgroup row box holds this one)
+    d.y = P.map.bbox ? P.map.bbox[(i / kBlock) * kBBoxRows + k] : kSumOpen;
     const int64_t c_i = P.iblk[P.nblk + i / kScanBlock] + P.rank_e[i];
     for (int p = 0; p < P.world; ++p) {
         const PackPlan &pl = P.plan[p];
         if (p == P.keep || i < pl.i0 || i >= pl.i1) continue;
-        reinterpret_cast<Desc *>(P.sbuf[p] + 64 + 64 * pl.K)[c_i - pl.c0 + k] = d;
+        reinterpret_cast<XDesc *>(P.sbuf[p] + 64 + 64 * pl.K)[c_i - pl.c0 + k] = d;
     }
 }
 
@@ -1355,7 +1358,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_refs(const ResampleParams P, 
     const RefPreamble pre = *pp.pre;
     const int rows = (h.cnt + kPageSlots - 1) / kPageSlots;
     for (int k = lane; k < rows; k += 64) {
-        Desc d = pp.refs[h.soff + k];
+        XDesc d = pp.refs[h.soff + k];
         if (ref_tag(d.x) == (uint32_t)P.rank + 1u) d.x = ref_id(d.x);
         d.y = recode_box(d.y, pre, P.map.frame);
         P.rdesc[(int64_t)r * P.map.rows + k] = d;
@@ -1381,8 +1384,8 @@ __global__ __launch_bounds__(kBlock) void k_scatter_recv(const ResampleParams P,
 // page freel[base + u], its slot j record rfreel[rbase + 8 u + j].  8 lanes per
 // page (lane j: slot j) rebuild the records (the initial covariance where the
 // page's mask says so) and the gate mirrors (mirror_of, the sender's own
-// function of the record); the page's descriptor from 8-lane reductions (the
-// same box as describe_page).
+// function of the record); the page's descriptor with its box from 8-lane
+// reductions (the same box as page_box), for the output row boxes.
 __global__ __launch_bounds__(kBlock) void k_unpack_pages(const ResampleParams P, int64_t nu) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t g = min(t / kPageSlots, max(nu - 1, (int64_t)0));
@@ -1429,7 +1432,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_pages(const ResampleParams P,
         finite = finite && (__shfl_xor((int)finite, o, 64) != 0);
     }
     if (live && j == 0) {
-        Desc d;
+        XDesc d;
         d.x = id;
         if (!(finite && fill > 0) || !(bs > 0.0f))
             d.y = kSumOpen;
@@ -1455,7 +1458,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_rows(const ResampleParams P, 
     const int rows = (h.cnt + kPageSlots - 1) / kPageSlots;
     for (int k = lane; k < rows; k += 64) {
         const uint32_t ent = pp.idx[h.soff + k];
-        Desc d = P.udesc[pp.ubase + (ent & ~kEntryOwned)];
+        XDesc d = P.udesc[pp.ubase + (ent & ~kEntryOwned)];
         d.x = (d.x & kIdMask) | ((ent & kEntryOwned) ? kOwned : 0u);
         P.rdesc[(int64_t)r * P.map.rows + k] = d;
     }
@@ -1491,8 +1494,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     int32_t s = 0;
     int rows = 0;                    // rows of this output's map
     uint32_t keep = 0xffffffffu;
-    const Desc *src = P.map.pt;      // the source's row 0; row k at src + k * stride
-    int64_t stride = 0;
+    const Desc *src = P.map.pt;      // a local source's row 0; row k at src + k * n
+    const XDesc *rsrc = nullptr;     // a received particle's rows (descriptors with boxes)
     if (m < n) {
         s = P.out_src[m];
         double w;
@@ -1508,7 +1511,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             // also sent to another rank is referenced there)
             keep = (P.refs ? P.mlo[s] == P.mhi[s] : hi == lo) ? 0xffffffffu : kIdMask;
             src = pt_entry(P.map, 0, s);
-            stride = n;
         } else {
             const int r = -s - 1;
             const int p = peer_of(P, r);
@@ -1518,8 +1520,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             P.oyaw[m] = h.yaw;
             w = h.w;
             c = h.cnt;
-            src = P.rdesc + (int64_t)r * P.map.rows;
-            stride = 1;
+            rsrc = P.rdesc + (int64_t)r * P.map.rows;
         }
         rows = (c + kPageSlots - 1) / kPageSlots;
         P.ocnt[m] = c;
@@ -1539,28 +1540,37 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     unsigned nremote = 0;            // page_refs: row entries naming another rank's page
     unsigned npages = 0;             //            of them, first sightings of a page (distinct)
     for (int k0 = 0; k0 < wrows; k0 += 8) {
-        Desc e[8];
+        uint32_t e[8], eb[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) e[u] = src[(int64_t)max(min(k0 + u, rows - 1), 0) * stride];
+        for (int u = 0; u < 8; ++u) {
+            const int64_t kk = max(min(k0 + u, rows - 1), 0);
+            if (rsrc) {
+                const XDesc x = rsrc[kk];
+                e[u] = x.x;
+                eb[u] = x.y;
+            } else {
+                e[u] = src[kk * n];
+                eb[u] = kBoxEmpty;
+            }
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if (k0 + u < rows) {
-                e[u].x &= keep;
-                if (P.refs && ref_tag(e[u].x)) {
+                e[u] &= keep;
+                if (P.refs && ref_tag(e[u])) {
                     ++nremote;
                     bool claimed = false;
-                    if (P.tkey && ptable_insert(P.tkey, P.tcap, P.tepoch, e[u].x, &claimed) >= 0 && claimed)
+                    if (P.tkey && ptable_insert(P.tkey, P.tcap, P.tepoch, e[u], &claimed) >= 0 && claimed)
                         ++npages;
                 }
-                __builtin_nontemporal_store(((unsigned long long)e[u].y << 32) | e[u].x,
-                                            reinterpret_cast<unsigned long long *>(P.opt + (int64_t)(k0 + u) * n + m));
+                __builtin_nontemporal_store(e[u], P.opt + (int64_t)(k0 + u) * n + m);
             }
         }
         if (recv) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 if (k0 + u < wrows) {
-                    const uint32_t b = wave_box_union((k0 + u < rows && s < 0) ? e[u].y : kBoxEmpty);
+                    const uint32_t b = wave_box_union((k0 + u < rows && s < 0) ? eb[u] : kBoxEmpty);
                     if ((threadIdx.x & 63) == 0) lds_box_merge(s_bb, k0 + u, b);
                 }
             }
@@ -1607,26 +1617,26 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     }
 }
 
-// Workgroup row boxes of every map from its descriptors (after imports, or when
-// the summary grid changes): the same row unions as k_gather_particles.
+// Workgroup row boxes of every map from its pages' mirrors (after imports, or
+// when the summary grid changes): per row, the wave union of its lanes' page
+// boxes, merged across the waves in LDS.
 __global__ __launch_bounds__(kBlock) void k_bbox_build(const MapRef map, const int32_t *cnt, int64_t n) {
     __shared__ BoxLds s_bb;
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     lds_box_set(s_bb, threadIdx.x, kBoxEmpty);
-    const int rows = (i < n) ? (cnt[i] + kPageSlots - 1) / kPageSlots : 0;
+    const int c = (i < n) ? cnt[i] : 0;
+    const int rows = (c + kPageSlots - 1) / kPageSlots;
     __syncthreads();
     const int wrows = wave_max_i(rows);
-    for (int k0 = 0; k0 < wrows; k0 += 8) {
-        uint32_t e[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) e[u] = pt_entry(map, max(min(k0 + u, rows - 1), 0), i < n ? i : 0)->y;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (k0 + u < wrows) {
-                const uint32_t b = wave_box_union(k0 + u < rows ? e[u] : kBoxEmpty);
-                if ((threadIdx.x & 63) == 0) lds_box_merge(s_bb, k0 + u, b);
-            }
+    for (int r = 0; r < wrows; ++r) {
+        uint32_t b = kBoxEmpty;
+        if (r < rows) {
+            // (page_refs: the page may live on another rank)
+            const float4 *mir = reinterpret_cast<const float4 *>(page_ptr_any(map, *pt_entry(map, r, i)));
+            b = page_box(mir, min(kPageSlots, c - r * kPageSlots), map.frame);
         }
+        b = wave_box_union(b);
+        if ((threadIdx.x & 63) == 0) lds_box_merge(s_bb, r, b);
     }
     __syncthreads();
     if ((int)threadIdx.x < map.rows) map.bbox[(int64_t)blockIdx.x * kBBoxRows + threadIdx.x] = lds_box_get(s_bb, threadIdx.x);

@@ -113,6 +113,7 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     __shared__ uint64_t s_list[kMaxCand][kBlock];
     __shared__ Band s_band[MAXM];
     __shared__ uint16_t s_rows[kBBoxRows];      // rows the row boxes leave open, ascending
+    __shared__ uint8_t s_rmask[kBBoxRows];      // their measurements (the row box's open mask)
     __shared__ int s_wc[kBlock / 64];
     const int tid = threadIdx.x;
     const int64_t n = P.n;
@@ -171,20 +172,12 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     int nc = 0;
     unsigned visited = 0, groups = 0, opened = 0;
 
-    // Page g: its descriptor's box codes are tested against every measurement's
-    // band first (integer compares; the next descriptors already in flight);
-    // only pages outside no band have their
-    // 8 mirrors loaded, and the wave loads them together (lanes without an open
-    // page read page 0, which stays in cache, and discard it).
-    // measurements whose gate page g (descriptor d) cannot rule out
-    auto open_mask = [&](const Desc &d, int g) -> unsigned {
-        unsigned om = 0u;
-        if (g * kPageSlots < c) {
-            const uint32_t s = d.y;
-            om = box_open_mask<MAXM>(s, bc, P.m);
-        }
-        return om;
-    };
+    // Every streamed row's page is opened for the measurements its workgroup row
+    // box leaves open (the row test below; without row boxes, all of them): its 8
+    // mirrors are loaded by the wave together (lanes past their map read page 0,
+    // which stays in cache, and discard it).  (Round 6: per-page boxes in 8-byte
+    // descriptors rejected ~1 % of these pages; they are gone.)
+    const unsigned all_m = (1u << P.m) - 1u;
     // slots of open page g (mirrors mir) tested against the measurements of om only
     auto test_page = [&](const float4 *mir, int g, unsigned om) {
         const int j0 = g * kPageSlots;
@@ -235,8 +228,9 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
     const bool use_bb = map.bbox != nullptr;
     int nrows = map.rows;
     if (use_bb) {
-        bool pass = false;
-        if (tid < map.rows) pass = box_open_mask<MAXM>(map.bbox[blk * kBBoxRows + tid], bc, P.m) != 0u;
+        unsigned rm = 0u;
+        if (tid < map.rows) rm = box_open_mask<MAXM>(map.bbox[blk * kBBoxRows + tid], bc, P.m);
+        const bool pass = rm != 0u;
         const uint64_t bm = __ballot(pass);
         const int wid = tid >> 6, lane = tid & 63;
         if (lane == 0) s_wc[wid] = __popcll(bm);
@@ -248,7 +242,11 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
             off += (w < wid) ? s_wc[w] : 0;
             nrows += s_wc[w];
         }
-        if (pass) s_rows[off + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)tid;
+        if (pass) {
+            const int at = off + __popcll(bm & ((1ull << lane) - 1ull));
+            s_rows[at] = (uint16_t)tid;
+            s_rmask[at] = (uint8_t)rm;
+        }
         __syncthreads();
     }
     // row of list entry q (past the end: row 0, a valid address whose load is discarded)
@@ -264,9 +262,9 @@ __global__ __launch_bounds__(kBlock) void k_candidates(const UpdateParams P) {
         for (int u = 0; u + 1 < kDescAhead; ++u) dq[u] = dq[u + 1];
         dq[kDescAhead - 1] = ptrow[(int64_t)row_at(q + kDescAhead) * n];
         if (g * kPageSlots < c) ++groups;
-        const unsigned om = open_mask(d, g);
+        const unsigned om = (g * kPageSlots < c) ? (use_bb ? (unsigned)s_rmask[q] : all_m) : 0u;
         if (!__any(om)) continue;
-        const char *pg = page_ptr(map.pool, om ? d.x : 0u);
+        const char *pg = page_ptr(map.pool, om ? d : 0u);
         float4 mir[kScanGroup];
 #pragma unroll
         for (int u = 0; u < kScanGroup; ++u) mir[u] = load_mirror(pg, u);
@@ -522,14 +520,17 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         auto scan = [&](unsigned want, bool skip_mods) {
             for (int g = 0; g < rows; ++g) {
                 const Desc d = *pt_entry(map, g, il);
+                // (the row's workgroup box holds this page's mirrors; without row boxes
+                // every page is opened)
+                const uint32_t rb = map.bbox ? lds_box_get(s_bb, g) : kSumOpen;
                 unsigned open = 0u;
 #pragma unroll
                 for (int k = 0; k < MAXM; ++k)
                     if (((want >> k) & 1u) &&
-                        !page_reject(d.y, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
+                        !page_reject(rb, map.frame, slb, P.meas.fx[k], P.meas.fy[k], P.meas.fe[k], P.gate2f))
                         open |= 1u << k;
                 if (!open) continue;
-                const char *pg = page_ptr(map.pool, d.x);
+                const char *pg = page_ptr(map.pool, d);
                 for (int u = 0; u < kPageSlots && g * kPageSlots + u < c; ++u) {
                     const int pos = g * kPageSlots + u;
                     if (skip_mods) {
@@ -652,6 +653,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     int rrow[NR];
     Desc rdesc[NR];
     int canon[NR];                   // first entry with the same row
+    unsigned cowm = 0u;              // entries whose page B1 copied (their descriptor changes)
 #pragma unroll
     for (int t = 0; t < NR; ++t) {
         rrow[t] = (t < nmod) ? (int)((mods >> (16 * t)) & 0xffffu) / kPageSlots
@@ -678,21 +680,22 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 #pragma unroll
             for (int u = 0; u < t; ++u)
                 if (canon[t] == t && u < nrows && rrow[u] == rrow[t]) canon[t] = u;
-            if (t < nrows && canon[t] == t && !(rdesc[t].x & kOwned)) {
+            if (t < nrows && canon[t] == t && !(rdesc[t] & kOwned)) {
                 task = true;
-                src = rdesc[t].x & kIdMask;
+                src = rdesc[t] & kIdMask;
                 dst = sel_u32(nalloc, fpage);
                 ++nalloc;
-                rdesc[t].x = dst | kOwned;
+                rdesc[t] = dst | kOwned;
+                cowm |= 1u << t;
                 ++cow;
             }
             const uint64_t bm = __ballot(task);
             if (task) s_ws[wid].cow[T + __popcll(bm & ((1ull << lane) - 1ull))] = make_uint2(src, dst);
             T += __popcll(bm);
         }
-        // (the owned pages' descriptors reach memory with their summaries: B2 stores
-        // the modified rows, the appends the partly filled row; nothing reads them
-        // from memory before)
+        // (the owned pages' descriptors reach memory after: B2 stores the modified
+        // rows', the appends the partly filled row's; nothing reads them from memory
+        // before)
         // the task list is per wave: a wave-level barrier orders its LDS writes and reads
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -724,7 +727,8 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
 
     FS2_PHASE(3);
     // (B2) modified slots: their mirrors (computed in phase A) into the owned
-    // pages; then the row summaries are read once, merged and written back.
+    // pages, each growing its row's workgroup box; the descriptors of the rows
+    // whose page was copied.
     {
 #pragma unroll
         for (int t = 0; t < MAXM; ++t) {
@@ -733,24 +737,16 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
                 uint32_t id = 0;
 #pragma unroll
                 for (int u = 0; u < NR; ++u)
-                    if (u == canon[t]) id = rdesc[u].x;
-                reinterpret_cast<float4 *>(page_ptr(map.pool, id))[j & (kPageSlots - 1)] = s_mv[t][tid];
+                    if (u == canon[t]) id = rdesc[u];
+                const float4 m = s_mv[t][tid];
+                reinterpret_cast<float4 *>(page_ptr(map.pool, id))[j & (kPageSlots - 1)] = m;
+                box_note(rrow[t], point_box(m, map.frame));
             }
         }
         nrec = nmod;
-        // summaries: rows in first-occurrence order, each merged with all its slots
 #pragma unroll
-        for (int t = 0; t < MAXM; ++t) {
-            if (t < nmod && canon[t] == t) {
-                Desc d = rdesc[t];       // loaded before B1, .x now the owned page
-#pragma unroll
-                for (int u = t; u < MAXM; ++u)
-                    if (u < nmod && canon[u] == t) d = merge_summary(d, s_mv[u][tid], map.frame);
-                *pt_entry(map, rrow[t], il) = d;
-                box_note(rrow[t], d.y);
-                rdesc[t] = d;
-            }
-        }
+        for (int t = 0; t < MAXM; ++t)
+            if (t < nmod && canon[t] == t && ((cowm >> t) & 1u)) *pt_entry(map, rrow[t], il) = rdesc[t];
     }
 
     FS2_PHASE(4);
@@ -759,16 +755,20 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
     // stored when the appends leave the row. ----
     int nap = 0;
     int arow = -1;
-    Desc ad = make_uint2(0u, 0u);
+    Desc ad = 0u;
+    bool ad_new = false;             // ad differs from the row's stored descriptor
     if (pend != 0u && c % kPageSlots != 0) {
-        // the partly filled last row: owned by B1, summary merged if a modified slot shares it
+        // the partly filled last row: owned by B1 (its descriptor stored below if B1 copied it)
         arow = c / kPageSlots;
 #pragma unroll
         for (int u = 0; u < NR; ++u)
-            if (u == canon[nmod]) ad = rdesc[u];
+            if (u == canon[nmod]) {
+                ad = rdesc[u];
+                ad_new = (cowm >> u) & 1u;
+            }
     }
     auto page_at = [&](int j) -> char * {
-        return (j / kPageSlots == arow) ? page_ptr(map.pool, ad.x) : page_of(map, j, il);
+        return (j / kPageSlots == arow) ? page_ptr(map.pool, ad) : page_of(map, j, il);
     };
     while (pend) {
         const int k = __builtin_ctz(pend);
@@ -799,8 +799,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             s_lik[k][tid] = ekf_update(s, px, py, pyaw, mk, R, singular);
             const float4 mv = store_slot(map, pg, jh, s, r, jh);
             smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
-            if (jh / kPageSlots == arow) ad = merge_summary(ad, mv, map.frame);
-            else box_note(jh / kPageSlots, note_write(map, jh, il, mv, false).y);
+            box_note(jh / kPageSlots, point_box(mv, map.frame));
             s_idx[k][tid] = (int16_t)(c + hit);
         } else {
             // new landmark in the world frame (fast_slam_2.py:108-111)
@@ -810,20 +809,19 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
             const uint32_t r = sel_u32(nrec, frec);
             ++nrec;
             if (ja % kPageSlots == 0) {
-                if (arow >= 0) {                                  // leaving that row
-                    *pt_entry(map, arow, il) = ad;
-                    box_note(arow, ad.y);
-                }
+                if (arow >= 0 && ad_new) *pt_entry(map, arow, il) = ad;     // leaving that row
                 const uint32_t id = take_page(P.alloc, map.n, il, nalloc);
                 arow = ja / kPageSlots;
                 const float4 mv = store_slot(map, page_ptr(map.pool, id), ja, s, r, ja);
                 smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
-                ad = describe_page(id | kOwned, &mv, 1, map.frame);
+                box_note(arow, point_box(mv, map.frame));
+                ad = id | kOwned;
+                ad_new = true;
                 ++fresh;
             } else {
-                const float4 mv = store_slot(map, page_ptr(map.pool, ad.x), ja, s, r, ja);
+                const float4 mv = store_slot(map, page_ptr(map.pool, ad), ja, s, r, ja);
                 smin_w = fminf(smin_w, mirror_s(mv) > 0.0f ? mirror_s(mv) : INFINITY);
-                ad = merge_summary(ad, mv, map.frame);
+                box_note(arow, point_box(mv, map.frame));
             }
             s_idx[k][tid] = (int16_t)-1;
             ++nap;
@@ -831,10 +829,7 @@ __global__ __launch_bounds__(kBlock) void k_update(const UpdateParams P) {
         }
         ++written;
     }
-    if (arow >= 0) {
-        *pt_entry(map, arow, il) = ad;
-        box_note(arow, ad.y);
-    }
+    if (arow >= 0 && ad_new) *pt_entry(map, arow, il) = ad;
     c += nap;
 
     FS2_PHASE(5);
@@ -957,9 +952,9 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
     }
     const int arow = (c % kPageSlots) ? c / kPageSlots : -1;     // an append may write this row
     auto row_at = [&](int q) -> int { return use_bb ? (int)s_rows[q] : q; };
-    auto wanted = [&](int r, const Desc &d) -> bool {
-        return r * kPageSlots < c && ref_tag(d.x) != 0u && (box_open_mask<MAXM>(d.y, bc, P.m) != 0u || r == arow);
-    };
+    // (the rows streamed below are those the row boxes leave open -- every row
+    // without row boxes -- so a remote page in one is one the pass may open)
+    auto wanted = [&](int r, const Desc &d) -> bool { return r * kPageSlots < c && ref_tag(d) != 0u; };
     // every wanted entry of this lane: the open rows' remote pages, then the append
     // row when it is remote and not among them
     auto for_wanted = [&](auto &&fn) {
@@ -976,7 +971,7 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
         }
         if (arow >= 0 && !arow_seen) {
             const Desc d = *pt_entry(map, arow, i);
-            if (ref_tag(d.x) != 0u) fn(arow, d);
+            if (ref_tag(d) != 0u) fn(arow, d);
         }
     };
     const unsigned long long ep = (unsigned long long)P.epoch << 32;
@@ -986,13 +981,13 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
         // every wanted entry names its page's copy (claimed and filled by phase 0)
         unsigned long long rows = 0;
         for_wanted([&](int r, const Desc &d) {
-            const unsigned long long want = ep | d.x;
-            uint64_t s = slot0(d.x);
+            const unsigned long long want = ep | d;
+            uint64_t s = slot0(d);
             for (int64_t probe = 0; probe < P.cap; ++probe, s = (s + 1) & mask)
                 if (P.key[s] == want) {
                     const uint32_t id = P.val[s];
                     if (!(id & 0x80000000u)) {        // (0xffffffff: the copy failed, left remote)
-                        *pt_entry(map, r, i) = make_uint2(id, d.y);
+                        *pt_entry(map, r, i) = id;
                         ++rows;
                     }
                     break;
@@ -1027,7 +1022,7 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
     };
     int need = 0;
     for_wanted([&](int, const Desc &d) {
-        if (find(d.x, true) <= -2) ++need;
+        if (find(d, true) <= -2) ++need;
     });
     // this workgroup's pages: one atomic, then each lane's run
     const int wid = tid >> 6, lane = tid & 63;
@@ -1062,14 +1057,14 @@ __global__ __launch_bounds__(kBlock) void k_localize(const LocalizeParams P) {
     const bool failed = s_base == ~0ull;
     int64_t k = (int64_t)s_base + woff + incl - need;            // this lane's first localised page
     for_wanted([&](int r, const Desc &d) {
-        const int64_t slot = find(d.x, false);
+        const int64_t slot = find(d, false);
         if (slot < 0 || P.val[slot] != marker) return;          // another lane's copy
         if (failed) {                                            // (phase 1 leaves the entry remote)
             P.val[slot] = 0xffffffffu;
             return;
         }
-        const uint32_t tg = ref_tag(d.x);
-        const float4 *src = reinterpret_cast<const float4 *>(map.peers->pool[tg - 1] + (int64_t)ref_id(d.x) * kPageBytes);
+        const uint32_t tg = ref_tag(d);
+        const float4 *src = reinterpret_cast<const float4 *>(map.peers->pool[tg - 1] + (int64_t)ref_id(d) * kPageBytes);
         const char *srecs = map.peers->recs[tg - 1];
         const uint32_t id = P.freel[P.ftail - 1 - k];
         // every row naming a page holds the same slots of it (sharers of a page have
@@ -1446,7 +1441,7 @@ __global__ __launch_bounds__(kBlock) void k_import(const double *stage, const in
         // row-major over the chunk's particles: the pages (and records) a wave reads
         // for one row (slot) of 64 consecutive particles are adjacent in the pools
         const uint32_t id = alloc.freel[alloc.base + (int64_t)row * count + p];
-        if (j % kPageSlots == 0) pt_entry(map, row, first + p)->x = id | kOwned;
+        if (j % kPageSlots == 0) *pt_entry(map, row, first + p) = id | kOwned;
         const double *s = stage + (p * lm_cap + slot) * 6;
         const float4 mv = store_slot(map, page_ptr(map.pool, id), j, Slot{s[0], s[1], M2{s[2], s[3], s[4], s[5]}},
                                      alloc.rfreel[alloc.rbase + (int64_t)j * count + p], slot);
@@ -1469,24 +1464,12 @@ __global__ __launch_bounds__(kBlock) void k_export(double *stage, int64_t first,
         const int j = (int)(e % lm_cap);
         if (j >= cnt[first + p]) continue;
         // position j holds slot mirror_slot (a remote page: its rank's pools)
-        const uint32_t pe = pt_entry(map, j / kPageSlots, first + p)->x;
+        const uint32_t pe = *pt_entry(map, j / kPageSlots, first + p);
         const float4 mv = load_mirror(page_ptr_any(map, pe), j);
         const Slot s = load_rec(recs_of(map, pe), mirror_rec(mv));
         double *d = stage + (p * lm_cap + mirror_slot(mv)) * 6;
         d[0] = s.mx; d[1] = s.my;
         d[2] = s.P.a00; d[3] = s.P.a01; d[4] = s.P.a10; d[5] = s.P.a11;
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_describe(MapRef map, const int32_t *cnt, int64_t first,
-                                                     int64_t count) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t total = count * map.rows;
-    for (int64_t e = t; e < total; e += (int64_t)gridDim.x * kBlock) {
-        const int64_t p = first + e % count;      // consecutive lanes: consecutive particles
-        const int row = (int)(e / count);
-        const int c = cnt[p];
-        if (row * kPageSlots < c) refresh_summary(map, row, p, c);
     }
 }
 
@@ -1505,12 +1488,6 @@ hipError_t launch_import(const double *stage, const int32_t *cnt_stage, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_describe(MapRef map, const int32_t *cnt, int64_t first, int64_t count, hipStream_t s) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_describe, dim3(grid_for(count * map.rows)), dim3(kBlock), 0, s, map, cnt, first,
-                       count);
-    return hipGetLastError();
-}
 
 hipError_t launch_export(double *stage, int64_t first, int64_t count, int32_t lm_cap, MapRef map,
                          const int32_t *cnt, hipStream_t s) {

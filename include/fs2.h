@@ -178,12 +178,13 @@ typedef struct fs2_profile {
     /* The counters of the algorithmic byte model, summed over the
      * timed candidate / exact launches, so that filter_bytes and update_bytes can be
      * recomputed from them:
-     *   k_candidates: 8 B per streamed descriptor + 128 B per opened page + 8 B per
+     *   k_candidates: 4 B per streamed descriptor + 128 B per opened page + 8 B per
      *                 list entry + 8 B per particle and pass + 4 B per row box read;
      *   k_update:     model_fixed_bytes (particle scalars, free-list ids, counts)
-     *                 + 8 B per list entry + 48 B per candidate record + 80 B per
-     *                 written slot (record 48, mirror 16, descriptor read + write 16)
-     *                 + 256 B per copied page + 8 B per row box read and written. */
+     *                 + 8 B per list entry + 48 B per candidate record + 68 B per
+     *                 written slot (record 48, mirror 16, descriptor read 4)
+     *                 + 260 B per copied page (its descriptor written) + 8 B per row
+     *                 box read and written. */
     uint64_t model_groups;      /* descriptors streamed */
     uint64_t model_opened;      /* pages whose 128-byte mirror line was loaded */
     uint64_t model_words;       /* candidate list entries */
