@@ -1474,6 +1474,66 @@ __global__ __launch_bounds__(kBlock) void k_unpack_rows(const ResampleParams P, 
 // maps consecutive outputs to non-decreasing sources).  Outputs received from
 // another rank have no such box: a workgroup holding some adds the unions of
 // their page boxes, row by row (a wave union per row, LDS across the waves).
+//
+// The page-table rows of outputs with a local source are copied by the launch's
+// last workgroups (gather_rows), in tiles of kTileRows rows x 256 outputs taken in
+// row-major order: the workgroups in flight then read and write the same few
+// rows, where a lane copying its own output's every row (as the received ones
+// still are, below) has each wave touch all 63 rows, 4 MB apart -- address
+// translation, not bytes, held that copy at ~200 us for 252 MB at config 3.
+#ifndef FS2_GATHER_TILE_ROWS
+#define FS2_GATHER_TILE_ROWS 8
+#endif
+constexpr int kTileRows = FS2_GATHER_TILE_ROWS;
+__device__ void gather_rows(const ResampleParams &P, int64_t wg, int64_t nwg, unsigned long long *lds_u) {
+    const int64_t n = P.n;
+    const int64_t nblk = (n + kBlock - 1) / kBlock;
+    const int64_t tiles = (int64_t)((P.map.rows + kTileRows - 1) / kTileRows) * nblk;
+    unsigned nremote = 0;            // page_refs: row entries naming another rank's page
+    unsigned npages = 0;             //            of them, first sightings of a page (distinct)
+    for (int64_t t = wg; t < tiles; t += nwg) {
+        const int r0 = (int)(t / nblk) * kTileRows;
+        const int64_t m = (t % nblk) * kBlock + threadIdx.x;
+        const int32_t s = m < n ? P.out_src[m] : -1;
+        if (s < 0) continue;         // (received outputs: their own rows, below)
+        const int rows = (P.cnt[s] + kPageSlots - 1) / kPageSlots;
+        if (r0 >= rows) continue;
+        const int64_t lo = max((int64_t)P.mlo[s], P.ao), hi = min((int64_t)P.mhi[s], P.ao + n - 1);
+        // (page_refs: only a source with one output in all keeps its pages -- a row
+        // also sent to another rank is referenced there)
+        const uint32_t keep = (P.refs ? P.mlo[s] == P.mhi[s] : hi == lo) ? 0xffffffffu : kIdMask;
+        uint32_t e[kTileRows];
+#pragma unroll
+        for (int u = 0; u < kTileRows; ++u) e[u] = *pt_entry(P.map, min(r0 + u, rows - 1), s);
+#pragma unroll
+        for (int u = 0; u < kTileRows; ++u) {
+            if (r0 + u < rows) {
+                e[u] &= keep;
+                if (P.refs && ref_tag(e[u])) {
+                    ++nremote;
+                    bool claimed = false;
+                    if (P.tkey && ptable_insert(P.tkey, P.tcap, P.tepoch, e[u], &claimed) >= 0 && claimed)
+                        ++npages;
+                }
+                __builtin_nontemporal_store(e[u], P.opt + (int64_t)(r0 + u) * n + m);
+            }
+        }
+    }
+    if (P.refs) {
+        const unsigned long long br = block_sum_u64<kBlock>(nremote, lds_u);
+        if (threadIdx.x == 0 && br) atomicAdd(&P.stats->remote_rows, br);
+        __syncthreads();             // lds_u is reused below
+        const unsigned long long bp = block_sum_u64<kBlock>(npages, lds_u);
+        if (threadIdx.x == 0 && bp) atomicAdd(&P.stats->remote_pages, bp);
+    }
+}
+
+// workgroups of launch_resample_apply's gather that copy rows (see above)
+static int64_t gather_row_groups(int64_t n, int rows) {
+    const int64_t tiles = (int64_t)((rows + kTileRows - 1) / kTileRows) * ((n + kBlock - 1) / kBlock);
+    return std::min<int64_t>(tiles, 2048);
+}
+
 __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParams P) {
     __shared__ double lds_d[kBlock / 64];
     __shared__ int64_t lds_l[kBlock / 64];
@@ -1482,9 +1542,16 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     __shared__ int s_sb[kBlock];     // the distinct ones, in order
     __shared__ int s_wc[kBlock / 64];
     if (P.go ? *(volatile const unsigned long long *)P.go != P.go_seq : !P.stats->resampled) return;
+    __shared__ unsigned long long lds_u[kBlock / 64];
+    {
+        const int64_t nblk = (P.n + kBlock - 1) / kBlock;
+        if ((int64_t)blockIdx.x >= nblk) {
+            gather_rows(P, (int64_t)blockIdx.x - nblk, (int64_t)gridDim.x - nblk, lds_u);
+            return;
+        }
+    }
     const int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (m == 0 && P.runs_n) *P.runs_n = 0u;      // the runs were filled before this kernel
-    __shared__ unsigned long long lds_u[kBlock / 64];
     const bool bb = P.obbox != nullptr && P.map.bbox != nullptr;
     if (bb) lds_box_set(s_bb, threadIdx.x, kBoxEmpty);      // kBBoxRows == kBlock
     double bv = -INFINITY;
@@ -1493,8 +1560,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     const int64_t n = P.n;
     int32_t s = 0;
     int rows = 0;                    // rows of this output's map
-    uint32_t keep = 0xffffffffu;
-    const Desc *src = P.map.pt;      // a local source's row 0; row k at src + k * n
     const XDesc *rsrc = nullptr;     // a received particle's rows (descriptors with boxes)
     if (m < n) {
         s = P.out_src[m];
@@ -1506,11 +1571,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             P.oyaw[m] = P.yaw[s];
             w = P.w[s];
             c = P.cnt[s];
-            const int64_t lo = max((int64_t)P.mlo[s], P.ao), hi = min((int64_t)P.mhi[s], P.ao + n - 1);
-            // (page_refs: only a source with one output in all keeps its pages -- a row
-            // also sent to another rank is referenced there)
-            keep = (P.refs ? P.mlo[s] == P.mhi[s] : hi == lo) ? 0xffffffffu : kIdMask;
-            src = pt_entry(P.map, 0, s);
         } else {
             const int r = -s - 1;
             const int p = peer_of(P, r);
@@ -1521,8 +1581,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
             w = h.w;
             c = h.cnt;
             rsrc = P.rdesc + (int64_t)r * P.map.rows;
+            rows = (c + kPageSlots - 1) / kPageSlots;     // (local outputs' rows: gather_rows)
         }
-        rows = (c + kPageSlots - 1) / kPageSlots;
         P.ocnt[m] = c;
         P.ow[m] = w;
         bv = w;
@@ -1533,9 +1593,10 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
     const bool recv = bb && __syncthreads_or(m < n && s < 0);
     if (bb) s_src[threadIdx.x] = (m < n && s >= 0) ? s / kBlock : -1;
     if (bb) __syncthreads();         // s_bb, s_src written
-    // the page-table row of every output, 8 independent loads in flight per lane
-    // (one per iteration would pay a full memory latency per row); the loop runs
-    // over the wave's longest map so that every lane takes part in the row unions
+    // the page-table row of every received output, 8 independent loads in flight
+    // per lane (one per iteration would pay a full memory latency per row); the
+    // loop runs over the wave's longest such map so that every lane takes part in
+    // the row unions
     const int wrows = wave_max_i(rows);
     unsigned nremote = 0;            // page_refs: row entries naming another rank's page
     unsigned npages = 0;             //            of them, first sightings of a page (distinct)
@@ -1543,20 +1604,17 @@ __global__ __launch_bounds__(kBlock) void k_gather_particles(const ResampleParam
         uint32_t e[8], eb[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int64_t kk = max(min(k0 + u, rows - 1), 0);
+            e[u] = 0u;
+            eb[u] = kBoxEmpty;
             if (rsrc) {
-                const XDesc x = rsrc[kk];
+                const XDesc x = rsrc[max(min(k0 + u, rows - 1), 0)];
                 e[u] = x.x;
                 eb[u] = x.y;
-            } else {
-                e[u] = src[kk * n];
-                eb[u] = kBoxEmpty;
             }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if (k0 + u < rows) {
-                e[u] &= keep;
                 if (P.refs && ref_tag(e[u])) {
                     ++nremote;
                     bool claimed = false;
@@ -1746,7 +1804,9 @@ hipError_t launch_resample_apply(const ResampleParams &p, bool estimate, hipStre
                                nrecv);
         }
     }
-    hipLaunchKernelGGL(k_gather_particles, dim3(g), dim3(kBlock), 0, s, p);
+    // (the per-output blocks first, then the row tiles: gather_rows)
+    hipLaunchKernelGGL(k_gather_particles, dim3(g + (unsigned)gather_row_groups(p.n, p.map.rows)), dim3(kBlock), 0,
+                       s, p);
     if (estimate) hipLaunchKernelGGL(k_estimate, dim3(1), dim3(1024), 0, s, p, (int32_t)g);
     return hipGetLastError();
 }
