@@ -357,7 +357,7 @@ struct MapRef {
     int64_t n;               // row stride (local particles)
     int32_t rows;            // rows allocated
     char *recs;              // record r at recs + r * kRecBytes
-    SumFrame frame;          // summary grid of the descriptors
+    SumFrame frame;          // summary grid of the row boxes
     float *slb;              // lower bound on every nonzero mirror s (lowered by every write)
     uint32_t *bbox;          // [nblocks][kBBoxRows] workgroup row boxes (null: rows > kBBoxRows)
     const PeerMaps *peers;   // page_refs mode: every rank's pools (device memory); null otherwise

@@ -1476,15 +1476,12 @@ __global__ __launch_bounds__(kBlock) void k_unpack_rows(const ResampleParams P, 
 // their page boxes, row by row (a wave union per row, LDS across the waves).
 //
 // The page-table rows of outputs with a local source are copied by the launch's
-// last workgroups (gather_rows), in tiles of kTileRows rows x 256 outputs taken in
+// last workgroups (gather_rows), in tiles of kTileRows (32) rows x 256 outputs taken in
 // row-major order: the workgroups in flight then read and write the same few
 // rows, where a lane copying its own output's every row (as the received ones
 // still are, below) has each wave touch all 63 rows, 4 MB apart -- address
 // translation, not bytes, held that copy at ~200 us for 252 MB at config 3.
-#ifndef FS2_GATHER_TILE_ROWS
-#define FS2_GATHER_TILE_ROWS 8
-#endif
-constexpr int kTileRows = FS2_GATHER_TILE_ROWS;
+constexpr int kTileRows = 32;        // 8 / 16 / 32 measured: profiles/r06_ab_gather_tiles.json
 __device__ void gather_rows(const ResampleParams &P, int64_t wg, int64_t nwg, unsigned long long *lds_u) {
     const int64_t n = P.n;
     const int64_t nblk = (n + kBlock - 1) / kBlock;
