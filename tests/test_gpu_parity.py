@@ -797,7 +797,7 @@ def test_maps_beyond_row_boxes(fs):
 
 
 @pytest.mark.parametrize("order,wild", [((3, 0, 2, 1), False), ((0, 3, 1, 2), False), ((2, 0, 1, 3), True)])
-def test_overflow_scan_only_where_candidates_remain(fs, order, wild):
+def test_overflow_in_every_measurement_order(fs, order, wild):
     """Round 6: the overflow path in every measurement order.  Two crowds of 30
     (interleaved indices, tight to loose covariances) and a grid hit, with the far
     miss (no candidate: it is appended, then re-observed on the slot it appended)
