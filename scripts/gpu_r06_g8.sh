@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6: the 8-process rehearsal (8 ranks on one GPU, shm transport, 300 K particles
+# round 6 (re-run on the final build): the 8-process rehearsal (8 ranks on one GPU, shm transport, 300 K particles
 # per rank), now with the bytes each rank receives and the exposed exchange time
 set -o pipefail
 cd "$(dirname "$0")/.."
